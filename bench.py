@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Benchmark: queries/sec of the batched IVF search hot path on MI355X.
+
+Metric (BASELINE.json): queries/sec @ recall@10, IVF4096 d=128 nq=10k
+nprobe=32; 1/2/4/8 GPUs.  One step = one batched search of nq=10k synthetic
+uniform queries (faiss float_rand, seed 5678) against IVF4096,Flat over 1M
+synthetic vectors (float_rand seed 1234), k=10, inputs resident in HBM.
+
+N=1: the whole path (coarse fp32-MFMA quantizer + list-centric scan + merge)
+through faiss_amd_Index_search_device.  N>1 (torch.distributed.run, one rank
+per GPU, RCCL): the 1M-vector index is sharded by id modulo N, every rank
+brings its own 10k queries (weak scaling in queries), see hnsw-ivf_amd/dist.py.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch  # loaded before libfaiss_amd so both share one HIP runtime
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+CONFIGS = {
+    # BASELINE.json configs[0..3]
+    "c1": dict(workload="IVF256,Flat", desc="IVF256,Flat", d=64, nb=100_000, nq=1_000,
+               nlist=256, nprobe=8, k=10, ntrain=100_000),
+    "c2": dict(workload="IVF4096,Flat", desc="IVF4096,Flat", d=128, nb=1_000_000, nq=10_000,
+               nlist=4096, nprobe=32, k=10, ntrain=200_000),
+    "c3": dict(workload="IVF4096,PQ32x8", desc="IVF4096,PQ32x8", d=128, nb=1_000_000,
+               nq=10_000, nlist=4096, nprobe=32, k=10, ntrain=200_000),
+    "c4": dict(workload="IVF16384_HNSW32,Flat", desc="IVF16384_HNSW32,Flat", d=128,
+               nb=10_000_000, nq=10_000, nlist=16384, nprobe=64, k=10, ntrain=638_976,
+               efSearch=64),
+}
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector == fp32 MFMA peak
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--recall-queries", type=int, default=1000)
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}"
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    amd = ge.load_package()
+    amd.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    d, nb, nq, k, nprobe = cfg["d"], cfg["nb"], cfg["nq"], cfg["k"], cfg["nprobe"]
+    t0 = time.time()
+    xb = amd.float_rand(nb * d, 1234).reshape(nb, d)
+    index = amd.index_factory(d, cfg["desc"])
+    index.train(xb[:cfg["ntrain"]])
+    ids = np.arange(rank, nb, world, dtype=np.int64)
+    index.add_with_ids(xb[ids], ids)
+    index.nprobe = nprobe
+    if "efSearch" in cfg:
+        amd.ParameterSpace().set_index_parameter(index, "quantizer_efSearch", cfg["efSearch"])
+    index.sync_device()
+    log(f"[rank {rank}] index {cfg['desc']} shard {len(ids)} vectors built in "
+        f"{time.time() - t0:.1f}s")
+
+    qseed = 5678 + 7919 * rank
+    xq = amd.float_rand(nq * d, qseed).reshape(nq, d)
+    x_t = torch.from_numpy(xq).to(dev)
+    D_t = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    I_t = torch.empty((nq, k), dtype=torch.int64, device=dev)
+
+    if world == 1:
+        def step():
+            index.search_device(nq, x_t.data_ptr(), k, D_t.data_ptr(), I_t.data_ptr(), stream)
+    else:
+        hdist = __import__("hnsw_ivf_amd.dist", fromlist=["sharded_search"])
+        cd_t = torch.empty((nq, nprobe), dtype=torch.float32, device=dev)
+        ci_t = torch.empty((nq, nprobe), dtype=torch.int32, device=dev)
+        Ds_t = torch.empty((world * nq, k), dtype=torch.float32, device=dev)
+        Is_t = torch.empty((world * nq, k), dtype=torch.int64, device=dev)
+
+        def quantize(x):
+            index.quantize_device(nq, x.data_ptr(), nprobe, cd_t.data_ptr(), ci_t.data_ptr(),
+                                  stream)
+            return cd_t, ci_t
+
+        def search_pre(xa, ca, cda):
+            index.search_preassigned_device(world * nq, xa.data_ptr(), k, nprobe, ca.data_ptr(),
+                                            cda.data_ptr(), Ds_t.data_ptr(), Is_t.data_ptr(),
+                                            stream)
+            return Ds_t, Is_t
+
+        def merge(Dr, Ir):
+            amd.merge_knn_results_device(nq, k, world, Dr.data_ptr(), Ir.data_ptr(),
+                                         D_t.data_ptr(), I_t.data_ptr(), amd.METRIC_L2, stream)
+            return D_t, I_t
+
+        def step():
+            hdist.sharded_search(x_t, k, quantize, search_pre, merge)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    amd.set_kernel_timing(True)
+    index.reset_kernel_times()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t1
+    amd.set_kernel_timing(False)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    qps = world * nq * args.steps / elapsed
+
+    # ---- dominant kernel: HIP events over the timed region (lib-side)
+    kt = index.kernel_times()
+    scan_name = "ivfpq_scan" if "PQ" in cfg["desc"] else "ivf_flat_scan"
+    scan = [ms for (nm, ms, _) in kt if nm == scan_name]
+    scan_ms = float(np.mean(scan)) if scan else float("nan")
+    # algorithmic work of one scan launch: sum over (query, probe) of the
+    # probed list length x per-candidate cost (Flat: 3*d flops; PQ: M bytes)
+    nq_launch = nq * world
+    cd_h = torch.empty((nq, nprobe), dtype=torch.float32, device=dev)
+    ci_h = torch.empty((nq, nprobe), dtype=torch.int32, device=dev)
+    index.quantize_device(nq, x_t.data_ptr(), nprobe, cd_h.data_ptr(), ci_h.data_ptr(), stream)
+    torch.cuda.synchronize()
+    sizes = np.array([index.get_list_size(l) for l in range(index.nlist)], dtype=np.int64)
+    cand_per_q = float(sizes[ci_h.cpu().numpy().astype(np.int64)].sum()) / nq
+    cands = cand_per_q * nq_launch
+    if "PQ" in cfg["desc"]:
+        M = index.pq_info()["M"]
+        work = cands * M  # code bytes streamed (LUT-gather bound)
+        achieved = work / (scan_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": None}
+    else:
+        work = cands * 3.0 * d  # flops: per candidate d x (sub + fma)
+        achieved = work / (scan_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
+                    "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
+                    "kernel": scan_name, "kernel_ms": scan_ms,
+                    "algorithmic_flops_per_launch": work,
+                    "streamed_bytes_per_launch": cands * d * 4.0}
+
+    # ---- recall@10 of this rank's queries vs exact search (subset)
+    recall = None
+    if rank == 0 and args.recall_queries > 0:
+        nr = min(args.recall_queries, nq)
+        D_t2, I_t2 = D_t.cpu().numpy(), I_t.cpu().numpy()
+        gt = amd.IndexFlatL2(d)
+        gt.add(xb)
+        _, Igt = gt.search(xq[:nr], k)
+        recall = float(np.mean([len(set(a) & set(b)) / k for a, b in zip(I_t2[:nr], Igt)]))
+        del gt
+
+    # ---- CPU baseline: the oracle restatement on the host cores, rank 0, N=1
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and "PQ" not in cfg["desc"] \
+            and "HNSW" not in cfg["desc"]:
+        orc = ge.load_oracle()
+        ncores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        ref = orc.IVFOracle.from_index(index)
+        probe = min(500, nq)
+        tc = time.perf_counter()
+        ref.search_fast(xq[:probe], k, nprobe, nthreads=ncores)
+        tp = time.perf_counter() - tc
+        ns = int(min(nq, max(probe, probe * args.cpu_seconds / max(tp, 1e-3))))
+        tc = time.perf_counter()
+        Dc, Ic = ref.search_fast(xq[:ns], k, nprobe, nthreads=ncores)
+        tcpu = time.perf_counter() - tc
+        agree = float(np.mean(Ic == I_t.cpu().numpy()[:ns]))
+        cpu = {"value": ns / tcpu, "unit": "queries/s", "cores": ncores, "kind": "port",
+               "sample": f"{ns} of the {nq} queries, same index, IVF-Flat scan with 8-way "
+                         f"vectorisable partial sums (oracle search_fast), {tcpu:.1f}s",
+               "id_agreement_vs_gpu": agree}
+
+    if rank == 0:
+        out = {
+            "metric": "queries/sec @ recall@10, IVF4096 d=128 nq=10k nprobe=32; 1/2/4/8 GPUs"
+            if args.config == "c2" else f"queries/sec, {cfg['workload']}",
+            "value": qps, "unit": "queries/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": cfg["workload"], "d": d, "nb": nb, "nq_per_gpu": nq,
+                       "nprobe": nprobe, "k": k, "global_batch": nq * world,
+                       "parallelism": f"shards{world}" if world > 1 else "single",
+                       "recall_at_10": recall, "candidates_per_query": cand_per_q},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

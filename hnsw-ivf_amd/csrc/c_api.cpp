@@ -1,0 +1,546 @@
+// c_api.cpp — the extern "C" boundary (include/faiss_amd_c.h).
+//
+// Conventions restated from the reference C API: every entry point returns
+// 0 / -2 (FaissException) / -4 (std::exception) / -1 (other), and stores the
+// message in a thread-local slot read by faiss_get_last_error()
+// (reference c_api/macros_impl.h:22-56, c_api/error_impl.cpp:15-26).
+#include <cstring>
+#include <string>
+
+#include "../../include/faiss_amd.h"
+#include "../../include/faiss_amd_c.h"
+#include "kernels.h"
+
+using namespace faiss_amd;
+
+namespace faiss_amd {
+void set_current_device(int d);
+}
+
+namespace {
+thread_local std::string g_last_error;
+
+struct SearchParamsC {
+    SearchParametersIVF ivf;
+    SearchParametersHNSW hnsw;
+    bool has_q = false;
+    SearchParamsC() { ivf.nprobe = 1; }
+};
+
+inline Index* IX(FaissIndex* p) { return reinterpret_cast<Index*>(p); }
+inline const Index* IX(const FaissIndex* p) { return reinterpret_cast<const Index*>(p); }
+inline FaissIndex* FX(Index* p) { return reinterpret_cast<FaissIndex*>(p); }
+
+IndexIVF* IVF(FaissIndex* p) {
+    auto r = dynamic_cast<IndexIVF*>(IX(p));
+    FAISS_THROW_IF_NOT_MSG(r, "index is not an IndexIVF");
+    return r;
+}
+const IndexIVF* IVF(const FaissIndex* p) {
+    auto r = dynamic_cast<const IndexIVF*>(IX(p));
+    FAISS_THROW_IF_NOT_MSG(r, "index is not an IndexIVF");
+    return r;
+}
+}  // namespace
+
+#define C_TRY try {
+#define C_CATCH                                   \
+    }                                             \
+    catch (FaissException & e) {                  \
+        g_last_error = e.what();                  \
+        return -2;                                \
+    }                                             \
+    catch (std::exception & e) {                  \
+        g_last_error = e.what();                  \
+        return -4;                                \
+    }                                             \
+    catch (...) {                                 \
+        g_last_error = "Unknown error";           \
+        return -1;                                \
+    }                                             \
+    return 0;
+
+extern "C" {
+
+const char* faiss_get_last_error(void) { return g_last_error.c_str(); }
+
+void faiss_Index_free(FaissIndex* obj) { delete IX(obj); }
+int faiss_Index_d(const FaissIndex* i) { return IX(i)->d; }
+int faiss_Index_is_trained(const FaissIndex* i) { return IX(i)->is_trained ? 1 : 0; }
+idx_t faiss_Index_ntotal(const FaissIndex* i) { return IX(i)->ntotal; }
+FaissMetricType faiss_Index_metric_type(const FaissIndex* i) {
+    return (FaissMetricType)IX(i)->metric_type;
+}
+int faiss_Index_verbose(const FaissIndex* i) { return IX(i)->verbose ? 1 : 0; }
+void faiss_Index_set_verbose(FaissIndex* i, int v) { IX(i)->verbose = v != 0; }
+
+int faiss_Index_train(FaissIndex* index, idx_t n, const float* x) {
+    C_TRY IX(index)->train(n, x);
+    C_CATCH
+}
+int faiss_Index_add(FaissIndex* index, idx_t n, const float* x) {
+    C_TRY IX(index)->add(n, x);
+    C_CATCH
+}
+int faiss_Index_add_with_ids(FaissIndex* index, idx_t n, const float* x, const idx_t* xids) {
+    C_TRY IX(index)->add_with_ids(n, x, xids);
+    C_CATCH
+}
+int faiss_Index_search(const FaissIndex* index, idx_t n, const float* x, idx_t k,
+                       float* distances, idx_t* labels) {
+    C_TRY IX(index)->search(n, x, k, distances, labels, nullptr);
+    C_CATCH
+}
+
+static const SearchParameters* resolve_params(const FaissSearchParameters* p) {
+    if (!p) return nullptr;
+    auto sp = reinterpret_cast<const SearchParamsC*>(p);
+    return &sp->ivf;
+}
+
+int faiss_Index_search_with_params(const FaissIndex* index, idx_t n, const float* x, idx_t k,
+                                   const FaissSearchParameters* params, float* distances,
+                                   idx_t* labels) {
+    C_TRY IX(index)->search(n, x, k, distances, labels, resolve_params(params));
+    C_CATCH
+}
+int faiss_Index_reset(FaissIndex* index) {
+    C_TRY IX(index)->reset();
+    C_CATCH
+}
+
+// ---------------- SearchParametersIVF
+int faiss_SearchParametersIVF_new(FaissSearchParametersIVF** p_sp) {
+    C_TRY* p_sp = reinterpret_cast<FaissSearchParametersIVF*>(new SearchParamsC());
+    C_CATCH
+}
+int faiss_SearchParametersIVF_new_with(FaissSearchParametersIVF** p_sp, void* sel, size_t nprobe,
+                                       size_t max_codes) {
+    C_TRY FAISS_THROW_IF_NOT_MSG(sel == nullptr, "IDSelector is not supported on this path");
+    auto sp = new SearchParamsC();
+    sp->ivf.nprobe = nprobe;
+    sp->ivf.max_codes = max_codes;
+    *p_sp = reinterpret_cast<FaissSearchParametersIVF*>(sp);
+    C_CATCH
+}
+void faiss_SearchParametersIVF_free(FaissSearchParametersIVF* obj) {
+    delete reinterpret_cast<SearchParamsC*>(obj);
+}
+size_t faiss_SearchParametersIVF_nprobe(const FaissSearchParametersIVF* p) {
+    return reinterpret_cast<const SearchParamsC*>(p)->ivf.nprobe;
+}
+void faiss_SearchParametersIVF_set_nprobe(FaissSearchParametersIVF* p, size_t v) {
+    reinterpret_cast<SearchParamsC*>(p)->ivf.nprobe = v;
+}
+void faiss_amd_SearchParametersIVF_set_quantizer_efSearch(FaissSearchParametersIVF* p, int ef) {
+    auto sp = reinterpret_cast<SearchParamsC*>(p);
+    if (ef > 0) {
+        sp->hnsw.efSearch = ef;
+        sp->ivf.quantizer_params = &sp->hnsw;
+    } else {
+        sp->ivf.quantizer_params = nullptr;
+    }
+}
+
+// ---------------- IndexFlat
+int faiss_IndexFlat_new_with(FaissIndexFlat** p_index, idx_t d, FaissMetricType metric) {
+    C_TRY* p_index = FX(new IndexFlat(d, (MetricType)metric));
+    C_CATCH
+}
+int faiss_IndexFlatL2_new_with(FaissIndexFlatL2** p_index, idx_t d) {
+    C_TRY* p_index = FX(new IndexFlatL2(d));
+    C_CATCH
+}
+int faiss_IndexFlatIP_new_with(FaissIndexFlat** p_index, idx_t d) {
+    C_TRY* p_index = FX(new IndexFlatIP(d));
+    C_CATCH
+}
+void faiss_IndexFlat_xb(FaissIndexFlat* index, float** p_xb, size_t* p_size) {
+    auto f = dynamic_cast<IndexFlat*>(IX(index));
+    if (!f) {
+        *p_xb = nullptr;
+        *p_size = 0;
+        return;
+    }
+    *p_xb = f->xb.data();
+    *p_size = f->xb.size();
+}
+
+// ---------------- IndexIVF (getters never throw: 0 / no-op on a wrong type)
+static const IndexIVF* IVFc(const FaissIndexIVF* i) { return dynamic_cast<const IndexIVF*>(IX(i)); }
+static IndexIVF* IVFm(FaissIndexIVF* i) { return dynamic_cast<IndexIVF*>(IX(i)); }
+const char* faiss_amd_Index_type(const FaissIndex* i) {
+    const Index* x = IX(i);
+    if (dynamic_cast<const IndexShardsIVF*>(x)) return "IndexShardsIVF";
+    if (dynamic_cast<const IndexIVFPQ*>(x)) return "IndexIVFPQ";
+    if (dynamic_cast<const IndexIVFFlat*>(x)) return "IndexIVFFlat";
+    if (dynamic_cast<const IndexHNSW*>(x)) return "IndexHNSWFlat";
+    if (dynamic_cast<const IndexFlat*>(x)) return "IndexFlat";
+    return "Index";
+}
+size_t faiss_IndexIVF_nlist(const FaissIndexIVF* i) {
+    if (auto s = dynamic_cast<const IndexShardsIVF*>(IX(i))) return s->nlist;
+    auto v = IVFc(i);
+    return v ? v->nlist : 0;
+}
+size_t faiss_IndexIVF_nprobe(const FaissIndexIVF* i) {
+    if (auto s = dynamic_cast<const IndexShardsIVF*>(IX(i))) return s->nprobe;
+    auto v = IVFc(i);
+    return v ? v->nprobe : 0;
+}
+void faiss_IndexIVF_set_nprobe(FaissIndexIVF* i, size_t v) {
+    if (auto s = dynamic_cast<IndexShardsIVF*>(IX(i))) {
+        s->nprobe = v;
+        for (auto* sh : s->shards) sh->nprobe = v;
+        return;
+    }
+    if (auto x = IVFm(i)) x->nprobe = v;
+}
+FaissIndex* faiss_IndexIVF_quantizer(const FaissIndexIVF* i) {
+    if (auto s = dynamic_cast<const IndexShardsIVF*>(IX(i))) return FX(s->quantizer);
+    auto v = IVFc(i);
+    return v ? FX(v->quantizer) : nullptr;
+}
+int faiss_IndexIVF_own_fields(const FaissIndexIVF* i) {
+    auto v = IVFc(i);
+    return v && v->own_fields ? 1 : 0;
+}
+void faiss_IndexIVF_set_own_fields(FaissIndexIVF* i, int v) {
+    if (auto x = IVFm(i)) x->own_fields = v != 0;
+}
+
+int faiss_IndexIVF_search_preassigned(const FaissIndexIVF* index, idx_t n, const float* x,
+                                      idx_t k, const idx_t* assign, const float* centroid_dis,
+                                      float* distances, idx_t* labels, int store_pairs) {
+    C_TRY IVF(index)->search_preassigned(n, x, k, assign, centroid_dis, distances, labels,
+                                         store_pairs != 0, nullptr);
+    C_CATCH
+}
+size_t faiss_IndexIVF_get_list_size(const FaissIndexIVF* index, size_t list_no) {
+    auto v = IVFc(index);
+    return v && list_no < v->nlist ? v->get_list_size(list_no) : 0;
+}
+void faiss_IndexIVF_invlists_get_ids(const FaissIndexIVF* index, size_t list_no, idx_t* out) {
+    auto v = IVFc(index);
+    if (!v || list_no >= v->nlist) return;
+    const auto& ids = v->invlists->ids[list_no];
+    memcpy(out, ids.data(), sizeof(idx_t) * ids.size());
+}
+void faiss_amd_IndexIVF_invlists_get_codes(const FaissIndexIVF* index, size_t list_no,
+                                           uint8_t* codes) {
+    auto v = IVFc(index);
+    if (!v || list_no >= v->nlist) return;
+    const auto& c = v->invlists->codes[list_no];
+    memcpy(codes, c.data(), c.size());
+}
+size_t faiss_amd_IndexIVF_code_size(const FaissIndexIVF* index) {
+    auto v = IVFc(index);
+    return v ? v->code_size : 0;
+}
+
+static FaissIndexIVFStats g_stats_c;
+void faiss_IndexIVFStats_reset(FaissIndexIVFStats* stats) { memset(stats, 0, sizeof(*stats)); }
+FaissIndexIVFStats* faiss_get_indexIVF_stats(void) {
+    g_stats_c.nq = indexIVF_stats.nq;
+    g_stats_c.nlist = indexIVF_stats.nlist;
+    g_stats_c.ndis = indexIVF_stats.ndis;
+    g_stats_c.nheap_updates = indexIVF_stats.nheap_updates;
+    g_stats_c.quantization_time = indexIVF_stats.quantization_time;
+    g_stats_c.search_time = indexIVF_stats.search_time;
+    return &g_stats_c;
+}
+
+// ---------------- IndexIVFFlat
+int faiss_IndexIVFFlat_new_with(FaissIndexIVFFlat** p_index, FaissIndex* quantizer, size_t d,
+                                size_t nlist) {
+    C_TRY* p_index = FX(new IndexIVFFlat(IX(quantizer), d, nlist, faiss_amd::METRIC_L2));
+    C_CATCH
+}
+int faiss_IndexIVFFlat_new_with_metric(FaissIndexIVFFlat** p_index, FaissIndex* quantizer,
+                                       size_t d, size_t nlist, FaissMetricType metric) {
+    C_TRY* p_index = FX(new IndexIVFFlat(IX(quantizer), d, nlist, (MetricType)metric));
+    C_CATCH
+}
+
+// ---------------- IndexIVFPQ
+int faiss_amd_IndexIVFPQ_new_with(FaissIndexIVFPQ** p_index, FaissIndex* quantizer, size_t d,
+                                  size_t nlist, size_t M, size_t nbits, FaissMetricType metric) {
+    C_TRY* p_index = FX(new IndexIVFPQ(IX(quantizer), d, nlist, M, nbits, (MetricType)metric));
+    C_CATCH
+}
+void faiss_amd_IndexIVFPQ_pq_centroids(FaissIndexIVFPQ* index, float** p, size_t* n) {
+    auto pq = dynamic_cast<IndexIVFPQ*>(IX(index));
+    if (!pq) {
+        *p = nullptr;
+        *n = 0;
+        return;
+    }
+    *p = pq->pq.centroids.data();
+    *n = pq->pq.centroids.size();
+}
+int faiss_amd_IndexIVFPQ_info(const FaissIndexIVFPQ* index, size_t* M, size_t* nbits,
+                              int* by_residual, int* use_precomputed_table) {
+    C_TRY auto pq = dynamic_cast<const IndexIVFPQ*>(IX(index));
+    FAISS_THROW_IF_NOT_MSG(pq, "not an IndexIVFPQ");
+    *M = pq->pq.M;
+    *nbits = pq->pq.nbits;
+    *by_residual = pq->by_residual ? 1 : 0;
+    *use_precomputed_table = pq->use_precomputed_table;
+    C_CATCH
+}
+
+// ---------------- IndexHNSW
+int faiss_amd_IndexHNSWFlat_new_with(FaissIndexHNSW** p_index, int d, int M,
+                                     FaissMetricType metric) {
+    C_TRY* p_index = FX(new IndexHNSWFlat(d, M, (MetricType)metric));
+    C_CATCH
+}
+static IndexHNSW* HN(const FaissIndexHNSW* p) {
+    auto h = dynamic_cast<IndexHNSW*>(const_cast<Index*>(IX(p)));
+    FAISS_THROW_IF_NOT_MSG(h, "not an IndexHNSW");
+    return h;
+}
+static IndexHNSW* HNnt(const FaissIndexHNSW* p) {
+    return dynamic_cast<IndexHNSW*>(const_cast<Index*>(IX(p)));
+}
+int faiss_amd_IndexHNSW_efSearch(const FaissIndexHNSW* p) {
+    auto h = HNnt(p);
+    return h ? h->hnsw.efSearch : 0;
+}
+void faiss_amd_IndexHNSW_set_efSearch(FaissIndexHNSW* p, int v) {
+    if (auto h = HNnt(p)) h->hnsw.efSearch = v;
+}
+int faiss_amd_IndexHNSW_efConstruction(const FaissIndexHNSW* p) {
+    auto h = HNnt(p);
+    return h ? h->hnsw.efConstruction : 0;
+}
+void faiss_amd_IndexHNSW_set_efConstruction(FaissIndexHNSW* p, int v) {
+    if (auto h = HNnt(p)) h->hnsw.efConstruction = v;
+}
+FaissIndex* faiss_amd_IndexHNSW_storage(const FaissIndexHNSW* p) {
+    auto h = HNnt(p);
+    return h ? FX(h->storage) : nullptr;
+}
+int faiss_amd_IndexHNSW_graph(const FaissIndexHNSW* p, int* entry_point, int* max_level,
+                              size_t* n_neighbors, size_t* n_cum, const int32_t** levels,
+                              const size_t** offsets, const int32_t** neighbors,
+                              const int32_t** cum) {
+    C_TRY auto h = HN(p);
+    *entry_point = h->hnsw.entry_point;
+    *max_level = h->hnsw.max_level;
+    *n_neighbors = h->hnsw.neighbors.size();
+    *n_cum = h->hnsw.cum_nneighbor_per_level.size();
+    if (levels) *levels = h->hnsw.levels.data();
+    if (offsets) *offsets = h->hnsw.offsets.data();
+    if (neighbors) *neighbors = h->hnsw.neighbors.data();
+    if (cum) *cum = h->hnsw.cum_nneighbor_per_level.data();
+    C_CATCH
+}
+
+// ---------------- shards
+int faiss_amd_IndexShardsIVF_new(FaissIndexShardsIVF** p_index, FaissIndex* quantizer,
+                                 size_t nlist, int threaded, int successive_ids) {
+    C_TRY* p_index =
+            FX(new IndexShardsIVF(IX(quantizer), nlist, threaded != 0, successive_ids != 0));
+    C_CATCH
+}
+int faiss_amd_IndexShardsIVF_add_shard(FaissIndexShardsIVF* index, FaissIndex* shard) {
+    C_TRY auto s = dynamic_cast<IndexShardsIVF*>(IX(index));
+    FAISS_THROW_IF_NOT_MSG(s, "not an IndexShardsIVF");
+    auto iv = dynamic_cast<IndexIVF*>(IX(shard));
+    FAISS_THROW_IF_NOT_MSG(iv, "shard is not an IndexIVF");
+    s->add_shard(iv);
+    C_CATCH
+}
+int faiss_amd_IndexShardsIVF_count(const FaissIndexShardsIVF* index) {
+    auto s = dynamic_cast<const IndexShardsIVF*>(IX(index));
+    return s ? (int)s->shards.size() : 0;
+}
+
+// ---------------- I/O
+int faiss_write_index(const FaissIndex* idx, FILE* f) {
+    C_TRY write_index(IX(idx), f);
+    C_CATCH
+}
+int faiss_write_index_fname(const FaissIndex* idx, const char* fname) {
+    C_TRY write_index(IX(idx), fname);
+    C_CATCH
+}
+int faiss_read_index(FILE* f, int io_flags, FaissIndex** p_out) {
+    C_TRY* p_out = FX(read_index(f, io_flags));
+    C_CATCH
+}
+int faiss_read_index_fname(const char* fname, int io_flags, FaissIndex** p_out) {
+    C_TRY* p_out = FX(read_index(fname, io_flags));
+    C_CATCH
+}
+
+// ---------------- factory / parameter space
+int faiss_index_factory(FaissIndex** p_index, int d, const char* description,
+                        FaissMetricType metric) {
+    C_TRY* p_index = FX(index_factory(d, description, (MetricType)metric));
+    C_CATCH
+}
+struct FaissParameterSpace_H {
+    int dummy;
+};
+int faiss_ParameterSpace_new(FaissParameterSpace** space) {
+    C_TRY* space = new FaissParameterSpace_H();
+    C_CATCH
+}
+void faiss_ParameterSpace_free(FaissParameterSpace* space) { delete space; }
+int faiss_ParameterSpace_set_index_parameter(const FaissParameterSpace*, FaissIndex* index,
+                                             const char* name, double val) {
+    // faiss/AutoTune.cpp:468-557 subset
+    C_TRY std::string n(name);
+    Index* ix = IX(index);
+    if (n == "nprobe") {
+        if (auto s = dynamic_cast<IndexShardsIVF*>(ix)) {
+            s->nprobe = (size_t)val;
+            for (auto* sh : s->shards) sh->nprobe = (size_t)val;
+        } else {
+            IVF(index)->nprobe = (size_t)val;
+        }
+    } else if (n == "efSearch") {
+        auto h = dynamic_cast<IndexHNSW*>(ix);
+        FAISS_THROW_IF_NOT_MSG(h, "efSearch needs an IndexHNSW");
+        h->hnsw.efSearch = (int)val;
+    } else if (n == "quantizer_efSearch") {
+        Index* q = nullptr;
+        if (auto s = dynamic_cast<IndexShardsIVF*>(ix)) q = s->quantizer;
+        else q = IVF(index)->quantizer;
+        auto h = dynamic_cast<IndexHNSW*>(q);
+        FAISS_THROW_IF_NOT_MSG(h, "quantizer is not an IndexHNSW");
+        h->hnsw.efSearch = (int)val;
+    } else {
+        FAISS_THROW_MSG("ParameterSpace::set_index_parameter: unknown parameter " + n);
+    }
+    C_CATCH
+}
+
+// ---------------- merge
+int faiss_amd_merge_knn_results(size_t n, size_t k, int nshard, const float* all_d,
+                                const idx_t* all_l, float* d, idx_t* l, FaissMetricType metric) {
+    C_TRY merge_knn_results(n, k, nshard, all_d, all_l, d, l, (MetricType)metric);
+    C_CATCH
+}
+
+// ---------------- device extensions
+int faiss_amd_device_count(int* count) {
+    C_TRY int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    C_CATCH
+}
+int faiss_amd_set_device(int device) {
+    C_TRY ensure_hip();
+    set_current_device(device);
+    C_CATCH
+}
+int faiss_amd_Index_sync_device(FaissIndex* index) {
+    C_TRY ensure_hip();
+    int prev = 0;
+    HIP_CHECK(hipGetDevice(&prev));
+    HIP_CHECK(hipSetDevice(IX(index)->device));
+    IX(index)->sync_device();
+    HIP_CHECK(hipSetDevice(prev));
+    C_CATCH
+}
+
+static hipStream_t pick_stream(const Index* ix, void* stream) {
+    return stream ? (hipStream_t)stream : ix->stream();
+}
+
+static int ldx_of(const Index* ix) { return (int)roundup((size_t)ix->d, 4); }
+
+int faiss_amd_Index_search_device(const FaissIndex* index, idx_t n, const float* x_dev, idx_t k,
+                                  float* d_dev, idx_t* l_dev, void* stream) {
+    C_TRY const Index* ix = IX(index);
+    FAISS_THROW_IF_NOT_MSG(ix->d % 4 == 0, "device entry points need d % 4 == 0");
+    ensure_hip();
+    ix->sync_device();
+    ix->search_device(n, x_dev, ldx_of(ix), k, d_dev, l_dev, nullptr, pick_stream(ix, stream));
+    C_CATCH
+}
+int faiss_amd_IndexIVF_search_preassigned_device(const FaissIndexIVF* index, idx_t n,
+                                                 const float* x_dev, idx_t k, int nprobe,
+                                                 const int32_t* assign_dev,
+                                                 const float* cdis_dev, float* d_dev,
+                                                 idx_t* l_dev, void* stream) {
+    C_TRY const IndexIVF* ix = IVF(index);
+    FAISS_THROW_IF_NOT_MSG(ix->d % 4 == 0, "device entry points need d % 4 == 0");
+    FAISS_THROW_IF_NOT(nprobe > 0 && nprobe <= kern::kMaxK);
+    ensure_hip();
+    ix->sync_device();
+    ix->search_preassigned_device(n, x_dev, ldx_of(ix), k, nprobe, assign_dev, cdis_dev, d_dev,
+                                  l_dev, pick_stream(ix, stream));
+    C_CATCH
+}
+int faiss_amd_IndexIVF_quantize_device(const FaissIndexIVF* index, idx_t n, const float* x_dev,
+                                       int nprobe, float* cdis_dev, int32_t* assign_dev,
+                                       void* stream) {
+    C_TRY const IndexIVF* ix = IVF(index);
+    FAISS_THROW_IF_NOT_MSG(ix->d % 4 == 0, "device entry points need d % 4 == 0");
+    ensure_hip();
+    ix->sync_device();
+    ix->quantize_device(n, x_dev, ldx_of(ix), nprobe, cdis_dev, assign_dev, nullptr,
+                        pick_stream(ix, stream));
+    C_CATCH
+}
+int faiss_amd_merge_knn_results_device(size_t n, size_t k, int nshard, const float* all_d,
+                                       const idx_t* all_l, float* d, idx_t* l,
+                                       FaissMetricType metric, void* stream) {
+    C_TRY ensure_hip();
+    FAISS_THROW_IF_NOT(nshard > 0 && nshard < 32768 && k <= 64);
+    kern::merge_rows(all_d, all_l, (int64_t)n, (nshard << 16) | (int)k, (int)k,
+                     metric == ::METRIC_L2, d, l, (hipStream_t)stream);
+    C_CATCH
+}
+int faiss_amd_set_kernel_timing(int enable) {
+    C_TRY set_kernel_timing_enabled(enable != 0);
+    C_CATCH
+}
+int faiss_amd_last_kernel_times(const FaissIndex* index, int* n_kernels, char* names,
+                                double* millis, double* units) {
+    C_TRY const Index* ix = IX(index);
+    std::vector<KernelTimes*> all{&ix->ktimes};
+    if (auto ivf = dynamic_cast<const IndexIVF*>(ix)) all.push_back(&ivf->quantizer->ktimes);
+    if (auto sh = dynamic_cast<const IndexShardsIVF*>(ix)) {
+        all.push_back(&sh->quantizer->ktimes);
+        for (auto* s : sh->shards) all.push_back(&s->ktimes);
+    }
+    int cnt = 0;
+    for (auto t : all) {
+        t->resolve();
+        cnt += (int)t->names.size();
+    }
+    if (names && millis) {
+        int i = 0;
+        for (auto t : all)
+            for (size_t j = 0; j < t->names.size() && i < *n_kernels; j++, i++) {
+                strncpy(names + 32 * i, t->names[j].c_str(), 31);
+                names[32 * i + 31] = 0;
+                millis[i] = t->millis[j];
+                if (units) units[i] = t->units[j];
+            }
+    }
+    *n_kernels = cnt;
+    C_CATCH
+}
+int faiss_amd_reset_kernel_times(FaissIndex* index) {
+    C_TRY Index* ix = IX(index);
+    ix->ktimes.clear();
+    if (auto ivf = dynamic_cast<IndexIVF*>(ix)) ivf->quantizer->ktimes.clear();
+    if (auto sh = dynamic_cast<IndexShardsIVF*>(ix)) {
+        sh->quantizer->ktimes.clear();
+        for (auto* s : sh->shards) s->ktimes.clear();
+    }
+    C_CATCH
+}
+int faiss_amd_float_rand(float* x, size_t n, int64_t seed) {
+    C_TRY float_rand(x, n, seed);
+    C_CATCH
+}
+
+}  // extern "C"

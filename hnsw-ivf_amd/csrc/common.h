@@ -1,0 +1,181 @@
+// common.h — error handling, HIP helpers and device memory for the
+// MI355X-native IVF search path.
+//
+// Error model mirrors the reference: preconditions throw a FaissException
+// (reference faiss/impl/FaissAssert.h, faiss/impl/FaissException.h) which the
+// C-ABI turns into return code -2 (reference c_api/macros_impl.h:22-56).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace faiss_amd {
+
+using idx_t = int64_t;
+
+enum MetricType { METRIC_INNER_PRODUCT = 0, METRIC_L2 = 1 };
+
+class FaissException : public std::exception {
+   public:
+    explicit FaissException(const std::string& m) : msg(m) {}
+    FaissException(const std::string& m, const char* func, const char* file, int line) {
+        char buf[1024];
+        snprintf(buf, sizeof(buf), "Error in %s at %s:%d: %s", func, file, line, m.c_str());
+        msg = buf;
+    }
+    const char* what() const noexcept override { return msg.c_str(); }
+    std::string msg;
+};
+
+#define FAISS_THROW_MSG(MSG) \
+    throw ::faiss_amd::FaissException(MSG, __PRETTY_FUNCTION__, __FILE__, __LINE__)
+
+#define FAISS_THROW_IF_NOT(X)                                         \
+    do {                                                              \
+        if (!(X)) {                                                   \
+            FAISS_THROW_MSG("Error: '" #X "' failed");                \
+        }                                                             \
+    } while (0)
+
+#define FAISS_THROW_IF_NOT_MSG(X, MSG)                                \
+    do {                                                              \
+        if (!(X)) {                                                   \
+            FAISS_THROW_MSG(std::string("Error: '" #X "' failed: ") + (MSG)); \
+        }                                                             \
+    } while (0)
+
+#define FAISS_THROW_FMT(FMT, ...)                                     \
+    do {                                                              \
+        char __buf[1024];                                             \
+        snprintf(__buf, sizeof(__buf), FMT, __VA_ARGS__);             \
+        FAISS_THROW_MSG(__buf);                                       \
+    } while (0)
+
+#define HIP_CHECK(expr)                                                            \
+    do {                                                                           \
+        hipError_t __e = (expr);                                                   \
+        if (__e != hipSuccess) {                                                   \
+            FAISS_THROW_FMT("HIP error %d (%s) in %s", (int)__e,                   \
+                            hipGetErrorString(__e), #expr);                        \
+        }                                                                          \
+    } while (0)
+
+// Launch check: surfaces launch-configuration errors immediately.
+#define HIP_LAUNCH_CHECK() HIP_CHECK(hipGetLastError())
+
+inline size_t roundup(size_t a, size_t b) { return (a + b - 1) / b * b; }
+inline size_t cdiv(size_t a, size_t b) { return (a + b - 1) / b; }
+
+// Owning device buffer (hipMalloc'ed), bound to the device current at alloc.
+struct DeviceBuffer {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    int device = -1;
+    DeviceBuffer() = default;
+    DeviceBuffer(const DeviceBuffer&) = delete;
+    DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+    DeviceBuffer(DeviceBuffer&& o) noexcept { *this = std::move(o); }
+    DeviceBuffer& operator=(DeviceBuffer&& o) noexcept {
+        if (this != &o) {
+            release();
+            ptr = o.ptr; bytes = o.bytes; device = o.device;
+            o.ptr = nullptr; o.bytes = 0;
+        }
+        return *this;
+    }
+    ~DeviceBuffer() { release(); }
+    void release() {
+        if (ptr) {
+            int cur = 0;
+            hipGetDevice(&cur);
+            if (device >= 0 && device != cur) hipSetDevice(device);
+            hipFree(ptr);
+            if (device >= 0 && device != cur) hipSetDevice(cur);
+            ptr = nullptr;
+            bytes = 0;
+        }
+    }
+    // grow-only reallocation (contents not preserved)
+    void reserve(size_t nbytes) {
+        if (nbytes <= bytes && ptr) return;
+        release();
+        size_t nb = nbytes ? nbytes : 16;
+        HIP_CHECK(hipGetDevice(&device));
+        HIP_CHECK(hipMalloc(&ptr, nb));
+        bytes = nb;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(ptr); }
+};
+
+// Per-device resources: one non-blocking stream per device, created lazily.
+struct DeviceContext {
+    int device = 0;
+    hipStream_t stream = nullptr;
+};
+
+DeviceContext& device_context(int device);
+int current_device();  // device selected by faiss_amd_set_device for this thread
+void ensure_hip();     // throws a FaissException when no HIP device is usable
+
+// Kernel-time recorder (HIP events) used by bench.py for the roofline line.
+// Events are recorded on the launch stream without synchronising; elapsed
+// times are resolved lazily when queried.
+struct KernelTimes {
+    std::vector<std::string> names;
+    std::vector<hipEvent_t> e0, e1;
+    std::vector<double> units;
+    std::vector<double> millis;  // resolved
+    size_t resolved = 0;
+    void clear() {
+        for (auto e : e0) (void)hipEventDestroy(e);
+        for (auto e : e1) (void)hipEventDestroy(e);
+        names.clear(); e0.clear(); e1.clear(); units.clear(); millis.clear();
+        resolved = 0;
+    }
+    void resolve() {
+        for (; resolved < e0.size(); resolved++) {
+            float ms = 0;
+            (void)hipEventSynchronize(e1[resolved]);
+            (void)hipEventElapsedTime(&ms, e0[resolved], e1[resolved]);
+            millis.push_back(ms);
+        }
+    }
+    ~KernelTimes() { clear(); }
+};
+bool kernel_timing_enabled();
+void set_kernel_timing_enabled(bool);
+
+// Brackets a launch with HIP events when timing is enabled.
+struct ScopedKernelTimer {
+    KernelTimes* sink;
+    hipStream_t stream;
+    hipEvent_t a = nullptr, b = nullptr;
+    ScopedKernelTimer(KernelTimes* s, const char* name, double units, hipStream_t st)
+            : sink(s), stream(st) {
+        if (sink && kernel_timing_enabled()) {
+            HIP_CHECK(hipEventCreate(&a));
+            HIP_CHECK(hipEventCreate(&b));
+            HIP_CHECK(hipEventRecord(a, stream));
+            sink->names.push_back(name);
+            sink->units.push_back(units);
+        }
+    }
+    ~ScopedKernelTimer() {
+        if (a) {
+            (void)hipEventRecord(b, stream);
+            sink->e0.push_back(a);
+            sink->e1.push_back(b);
+        }
+    }
+};
+
+}  // namespace faiss_amd

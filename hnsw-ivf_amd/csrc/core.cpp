@@ -1,0 +1,401 @@
+// core.cpp — device contexts, Index base, IndexFlat (coarse quantizer),
+// GPU k-means, host merge_knn_results and the float_rand restatement.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+#include "../../include/faiss_amd.h"
+#include "kernels.h"
+
+namespace faiss_amd {
+
+IndexIVFStats indexIVF_stats;
+
+// ---------------------------------------------------------------- devices
+namespace {
+std::mutex g_ctx_mu;
+std::vector<std::unique_ptr<DeviceContext>> g_ctx;
+thread_local int tl_device = 0;
+bool g_timing = false;
+}  // namespace
+
+void ensure_hip() {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) {
+        FAISS_THROW_MSG(
+                "no usable HIP device: the MI355X IVF search path has no CPU fallback "
+                "(hipGetDeviceCount: " +
+                std::string(hipGetErrorString(e)) + ")");
+    }
+}
+
+DeviceContext& device_context(int device) {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    if ((int)g_ctx.size() <= device) g_ctx.resize(device + 1);
+    if (!g_ctx[device]) {
+        ensure_hip();
+        auto c = std::make_unique<DeviceContext>();
+        c->device = device;
+        int cur = 0;
+        HIP_CHECK(hipGetDevice(&cur));
+        HIP_CHECK(hipSetDevice(device));
+        HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIP_CHECK(hipSetDevice(cur));
+        g_ctx[device] = std::move(c);
+    }
+    return *g_ctx[device];
+}
+
+int current_device() { return tl_device; }
+void set_current_device(int d) { tl_device = d; }
+bool kernel_timing_enabled() { return g_timing; }
+void set_kernel_timing_enabled(bool b) { g_timing = b; }
+
+struct DeviceGuard {
+    int prev = 0;
+    explicit DeviceGuard(int dev) {
+        ensure_hip();
+        HIP_CHECK(hipGetDevice(&prev));
+        if (prev != dev) HIP_CHECK(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        int cur = 0;
+        hipGetDevice(&cur);
+        if (cur != prev) hipSetDevice(prev);
+    }
+};
+
+// ---------------------------------------------------------------- Index
+Index::Index(idx_t d_, MetricType metric) : d((int)d_), metric_type(metric) {
+    device = current_device();
+}
+Index::~Index() = default;
+
+void Index::train(idx_t, const float*) {}
+
+void Index::add_with_ids(idx_t, const float*, const idx_t*) {
+    FAISS_THROW_MSG("add_with_ids not implemented for this type of index");
+}
+
+void Index::assign_device(idx_t, const float*, int, int, float*, int32_t*,
+                          const SearchParameters*, hipStream_t) const {
+    FAISS_THROW_MSG("this index cannot be used as a coarse quantizer");
+}
+
+void Index::reconstruct(idx_t, float*) const {
+    FAISS_THROW_MSG("reconstruct not implemented for this type of index");
+}
+
+hipStream_t Index::stream() const { return device_context(device).stream; }
+
+// Host entry: upload (zero-padded rows), search_device, download.
+void Index::search(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                   const SearchParameters* params) const {
+    FAISS_THROW_IF_NOT(k > 0);
+    if (n == 0) return;
+    DeviceGuard g(device);
+    sync_device();
+    hipStream_t s = stream();
+    const int ldx = ld();
+    DeviceBuffer bx, bd, bi;
+    bx.reserve(sizeof(float) * n * ldx);
+    bd.reserve(sizeof(float) * n * k);
+    bi.reserve(sizeof(idx_t) * n * k);
+    if (ldx != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * n * ldx, s));
+    HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ldx, x, sizeof(float) * d,
+                               sizeof(float) * d, n, hipMemcpyHostToDevice, s));
+    search_device(n, bx.as<float>(), ldx, k, bd.as<float>(), bi.as<idx_t>(), params, s);
+    HIP_CHECK(hipMemcpyAsync(distances, bd.ptr, sizeof(float) * n * k, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
+// ---------------------------------------------------------------- IndexFlat
+IndexFlat::IndexFlat(idx_t d_, MetricType metric) : Index(d_, metric) {}
+
+void IndexFlat::add(idx_t n, const float* x) {
+    FAISS_THROW_IF_NOT(n >= 0);
+    xb.insert(xb.end(), x, x + (size_t)n * d);
+    ntotal += n;
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    dirty_ = true;
+}
+
+void IndexFlat::reset() {
+    xb.clear();
+    ntotal = 0;
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    dirty_ = true;
+}
+
+void IndexFlat::reconstruct(idx_t key, float* recons) const {
+    FAISS_THROW_IF_NOT(key >= 0 && key < ntotal);
+    memcpy(recons, xb.data() + (size_t)key * d, sizeof(float) * d);
+}
+
+void IndexFlat::sync_device() const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    if (!dirty_) return;
+    DeviceGuard dg(device);
+    hipStream_t s = stream();
+    const int l = ld();
+    d_xb_.reserve(sizeof(float) * std::max<idx_t>(ntotal, 1) * l);
+    d_norms_.reserve(sizeof(float) * std::max<idx_t>(ntotal, 1));
+    if (ntotal > 0) {
+        if (l != d) HIP_CHECK(hipMemsetAsync(d_xb_.ptr, 0, sizeof(float) * ntotal * l, s));
+        HIP_CHECK(hipMemcpy2DAsync(d_xb_.ptr, sizeof(float) * l, xb.data(), sizeof(float) * d,
+                                   sizeof(float) * d, ntotal, hipMemcpyHostToDevice, s));
+        kern::row_norms(d_xb_.as<float>(), ntotal, d, l, d_norms_.as<float>(), s);
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    dirty_ = false;
+}
+
+const float* IndexFlat::device_vectors() const {
+    sync_device();
+    return d_xb_.as<float>();
+}
+const float* IndexFlat::device_norms() const {
+    sync_device();
+    return d_norms_.as<float>();
+}
+
+template <class OutIdx>
+void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* distances,
+                           OutIdx* labels, hipStream_t s) const {
+    FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kern::kMaxK, "k must be in [1, 64] on this path");
+    sync_device();
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    const int l = ld();
+    const int metric_l2 = metric_type == METRIC_L2;
+    constexpr bool i32 = sizeof(OutIdx) == 4;
+    int32_t* o32 = i32 ? (int32_t*)labels : nullptr;
+    int64_t* o64 = i32 ? nullptr : (int64_t*)labels;
+    const idx_t ny = ntotal;
+    s_xn_.reserve(sizeof(float) * std::max<idx_t>(n, 1));
+    if (metric_l2) kern::row_norms(x, n, d, ldx, s_xn_.as<float>(), s);
+    const idx_t Yc = std::min<idx_t>(std::max<idx_t>(ny, 1), 1 << 20);
+    const idx_t nyc = (idx_t)cdiv(std::max<idx_t>(ny, 1), Yc);
+    FAISS_THROW_IF_NOT_MSG(!(i32 && nyc > 1), "coarse quantizer larger than 2^20 centroids");
+    const size_t tile_budget = (size_t)256 << 20;  // bytes
+    idx_t qchunk = std::max<idx_t>(128, (idx_t)(tile_budget / (sizeof(float) * Yc)) / 128 * 128);
+    qchunk = std::min<idx_t>(qchunk, n);
+    s_tile_.reserve(sizeof(float) * qchunk * Yc);
+    if (nyc > 1) {
+        s_cand_d_.reserve(sizeof(float) * nyc * qchunk * k);
+        s_cand_i_.reserve(sizeof(idx_t) * nyc * qchunk * k);
+    }
+    double flops = 2.0 * (double)n * (double)ny * (double)d;
+    ScopedKernelTimer tm(&ktimes, "flat_distance+select", flops, s);
+    for (idx_t q0 = 0; q0 < n; q0 += qchunk) {
+        const idx_t nq = std::min(qchunk, n - q0);
+        const float* xq = x + q0 * ldx;
+        const float* xn = s_xn_.as<float>() + q0;
+        if (nyc == 1) {
+            if (ny > 0)
+                kern::pairwise_distances(xq, nq, ldx, xn, d_xb_.as<float>(), ny, l,
+                                         d_norms_.as<float>(), l, metric_l2,
+                                         s_tile_.as<float>(), ny, s);
+            kern::select_rows(s_tile_.as<float>(), nq, ny, ny, k, metric_l2, 0,
+                              distances + q0 * k, o32 ? o32 + q0 * k : nullptr,
+                              o64 ? o64 + q0 * k : nullptr, k, s);
+        } else {
+            for (idx_t c = 0; c < nyc; c++) {
+                const idx_t y0 = c * Yc, nyy = std::min(Yc, ny - y0);
+                kern::pairwise_distances(xq, nq, ldx, xn, d_xb_.as<float>() + y0 * l, nyy, l,
+                                         d_norms_.as<float>() + y0, l, metric_l2,
+                                         s_tile_.as<float>(), nyy, s);
+                kern::select_rows(s_tile_.as<float>(), nq, nyy, nyy, k, metric_l2, y0,
+                                  s_cand_d_.as<float>() + c * nq * k, nullptr,
+                                  s_cand_i_.as<int64_t>() + c * nq * k, k, s);
+            }
+            kern::merge_rows(s_cand_d_.as<float>(), s_cand_i_.as<int64_t>(), nq,
+                             (int)((nyc << 16) | k), k, metric_l2, distances + q0 * k,
+                             o64 + q0 * k, s);
+        }
+    }
+}
+
+void IndexFlat::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                              idx_t* labels, const SearchParameters*, hipStream_t s) const {
+    DeviceGuard g(device);
+    knn_device<idx_t>(n, x, ldx, (int)k, distances, labels, s);
+}
+
+void IndexFlat::assign_device(idx_t n, const float* x, int ldx, int k, float* distances,
+                              int32_t* labels, const SearchParameters*, hipStream_t s) const {
+    DeviceGuard g(device);
+    knn_device<int32_t>(n, x, ldx, k, distances, labels, s);
+}
+
+// ---------------------------------------------------------------- k-means
+// faiss/Clustering.cpp semantics kept where they matter for index quality:
+// subsample to 256 points per centroid, random initial centroids, niter
+// Lloyd iterations, split_clusters for empty clusters (EPS = 1/1024).
+void kmeans_train(int d, idx_t n, const float* x, int k, int niter, int64_t seed,
+                  float* centroids, int device, bool verbose) {
+    FAISS_THROW_IF_NOT_MSG(n >= k, "Number of training points should be at least as large as "
+                                   "number of clusters");
+    DeviceGuard g(device);
+    std::mt19937 rng((unsigned)seed);
+    std::vector<idx_t> perm(n);
+    for (idx_t i = 0; i < n; i++) perm[i] = i;
+    const idx_t max_pts = (idx_t)k * 256;
+    std::vector<float> xs;
+    const float* xt = x;
+    idx_t nt = n;
+    if (n > max_pts) {
+        std::shuffle(perm.begin(), perm.end(), rng);
+        nt = max_pts;
+        xs.resize((size_t)nt * d);
+        for (idx_t i = 0; i < nt; i++)
+            memcpy(xs.data() + (size_t)i * d, x + (size_t)perm[i] * d, sizeof(float) * d);
+        xt = xs.data();
+        for (idx_t i = 0; i < nt; i++) perm[i] = i;
+        perm.resize(nt);
+    }
+    std::shuffle(perm.begin(), perm.end(), rng);
+    for (int c = 0; c < k; c++)
+        memcpy(centroids + (size_t)c * d, xt + (size_t)perm[c] * d, sizeof(float) * d);
+
+    const int ld = (int)roundup((size_t)d, 4);
+    hipStream_t s = device_context(device).stream;
+    DeviceBuffer bx, bd, bi;
+    bx.reserve(sizeof(float) * nt * ld);
+    bd.reserve(sizeof(float) * nt);
+    bi.reserve(sizeof(int32_t) * nt);
+    if (ld != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * nt * ld, s));
+    HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ld, xt, sizeof(float) * d,
+                               sizeof(float) * d, nt, hipMemcpyHostToDevice, s));
+    std::vector<int32_t> assign(nt);
+    std::vector<float> dis(nt);
+    std::vector<double> sums((size_t)k * d);
+    std::vector<idx_t> counts(k);
+    IndexFlat cent(d, METRIC_L2);
+    cent.device = device;
+    for (int it = 0; it < niter; it++) {
+        cent.reset();
+        cent.add(k, centroids);
+        cent.assign_device(nt, bx.as<float>(), ld, 1, bd.as<float>(), bi.as<int32_t>(), nullptr,
+                           s);
+        HIP_CHECK(hipMemcpyAsync(assign.data(), bi.ptr, sizeof(int32_t) * nt,
+                                 hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipMemcpyAsync(dis.data(), bd.ptr, sizeof(float) * nt, hipMemcpyDeviceToHost,
+                                 s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        std::fill(sums.begin(), sums.end(), 0.0);
+        std::fill(counts.begin(), counts.end(), 0);
+        double obj = 0;
+        for (idx_t i = 0; i < nt; i++) {
+            int a = assign[i];
+            FAISS_THROW_IF_NOT(a >= 0 && a < k);
+            counts[a]++;
+            obj += dis[i];
+            const float* xi = xt + (size_t)i * d;
+            double* sa = sums.data() + (size_t)a * d;
+            for (int j = 0; j < d; j++) sa[j] += xi[j];
+        }
+        for (int c = 0; c < k; c++) {
+            if (counts[c] == 0) continue;
+            for (int j = 0; j < d; j++)
+                centroids[(size_t)c * d + j] = (float)(sums[(size_t)c * d + j] / counts[c]);
+        }
+        // split_clusters (faiss/Clustering.cpp)
+        const float EPS = 1.f / 1024.f;
+        std::uniform_real_distribution<float> U(0.f, 1.f);
+        for (int ci = 0; ci < k; ci++) {
+            if (counts[ci] != 0) continue;
+            int cj = 0;
+            for (;; cj = (cj + 1) % k) {
+                float p = (counts[cj] - 1.0f) / (float)(nt - k);
+                if (U(rng) < p) break;
+            }
+            memcpy(centroids + (size_t)ci * d, centroids + (size_t)cj * d, sizeof(float) * d);
+            for (int j = 0; j < d; j++) {
+                if (j % 2 == 0) {
+                    centroids[(size_t)ci * d + j] *= 1 + EPS;
+                    centroids[(size_t)cj * d + j] *= 1 - EPS;
+                } else {
+                    centroids[(size_t)ci * d + j] *= 1 - EPS;
+                    centroids[(size_t)cj * d + j] *= 1 + EPS;
+                }
+            }
+            counts[ci] = counts[cj] / 2;
+            counts[cj] -= counts[ci];
+        }
+        if (verbose) fprintf(stderr, "kmeans iter %d obj %g\n", it, obj);
+    }
+}
+
+// ---------------------------------------------------------------- merge
+// faiss/utils/Heap.cpp:159-230: per query, repeatedly take the best shard
+// head (ties -> lower shard for L2, higher shard for IP, as the CMin/CMax
+// heap pops them), stop a shard at its first -1, pad with the neutral value.
+void merge_knn_results(size_t n, size_t k, int nshard, const float* all_distances,
+                       const idx_t* all_labels, float* distances, idx_t* labels,
+                       MetricType metric) {
+    const size_t stride = n * k;
+    const bool l2 = metric == METRIC_L2;
+    std::vector<size_t> ptr(nshard);
+    for (size_t i = 0; i < n; i++) {
+        std::fill(ptr.begin(), ptr.end(), 0);
+        size_t j = 0;
+        for (; j < k; j++) {
+            int best = -1;
+            float bd = 0;
+            for (int s = 0; s < nshard; s++) {
+                size_t p = ptr[s];
+                if (p >= k) continue;
+                const idx_t lab = all_labels[s * stride + i * k + p];
+                if (lab < 0) continue;
+                float v = all_distances[s * stride + i * k + p];
+                bool better;
+                if (best < 0) better = true;
+                else if (l2) better = v < bd;           // ties keep the lower shard
+                else better = v > bd || v == bd;        // ties move to the higher shard
+                if (better) {
+                    best = s;
+                    bd = v;
+                }
+            }
+            if (best < 0) break;
+            distances[i * k + j] = bd;
+            labels[i * k + j] = all_labels[best * stride + i * k + ptr[best]];
+            ptr[best]++;
+        }
+        for (; j < k; j++) {
+            distances[i * k + j] = l2 ? FLT_MAX : -FLT_MAX;
+            labels[i * k + j] = -1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- float_rand
+// faiss/utils/random.cpp:35-53,95-112 — std::mt19937 streams, 1024 blocks.
+void float_rand(float* x, size_t n, int64_t seed) {
+    const size_t nblock = n < 1024 ? 1 : 1024;
+    std::mt19937 rng0((unsigned int)seed);
+    int a0 = (int)(rng0() & 0x7fffffff), b0 = (int)(rng0() & 0x7fffffff);
+    auto run = [&](int64_t j0, int64_t j1) {
+        for (int64_t j = j0; j < j1; j++) {
+            std::mt19937 rng((unsigned int)(int64_t)(a0 + j * b0));
+            const size_t istart = j * n / nblock;
+            const size_t iend = (j + 1) * n / nblock;
+            const float mx = (float)std::mt19937::max();
+            for (size_t i = istart; i < iend; i++) x[i] = (float)rng() / mx;
+        }
+    };
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < (1 << 20)) nt = 1;
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++) {
+        int64_t j0 = (int64_t)nblock * t / nt, j1 = (int64_t)nblock * (t + 1) / nt;
+        th.emplace_back(run, j0, j1);
+    }
+    for (auto& t : th) t.join();
+}
+
+}  // namespace faiss_amd

@@ -1,0 +1,391 @@
+// hnsw.cpp — HNSW graph (host build) and IndexHNSW(Flat) with GPU search.
+//
+// Graph construction restates faiss/impl/HNSW.cpp (set_default_probas :62-75,
+// random_level :51-60, prepare_level_tab :210-235, shrink_neighbor_list
+// :237-270, add_link :300-335, search_neighbors_to_add :340-490,
+// add_links_starting_from :492-527, add_with_locks :533-575) and the vertex
+// ordering of faiss/IndexHNSW.cpp:68-230 (hnsw_add_vertices), run serially so
+// the graph is deterministic.  It is index building, not the search path; the
+// search runs on the GPU (kernels_hnsw.hip).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <queue>
+
+#include "../../include/faiss_amd.h"
+#include "kernels.h"
+
+namespace faiss_amd {
+
+namespace {
+struct DevGuard2 {
+    int prev = 0;
+    explicit DevGuard2(int dev) {
+        ensure_hip();
+        HIP_CHECK(hipGetDevice(&prev));
+        if (prev != dev) HIP_CHECK(hipSetDevice(dev));
+    }
+    ~DevGuard2() {
+        int cur = 0;
+        hipGetDevice(&cur);
+        if (cur != prev) hipSetDevice(prev);
+    }
+};
+
+// sequential fma chain, the evaluation order shared with the GPU kernels
+inline float l2_seq(const float* a, const float* b, int d) {
+    float acc = 0.f;
+    for (int j = 0; j < d; j++) {
+        float t = a[j] - b[j];
+        acc = fmaf(t, t, acc);
+    }
+    return acc;
+}
+
+struct NodeDistCloser {  // faiss/impl/HNSW.h NodeDistCloser
+    float d;
+    int id;
+    NodeDistCloser(float d_, int i) : d(d_), id(i) {}
+    bool operator<(const NodeDistCloser& o) const { return d < o.d; }
+};
+struct NodeDistFarther {
+    float d;
+    int id;
+    NodeDistFarther(float d_, int i) : d(d_), id(i) {}
+    bool operator<(const NodeDistFarther& o) const { return d > o.d; }
+};
+
+struct Builder {
+    HNSW& h;
+    const float* xb;
+    int d;
+    std::vector<uint8_t> visited;
+    Builder(HNSW& h_, const float* xb_, int d_, size_t n) : h(h_), xb(xb_), d(d_), visited(n, 0) {}
+    float dis(const float* q, int id) const { return l2_seq(q, xb + (size_t)id * d, d); }
+    float sym(int a, int b) const { return l2_seq(xb + (size_t)a * d, xb + (size_t)b * d, d); }
+
+    void greedy(const float* q, int level, int& nearest, float& d_nearest) {
+        for (;;) {
+            int prev = nearest;
+            size_t b, e;
+            h.neighbor_range(nearest, level, &b, &e);
+            for (size_t j = b; j < e; j++) {
+                int v = h.neighbors[j];
+                if (v < 0) break;
+                float dv = dis(q, v);
+                if (dv < d_nearest) {
+                    nearest = v;
+                    d_nearest = dv;
+                }
+            }
+            if (nearest == prev) return;
+        }
+    }
+
+    void shrink(std::priority_queue<NodeDistFarther>& input, std::vector<NodeDistFarther>& output,
+                int max_size) {
+        while (!input.empty()) {
+            NodeDistFarther v1 = input.top();
+            input.pop();
+            bool good = true;
+            for (const auto& v2 : output) {
+                if (sym(v2.id, v1.id) < v1.d) {
+                    good = false;
+                    break;
+                }
+            }
+            if (good) {
+                output.push_back(v1);
+                if ((int)output.size() >= max_size) return;
+            }
+        }
+    }
+    void shrink_closer(std::priority_queue<NodeDistCloser>& rs1, int max_size) {
+        if ((int)rs1.size() < max_size) return;
+        std::priority_queue<NodeDistFarther> rs;
+        std::vector<NodeDistFarther> ret;
+        while (!rs1.empty()) {
+            rs.emplace(rs1.top().d, rs1.top().id);
+            rs1.pop();
+        }
+        shrink(rs, ret, max_size);
+        for (const auto& c : ret) rs1.emplace(c.d, c.id);
+    }
+    void add_link(int src, int dest, int level) {
+        size_t b, e;
+        h.neighbor_range(src, level, &b, &e);
+        if (h.neighbors[e - 1] == -1) {
+            size_t i = e;
+            while (i > b) {
+                if (h.neighbors[i - 1] != -1) break;
+                i--;
+            }
+            h.neighbors[i] = dest;
+            return;
+        }
+        std::priority_queue<NodeDistCloser> rs;
+        rs.emplace(sym(src, dest), dest);
+        for (size_t i = b; i < e; i++) {
+            int ng = h.neighbors[i];
+            rs.emplace(sym(src, ng), ng);
+        }
+        shrink_closer(rs, (int)(e - b));
+        size_t i = b;
+        while (!rs.empty()) {
+            h.neighbors[i++] = rs.top().id;
+            rs.pop();
+        }
+        while (i < e) h.neighbors[i++] = -1;
+    }
+    void search_to_add(const float* q, std::priority_queue<NodeDistCloser>& results, int entry,
+                       float d_entry, int level) {
+        std::priority_queue<NodeDistFarther> cand;
+        cand.emplace(d_entry, entry);
+        results.emplace(d_entry, entry);
+        std::vector<int> touched;
+        visited[entry] = 1;
+        touched.push_back(entry);
+        while (!cand.empty()) {
+            const NodeDistFarther cur = cand.top();
+            if (cur.d > results.top().d) break;
+            cand.pop();
+            size_t b, e;
+            h.neighbor_range(cur.id, level, &b, &e);
+            for (size_t j = b; j < e; j++) {
+                int v = h.neighbors[j];
+                if (v < 0) break;
+                if (visited[v]) continue;
+                visited[v] = 1;
+                touched.push_back(v);
+                float dv = dis(q, v);
+                if ((int)results.size() < h.efConstruction || results.top().d > dv) {
+                    results.emplace(dv, v);
+                    cand.emplace(dv, v);
+                    if ((int)results.size() > h.efConstruction) results.pop();
+                }
+            }
+        }
+        for (int v : touched) visited[v] = 0;
+    }
+    void add_links_from(const float* q, int pt, int nearest, float d_nearest, int level) {
+        std::priority_queue<NodeDistCloser> targets;
+        search_to_add(q, targets, nearest, d_nearest, level);
+        shrink_closer(targets, h.nb_neighbors(level));
+        std::vector<int> to_add;
+        while (!targets.empty()) {
+            int other = targets.top().id;
+            add_link(pt, other, level);
+            to_add.push_back(other);
+            targets.pop();
+        }
+        for (int other : to_add) add_link(other, pt, level);
+    }
+    void add_point(int pt, int pt_level) {
+        const float* q = xb + (size_t)pt * d;
+        int nearest = h.entry_point;
+        if (nearest == -1) {
+            h.max_level = pt_level;
+            h.entry_point = pt;
+            return;
+        }
+        int level = h.max_level;
+        float d_nearest = dis(q, nearest);
+        for (; level > pt_level; level--) greedy(q, level, nearest, d_nearest);
+        for (; level >= 0; level--) add_links_from(q, pt, nearest, d_nearest, level);
+        if (pt_level > h.max_level) {
+            h.max_level = pt_level;
+            h.entry_point = pt;
+        }
+    }
+};
+}  // namespace
+
+// ---------------------------------------------------------------- HNSW
+HNSW::HNSW(int M) {
+    set_default_probas(M, 1.0f / logf((float)M));
+    offsets.push_back(0);
+}
+void HNSW::set_default_probas(int M, float levelMult) {
+    int nn = 0;
+    cum_nneighbor_per_level.push_back(0);
+    for (int level = 0;; level++) {
+        float proba = expf(-level / levelMult) * (1 - expf(-1 / levelMult));
+        if (proba < 1e-9) break;
+        assign_probas.push_back(proba);
+        nn += level == 0 ? M * 2 : M;
+        cum_nneighbor_per_level.push_back(nn);
+    }
+}
+int HNSW::nb_neighbors(int l) const {
+    return cum_nneighbor_per_level[l + 1] - cum_nneighbor_per_level[l];
+}
+int HNSW::cum_nb_neighbors(int l) const { return cum_nneighbor_per_level[l]; }
+void HNSW::neighbor_range(idx_t no, int l, size_t* b, size_t* e) const {
+    size_t o = offsets[no];
+    *b = o + cum_nb_neighbors(l);
+    *e = o + cum_nb_neighbors(l + 1);
+}
+int HNSW::random_level(std::mt19937& rng) const {
+    double f = rng() / float(std::mt19937::max());
+    for (int level = 0; level < (int)assign_probas.size(); level++) {
+        if (f < assign_probas[level]) return level;
+        f -= assign_probas[level];
+    }
+    return (int)assign_probas.size() - 1;
+}
+
+// ---------------------------------------------------------------- IndexHNSW
+IndexHNSW::IndexHNSW(IndexFlat* st, int M)
+        : Index(st ? st->d : 0, st ? st->metric_type : METRIC_L2), hnsw(M), storage(st) {
+    is_trained = true;
+    if (st) device = st->device;
+}
+IndexHNSW::~IndexHNSW() {
+    if (own_fields) delete storage;
+}
+IndexHNSWFlat::IndexHNSWFlat(int d_, int M, MetricType metric)
+        : IndexHNSW(new IndexFlat(d_, metric), M) {
+    own_fields = true;
+    FAISS_THROW_IF_NOT_MSG(metric == METRIC_L2, "HNSW inner product not supported on GPU");
+}
+
+void IndexHNSW::add(idx_t n, const float* x) {
+    // faiss/IndexHNSW.cpp:386-397 + hnsw_add_vertices (:68-230)
+    FAISS_THROW_IF_NOT_MSG(storage, "Please use IndexHNSWFlat (or variants)");
+    const idx_t n0 = ntotal;
+    storage->add(n, x);
+    ntotal = storage->ntotal;
+    if (n == 0) return;
+    // prepare_level_tab
+    std::mt19937 rng(12345);
+    for (idx_t i = 0; i < (idx_t)hnsw.levels.size(); i++) rng();  // keep stream position
+    int max_level2 = 0;
+    for (idx_t i = 0; i < n; i++) {
+        int pl = hnsw.random_level(rng);
+        hnsw.levels.push_back(pl + 1);
+    }
+    for (idx_t i = 0; i < n; i++) {
+        int pl = hnsw.levels[n0 + i] - 1;
+        max_level2 = std::max(max_level2, pl);
+        hnsw.offsets.push_back(hnsw.offsets.back() + hnsw.cum_nb_neighbors(pl + 1));
+    }
+    hnsw.neighbors.resize(hnsw.offsets.back(), -1);
+    // order: by level, highest first, shuffled within a level (rng2 = 789)
+    std::vector<int> hist;
+    std::vector<int> order(n);
+    for (idx_t i = 0; i < n; i++) {
+        int pl = hnsw.levels[n0 + i] - 1;
+        while (pl >= (int)hist.size()) hist.push_back(0);
+        hist[pl]++;
+    }
+    std::vector<int> offs(hist.size() + 1, 0);
+    for (size_t i = 0; i + 1 < hist.size(); i++) offs[i + 1] = offs[i] + hist[i];
+    for (idx_t i = 0; i < n; i++) {
+        int pl = hnsw.levels[n0 + i] - 1;
+        order[offs[pl]++] = (int)(n0 + i);
+    }
+    std::mt19937 rng2(789);
+    Builder bld(hnsw, storage->xb.data(), d, ntotal);
+    int i1 = (int)n;
+    for (int pl = (int)hist.size() - 1; pl >= 0; pl--) {
+        int i0 = i1 - hist[pl];
+        for (int j = i0; j < i1; j++) std::swap(order[j], order[j + rng2() % (i1 - j)]);
+        for (int j = i0; j < i1; j++) bld.add_point(order[j], hnsw.levels[order[j]] - 1);
+        i1 = i0;
+    }
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    dirty_ = true;
+}
+
+void IndexHNSW::reset() {
+    hnsw = HNSW((int)(hnsw.cum_nneighbor_per_level.size() > 1 ? hnsw.nb_neighbors(1) : 32));
+    storage->reset();
+    ntotal = 0;
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    dirty_ = true;
+}
+
+void IndexHNSW::reconstruct(idx_t key, float* recons) const { storage->reconstruct(key, recons); }
+
+void IndexHNSW::sync_device() const {
+    storage->sync_device();
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    if (!dirty_) return;
+    DevGuard2 dg(device);
+    hipStream_t s = stream();
+    FAISS_THROW_IF_NOT_MSG(hnsw.nb_neighbors(0) <= 64 &&
+                                   (hnsw.cum_nneighbor_per_level.size() < 3 ||
+                                    hnsw.nb_neighbors(1) <= 64),
+                           "HNSW M > 32 not supported on this path");
+    const size_t nl = std::max<size_t>(hnsw.levels.size(), 1);
+    d_levels_.reserve(sizeof(int32_t) * nl);
+    d_offsets_.reserve(sizeof(uint64_t) * (nl + 1));
+    d_neighbors_.reserve(sizeof(int32_t) * std::max<size_t>(hnsw.neighbors.size(), 1));
+    d_cum_.reserve(sizeof(int32_t) * hnsw.cum_nneighbor_per_level.size() + 8);
+    std::vector<uint64_t> offs(hnsw.offsets.begin(), hnsw.offsets.end());
+    if (!hnsw.levels.empty())
+        HIP_CHECK(hipMemcpyAsync(d_levels_.ptr, hnsw.levels.data(),
+                                 sizeof(int32_t) * hnsw.levels.size(), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(d_offsets_.ptr, offs.data(), sizeof(uint64_t) * offs.size(),
+                             hipMemcpyHostToDevice, s));
+    if (!hnsw.neighbors.empty())
+        HIP_CHECK(hipMemcpyAsync(d_neighbors_.ptr, hnsw.neighbors.data(),
+                                 sizeof(int32_t) * hnsw.neighbors.size(), hipMemcpyHostToDevice,
+                                 s));
+    HIP_CHECK(hipMemcpyAsync(d_cum_.ptr, hnsw.cum_nneighbor_per_level.data(),
+                             sizeof(int32_t) * hnsw.cum_nneighbor_per_level.size(),
+                             hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    dirty_ = false;
+}
+
+template <class OutIdx>
+void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* distances,
+                            OutIdx* labels, const SearchParameters* params,
+                            hipStream_t s) const {
+    // faiss/IndexHNSW.cpp:246-343 (hnsw_search)
+    FAISS_THROW_IF_NOT(k > 0);
+    int efSearch = hnsw.efSearch;
+    if (params) {
+        auto p = dynamic_cast<const SearchParametersHNSW*>(params);
+        FAISS_THROW_IF_NOT_MSG(p, "params type invalid");
+        efSearch = p->efSearch;
+    }
+    sync_device();
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    kern::HNSWDevice gd;
+    gd.storage = storage->device_vectors();
+    gd.norms = nullptr;
+    gd.ld = ld();
+    gd.d = d;
+    gd.levels = d_levels_.as<int32_t>();
+    gd.offsets = d_offsets_.as<uint64_t>();
+    gd.neighbors = d_neighbors_.as<int32_t>();
+    gd.cum_nb = d_cum_.as<int32_t>();
+    gd.nlevels_cum = (int)hnsw.cum_nneighbor_per_level.size();
+    gd.entry_point = ntotal > 0 ? hnsw.entry_point : -1;
+    gd.max_level = hnsw.max_level;
+    gd.ntotal = (int)ntotal;
+    const int64_t vwords = (int64_t)cdiv(std::max<idx_t>(ntotal, 1), 32);
+    if (vwords * 4 > 64 * 1024) s_visited_.reserve(sizeof(uint32_t) * vwords * n);
+    constexpr bool i32 = sizeof(OutIdx) == 4;
+    ScopedKernelTimer tm(&ktimes, "hnsw_search", 0.0, s);
+    kern::hnsw_search(gd, x, ldx, n, k, efSearch, distances, i32 ? nullptr : (int64_t*)labels,
+                      i32 ? (int32_t*)labels : nullptr, s_visited_.as<uint32_t>(), vwords, s);
+}
+
+void IndexHNSW::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                              idx_t* labels, const SearchParameters* params,
+                              hipStream_t s) const {
+    DevGuard2 dg(device);
+    hnsw_device<idx_t>(n, x, ldx, (int)k, distances, labels, params, s);
+}
+
+void IndexHNSW::assign_device(idx_t n, const float* x, int ldx, int k, float* distances,
+                              int32_t* labels, const SearchParameters* params,
+                              hipStream_t s) const {
+    DevGuard2 dg(device);
+    hnsw_device<int32_t>(n, x, ldx, k, distances, labels, params, s);
+}
+
+}  // namespace faiss_amd

@@ -1,0 +1,409 @@
+// io.cpp — the reference on-disk format for the five index types on the path
+// and a subset index_factory.
+//
+// Format (reference faiss/impl/index_write.cpp, faiss/impl/index_read.cpp):
+//   header  = d:i32 ntotal:i64 dummy:i64 dummy:i64 is_trained:u8 metric:i32
+//             [metric_arg:f32 if metric > 1]                 (write :79-90)
+//   IxF2/IxFI = header, size_t n4, n4*4 bytes of floats       (:396-403)
+//   IVF hdr = header, nlist:size_t, nprobe:size_t, nested quantizer,
+//             direct map (char type, vector<idx_t>)           (:367-389)
+//   IwFl    = IVF hdr, invlists                               (:631-638)
+//   IwPQ    = IVF hdr, by_residual:u8, code_size:size_t, PQ (d,M,nbits:size_t,
+//             vector<float> centroids), invlists               (:697-705,155-160)
+//   ilar    = nlist:size_t, code_size:size_t, "full"+vector<size_t> sizes |
+//             "sprs"+vector<size_t>(list,size pairs), then per non-empty list
+//             codes then ids                                  (:243-297)
+//   IHNf    = header, HNSW (vector<double> assign_probas, vector<int> cum,
+//             vector<int> levels, vector<size_t> offsets, vector<i32>
+//             neighbors, entry_point:i32, max_level, efConstruction,
+//             efSearch:int, dummy int), storage index         (:300-316,760-778)
+//   vectors carry a size_t element-count prefix (faiss/impl/io_macros.h:62-67)
+//   fourcc = little-endian chars (faiss/impl/io.cpp:237-241)
+#include <cstring>
+#include <string>
+
+#include "../../include/faiss_amd.h"
+
+namespace faiss_amd {
+
+namespace {
+uint32_t fourcc(const char* s) {
+    return (uint32_t)(uint8_t)s[0] | ((uint32_t)(uint8_t)s[1] << 8) |
+           ((uint32_t)(uint8_t)s[2] << 16) | ((uint32_t)(uint8_t)s[3] << 24);
+}
+std::string fourcc_str(uint32_t h) {
+    std::string s(4, ' ');
+    for (int i = 0; i < 4; i++) {
+        char c = (char)((h >> (8 * i)) & 0xff);
+        s[i] = (c >= 32 && c < 127) ? c : '?';
+    }
+    return s;
+}
+
+struct Writer {
+    FILE* f;
+    void bytes(const void* p, size_t n) {
+        if (n && fwrite(p, 1, n, f) != n) FAISS_THROW_MSG("write error");
+    }
+    template <class T>
+    void one(const T& v) { bytes(&v, sizeof(T)); }
+    template <class T>
+    void vec(const std::vector<T>& v) {
+        size_t n = v.size();
+        one(n);
+        bytes(v.data(), sizeof(T) * n);
+    }
+};
+struct Reader {
+    FILE* f;
+    void bytes(void* p, size_t n) {
+        if (n && fread(p, 1, n, f) != n) FAISS_THROW_MSG("read error: truncated index file");
+    }
+    template <class T>
+    T one() {
+        T v;
+        bytes(&v, sizeof(T));
+        return v;
+    }
+    template <class T>
+    void vec(std::vector<T>& v) {
+        size_t n = one<size_t>();
+        FAISS_THROW_IF_NOT_MSG(n < ((size_t)1 << 40), "corrupt vector size");
+        v.resize(n);
+        bytes(v.data(), sizeof(T) * n);
+    }
+};
+
+void write_header(const Index* idx, Writer& w) {
+    w.one<int32_t>(idx->d);
+    w.one<int64_t>(idx->ntotal);
+    int64_t dummy = 1 << 20;
+    w.one(dummy);
+    w.one(dummy);
+    w.one<uint8_t>(idx->is_trained ? 1 : 0);
+    w.one<int32_t>((int32_t)idx->metric_type);
+    if ((int)idx->metric_type > 1) w.one<float>(idx->metric_arg);
+}
+struct Header {
+    int32_t d;
+    int64_t ntotal;
+    bool is_trained;
+    int32_t metric;
+    float metric_arg = 0;
+};
+Header read_header(Reader& r) {
+    Header h;
+    h.d = r.one<int32_t>();
+    h.ntotal = r.one<int64_t>();
+    r.one<int64_t>();
+    r.one<int64_t>();
+    h.is_trained = r.one<uint8_t>() != 0;
+    h.metric = r.one<int32_t>();
+    if (h.metric > 1) h.metric_arg = r.one<float>();
+    FAISS_THROW_IF_NOT_MSG(h.metric == METRIC_L2 || h.metric == METRIC_INNER_PRODUCT,
+                           "only L2 / inner-product indexes are supported");
+    return h;
+}
+void apply_header(Index* idx, const Header& h) {
+    idx->d = h.d;
+    idx->ntotal = h.ntotal;
+    idx->is_trained = h.is_trained;
+    idx->metric_type = (MetricType)h.metric;
+    idx->metric_arg = h.metric_arg;
+}
+
+void write_invlists(const ArrayInvertedLists* il, Writer& w) {
+    w.one(fourcc("ilar"));
+    w.one<size_t>(il->nlist);
+    w.one<size_t>(il->code_size);
+    size_t n_non0 = 0;
+    for (size_t i = 0; i < il->nlist; i++)
+        if (!il->ids[i].empty()) n_non0++;
+    std::vector<size_t> sizes;
+    if (n_non0 > il->nlist / 2) {
+        w.one(fourcc("full"));
+        for (size_t i = 0; i < il->nlist; i++) sizes.push_back(il->ids[i].size());
+    } else {
+        w.one(fourcc("sprs"));
+        for (size_t i = 0; i < il->nlist; i++) {
+            if (!il->ids[i].empty()) {
+                sizes.push_back(i);
+                sizes.push_back(il->ids[i].size());
+            }
+        }
+    }
+    w.vec(sizes);
+    for (size_t i = 0; i < il->nlist; i++) {
+        size_t n = il->ids[i].size();
+        if (n) {
+            w.bytes(il->codes[i].data(), n * il->code_size);
+            w.bytes(il->ids[i].data(), n * sizeof(idx_t));
+        }
+    }
+}
+void read_invlists(ArrayInvertedLists* il, Reader& r, size_t nlist, size_t code_size) {
+    uint32_t h = r.one<uint32_t>();
+    FAISS_THROW_IF_NOT_MSG(h == fourcc("ilar"),
+                           "unsupported inverted-list type " + fourcc_str(h));
+    size_t nl = r.one<size_t>(), cs = r.one<size_t>();
+    FAISS_THROW_IF_NOT(nl == nlist && cs == code_size);
+    std::vector<size_t> sizes(nl, 0);
+    uint32_t lt = r.one<uint32_t>();
+    if (lt == fourcc("full")) {
+        r.vec(sizes);
+        FAISS_THROW_IF_NOT(sizes.size() == nl);
+    } else if (lt == fourcc("sprs")) {
+        std::vector<size_t> idsz;
+        r.vec(idsz);
+        for (size_t j = 0; j + 1 < idsz.size(); j += 2) {
+            FAISS_THROW_IF_NOT(idsz[j] < nl);
+            sizes[idsz[j]] = idsz[j + 1];
+        }
+    } else {
+        FAISS_THROW_MSG("list_type not recognized: " + fourcc_str(lt));
+    }
+    for (size_t i = 0; i < nl; i++) {
+        il->ids[i].resize(sizes[i]);
+        il->codes[i].resize(sizes[i] * cs);
+    }
+    for (size_t i = 0; i < nl; i++) {
+        if (sizes[i]) {
+            r.bytes(il->codes[i].data(), sizes[i] * cs);
+            r.bytes(il->ids[i].data(), sizes[i] * sizeof(idx_t));
+        }
+    }
+}
+
+void write_index_impl(const Index* idx, Writer& w);
+
+void write_ivf_header(const IndexIVF* ivf, Writer& w) {
+    write_header(ivf, w);
+    w.one<size_t>(ivf->nlist);
+    w.one<size_t>(ivf->nprobe);
+    write_index_impl(ivf->quantizer, w);
+    w.one<char>(0);  // DirectMap::NoMap
+    std::vector<idx_t> empty;
+    w.vec(empty);
+}
+
+void write_index_impl(const Index* idx, Writer& w) {
+    if (idx == nullptr) {
+        w.one(fourcc("null"));
+    } else if (auto f = dynamic_cast<const IndexFlat*>(idx)) {
+        w.one(fourcc(f->metric_type == METRIC_INNER_PRODUCT ? "IxFI" : "IxF2"));
+        write_header(f, w);
+        size_t n4 = f->xb.size();  // number of 4-byte words
+        w.one(n4);
+        w.bytes(f->xb.data(), n4 * 4);
+    } else if (auto h = dynamic_cast<const IndexHNSW*>(idx)) {
+        w.one(fourcc("IHNf"));
+        write_header(h, w);
+        w.vec(h->hnsw.assign_probas);
+        w.vec(h->hnsw.cum_nneighbor_per_level);
+        w.vec(h->hnsw.levels);
+        w.vec(h->hnsw.offsets);
+        w.vec(h->hnsw.neighbors);
+        w.one<int32_t>(h->hnsw.entry_point);
+        w.one<int32_t>(h->hnsw.max_level);
+        w.one<int32_t>(h->hnsw.efConstruction);
+        w.one<int32_t>(h->hnsw.efSearch);
+        w.one<int32_t>(1);  // deprecated upper_beam
+        write_index_impl(h->storage, w);
+    } else if (auto fl = dynamic_cast<const IndexIVFFlat*>(idx)) {
+        w.one(fourcc("IwFl"));
+        write_ivf_header(fl, w);
+        write_invlists(fl->invlists.get(), w);
+    } else if (auto pq = dynamic_cast<const IndexIVFPQ*>(idx)) {
+        w.one(fourcc("IwPQ"));
+        write_ivf_header(pq, w);
+        w.one<uint8_t>(pq->by_residual ? 1 : 0);
+        w.one<size_t>(pq->code_size);
+        w.one<size_t>(pq->pq.d);
+        w.one<size_t>(pq->pq.M);
+        w.one<size_t>(pq->pq.nbits);
+        w.vec(pq->pq.centroids);
+        write_invlists(pq->invlists.get(), w);
+    } else {
+        FAISS_THROW_MSG("don't know how to serialize this type of index");
+    }
+}
+
+Index* read_index_impl(Reader& r, int io_flags) {
+    uint32_t h = r.one<uint32_t>();
+    if (h == fourcc("null")) return nullptr;
+    if (h == fourcc("IxF2") || h == fourcc("IxFI")) {
+        Header hd = read_header(r);
+        auto f = new IndexFlat(hd.d, (MetricType)hd.metric);
+        apply_header(f, hd);
+        size_t n4 = r.one<size_t>();
+        FAISS_THROW_IF_NOT(n4 == (size_t)hd.ntotal * hd.d);
+        f->xb.resize(n4);
+        r.bytes(f->xb.data(), n4 * 4);
+        return f;
+    }
+    if (h == fourcc("IHNf")) {
+        Header hd = read_header(r);
+        auto ix = new IndexHNSW(nullptr, 32);
+        apply_header(ix, hd);
+        ix->hnsw.assign_probas.clear();
+        ix->hnsw.cum_nneighbor_per_level.clear();
+        ix->hnsw.offsets.clear();
+        r.vec(ix->hnsw.assign_probas);
+        r.vec(ix->hnsw.cum_nneighbor_per_level);
+        r.vec(ix->hnsw.levels);
+        r.vec(ix->hnsw.offsets);
+        r.vec(ix->hnsw.neighbors);
+        ix->hnsw.entry_point = r.one<int32_t>();
+        ix->hnsw.max_level = r.one<int32_t>();
+        ix->hnsw.efConstruction = r.one<int32_t>();
+        ix->hnsw.efSearch = r.one<int32_t>();
+        r.one<int32_t>();
+        Index* st = read_index_impl(r, io_flags);
+        auto stf = dynamic_cast<IndexFlat*>(st);
+        FAISS_THROW_IF_NOT_MSG(stf, "IHNf storage must be a flat index");
+        ix->storage = stf;
+        ix->own_fields = true;
+        ix->device = stf->device;
+        return ix;
+    }
+    if (h == fourcc("IwFl") || h == fourcc("IwPQ")) {
+        Header hd = read_header(r);
+        size_t nlist = r.one<size_t>();
+        size_t nprobe = r.one<size_t>();
+        Index* q = read_index_impl(r, io_flags);
+        FAISS_THROW_IF_NOT_MSG(q, "IVF index without quantizer");
+        char dm = r.one<char>();
+        std::vector<idx_t> dmarr;
+        r.vec(dmarr);
+        FAISS_THROW_IF_NOT_MSG(dm == 0, "direct maps are not supported");
+        IndexIVF* ivf;
+        if (h == fourcc("IwFl")) {
+            ivf = new IndexIVFFlat(q, hd.d, nlist, (MetricType)hd.metric);
+        } else {
+            bool by_res = r.one<uint8_t>() != 0;
+            size_t code_size = r.one<size_t>();
+            size_t pd = r.one<size_t>(), M = r.one<size_t>(), nbits = r.one<size_t>();
+            FAISS_THROW_IF_NOT(pd == (size_t)hd.d);
+            auto pqi = new IndexIVFPQ(q, hd.d, nlist, M, nbits, (MetricType)hd.metric);
+            pqi->by_residual = by_res;
+            FAISS_THROW_IF_NOT(code_size == pqi->code_size);
+            r.vec(pqi->pq.centroids);
+            FAISS_THROW_IF_NOT(pqi->pq.centroids.size() == pd * ((size_t)1 << nbits));
+            ivf = pqi;
+        }
+        ivf->own_fields = true;
+        apply_header(ivf, hd);
+        ivf->nprobe = nprobe;
+        read_invlists(ivf->invlists.get(), r, nlist, ivf->code_size);
+        if (auto pqi = dynamic_cast<IndexIVFPQ*>(ivf)) {
+            // faiss/impl/index_read.cpp:510-516
+            if (pqi->is_trained && pqi->by_residual) pqi->precompute_table();
+        }
+        return ivf;
+    }
+    FAISS_THROW_MSG("Index type " + fourcc_str(h) + " not supported on this path");
+}
+}  // namespace
+
+void write_index(const Index* idx, FILE* f) {
+    Writer w{f};
+    write_index_impl(idx, w);
+}
+void write_index(const Index* idx, const char* fname) {
+    FILE* f = fopen(fname, "wb");
+    FAISS_THROW_IF_NOT_MSG(f, std::string("could not open ") + fname + " for writing");
+    try {
+        write_index(idx, f);
+    } catch (...) {
+        fclose(f);
+        throw;
+    }
+    fclose(f);
+}
+Index* read_index(FILE* f, int io_flags) {
+    Reader r{f};
+    return read_index_impl(r, io_flags);
+}
+Index* read_index(const char* fname, int io_flags) {
+    FILE* f = fopen(fname, "rb");
+    FAISS_THROW_IF_NOT_MSG(f, std::string("could not open ") + fname + " for reading");
+    Index* idx = nullptr;
+    try {
+        idx = read_index(f, io_flags);
+    } catch (...) {
+        fclose(f);
+        throw;
+    }
+    fclose(f);
+    return idx;
+}
+
+// ---------------------------------------------------------------- factory
+// faiss/index_factory.cpp:242-345 subset.
+Index* index_factory(int d, const char* description, MetricType metric) {
+    std::string s(description);
+    auto parse_int = [&](size_t& pos) {
+        size_t st = pos;
+        while (pos < s.size() && isdigit((unsigned char)s[pos])) pos++;
+        FAISS_THROW_IF_NOT_MSG(pos > st, "could not parse index_factory string " + s);
+        return std::stol(s.substr(st, pos - st));
+    };
+    if (s == "Flat") return new IndexFlat(d, metric);
+    if (s.rfind("HNSW", 0) == 0) {
+        size_t pos = 4;
+        int M = s.size() > 4 ? (int)parse_int(pos) : 32;
+        std::string rest = s.substr(pos);
+        FAISS_THROW_IF_NOT_MSG(rest.empty() || rest == ",Flat" || rest == "_Flat",
+                               "unsupported HNSW description " + s);
+        return new IndexHNSWFlat(d, M, metric);
+    }
+    FAISS_THROW_IF_NOT_MSG(s.rfind("IVF", 0) == 0, "unsupported index_factory string " + s);
+    size_t pos = 3;
+    size_t nlist = (size_t)parse_int(pos);
+    Index* q = nullptr;
+    if (s.compare(pos, 5, "_HNSW") == 0) {
+        pos += 5;
+        int M = (int)parse_int(pos);
+        q = new IndexHNSWFlat(d, M, metric);
+    } else if (s.compare(pos, 5, "_Flat") == 0) {
+        pos += 5;
+        q = new IndexFlat(d, metric);
+    } else {
+        q = new IndexFlat(d, metric);
+    }
+    FAISS_THROW_IF_NOT_MSG(pos < s.size() && s[pos] == ',', "unsupported string " + s);
+    pos++;
+    std::string enc = s.substr(pos);
+    IndexIVF* ivf = nullptr;
+    try {
+        if (enc == "Flat") {
+            ivf = new IndexIVFFlat(q, d, nlist, metric);
+        } else if (enc.rfind("PQ", 0) == 0) {
+            size_t p2 = 2;
+            std::string& ss = s;
+            (void)ss;
+            size_t st = p2;
+            while (p2 < enc.size() && isdigit((unsigned char)enc[p2])) p2++;
+            size_t M = std::stoul(enc.substr(st, p2 - st));
+            size_t nbits = 8;
+            if (p2 < enc.size() && enc[p2] == 'x') {
+                p2++;
+                st = p2;
+                while (p2 < enc.size() && isdigit((unsigned char)enc[p2])) p2++;
+                nbits = std::stoul(enc.substr(st, p2 - st));
+            }
+            std::string tail = enc.substr(p2);
+            FAISS_THROW_IF_NOT_MSG(tail.empty() || tail == "np", "unsupported PQ spec " + enc);
+            ivf = new IndexIVFPQ(q, d, nlist, M, nbits, metric);
+        } else {
+            FAISS_THROW_MSG("unsupported IVF encoding " + enc);
+        }
+    } catch (...) {
+        delete q;
+        throw;
+    }
+    ivf->own_fields = true;
+    return ivf;
+}
+
+}  // namespace faiss_amd

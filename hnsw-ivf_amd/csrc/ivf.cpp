@@ -1,0 +1,543 @@
+// ivf.cpp — IndexIVF / IndexIVFFlat / IndexIVFPQ / IndexShardsIVF host side.
+//
+// Reference: faiss/IndexIVF.cpp:303-397 (search), :399-723
+// (search_preassigned), :187-285 (add), faiss/IndexIVFFlat.cpp,
+// faiss/IndexIVFPQ.cpp, faiss/IndexShardsIVF.cpp:88-245.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+#include "../../include/faiss_amd.h"
+#include "kernels.h"
+
+namespace faiss_amd {
+
+namespace {
+struct DevGuard {
+    int prev = 0;
+    explicit DevGuard(int dev) {
+        ensure_hip();
+        HIP_CHECK(hipGetDevice(&prev));
+        if (prev != dev) HIP_CHECK(hipSetDevice(dev));
+    }
+    ~DevGuard() {
+        int cur = 0;
+        hipGetDevice(&cur);
+        if (cur != prev) hipSetDevice(prev);
+    }
+};
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+                   std::chrono::steady_clock::now().time_since_epoch())
+            .count();
+}
+}  // namespace
+
+// ---------------------------------------------------------------- invlists
+ArrayInvertedLists::ArrayInvertedLists(size_t nl, size_t cs) : nlist(nl), code_size(cs) {
+    codes.resize(nl);
+    ids.resize(nl);
+}
+void ArrayInvertedLists::add_entries(size_t l, size_t n, const idx_t* ids_in,
+                                     const uint8_t* codes_in) {
+    FAISS_THROW_IF_NOT(l < nlist);
+    ids[l].insert(ids[l].end(), ids_in, ids_in + n);
+    codes[l].insert(codes[l].end(), codes_in, codes_in + n * code_size);
+}
+void ArrayInvertedLists::reset() {
+    for (size_t l = 0; l < nlist; l++) {
+        codes[l].clear();
+        ids[l].clear();
+    }
+}
+
+// ---------------------------------------------------------------- IndexIVF
+IndexIVF::IndexIVF(Index* q, size_t d_, size_t nl, size_t cs, MetricType metric)
+        : Index(d_, metric), quantizer(q), nlist(nl), code_size(cs) {
+    FAISS_THROW_IF_NOT(q != nullptr);
+    FAISS_THROW_IF_NOT((size_t)q->d == d_);
+    is_trained = q->is_trained && (size_t)q->ntotal == nlist;
+    invlists = std::make_unique<ArrayInvertedLists>(nlist, code_size);
+    device = q->device;
+}
+
+IndexIVF::~IndexIVF() {
+    if (own_fields) delete quantizer;
+}
+
+int IndexIVF::device_code_stride() const {
+    // IVF-Flat keeps 16-B aligned float rows; PQ keeps 4-B aligned code rows
+    return (int)roundup(code_size, 4);
+}
+
+void IndexIVF::train(idx_t n, const float* x) {
+    // faiss/IndexIVF.cpp:1221-1260 (train) + Level1Quantizer::train_q1
+    if (quantizer->is_trained && (size_t)quantizer->ntotal == nlist) {
+        if (verbose) fprintf(stderr, "IVF quantizer does not need training\n");
+    } else {
+        std::vector<float> cent((size_t)nlist * d);
+        kmeans_train(d, n, x, (int)nlist, niter, 1234, cent.data(), device, verbose);
+        quantizer->reset();
+        quantizer->train(nlist, cent.data());
+        quantizer->add(nlist, cent.data());
+        quantizer->is_trained = true;
+    }
+    FAISS_THROW_IF_NOT((size_t)quantizer->ntotal == nlist);
+    // train the encoder on (a subset of) the assigned training vectors
+    std::vector<idx_t> assign(n);
+    std::vector<float> dis(n);
+    if (by_residual || dynamic_cast<IndexIVFPQ*>(this)) {
+        quantizer->search(n, x, 1, dis.data(), assign.data());
+        train_encoder(n, x, assign.data());
+    }
+    is_trained = true;
+}
+
+void IndexIVF::add(idx_t n, const float* x) { add_with_ids(n, x, nullptr); }
+
+void IndexIVF::add_with_ids(idx_t n, const float* x, const idx_t* xids) {
+    FAISS_THROW_IF_NOT(is_trained);
+    const idx_t bs = 1 << 20;
+    std::vector<idx_t> assign;
+    std::vector<float> dis;
+    std::vector<uint8_t> codes;
+    for (idx_t i0 = 0; i0 < n; i0 += bs) {
+        idx_t nb = std::min(bs, n - i0);
+        assign.resize(nb);
+        dis.resize(nb);
+        codes.resize((size_t)nb * code_size);
+        const float* xb = x + (size_t)i0 * d;
+        quantizer->search(nb, xb, 1, dis.data(), assign.data());
+        encode_vectors(nb, xb, assign.data(), codes.data());
+        for (idx_t i = 0; i < nb; i++) {
+            idx_t l = assign[i];
+            if (l < 0) continue;
+            idx_t id = xids ? xids[i0 + i] : ntotal + i0 + i;
+            invlists->add_entries(l, 1, &id, codes.data() + (size_t)i * code_size);
+        }
+    }
+    ntotal += n;
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    dirty_ = true;
+}
+
+void IndexIVF::reset() {
+    invlists->reset();
+    ntotal = 0;
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    dirty_ = true;
+}
+
+// Arena upload: lists packed contiguously, each list start aligned to 16
+// rows; rows padded to the device stride; ids / owning list per row.
+void IndexIVF::sync_device() const {
+    quantizer->sync_device();
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    if (!dirty_) return;
+    DevGuard dg(device);
+    hipStream_t s = stream();
+    const size_t stride = device_code_stride();
+    const bool flat = dynamic_cast<const IndexIVFFlat*>(this) != nullptr;
+    const size_t dstride = flat ? sizeof(float) * roundup((size_t)d, 4) : stride;
+    std::vector<uint32_t> off(nlist + 1), len(nlist);
+    size_t rows = 0;
+    for (size_t l = 0; l < nlist; l++) {
+        off[l] = (uint32_t)rows;
+        len[l] = (uint32_t)invlists->list_size(l);
+        rows += roundup(len[l], 16);
+        FAISS_THROW_IF_NOT_MSG(rows < (1ull << 32), "arena larger than 2^32 rows");
+    }
+    off[nlist] = (uint32_t)rows;
+    arena_rows_ = rows;
+    std::vector<uint8_t> hc(std::max<size_t>(rows, 1) * dstride, 0);
+    std::vector<idx_t> hi(std::max<size_t>(rows, 1), -1);
+    std::vector<uint32_t> hl(std::max<size_t>(rows, 1), 0xffffffffu);
+    for (size_t l = 0; l < nlist; l++) {
+        const size_t n = len[l];
+        for (size_t i = 0; i < n; i++) {
+            memcpy(hc.data() + (off[l] + i) * dstride, invlists->codes[l].data() + i * code_size,
+                   code_size);
+            hl[off[l] + i] = (uint32_t)l;
+        }
+        if (n) memcpy(hi.data() + off[l], invlists->ids[l].data(), sizeof(idx_t) * n);
+    }
+    d_codes_.reserve(hc.size());
+    d_ids_.reserve(sizeof(idx_t) * hi.size());
+    d_row_list_.reserve(sizeof(uint32_t) * hl.size());
+    d_list_off_.reserve(sizeof(uint32_t) * (nlist + 1));
+    d_list_len_.reserve(sizeof(uint32_t) * std::max<size_t>(nlist, 1));
+    HIP_CHECK(hipMemcpyAsync(d_codes_.ptr, hc.data(), hc.size(), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(d_ids_.ptr, hi.data(), sizeof(idx_t) * hi.size(),
+                             hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(d_row_list_.ptr, hl.data(), sizeof(uint32_t) * hl.size(),
+                             hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(d_list_off_.ptr, off.data(), sizeof(uint32_t) * (nlist + 1),
+                             hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(d_list_len_.ptr, len.data(), sizeof(uint32_t) * nlist,
+                             hipMemcpyHostToDevice, s));
+    upload_extra();
+    HIP_CHECK(hipStreamSynchronize(s));
+    dirty_ = false;
+}
+
+void IndexIVF::quantize_device(idx_t n, const float* x, int ldx, int np, float* coarse_dis,
+                               int32_t* assign, const SearchParameters* qparams,
+                               hipStream_t s) const {
+    quantizer->assign_device(n, x, ldx, np, coarse_dis, assign, qparams, s);
+}
+
+void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                             idx_t* labels, const SearchParameters* params_in,
+                             hipStream_t s) const {
+    // faiss/IndexIVF.cpp:303-397
+    FAISS_THROW_IF_NOT(k > 0);
+    const SearchParametersIVF* params = nullptr;
+    if (params_in) {
+        params = dynamic_cast<const SearchParametersIVF*>(params_in);
+        FAISS_THROW_IF_NOT_MSG(params, "IndexIVF params have incorrect type");
+    }
+    const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
+    FAISS_THROW_IF_NOT(np > 0);
+    FAISS_THROW_IF_NOT_MSG((params ? params->max_codes : max_codes) == 0,
+                           "max_codes is not supported on the GPU path");
+    FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
+    DevGuard dg(device);
+    sync_device();
+    const double t0 = now_ms();
+    // bound the partial-result scratch to ~1 GiB per chunk
+    const size_t per_q = np * (size_t)k * 12 + np * 12;
+    idx_t qchunk = std::max<idx_t>(1, (idx_t)(((size_t)1 << 30) / per_q));
+    qchunk = std::min<idx_t>(qchunk, n);
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    s_cd_.reserve(sizeof(float) * qchunk * np);
+    s_ci_.reserve(sizeof(int32_t) * qchunk * np);
+    for (idx_t q0 = 0; q0 < n; q0 += qchunk) {
+        const idx_t nq = std::min(qchunk, n - q0);
+        quantize_device(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(), s_ci_.as<int32_t>(),
+                        params ? params->quantizer_params : nullptr, s);
+        search_preassigned_device(nq, x + q0 * ldx, ldx, k, (int)np, s_ci_.as<int32_t>(),
+                                  s_cd_.as<float>(), distances + q0 * k, labels + q0 * k, s);
+    }
+    indexIVF_stats.nq += n;
+    indexIVF_stats.search_time += now_ms() - t0;
+}
+
+void IndexIVF::search_preassigned(idx_t n, const float* x, idx_t k, const idx_t* assign,
+                                  const float* centroid_dis, float* distances, idx_t* labels,
+                                  bool store_pairs, const SearchParametersIVF* params) const {
+    // faiss/IndexIVF.cpp:399-723 (parallel_mode 0 semantics)
+    FAISS_THROW_IF_NOT(k > 0);
+    FAISS_THROW_IF_NOT_MSG(!store_pairs, "store_pairs is not supported on the GPU path");
+    const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
+    FAISS_THROW_IF_NOT(np > 0);
+    if (n == 0) return;
+    std::vector<int32_t> a32((size_t)n * np);
+    for (size_t i = 0; i < (size_t)n * np; i++) {
+        idx_t key = assign[i];
+        FAISS_THROW_IF_NOT_MSG(key < (idx_t)nlist, "Invalid key");
+        a32[i] = (int32_t)(key < 0 ? -1 : key);
+    }
+    DevGuard dg(device);
+    sync_device();
+    hipStream_t s = stream();
+    const int ldx = ld();
+    DeviceBuffer bx, ba, bc, bd, bi;
+    bx.reserve(sizeof(float) * n * ldx);
+    ba.reserve(sizeof(int32_t) * n * np);
+    bc.reserve(sizeof(float) * n * np);
+    bd.reserve(sizeof(float) * n * k);
+    bi.reserve(sizeof(idx_t) * n * k);
+    if (ldx != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * n * ldx, s));
+    HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ldx, x, sizeof(float) * d,
+                               sizeof(float) * d, n, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(ba.ptr, a32.data(), sizeof(int32_t) * n * np,
+                             hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(bc.ptr, centroid_dis, sizeof(float) * n * np,
+                             hipMemcpyHostToDevice, s));
+    search_preassigned_device(n, bx.as<float>(), ldx, k, (int)np, ba.as<int32_t>(),
+                              bc.as<float>(), bd.as<float>(), bi.as<idx_t>(), s);
+    HIP_CHECK(hipMemcpyAsync(distances, bd.ptr, sizeof(float) * n * k, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
+// ---------------------------------------------------------------- IVFFlat
+IndexIVFFlat::IndexIVFFlat(Index* q, size_t d_, size_t nl, MetricType metric)
+        : IndexIVF(q, d_, nl, sizeof(float) * d_, metric) {
+    by_residual = false;  // faiss/IndexIVFFlat.cpp:37-39
+}
+
+void IndexIVFFlat::encode_vectors(idx_t n, const float* x, const idx_t*, uint8_t* codes) const {
+    memcpy(codes, x, sizeof(float) * n * d);
+}
+
+void IndexIVFFlat::reconstruct(idx_t key, float* recons) const {
+    for (size_t l = 0; l < nlist; l++) {
+        const auto& ids = invlists->ids[l];
+        for (size_t i = 0; i < ids.size(); i++)
+            if (ids[i] == key) {
+                memcpy(recons, invlists->codes[l].data() + i * code_size, code_size);
+                return;
+            }
+    }
+    FAISS_THROW_MSG("key not found");
+}
+
+void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
+                                             const int32_t* assign, const float*,
+                                             float* distances, idx_t* labels,
+                                             hipStream_t s) const {
+    if (n <= 0) return;
+    sync_device();
+    const int QT = 64;
+    const int l = (int)roundup((size_t)d, 4);
+    s_counts_.reserve(sizeof(uint32_t) * nlist);
+    s_cur_.reserve(sizeof(uint32_t) * nlist);
+    s_boff_.reserve(sizeof(uint32_t) * (nlist + 1));
+    s_ioff_.reserve(sizeof(uint32_t) * (nlist + 1));
+    s_ent_.reserve(sizeof(uint32_t) * n * np);
+    s_pk1_.reserve(sizeof(float) * n * np * k);
+    s_pk2_.reserve(sizeof(long long) * n * np * k);
+    kern::IVFBuckets b{s_counts_.as<uint32_t>(), s_boff_.as<uint32_t>(), s_ioff_.as<uint32_t>(),
+                       s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
+    kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), (int)nlist, QT, b, s);
+    const int64_t max_items = kern::ivf_max_items(n, np, (int)nlist, QT);
+    {
+        ScopedKernelTimer tm(&ktimes, "ivf_flat_scan", 0.0, s);
+        kern::ivf_flat_scan(x, ldx, d_codes_.as<float>(), l, d_ids_.as<int64_t>(),
+                            d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(), (int)nlist, l,
+                            n, np, (int)k, metric_type == METRIC_L2, b, max_items,
+                            s_pk1_.as<float>(), s_pk2_.as<long long>(), s);
+    }
+    kern::ivf_merge(s_pk1_.as<float>(), s_pk2_.as<long long>(), assign,
+                    d_list_len_.as<uint32_t>(), (int)nlist, n, np, (int)k,
+                    metric_type == METRIC_L2, distances, labels, s);
+}
+
+// ---------------------------------------------------------------- PQ
+ProductQuantizer::ProductQuantizer(size_t d_, size_t M_, size_t nbits_)
+        : d(d_), M(M_), nbits(nbits_) {
+    set_derived_values();
+}
+void ProductQuantizer::set_derived_values() {
+    FAISS_THROW_IF_NOT_MSG(M > 0 && d % M == 0,
+                           "The dimension of the vector (d) should be a multiple of the number "
+                           "of subquantizers (M)");
+    dsub = d / M;
+    ksub = (size_t)1 << nbits;
+    centroids.resize(d * ksub);
+}
+
+IndexIVFPQ::IndexIVFPQ(Index* q, size_t d_, size_t nl, size_t M, size_t nbits, MetricType metric)
+        : IndexIVF(q, d_, nl, 0, metric), pq(d_, M, nbits) {
+    FAISS_THROW_IF_NOT_MSG(nbits == 8, "only nbits = 8 is supported on this path");
+    code_size = M;  // (M * nbits + 7) / 8
+    invlists = std::make_unique<ArrayInvertedLists>(nlist, code_size);
+    by_residual = true;
+    is_trained = false;
+}
+
+void IndexIVFPQ::train_encoder(idx_t n, const float* x, const idx_t* assign) {
+    // faiss/IndexIVFPQ.cpp:61-131: residuals, ProductQuantizer::train per
+    // sub-space, then precompute_table()
+    const idx_t max_train = (idx_t)pq.ksub * 256;
+    const idx_t nt = std::min(n, max_train);
+    std::vector<float> resid((size_t)nt * d);
+    std::vector<float> c(d);
+    for (idx_t i = 0; i < nt; i++) {
+        const float* xi = x + (size_t)i * d;
+        float* ri = resid.data() + (size_t)i * d;
+        if (by_residual && assign[i] >= 0) {
+            quantizer->reconstruct(assign[i], c.data());
+            for (int j = 0; j < d; j++) ri[j] = xi[j] - c[j];
+        } else {
+            memcpy(ri, xi, sizeof(float) * d);
+        }
+    }
+    std::vector<float> sub((size_t)nt * pq.dsub), cent(pq.ksub * pq.dsub);
+    for (size_t m = 0; m < pq.M; m++) {
+        for (idx_t i = 0; i < nt; i++)
+            memcpy(sub.data() + (size_t)i * pq.dsub, resid.data() + (size_t)i * d + m * pq.dsub,
+                   sizeof(float) * pq.dsub);
+        kmeans_train((int)pq.dsub, nt, sub.data(), (int)pq.ksub, 25, 1234 + (int64_t)m,
+                     cent.data(), device, false);
+        memcpy(pq.centroids.data() + m * pq.ksub * pq.dsub, cent.data(),
+               sizeof(float) * pq.ksub * pq.dsub);
+    }
+    precompute_table();
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    dirty_ = true;
+}
+
+void IndexIVFPQ::precompute_table() {
+    // faiss/IndexIVFPQ.cpp:380-406 decision rule (2 GiB limit)
+    use_precomputed_table = 0;
+    if (metric_type == METRIC_L2 && by_residual) {
+        size_t table_size = pq.M * pq.ksub * nlist * sizeof(float);
+        use_precomputed_table = table_size > ((size_t)1 << 31) ? 0 : 1;
+    }
+}
+
+void IndexIVFPQ::encode_vectors(idx_t n, const float* x, const idx_t* list_nos,
+                                uint8_t* codes) const {
+    if (n <= 0) return;
+    DevGuard dg(device);
+    hipStream_t s = stream();
+    const int ldx = ld();
+    const int cs = device_code_stride();
+    std::vector<int32_t> a32(n);
+    for (idx_t i = 0; i < n; i++) a32[i] = (int32_t)std::max<idx_t>(list_nos[i], 0);
+    std::vector<float> cent((size_t)nlist * ldx, 0.f);
+    if (by_residual)
+        for (size_t l = 0; l < nlist; l++) quantizer->reconstruct(l, cent.data() + l * ldx);
+    DeviceBuffer bx, ba, bc, bp, bo;
+    bx.reserve(sizeof(float) * n * ldx);
+    ba.reserve(sizeof(int32_t) * n);
+    bc.reserve(sizeof(float) * cent.size());
+    bp.reserve(sizeof(float) * pq.centroids.size());
+    bo.reserve((size_t)n * cs);
+    if (ldx != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * n * ldx, s));
+    HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ldx, x, sizeof(float) * d,
+                               sizeof(float) * d, n, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(ba.ptr, a32.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(bc.ptr, cent.data(), sizeof(float) * cent.size(),
+                             hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(bp.ptr, pq.centroids.data(), sizeof(float) * pq.centroids.size(),
+                             hipMemcpyHostToDevice, s));
+    kern::pq_encode(bx.as<float>(), ldx, n, ba.as<int32_t>(),
+                    by_residual ? bc.as<float>() : nullptr, ldx, bp.as<float>(), (int)pq.M,
+                    (int)pq.ksub, (int)pq.dsub, bo.as<uint8_t>(), s);
+    std::vector<uint8_t> hc((size_t)n * cs);
+    HIP_CHECK(hipMemcpyAsync(hc.data(), bo.ptr, hc.size(), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    for (idx_t i = 0; i < n; i++) memcpy(codes + (size_t)i * code_size, hc.data() + (size_t)i * cs,
+                                         code_size);
+}
+
+void IndexIVFPQ::upload_extra() const {
+    hipStream_t s = stream();
+    const int ldc = ld();
+    std::vector<float> cent((size_t)nlist * ldc, 0.f);
+    for (size_t l = 0; l < nlist; l++) quantizer->reconstruct(l, cent.data() + l * ldc);
+    d_pq_.reserve(sizeof(float) * pq.centroids.size());
+    d_cent_.reserve(sizeof(float) * cent.size());
+    d_terms_.reserve(sizeof(float) * std::max<size_t>(arena_rows_, 1));
+    HIP_CHECK(hipMemcpyAsync(d_pq_.ptr, pq.centroids.data(), sizeof(float) * pq.centroids.size(),
+                             hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(d_cent_.ptr, cent.data(), sizeof(float) * cent.size(),
+                             hipMemcpyHostToDevice, s));
+    if (by_residual && arena_rows_ > 0)
+        kern::ivfpq_terms(d_codes_.as<uint8_t>(), d_row_list_.as<uint32_t>(), arena_rows_,
+                          d_cent_.as<float>(), ldc, d_pq_.as<float>(), (int)pq.M, (int)pq.ksub,
+                          (int)pq.dsub, d_terms_.as<float>(), s);
+}
+
+void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
+                                           const int32_t* assign, const float* centroid_dis,
+                                           float* distances, idx_t* labels,
+                                           hipStream_t s) const {
+    if (n <= 0) return;
+    FAISS_THROW_IF_NOT_MSG(metric_type == METRIC_L2, "IVFPQ inner product not supported on GPU");
+    sync_device();
+    ScopedKernelTimer tm(&ktimes, "ivfpq_scan", 0.0, s);
+    kern::ivfpq_scan(x, ldx, d_pq_.as<float>(), (int)pq.M, (int)pq.ksub, (int)pq.dsub,
+                     d_codes_.as<uint8_t>(), d_terms_.as<float>(), d_ids_.as<int64_t>(),
+                     d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(), (int)nlist, assign,
+                     centroid_dis, n, np, (int)k, by_residual ? 1 : 0, distances, labels, s);
+}
+
+// ---------------------------------------------------------------- shards
+IndexShardsIVF::IndexShardsIVF(Index* q, size_t nl, bool th, bool succ)
+        : Index(q->d, q->metric_type), quantizer(q), nlist(nl), threaded(th),
+          successive_ids(succ) {
+    device = q->device;
+    is_trained = q->is_trained && (size_t)q->ntotal == nlist;
+}
+
+void IndexShardsIVF::add_shard(IndexIVF* idx) {
+    FAISS_THROW_IF_NOT(idx && idx->d == d && idx->nlist == nlist);
+    FAISS_THROW_IF_NOT_MSG(idx->device == device, "in-process shards must share the device; "
+                                                  "use one process per GPU for multi-GPU");
+    shards.push_back(idx);
+    ntotal += idx->ntotal;
+}
+
+void IndexShardsIVF::train(idx_t n, const float* x) {
+    // faiss/IndexShardsIVF.cpp:44-86: train the common quantizer, copy to shards
+    std::vector<float> cent((size_t)nlist * d);
+    if (!(quantizer->is_trained && (size_t)quantizer->ntotal == nlist)) {
+        kmeans_train(d, n, x, (int)nlist, 25, 1234, cent.data(), device, verbose);
+        quantizer->reset();
+        quantizer->add(nlist, cent.data());
+        quantizer->is_trained = true;
+    }
+    for (auto* s : shards) {
+        if (!s->is_trained) s->train(n, x);
+    }
+    is_trained = true;
+}
+
+void IndexShardsIVF::add(idx_t n, const float* x) { add_with_ids(n, x, nullptr); }
+
+void IndexShardsIVF::add_with_ids(idx_t n, const float* x, const idx_t* xids) {
+    // faiss/IndexShardsIVF.cpp:88-156: contiguous slices per shard
+    FAISS_THROW_IF_NOT_MSG(!(successive_ids && xids),
+                           "It makes no sense to pass in ids and request them to be shifted");
+    if (successive_ids)
+        FAISS_THROW_IF_NOT_MSG(ntotal == 0, "when adding to IndexShards with successive_ids, "
+                                            "only add() in a single pass is supported");
+    const idx_t ns = (idx_t)shards.size();
+    FAISS_THROW_IF_NOT(ns > 0);
+    std::vector<idx_t> aids;
+    const idx_t* ids = xids;
+    if (!ids && !successive_ids) {
+        aids.resize(n);
+        for (idx_t i = 0; i < n; i++) aids[i] = ntotal + i;
+        ids = aids.data();
+    }
+    for (idx_t no = 0; no < ns; no++) {
+        idx_t i0 = no * n / ns, i1 = (no + 1) * n / ns;
+        shards[no]->add_with_ids(i1 - i0, x + (size_t)i0 * d, ids ? ids + i0 : nullptr);
+    }
+    ntotal += n;
+}
+
+void IndexShardsIVF::reset() {
+    for (auto* s : shards) s->reset();
+    ntotal = 0;
+}
+
+void IndexShardsIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                                   idx_t* labels, const SearchParameters* params_in,
+                                   hipStream_t s) const {
+    // faiss/IndexShardsIVF.cpp:158-245
+    const SearchParametersIVF* params = dynamic_cast<const SearchParametersIVF*>(params_in);
+    const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
+    FAISS_THROW_IF_NOT(np > 0 && k > 0);
+    const int ns = (int)shards.size();
+    FAISS_THROW_IF_NOT(ns > 0);
+    DevGuard dg(device);
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    s_cd_.reserve(sizeof(float) * n * np);
+    s_ci_.reserve(sizeof(int32_t) * n * np);
+    s_all_d_.reserve(sizeof(float) * ns * n * k);
+    s_all_i_.reserve(sizeof(idx_t) * ns * n * k);
+    quantizer->assign_device(n, x, ldx, (int)np, s_cd_.as<float>(), s_ci_.as<int32_t>(),
+                             params ? params->quantizer_params : nullptr, s);
+    idx_t translation = 0;
+    for (int no = 0; no < ns; no++) {
+        FAISS_THROW_IF_NOT_MSG(shards[no]->nprobe == np || params, "inconsistent nprobe");
+        idx_t* li = s_all_i_.as<idx_t>() + (size_t)no * n * k;
+        shards[no]->search_preassigned_device(n, x, ldx, k, (int)np, s_ci_.as<int32_t>(),
+                                              s_cd_.as<float>(),
+                                              s_all_d_.as<float>() + (size_t)no * n * k, li, s);
+        if (successive_ids) kern::translate_labels(li, (int64_t)n * k, translation, s);
+        translation += shards[no]->ntotal;
+    }
+    kern::merge_rows(s_all_d_.as<float>(), s_all_i_.as<idx_t>(), n, (ns << 16) | (int)k, (int)k,
+                     metric_type == METRIC_L2, distances, labels, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
+}  // namespace faiss_amd

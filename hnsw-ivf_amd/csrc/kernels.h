@@ -1,0 +1,123 @@
+// kernels.h — host-side launchers of the gfx950 kernels.
+//
+// Data layout conventions (HBM):
+//  * vectors are row-major f32 with a leading dimension `ld` that is a
+//    multiple of 4 floats (16 B) and zero padded beyond d, so every row is
+//    16-B aligned and dims can be streamed as float4.
+//  * coarse assignments are int32 list numbers ([n][nprobe], -1 = none).
+//  * inverted lists live in one arena: list l occupies rows
+//    [list_off[l], list_off[l] + list_len[l]) of `codes` (row = code_size
+//    bytes) and of `ids` (int64).  list_off is aligned to 16 rows.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace faiss_amd {
+namespace kern {
+
+constexpr int kMaxK = 64;  // largest k / nprobe served by the wave queues
+
+// out[i] = sum_j x[i*ld + j]^2, j < d
+void row_norms(const float* x, int64_t n, int d, int ld, float* out, hipStream_t s);
+
+// Distance tile on fp32 MFMA (v_mfma_f32_32x32x2_f32):
+//   L2: D[i][j] = max(0, fma(-2, <x_i, y_j>, xn[i] + yn[j]))
+//   IP: D[i][j] = <x_i, y_j>
+// reference: faiss/utils/distances.cpp:259-342 (exhaustive_L2sqr_blas)
+void pairwise_distances(const float* x, int64_t nx, int ldx, const float* xn,
+                        const float* y, int64_t ny, int ldy, const float* yn, int dp,
+                        int metric_l2, float* D, int64_t ldD, hipStream_t s);
+
+// k smallest (L2) / largest (IP) per row of D, ties by column index,
+// reference faiss/impl/ResultHandler.h:187-287 (HeapBlockResultHandler).
+// Outputs are sorted; missing slots are (+-FLT_MAX, -1).  Either of out_i32 /
+// out_i64 may be null.  `col0` is added to output column indices.
+void select_rows(const float* D, int64_t nx, int64_t ny, int64_t ldD, int k, int metric_l2,
+                 int64_t col0, float* out_d, int32_t* out_i32, int64_t* out_i64,
+                 int64_t ldo, hipStream_t s);
+
+// Merge `nin` sorted candidate tables per row: cand_d/cand_i [n][nin*kin]
+// (already final (dis,label) form, label -1 = empty) -> [n][k].
+void merge_rows(const float* cand_d, const int64_t* cand_i, int64_t n, int nin_x_kin, int k,
+                int metric_l2, float* out_d, int64_t* out_i, hipStream_t s);
+
+// labels >= 0 get += offset (faiss/IndexShardsIVF.cpp translate_labels)
+void translate_labels(int64_t* labels, int64_t n, int64_t offset, hipStream_t s);
+
+// ---------------- IVF list-centric batching ----------------
+// Work item = (list, chunk of <= QT queries probing it).
+struct IVFBuckets {
+    uint32_t* counts;      // [nlist]
+    uint32_t* bucket_off;  // [nlist + 1]
+    uint32_t* item_off;    // [nlist + 1]
+    uint32_t* cursor;      // [nlist]
+    uint32_t* entries;     // [n * nprobe], entry = q * nprobe + rank
+};
+void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
+                int nlist, int QT, IVFBuckets b, hipStream_t s);
+// upper bound on the number of work items (grid size without a host sync)
+inline int64_t ivf_max_items(int64_t n, int nprobe, int nlist, int QT) {
+    return (n * nprobe + QT - 1) / QT + nlist;
+}
+
+// IVF-Flat scan, reference faiss/IndexIVFFlat.cpp:155-179 (IVFFlatScanner):
+// exact per-(query, list) top-k of sum (x - y)^2 (or <x,y>) written as
+// internal keys to part_k1/part_k2 [n*nprobe][k].
+void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const int64_t* ids,
+                   const uint32_t* list_off, const uint32_t* list_len, int nlist, int dp,
+                   int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b, int64_t max_items,
+                   float* part_k1, long long* part_k2, hipStream_t s);
+
+// per-query merge of the nprobe partial top-k, reference
+// faiss/IndexIVF.cpp:595-631 (heap over probes) + Heap.h:421-450 (reorder)
+void ivf_merge(const float* part_k1, const long long* part_k2, const int32_t* assign,
+               const uint32_t* list_len, int nlist, int64_t n, int nprobe, int k, int metric_l2,
+               float* D, int64_t* I, hipStream_t s);
+
+// ---------------- IVF-PQ ----------------
+// query-centric PQ scan with the LUT in LDS, reference
+// faiss/IndexIVFPQ.cpp:560-566,634-700 (tables), :861-933 (scan).
+// dis = coarse_dis + term[v] + sum_m T[m][code_m]
+//   by_residual: T = -2 <x_m, c_mj>, term[v] = sum_m ||c||^2 + 2<yC_m, c>
+//   otherwise:   T = ||x_m - c_mj||^2, term = 0, coarse_dis = 0
+void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int ksub, int dsub,
+                const uint8_t* codes, const float* terms, const int64_t* ids,
+                const uint32_t* list_off, const uint32_t* list_len, int nlist,
+                const int32_t* assign, const float* coarse_dis, int64_t n, int nprobe, int k,
+                int by_residual, float* D, int64_t* I, hipStream_t s);
+
+// term[v] = sum_m (||c_{m,code}||^2 + 2 <yC_m, c_{m,code}>) for every arena row
+void ivfpq_terms(const uint8_t* codes, const uint32_t* row_list, int64_t nrows,
+                 const float* centroids, int ldcent, const float* pq_centroids, int M, int ksub,
+                 int dsub, float* terms, hipStream_t s);
+
+// PQ encoding: codes[i][m] = argmin_j ||r_im - c_mj||^2 (first minimum)
+// residual r = x - centroid[assign[i]] when centroids != null.
+void pq_encode(const float* x, int ldx, int64_t n, const int32_t* assign,
+               const float* centroids, int ldcent, const float* pq_centroids, int M, int ksub,
+               int dsub, uint8_t* codes, hipStream_t s);
+
+// ---------------- HNSW (one wavefront per query) ----------------
+struct HNSWDevice {
+    const float* storage;     // [ntotal][ld]
+    const float* norms;       // unused (reserved)
+    int ld;
+    int d;
+    const int32_t* levels;    // [ntotal] (level+1 as in faiss)
+    const uint64_t* offsets;  // [ntotal+1]
+    const int32_t* neighbors;
+    const int32_t* cum_nb;    // cum_nneighbor_per_level
+    int nlevels_cum;
+    int entry_point;
+    int max_level;
+    int ntotal;
+};
+// reference faiss/impl/HNSW.cpp:943-996 (HNSW::search), :852-924 (greedy),
+// :605-741 (search_from_candidates), :1096-1342 (MinimaxHeap)
+void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
+                 float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
+                 int64_t visited_words_per_query, hipStream_t s);
+
+}  // namespace kern
+}  // namespace faiss_amd

@@ -1,0 +1,343 @@
+// kernels_ivf.hip — list-centric batched IVF-Flat scan for gfx950.
+//
+// Reference hot loop: faiss/IndexIVFFlat.cpp:155-179 (IVFFlatScanner::
+// scan_codes: for each code, dis = fvec_L2sqr(x, y, d); heap_replace_top on
+// strict improvement) driven per query by faiss/IndexIVF.cpp:595-631.
+//
+// MI355X design: instead of streaming every probed list once per query (the
+// CPU order, ~4 MB/query at nlist 4096 nprobe 32), the (query, list) pairs of
+// the whole batch are bucketed by list.  A workgroup owns one list and up to
+// 64 of the queries probing it: the list is read from HBM once per 64 queries,
+// tiles of 64 queries x 64 codes live in LDS, and each thread computes a 4x4
+// micro-tile of exact sum (x-y)^2 (same arithmetic as the reference, not the
+// norm expansion).  Each wave then folds its 16 queries' distance rows into
+// wave64 top-k queues and the per-(query, list) top-k is written out; a
+// second kernel merges the nprobe partial lists of each query.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "common.h"
+#include "kernels.h"
+#include "wave_select.h"
+
+namespace faiss_amd {
+namespace kern {
+
+// ---------------------------------------------------------------- bucketing
+__global__ void k_bucket_count(const int32_t* __restrict__ assign, int64_t total,
+                               const uint32_t* __restrict__ list_len, int nlist,
+                               uint32_t* __restrict__ counts) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    int l = assign[e];
+    if (l >= 0 && l < nlist && list_len[l] > 0) atomicAdd(&counts[l], 1u);
+}
+
+// single-workgroup exclusive scan of counts -> bucket_off, ceil(counts/QT)
+// -> item_off
+__global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict__ counts,
+                                                      int nlist, int QT,
+                                                      uint32_t* __restrict__ bucket_off,
+                                                      uint32_t* __restrict__ item_off) {
+    __shared__ uint32_t sb[1024], si[1024];
+    const int t = threadIdx.x;
+    const int per = (nlist + 1023) / 1024;
+    const int l0 = t * per, l1 = min(nlist, l0 + per);
+    uint32_t sbk = 0, sit = 0;
+    for (int l = l0; l < l1; l++) {
+        uint32_t c = counts[l];
+        sbk += c;
+        sit += (c + QT - 1) / QT;
+    }
+    sb[t] = sbk;
+    si[t] = sit;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over 1024 partials
+    for (int off = 1; off < 1024; off <<= 1) {
+        uint32_t vb = t >= off ? sb[t - off] : 0u;
+        uint32_t vi = t >= off ? si[t - off] : 0u;
+        __syncthreads();
+        sb[t] += vb;
+        si[t] += vi;
+        __syncthreads();
+    }
+    uint32_t rb = sb[t] - sbk, ri = si[t] - sit;  // exclusive prefix
+    for (int l = l0; l < l1; l++) {
+        bucket_off[l] = rb;
+        item_off[l] = ri;
+        uint32_t c = counts[l];
+        rb += c;
+        ri += (c + QT - 1) / QT;
+    }
+    if (t == 1023) {
+        bucket_off[nlist] = sb[1023];
+        item_off[nlist] = si[1023];
+    }
+}
+
+__global__ void k_bucket_fill(const int32_t* __restrict__ assign, int64_t total,
+                              const uint32_t* __restrict__ list_len, int nlist,
+                              const uint32_t* __restrict__ bucket_off,
+                              uint32_t* __restrict__ cursor, uint32_t* __restrict__ entries) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    int l = assign[e];
+    if (l >= 0 && l < nlist && list_len[l] > 0) {
+        uint32_t pos = bucket_off[l] + atomicAdd(&cursor[l], 1u);
+        entries[pos] = (uint32_t)e;
+    }
+}
+
+void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
+                int nlist, int QT, IVFBuckets b, hipStream_t s) {
+    int64_t total = n * nprobe;
+    FAISS_THROW_IF_NOT_MSG(total < (1ll << 32), "n * nprobe must fit in 32 bits");
+    HIP_CHECK(hipMemsetAsync(b.counts, 0, sizeof(uint32_t) * nlist, s));
+    HIP_CHECK(hipMemsetAsync(b.cursor, 0, sizeof(uint32_t) * nlist, s));
+    if (total > 0) {
+        k_bucket_count<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
+                assign, total, list_len, nlist, b.counts);
+        HIP_LAUNCH_CHECK();
+    }
+    k_bucket_scan<<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off, b.item_off);
+    HIP_LAUNCH_CHECK();
+    if (total > 0) {
+        k_bucket_fill<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
+                assign, total, list_len, nlist, b.bucket_off, b.cursor, b.entries);
+        HIP_LAUNCH_CHECK();
+    }
+}
+
+// ---------------------------------------------------------------- scan
+constexpr int SQT = 64;   // queries per work item
+constexpr int SVT = 64;   // codes per tile
+constexpr int SDC = 128;  // dims per LDS chunk
+constexpr int SSD = SDC + 4;  // LDS row stride (floats): 528 B, 16-B aligned
+
+template <bool L2>
+__global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
+        const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
+        const int64_t* __restrict__ ids, const uint32_t* __restrict__ list_off,
+        const uint32_t* __restrict__ list_len, int nlist, int dp, int nprobe, int k,
+        const uint32_t* __restrict__ bucket_off, const uint32_t* __restrict__ item_off,
+        const uint32_t* __restrict__ entries, float* __restrict__ part_k1,
+        long long* __restrict__ part_k2) {
+    __shared__ __attribute__((aligned(16))) float Xs[SQT * SSD];
+    __shared__ __attribute__((aligned(16))) float Ys[SVT * SSD];
+    __shared__ long long ids_s[SVT];
+    __shared__ uint32_t ent_s[SQT];
+    __shared__ int32_t qrow_s[SQT];
+
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int w = t >> 6;
+    const uint32_t item = blockIdx.x;
+    const uint32_t total_items = item_off[nlist];
+    if (item >= total_items) return;
+    // list owning this item: largest l with item_off[l] <= item
+    int lo = 0, hi = nlist;
+    while (hi - lo > 1) {
+        int mid = (lo + hi) >> 1;
+        if (item_off[mid] <= item) lo = mid; else hi = mid;
+    }
+    const int l = lo;
+    const uint32_t chunk = item - item_off[l];
+    const uint32_t qb = bucket_off[l] + chunk * SQT;
+    const int nQ = (int)min((uint32_t)SQT, bucket_off[l + 1] - qb);
+    if (t < SQT) {
+        uint32_t e = t < nQ ? entries[qb + t] : 0u;
+        ent_s[t] = e;
+        qrow_s[t] = t < nQ ? (int32_t)(e / (uint32_t)nprobe) : -1;
+    }
+    const int len = (int)list_len[l];
+    const int64_t row0 = list_off[l];
+    __syncthreads();
+
+    const bool one_chunk = dp <= SDC;
+    auto load_x = [&](int dc) {
+        const int dl = min(SDC, dp - dc);
+        for (int e = t; e < SQT * (SDC / 4); e += 256) {
+            int r = e >> 5, c4 = e & 31;
+            int kc = 4 * c4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            int qr = qrow_s[r];
+            if (qr >= 0 && kc < dl) v = *(const float4*)(x + (int64_t)qr * ldx + dc + kc);
+            *(float4*)(Xs + r * SSD + kc) = v;
+        }
+    };
+    if (one_chunk) load_x(0);
+
+    float qd[16];
+    long long qi[16];
+#pragma unroll
+    for (int qq = 0; qq < 16; qq++) {
+        qd[qq] = WS_INF;
+        qi[qq] = WS_NOID;
+    }
+    const int qg = t >> 4, vg = t & 15;
+
+    for (int v0 = 0; v0 < len; v0 += SVT) {
+        const int nv = min(SVT, len - v0);
+        float acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][j] = 0.f;
+
+        for (int dc = 0; dc < dp; dc += SDC) {
+            const int dl = min(SDC, dp - dc);
+            if (!one_chunk) load_x(dc);
+            for (int e = t; e < SVT * (SDC / 4); e += 256) {
+                int r = e >> 5, c4 = e & 31;
+                int kc = 4 * c4;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (r < nv && kc < dl)
+                    v = *(const float4*)(codes + (row0 + v0 + r) * (int64_t)ldc + dc + kc);
+                *(float4*)(Ys + r * SSD + kc) = v;
+            }
+            __syncthreads();
+#pragma unroll 2
+            for (int dd = 0; dd < dl; dd += 4) {
+                float4 xa[4], yb[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) xa[i] = *(const float4*)(Xs + (qg + 16 * i) * SSD + dd);
+#pragma unroll
+                for (int j = 0; j < 4; j++) yb[j] = *(const float4*)(Ys + (vg + 16 * j) * SSD + dd);
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        if (L2) {
+                            float d0 = xa[i].x - yb[j].x;
+                            float d1 = xa[i].y - yb[j].y;
+                            float d2 = xa[i].z - yb[j].z;
+                            float d3 = xa[i].w - yb[j].w;
+                            float a = acc[i][j];
+                            a = fmaf(d0, d0, a);
+                            a = fmaf(d1, d1, a);
+                            a = fmaf(d2, d2, a);
+                            a = fmaf(d3, d3, a);
+                            acc[i][j] = a;
+                        } else {
+                            float a = acc[i][j];
+                            a = fmaf(xa[i].x, yb[j].x, a);
+                            a = fmaf(xa[i].y, yb[j].y, a);
+                            a = fmaf(xa[i].z, yb[j].z, a);
+                            a = fmaf(xa[i].w, yb[j].w, a);
+                            acc[i][j] = a;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        // distance tile -> LDS (aliases the Y tile), ids of this tile
+        float* Ds = Ys;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) Ds[(qg + 16 * i) * (SVT + 1) + vg + 16 * j] = acc[i][j];
+        if (t < SVT) ids_s[t] = t < nv ? (long long)ids[row0 + v0 + t] : 0ll;
+        __syncthreads();
+        // selection: wave w owns queries w*16 .. w*16+15
+        const bool lane_ok = lane < nv;
+        const long long my_id = ids_s[lane];
+#pragma unroll
+        for (int qq = 0; qq < 16; qq++) {
+            const int q = w * 16 + qq;
+            if (q < nQ) {
+                float dis = Ds[q * (SVT + 1) + lane];
+                float k1;
+                long long k2;
+                to_key(L2 ? 1 : 0, dis, my_id, k1, k2);
+                if (!lane_ok || !key_admissible(k1)) {
+                    k1 = WS_INF;
+                    k2 = WS_NOID;
+                }
+                wave_offer_q(qd[qq], qi[qq], k1, k2, k, lane);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int qq = 0; qq < 16; qq++) {
+        const int q = w * 16 + qq;
+        if (q < nQ && lane < k) {
+            const int64_t e = ent_s[q];
+            part_k1[e * k + lane] = qd[qq];
+            part_k2[e * k + lane] = qi[qq];
+        }
+    }
+}
+
+void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const int64_t* ids,
+                   const uint32_t* list_off, const uint32_t* list_len, int nlist, int dp,
+                   int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b, int64_t max_items,
+                   float* part_k1, long long* part_k2, hipStream_t s) {
+    if (n <= 0) return;
+    FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
+    FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldc % 4 == 0 && dp % 4 == 0);
+    FAISS_THROW_IF_NOT(max_items < (1ll << 31));
+    if (metric_l2)
+        k_ivf_flat_scan<true><<<dim3((unsigned)max_items), dim3(256), 0, s>>>(
+                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, nprobe, k, b.bucket_off,
+                b.item_off, b.entries, part_k1, part_k2);
+    else
+        k_ivf_flat_scan<false><<<dim3((unsigned)max_items), dim3(256), 0, s>>>(
+                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, nprobe, k, b.bucket_off,
+                b.item_off, b.entries, part_k1, part_k2);
+    HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------- merge
+__global__ __launch_bounds__(256) void k_ivf_merge(const float* __restrict__ part_k1,
+                                                   const long long* __restrict__ part_k2,
+                                                   const int32_t* __restrict__ assign,
+                                                   const uint32_t* __restrict__ list_len,
+                                                   int64_t n, int nprobe, int nlist, int k,
+                                                   int metric_l2, float* __restrict__ D,
+                                                   int64_t* __restrict__ I) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= n) return;
+    float qd = WS_INF;
+    long long qi = WS_NOID;
+    float thr_d = WS_INF;
+    long long thr_i = WS_NOID;
+    const int total = nprobe * k;
+    for (int c = 0; c < total; c += 64) {
+        int e = c + lane;
+        float k1 = WS_INF;
+        long long k2 = WS_NOID;
+        if (e < total) {
+            int r = e / k;
+            int lst = assign[q * nprobe + r];
+            if (lst >= 0 && lst < nlist && list_len[lst] > 0) {
+                int64_t p = (q * nprobe) * (int64_t)k + e;
+                k1 = part_k1[p];
+                k2 = part_k2[p];
+            }
+        }
+        wave_offer(qd, qi, k1, k2, thr_d, thr_i, k, lane);
+    }
+    if (lane < k) {
+        float dis;
+        long long id;
+        from_key(metric_l2, qd, qi, dis, id);
+        D[q * k + lane] = dis;
+        I[q * k + lane] = id;
+    }
+}
+
+void ivf_merge(const float* part_k1, const long long* part_k2, const int32_t* assign,
+               const uint32_t* list_len, int nlist, int64_t n, int nprobe, int k, int metric_l2,
+               float* D, int64_t* I, hipStream_t s) {
+    if (n <= 0) return;
+    k_ivf_merge<<<dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s>>>(
+            part_k1, part_k2, assign, list_len, n, nprobe, nlist, k, metric_l2, D, I);
+    HIP_LAUNCH_CHECK();
+}
+
+}  // namespace kern
+}  // namespace faiss_amd

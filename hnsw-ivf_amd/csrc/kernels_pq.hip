@@ -1,0 +1,240 @@
+// kernels_pq.hip — IVF-PQ search, encoding and per-code terms for gfx950.
+//
+// Reference: faiss/IndexIVFPQ.cpp
+//   * precomputed "table 1": dis = coarse_dis + sum_m (P[key][m][c_m]
+//     - 2 <x_m, c_{m,c_m}>) with P[key][m][j] = ||c_mj||^2 + 2 <yC_m, c_mj>
+//     (:332-459, :634-653) — here the list-dependent part sum_m P[key][m][c_m]
+//     is folded into one f32 "term" per stored code (computed once when the
+//     lists are uploaded), so the 128 MB (nlist 4096) / 3.2 GB (nlist 65536)
+//     table never has to be streamed and the query-only LUT T[m][j] =
+//     -2 <x_m, c_mj> (M x 256 f32 = 32-48 KB) lives in LDS.
+//   * table 0 (:637-643) computes ||r_m - c_mj||^2 with r = x - yC; it is the
+//     same quantity, so one kernel serves both.
+//   * scan: sum of M LUT gathers per code (:861-933, code_distance-generic.h).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "common.h"
+#include "kernels.h"
+#include "wave_select.h"
+
+namespace faiss_amd {
+namespace kern {
+
+// ---------------------------------------------------------------- scan
+// One workgroup (4 waves) per query.  LUT built in LDS; wave w scans probes
+// w, w+4, ...; 64 codes per step (one per lane); the four per-wave queues are
+// merged through LDS at the end.
+__global__ __launch_bounds__(256) void k_ivfpq_scan(
+        const float* __restrict__ x, int ldx, const float* __restrict__ pq_cent, int M, int ksub,
+        int dsub, const uint8_t* __restrict__ codes, int code_stride,
+        const float* __restrict__ terms, const int64_t* __restrict__ ids,
+        const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
+        const int32_t* __restrict__ assign, const float* __restrict__ coarse_dis, int nprobe,
+        int k, int by_residual, float* __restrict__ D, int64_t* __restrict__ I) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* T = smem;                    // [M * ksub]
+    float* xq = T + M * ksub;           // [M * dsub]
+    float* md = xq + ((M * dsub + 3) & ~3);
+    long long* mi = (long long*)(md + 256);
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t q = blockIdx.x;
+    const int d = M * dsub;
+    for (int j = t; j < d; j += 256) xq[j] = x[q * ldx + j];
+    __syncthreads();
+    for (int e = t; e < M * ksub; e += 256) {
+        const int m = e / ksub;
+        const float* c = pq_cent + (int64_t)e * dsub;
+        const float* xm = xq + m * dsub;
+        float s = 0.f;
+        if (by_residual) {
+            for (int i = 0; i < dsub; i++) s = fmaf(xm[i], c[i], s);
+            T[e] = -2.f * s;
+        } else {
+            for (int i = 0; i < dsub; i++) {
+                float df = xm[i] - c[i];
+                s = fmaf(df, df, s);
+            }
+            T[e] = s;
+        }
+    }
+    __syncthreads();
+
+    float qd = WS_INF;
+    long long qi = WS_NOID;
+    float thr_d = WS_INF;
+    long long thr_i = WS_NOID;
+    for (int r = w; r < nprobe; r += 4) {
+        const int lst = assign[q * nprobe + r];
+        if (lst < 0 || lst >= nlist) continue;
+        const int len = (int)list_len[lst];
+        if (len == 0) continue;
+        const float dis0 = by_residual ? coarse_dis[q * nprobe + r] : 0.f;
+        const int64_t row0 = list_off[lst];
+        for (int v0 = 0; v0 < len; v0 += 64) {
+            const int v = v0 + lane;
+            float k1 = WS_INF;
+            long long k2 = WS_NOID;
+            if (v < len) {
+                const int64_t row = row0 + v;
+                const uint32_t* cw = (const uint32_t*)(codes + row * code_stride);
+                float s = 0.f;
+                int m = 0;
+                for (int wd = 0; m < M; wd++) {
+                    uint32_t word = cw[wd];
+#pragma unroll
+                    for (int b = 0; b < 4; b++, m++) {
+                        if (m < M) s += T[m * ksub + ((word >> (8 * b)) & 0xff)];
+                    }
+                }
+                float dis = by_residual ? dis0 + terms[row] + s : s;
+                k1 = dis;
+                k2 = ids[row];
+                if (!key_admissible(k1)) {
+                    k1 = WS_INF;
+                    k2 = WS_NOID;
+                }
+            }
+            wave_offer(qd, qi, k1, k2, thr_d, thr_i, k, lane);
+        }
+    }
+    // merge the 4 wave queues
+    md[w * 64 + lane] = qd;
+    mi[w * 64 + lane] = qi;
+    __syncthreads();
+    if (w == 0) {
+        float fd = WS_INF;
+        long long fi = WS_NOID;
+        float td = WS_INF;
+        long long ti = WS_NOID;
+        for (int ww = 0; ww < 4; ww++) {
+            float cd = lane < k ? md[ww * 64 + lane] : WS_INF;
+            long long ci = lane < k ? mi[ww * 64 + lane] : WS_NOID;
+            wave_offer(fd, fi, cd, ci, td, ti, k, lane);
+        }
+        if (lane < k) {
+            float dis;
+            long long id;
+            from_key(1, fd, fi, dis, id);
+            D[q * k + lane] = dis;
+            I[q * k + lane] = id;
+        }
+    }
+}
+
+void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int ksub, int dsub,
+                const uint8_t* codes, const float* terms, const int64_t* ids,
+                const uint32_t* list_off, const uint32_t* list_len, int nlist,
+                const int32_t* assign, const float* coarse_dis, int64_t n, int nprobe, int k,
+                int by_residual, float* D, int64_t* I, hipStream_t s) {
+    if (n <= 0) return;
+    FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
+    FAISS_THROW_IF_NOT_MSG(ksub == 256, "only 8-bit PQ codes are supported on this path");
+    const int code_stride = (int)roundup((size_t)M, 4);
+    size_t lds = sizeof(float) * ((size_t)M * ksub + roundup((size_t)M * dsub, 4) + 256) +
+                 sizeof(long long) * 256;
+    FAISS_THROW_IF_NOT_MSG(lds <= 160 * 1024, "PQ LUT does not fit in LDS");
+    k_ivfpq_scan<<<dim3((unsigned)n), dim3(256), lds, s>>>(
+            x, ldx, pq_centroids, M, ksub, dsub, codes, code_stride, terms, ids, list_off,
+            list_len, nlist, assign, coarse_dis, nprobe, k, by_residual, D, I);
+    HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------- terms
+__global__ void k_ivfpq_terms(const uint8_t* __restrict__ codes, int code_stride,
+                              const uint32_t* __restrict__ row_list, int64_t nrows,
+                              const float* __restrict__ cent, int ldcent,
+                              const float* __restrict__ pq_cent, int M, int ksub, int dsub,
+                              float* __restrict__ terms) {
+    int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= nrows) return;
+    uint32_t l = row_list[row];
+    if (l == 0xffffffffu) {
+        terms[row] = 0.f;
+        return;
+    }
+    const float* yc = cent + (int64_t)l * ldcent;
+    const uint8_t* c = codes + row * code_stride;
+    float s = 0.f;
+    for (int m = 0; m < M; m++) {
+        const float* cm = pq_cent + ((int64_t)m * ksub + c[m]) * dsub;
+        const float* ym = yc + m * dsub;
+        float nrm = 0.f, ip = 0.f;
+        for (int i = 0; i < dsub; i++) {
+            nrm = fmaf(cm[i], cm[i], nrm);
+            ip = fmaf(ym[i], cm[i], ip);
+        }
+        s += fmaf(2.f, ip, nrm);
+    }
+    terms[row] = s;
+}
+
+void ivfpq_terms(const uint8_t* codes, const uint32_t* row_list, int64_t nrows,
+                 const float* centroids, int ldcent, const float* pq_centroids, int M, int ksub,
+                 int dsub, float* terms, hipStream_t s) {
+    if (nrows <= 0) return;
+    const int code_stride = (int)roundup((size_t)M, 4);
+    k_ivfpq_terms<<<dim3((unsigned)cdiv(nrows, 256)), dim3(256), 0, s>>>(
+            codes, code_stride, row_list, nrows, centroids, ldcent, pq_centroids, M, ksub, dsub,
+            terms);
+    HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------- encode
+// thread per (vector, sub-quantizer); the 256 sub-centroids of m are staged in
+// LDS by the workgroup (blockIdx.y = m).
+__global__ __launch_bounds__(256) void k_pq_encode(const float* __restrict__ x, int ldx,
+                                                   int64_t n, const int32_t* __restrict__ assign,
+                                                   const float* __restrict__ cent, int ldcent,
+                                                   const float* __restrict__ pq_cent, int M,
+                                                   int ksub, int dsub,
+                                                   uint8_t* __restrict__ codes, int code_stride) {
+    extern __shared__ float cs[];  // [ksub * dsub]
+    const int m = blockIdx.y;
+    for (int e = threadIdx.x; e < ksub * dsub; e += 256)
+        cs[e] = pq_cent[(int64_t)m * ksub * dsub + e];
+    __syncthreads();
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float r[32];
+    const int dd = dsub < 32 ? dsub : 32;
+    for (int j = 0; j < dd; j++) {
+        float v = x[i * ldx + m * dsub + j];
+        if (cent) v -= cent[(int64_t)assign[i] * ldcent + m * dsub + j];
+        r[j] = v;
+    }
+    float best = WS_INF;
+    int bj = 0;
+    for (int j = 0; j < ksub; j++) {
+        const float* c = cs + j * dsub;
+        float s = 0.f;
+        for (int t = 0; t < dd; t++) {
+            float df = r[t] - c[t];
+            s = fmaf(df, df, s);
+        }
+        if (s < best) {
+            best = s;
+            bj = j;
+        }
+    }
+    codes[i * code_stride + m] = (uint8_t)bj;
+}
+
+void pq_encode(const float* x, int ldx, int64_t n, const int32_t* assign, const float* centroids,
+               int ldcent, const float* pq_centroids, int M, int ksub, int dsub, uint8_t* codes,
+               hipStream_t s) {
+    if (n <= 0) return;
+    FAISS_THROW_IF_NOT_MSG(dsub <= 32, "dsub > 32 not supported on this path");
+    FAISS_THROW_IF_NOT(ksub <= 256);
+    const int code_stride = (int)roundup((size_t)M, 4);
+    k_pq_encode<<<dim3((unsigned)cdiv(n, 256), (unsigned)M), dim3(256),
+                  sizeof(float) * ksub * dsub, s>>>(x, ldx, n, assign, centroids, ldcent,
+                                                    pq_centroids, M, ksub, dsub, codes,
+                                                    code_stride);
+    HIP_LAUNCH_CHECK();
+}
+
+}  // namespace kern
+}  // namespace faiss_amd

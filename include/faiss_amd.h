@@ -1,0 +1,329 @@
+// faiss_amd.h — C++ host API of the MI355X-native IVF search path.
+//
+// Mirrors the reference faiss::Index hierarchy for the hot path
+// (faiss/Index.h:108-181, faiss/IndexFlat.h, faiss/IndexIVF.h:39-587,
+// faiss/IndexIVFFlat.h, faiss/IndexIVFPQ.h, faiss/IndexHNSW.h,
+// faiss/IndexShardsIVF.h): same class names, method signatures, argument
+// meaning and exceptions, in namespace faiss_amd.  Indexes are GPU-resident:
+// host mirrors keep the faiss data structures (for I/O and reconstruction),
+// HBM holds the search layout.  `search()` takes host pointers and is
+// synchronous; `search_device()` takes device pointers and a hipStream_t.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../hnsw-ivf_amd/csrc/common.h"
+
+namespace faiss_amd {
+
+// ---------------------------------------------------------------- params
+struct SearchParameters {  // faiss/Index.h:63-70
+    virtual ~SearchParameters() = default;
+};
+struct SearchParametersHNSW : SearchParameters {  // faiss/impl/HNSW.h:46-52
+    int efSearch = 16;
+};
+struct SearchParametersIVF : SearchParameters {  // faiss/IndexIVF.h:77-85
+    size_t nprobe = 1;
+    size_t max_codes = 0;
+    SearchParameters* quantizer_params = nullptr;
+};
+
+// faiss/IndexIVF.h:567-583
+struct IndexIVFStats {
+    size_t nq = 0, nlist = 0, ndis = 0, nheap_updates = 0;
+    double quantization_time = 0, search_time = 0;
+    void reset() { *this = IndexIVFStats(); }
+};
+extern IndexIVFStats indexIVF_stats;
+
+// ---------------------------------------------------------------- Index
+struct Index {
+    int d = 0;
+    idx_t ntotal = 0;
+    bool verbose = false;
+    bool is_trained = true;
+    MetricType metric_type = METRIC_L2;
+    float metric_arg = 0;
+    int device = 0;  // HIP device holding the HBM copy
+
+    mutable KernelTimes ktimes;  // dominant-kernel timings of the last search
+
+    explicit Index(idx_t d = 0, MetricType metric = METRIC_L2);
+    virtual ~Index();
+
+    virtual void train(idx_t n, const float* x);
+    virtual void add(idx_t n, const float* x) = 0;
+    virtual void add_with_ids(idx_t n, const float* x, const idx_t* xids);
+    // faiss/Index.h:165-171: host pointers, synchronous
+    virtual void search(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                        const SearchParameters* params = nullptr) const;
+    // device pointers; x rows have leading dimension ldx (multiple of 4)
+    virtual void search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                               idx_t* labels, const SearchParameters* params,
+                               hipStream_t stream) const = 0;
+    // coarse-quantizer entry: top-k as int32 labels (device)
+    virtual void assign_device(idx_t n, const float* x, int ldx, int k, float* distances,
+                               int32_t* labels, const SearchParameters* params,
+                               hipStream_t stream) const;
+    virtual void reset() = 0;
+    virtual void reconstruct(idx_t key, float* recons) const;
+    virtual void sync_device() const {}
+
+    hipStream_t stream() const;
+    int ld() const { return (int)roundup((size_t)d, 4); }
+};
+
+// ---------------------------------------------------------------- flat
+// faiss/IndexFlat.h: exhaustive search.  Coarse quantizer of the IVF path.
+struct IndexFlat : Index {
+    std::vector<float> xb;  // host mirror [ntotal][d] (faiss IndexFlatCodes::codes)
+
+    explicit IndexFlat(idx_t d = 0, MetricType metric = METRIC_L2);
+    void add(idx_t n, const float* x) override;
+    void search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                       idx_t* labels, const SearchParameters* params,
+                       hipStream_t stream) const override;
+    void assign_device(idx_t n, const float* x, int ldx, int k, float* distances,
+                       int32_t* labels, const SearchParameters* params,
+                       hipStream_t stream) const override;
+    void reset() override;
+    void reconstruct(idx_t key, float* recons) const override;
+    void sync_device() const override;
+
+    const float* device_vectors() const;  // [ntotal][ld]
+    const float* device_norms() const;
+
+   private:
+    template <class OutIdx>
+    void knn_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
+                    hipStream_t stream) const;
+    mutable DeviceBuffer d_xb_, d_norms_;
+    mutable bool dirty_ = true;
+    mutable std::recursive_mutex mu_;
+    mutable DeviceBuffer s_xn_, s_tile_, s_cand_d_, s_cand_i_;
+};
+struct IndexFlatL2 : IndexFlat {
+    explicit IndexFlatL2(idx_t d = 0) : IndexFlat(d, METRIC_L2) {}
+};
+struct IndexFlatIP : IndexFlat {
+    explicit IndexFlatIP(idx_t d = 0) : IndexFlat(d, METRIC_INNER_PRODUCT) {}
+};
+
+// ---------------------------------------------------------------- HNSW
+// faiss/impl/HNSW.h:54-232 graph, faiss/IndexHNSW.h IndexHNSWFlat.
+struct HNSW {
+    std::vector<double> assign_probas;
+    std::vector<int> cum_nneighbor_per_level;
+    std::vector<int> levels;
+    std::vector<size_t> offsets;
+    std::vector<int32_t> neighbors;
+    int32_t entry_point = -1;
+    int max_level = -1;
+    int efConstruction = 40;
+    int efSearch = 16;
+    bool check_relative_distance = true;
+    bool search_bounded_queue = true;
+
+    explicit HNSW(int M = 32);
+    void set_default_probas(int M, float levelMult);
+    int nb_neighbors(int layer_no) const;
+    int cum_nb_neighbors(int layer_no) const;
+    void neighbor_range(idx_t no, int layer_no, size_t* begin, size_t* end) const;
+    int random_level(std::mt19937& rng) const;
+};
+
+struct IndexHNSW : Index {
+    HNSW hnsw;
+    IndexFlat* storage = nullptr;
+    bool own_fields = false;
+    IndexHNSW(IndexFlat* storage, int M);
+    ~IndexHNSW() override;
+    void add(idx_t n, const float* x) override;
+    void search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                       idx_t* labels, const SearchParameters* params,
+                       hipStream_t stream) const override;
+    void assign_device(idx_t n, const float* x, int ldx, int k, float* distances,
+                       int32_t* labels, const SearchParameters* params,
+                       hipStream_t stream) const override;
+    void reset() override;
+    void reconstruct(idx_t key, float* recons) const override;
+    void sync_device() const override;
+
+   private:
+    template <class OutIdx>
+    void hnsw_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
+                     const SearchParameters* params, hipStream_t stream) const;
+    mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, s_visited_;
+    mutable bool dirty_ = true;
+    mutable std::recursive_mutex mu_;
+};
+struct IndexHNSWFlat : IndexHNSW {
+    IndexHNSWFlat(int d = 0, int M = 32, MetricType metric = METRIC_L2);
+};
+
+// ---------------------------------------------------------------- IVF
+// faiss/invlists/InvertedLists.h:243-275 (ArrayInvertedLists) on the host,
+// one contiguous arena in HBM.
+struct ArrayInvertedLists {
+    size_t nlist = 0, code_size = 0;
+    std::vector<std::vector<uint8_t>> codes;
+    std::vector<std::vector<idx_t>> ids;
+    ArrayInvertedLists(size_t nlist, size_t code_size);
+    size_t list_size(size_t l) const { return ids[l].size(); }
+    void add_entries(size_t l, size_t n, const idx_t* ids, const uint8_t* codes);
+    void reset();
+};
+
+struct IndexIVF : Index {
+    Index* quantizer = nullptr;
+    bool own_fields = false;
+    size_t nlist = 0;
+    size_t nprobe = 1;
+    size_t max_codes = 0;
+    size_t code_size = 0;
+    bool by_residual = true;
+    int niter = 25;  // k-means iterations (faiss ClusteringParameters::niter)
+    std::unique_ptr<ArrayInvertedLists> invlists;
+
+    IndexIVF(Index* quantizer, size_t d, size_t nlist, size_t code_size, MetricType metric);
+    ~IndexIVF() override;
+
+    void train(idx_t n, const float* x) override;
+    void add(idx_t n, const float* x) override;
+    void add_with_ids(idx_t n, const float* x, const idx_t* xids) override;
+    void search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                       idx_t* labels, const SearchParameters* params,
+                       hipStream_t stream) const override;
+    // faiss/IndexIVF.h:120-130; assign = [n][nprobe] host list numbers
+    void search_preassigned(idx_t n, const float* x, idx_t k, const idx_t* assign,
+                            const float* centroid_dis, float* distances, idx_t* labels,
+                            bool store_pairs, const SearchParametersIVF* params = nullptr) const;
+    // device form (int32 assignments)
+    virtual void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k,
+                                           int nprobe, const int32_t* assign,
+                                           const float* centroid_dis, float* distances,
+                                           idx_t* labels, hipStream_t stream) const = 0;
+    void quantize_device(idx_t n, const float* x, int ldx, int nprobe, float* coarse_dis,
+                         int32_t* assign, const SearchParameters* qparams,
+                         hipStream_t stream) const;
+    void reset() override;
+    void sync_device() const override;
+
+    virtual void train_encoder(idx_t n, const float* x, const idx_t* assign) {}
+    // encode n vectors assigned to lists (host in/out); codes [n][code_size]
+    virtual void encode_vectors(idx_t n, const float* x, const idx_t* list_nos,
+                                uint8_t* codes) const = 0;
+    size_t get_list_size(size_t l) const { return invlists->list_size(l); }
+    int device_code_stride() const;  // bytes per arena row
+
+   protected:
+    virtual void upload_extra() const {}
+    mutable bool dirty_ = true;
+    mutable std::recursive_mutex mu_;
+    // arena
+    mutable DeviceBuffer d_codes_, d_ids_, d_list_off_, d_list_len_, d_row_list_;
+    mutable size_t arena_rows_ = 0;
+    // scratch
+    mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_counts_, s_boff_, s_ioff_, s_cur_, s_ent_,
+            s_pk1_, s_pk2_, s_q_;
+    mutable DeviceBuffer s_as_, s_ad_;
+};
+
+struct IndexIVFFlat : IndexIVF {
+    IndexIVFFlat(Index* quantizer, size_t d, size_t nlist, MetricType metric = METRIC_L2);
+    void encode_vectors(idx_t n, const float* x, const idx_t* list_nos,
+                        uint8_t* codes) const override;
+    void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
+                                   const int32_t* assign, const float* centroid_dis,
+                                   float* distances, idx_t* labels,
+                                   hipStream_t stream) const override;
+    void reconstruct(idx_t key, float* recons) const override;
+};
+
+// faiss/impl/ProductQuantizer.h:29-186
+struct ProductQuantizer {
+    size_t d = 0, M = 0, nbits = 8, dsub = 0, ksub = 256;
+    std::vector<float> centroids;  // [M][ksub][dsub]
+    ProductQuantizer() = default;
+    ProductQuantizer(size_t d, size_t M, size_t nbits);
+    void set_derived_values();
+};
+
+struct IndexIVFPQ : IndexIVF {
+    ProductQuantizer pq;
+    int use_precomputed_table = 0;  // faiss semantics: 0 / 1 (decided at train/read)
+    int polysemous_ht = 0;
+    IndexIVFPQ(Index* quantizer, size_t d, size_t nlist, size_t M, size_t nbits,
+               MetricType metric = METRIC_L2);
+    void train_encoder(idx_t n, const float* x, const idx_t* assign) override;
+    void encode_vectors(idx_t n, const float* x, const idx_t* list_nos,
+                        uint8_t* codes) const override;
+    void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
+                                   const int32_t* assign, const float* centroid_dis,
+                                   float* distances, idx_t* labels,
+                                   hipStream_t stream) const override;
+    // faiss/IndexIVFPQ.cpp:364-459: choose 0/1 like the reference (the GPU
+    // path uses per-code terms either way)
+    void precompute_table();
+
+   protected:
+    void upload_extra() const override;
+    mutable DeviceBuffer d_pq_, d_terms_, d_cent_;
+};
+
+// ---------------------------------------------------------------- shards
+// faiss/IndexShardsIVF.h:19-40 — shards sharing one coarse quantizer.
+struct IndexShardsIVF : Index {
+    Index* quantizer = nullptr;
+    size_t nlist = 0;
+    bool threaded = false, successive_ids = true;
+    std::vector<IndexIVF*> shards;
+    IndexShardsIVF(Index* quantizer, size_t nlist, bool threaded = false,
+                   bool successive_ids = true);
+    void add_shard(IndexIVF* idx);
+    void add(idx_t n, const float* x) override;
+    void add_with_ids(idx_t n, const float* x, const idx_t* xids) override;
+    void train(idx_t n, const float* x) override;
+    void search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                       idx_t* labels, const SearchParameters* params,
+                       hipStream_t stream) const override;
+    void reset() override;
+    size_t nprobe = 1;
+
+   private:
+    mutable std::recursive_mutex mu_;
+    mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_all_d_, s_all_i_;
+};
+
+// ---------------------------------------------------------------- misc
+// GPU k-means (faiss/Clustering.h:23-59 defaults); assignment on the GPU
+// (fp32 MFMA distance tiles + top-1), centroid update in double on the host.
+void kmeans_train(int d, idx_t n, const float* x, int k, int niter, int64_t seed,
+                  float* centroids, int device, bool verbose);
+
+// faiss/utils/Heap.cpp:159-230 (host form)
+void merge_knn_results(size_t n, size_t k, int nshard, const float* all_distances,
+                       const idx_t* all_labels, float* distances, idx_t* labels,
+                       MetricType metric);
+
+// faiss/index_io.h
+void write_index(const Index* idx, const char* fname);
+void write_index(const Index* idx, FILE* f);
+Index* read_index(const char* fname, int io_flags = 0);
+Index* read_index(FILE* f, int io_flags = 0);
+
+// faiss/index_factory.h (subset: Flat, IVFn[_HNSWm],Flat|PQm[xb][np], HNSWm)
+Index* index_factory(int d, const char* description, MetricType metric = METRIC_L2);
+
+// float_rand (faiss/utils/random.cpp:95-112), bit-exact restatement
+void float_rand(float* x, size_t n, int64_t seed);
+
+}  // namespace faiss_amd

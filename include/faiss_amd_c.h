@@ -1,0 +1,365 @@
+/*
+ * faiss_amd_c.h — C-ABI of the MI355X-native batched IVF search path.
+ *
+ * This is the drop-in boundary.  Every `faiss_*` entry point below carries the
+ * exact name, argument meaning, ownership rule and return-code convention of
+ * the reference's C API (Quaternijkon/hnsw-ivf = Faiss 1.10.0, `c_api/`), so a
+ * program linked against the reference `libfaiss_c` relinks against
+ * `libfaiss_amd.so` unchanged.  Each declaration cites the
+ * reference declaration it replaces.
+ *
+ * Return codes (reference c_api/error_c.h:19-32, c_api/macros_impl.h:22-56):
+ *    0 OK, -1 unknown exception, -2 FaissException, -4 std::exception.
+ * The message of the last failure on the calling thread is available from
+ * faiss_get_last_error() (reference c_api/error_impl.cpp:15-26).
+ *
+ * All host-side pointers (x, distances, labels) are owned by the caller.
+ * `faiss_amd_*` entry points are extensions with no reference counterpart:
+ * they take DEVICE pointers (already resident in HBM) and an optional
+ * hipStream_t (passed as void*; NULL = the index's own stream) so that
+ * benchmarks and multi-GPU drivers can keep data in HBM.
+ */
+#ifndef FAISS_AMD_C_H
+#define FAISS_AMD_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int64_t faiss_idx_t; /* reference c_api/faiss_c.h:17 */
+typedef faiss_idx_t idx_t;   /* reference c_api/faiss_c.h:18 */
+
+/* reference c_api/Index_c.h:27-40 */
+typedef enum FaissMetricType {
+    METRIC_INNER_PRODUCT = 0,
+    METRIC_L2 = 1,
+} FaissMetricType;
+
+/* reference c_api/error_c.h:19-32 */
+typedef enum FaissErrorCode {
+    OK = 0,
+    UNKNOWN_EXCEPT = -1,
+    FAISS_EXCEPT = -2,
+    STD_EXCEPT = -4
+} FaissErrorCode;
+
+/* Opaque handles.  As in the reference, every index handle is usable as a
+ * FaissIndex* (reference c_api/faiss_c.h:28-40, FAISS_DECLARE_CLASS). */
+typedef struct FaissIndex_H FaissIndex;
+typedef struct FaissIndex_H FaissIndexFlat;
+typedef struct FaissIndex_H FaissIndexFlatL2;
+typedef struct FaissIndex_H FaissIndexIVF;
+typedef struct FaissIndex_H FaissIndexIVFFlat;
+typedef struct FaissIndex_H FaissIndexIVFPQ;
+typedef struct FaissIndex_H FaissIndexHNSW;
+typedef struct FaissIndex_H FaissIndexShardsIVF;
+typedef struct FaissSearchParameters_H FaissSearchParameters;
+typedef struct FaissSearchParameters_H FaissSearchParametersIVF;
+typedef struct FaissParameterSpace_H FaissParameterSpace;
+
+/* ---------------- errors ---------------- */
+/* reference c_api/error_c.h:35 */
+const char* faiss_get_last_error(void);
+
+/* ---------------- Index (reference c_api/Index_c.h) ---------------- */
+void faiss_Index_free(FaissIndex* obj);                     /* Index_c.h:50 */
+int faiss_Index_d(const FaissIndex*);                       /* Index_c.h:53 */
+int faiss_Index_is_trained(const FaissIndex*);              /* Index_c.h:56 */
+idx_t faiss_Index_ntotal(const FaissIndex*);                /* Index_c.h:59 */
+FaissMetricType faiss_Index_metric_type(const FaissIndex*); /* Index_c.h:62 */
+int faiss_Index_verbose(const FaissIndex*);                 /* Index_c.h:64 */
+void faiss_Index_set_verbose(FaissIndex*, int);             /* Index_c.h:64 */
+
+/* Index_c.h:72 */
+int faiss_Index_train(FaissIndex* index, idx_t n, const float* x);
+/* Index_c.h:82 */
+int faiss_Index_add(FaissIndex* index, idx_t n, const float* x);
+/* Index_c.h:92-96 */
+int faiss_Index_add_with_ids(
+        FaissIndex* index,
+        idx_t n,
+        const float* x,
+        const idx_t* xids);
+/* Index_c.h:108-114 — the hot path: D/I on the host, ascending (dist,id) for
+ * L2, descending for IP, unfilled slots = (+FLT_MAX,-1) / (-FLT_MAX,-1). */
+int faiss_Index_search(
+        const FaissIndex* index,
+        idx_t n,
+        const float* x,
+        idx_t k,
+        float* distances,
+        idx_t* labels);
+/* Index_c.h:128-135 (params may be a FaissSearchParametersIVF) */
+int faiss_Index_search_with_params(
+        const FaissIndex* index,
+        idx_t n,
+        const float* x,
+        idx_t k,
+        const FaissSearchParameters* params,
+        float* distances,
+        idx_t* labels);
+/* Index_c.h:172 */
+int faiss_Index_reset(FaissIndex* index);
+
+/* ---------------- SearchParametersIVF (c_api/IndexIVF_c.h:22-35) -------- */
+int faiss_SearchParametersIVF_new(FaissSearchParametersIVF** p_sp);
+int faiss_SearchParametersIVF_new_with(
+        FaissSearchParametersIVF** p_sp,
+        void* sel, /* FaissIDSelector*: must be NULL (selectors not supported) */
+        size_t nprobe,
+        size_t max_codes);
+void faiss_SearchParametersIVF_free(FaissSearchParametersIVF* obj);
+size_t faiss_SearchParametersIVF_nprobe(const FaissSearchParametersIVF*);
+void faiss_SearchParametersIVF_set_nprobe(FaissSearchParametersIVF*, size_t);
+/* extension: efSearch of an HNSW coarse quantizer for this call, 0 = keep
+ * (reference SearchParametersIVF::quantizer_params -> SearchParametersHNSW,
+ * faiss/IndexIVF.h:77-85, faiss/impl/HNSW.h:46-52) */
+void faiss_amd_SearchParametersIVF_set_quantizer_efSearch(
+        FaissSearchParametersIVF*,
+        int);
+
+/* ---------------- IndexFlat (c_api/IndexFlat_c.h) ---------------- */
+/* IndexFlat_c.h:28-31 */
+int faiss_IndexFlat_new_with(FaissIndexFlat** p_index, idx_t d, FaissMetricType metric);
+/* IndexFlat_c.h:87 */
+int faiss_IndexFlatL2_new_with(FaissIndexFlatL2** p_index, idx_t d);
+/* IndexFlat_c.h:77 */
+int faiss_IndexFlatIP_new_with(FaissIndexFlat** p_index, idx_t d);
+/* IndexFlat_c.h:40: pointer to the host mirror of xb (d*ntotal floats) */
+void faiss_IndexFlat_xb(FaissIndexFlat* index, float** p_xb, size_t* p_size);
+
+/* ---------------- IndexIVF (c_api/IndexIVF_c.h) ---------------- */
+size_t faiss_IndexIVF_nlist(const FaissIndexIVF*);              /* :59 */
+size_t faiss_IndexIVF_nprobe(const FaissIndexIVF*);             /* :61 */
+void faiss_IndexIVF_set_nprobe(FaissIndexIVF*, size_t);         /* :61 */
+FaissIndex* faiss_IndexIVF_quantizer(const FaissIndexIVF*);     /* :63 */
+int faiss_IndexIVF_own_fields(const FaissIndexIVF*);            /* :72 */
+void faiss_IndexIVF_set_own_fields(FaissIndexIVF*, int);        /* :72 */
+/* IndexIVF_c.h:112-121: assign/centroid_dis are [n*nprobe] host arrays */
+int faiss_IndexIVF_search_preassigned(
+        const FaissIndexIVF* index,
+        idx_t n,
+        const float* x,
+        idx_t k,
+        const idx_t* assign,
+        const float* centroid_dis,
+        float* distances,
+        idx_t* labels,
+        int store_pairs);
+/* IndexIVF_c.h:123 */
+size_t faiss_IndexIVF_get_list_size(const FaissIndexIVF* index, size_t list_no);
+/* IndexIVF_c.h:151-155 */
+void faiss_IndexIVF_invlists_get_ids(
+        const FaissIndexIVF* index,
+        size_t list_no,
+        idx_t* invlist);
+/* extension: copy the list's codes (list_size * code_size bytes) */
+void faiss_amd_IndexIVF_invlists_get_codes(
+        const FaissIndexIVF* index,
+        size_t list_no,
+        uint8_t* codes);
+/* extension: code size in bytes of one stored vector */
+size_t faiss_amd_IndexIVF_code_size(const FaissIndexIVF* index);
+
+/* reference IndexIVF_c.h:162-178 (global stats, like indexIVF_stats) */
+typedef struct FaissIndexIVFStats {
+    size_t nq;
+    size_t nlist;
+    size_t ndis;
+    size_t nheap_updates;
+    double quantization_time;
+    double search_time;
+} FaissIndexIVFStats;
+void faiss_IndexIVFStats_reset(FaissIndexIVFStats* stats);
+FaissIndexIVFStats* faiss_get_indexIVF_stats(void);
+
+/* ---------------- IndexIVFFlat (c_api/IndexIVFFlat_c.h) ---------------- */
+/* IndexIVFFlat_c.h:47-51 */
+int faiss_IndexIVFFlat_new_with(
+        FaissIndexIVFFlat** p_index,
+        FaissIndex* quantizer,
+        size_t d,
+        size_t nlist);
+/* IndexIVFFlat_c.h:53-58 */
+int faiss_IndexIVFFlat_new_with_metric(
+        FaissIndexIVFFlat** p_index,
+        FaissIndex* quantizer,
+        size_t d,
+        size_t nlist,
+        FaissMetricType metric);
+
+/* ---------------- IndexIVFPQ (no reference C binding; mirrors the C++
+ * constructor faiss/IndexIVFPQ.h:IndexIVFPQ(quantizer,d,nlist,M,nbits)) --- */
+int faiss_amd_IndexIVFPQ_new_with(
+        FaissIndexIVFPQ** p_index,
+        FaissIndex* quantizer,
+        size_t d,
+        size_t nlist,
+        size_t M,
+        size_t nbits,
+        FaissMetricType metric);
+/* pointer to the PQ centroids [M][ksub][dsub] (host) */
+void faiss_amd_IndexIVFPQ_pq_centroids(
+        FaissIndexIVFPQ* index,
+        float** p_centroids,
+        size_t* p_size);
+/* M, nbits, by_residual, use_precomputed_table */
+int faiss_amd_IndexIVFPQ_info(
+        const FaissIndexIVFPQ* index,
+        size_t* M,
+        size_t* nbits,
+        int* by_residual,
+        int* use_precomputed_table);
+
+/* ---------------- IndexHNSWFlat (C++ faiss/IndexHNSW.h:IndexHNSWFlat) ---- */
+int faiss_amd_IndexHNSWFlat_new_with(
+        FaissIndexHNSW** p_index,
+        int d,
+        int M,
+        FaissMetricType metric);
+int faiss_amd_IndexHNSW_efSearch(const FaissIndexHNSW*);
+void faiss_amd_IndexHNSW_set_efSearch(FaissIndexHNSW*, int);
+int faiss_amd_IndexHNSW_efConstruction(const FaissIndexHNSW*);
+void faiss_amd_IndexHNSW_set_efConstruction(FaissIndexHNSW*, int);
+/* the flat storage index of an IndexHNSW (owned by it) */
+FaissIndex* faiss_amd_IndexHNSW_storage(const FaissIndexHNSW* index);
+/* graph export for tests: levels[ntotal], offsets[ntotal+1], neighbors[],
+ * cum_nneighbor_per_level[]; pass NULL to query sizes only */
+int faiss_amd_IndexHNSW_graph(
+        const FaissIndexHNSW* index,
+        int* entry_point,
+        int* max_level,
+        size_t* n_neighbors,
+        size_t* n_cum,
+        const int32_t** levels,
+        const size_t** offsets,
+        const int32_t** neighbors,
+        const int32_t** cum_nneighbor_per_level);
+
+/* ---------------- IndexShardsIVF (faiss/IndexShardsIVF.h:19-40) -------- */
+/* A set of IVF shards sharing one coarse quantizer; search = one coarse pass
+ * then search_preassigned on every shard then merge_knn_results. */
+int faiss_amd_IndexShardsIVF_new(
+        FaissIndexShardsIVF** p_index,
+        FaissIndex* quantizer,
+        size_t nlist,
+        int threaded,
+        int successive_ids);
+int faiss_amd_IndexShardsIVF_add_shard(FaissIndexShardsIVF* index, FaissIndex* shard);
+int faiss_amd_IndexShardsIVF_count(const FaissIndexShardsIVF* index);
+
+/* ---------------- I/O (c_api/index_io_c.h) ---------------- */
+int faiss_write_index(const FaissIndex* idx, FILE* f);                   /* :28 */
+int faiss_write_index_fname(const FaissIndex* idx, const char* fname);   /* :33 */
+int faiss_read_index(FILE* f, int io_flags, FaissIndex** p_out);         /* :41 */
+int faiss_read_index_fname(const char* fname, int io_flags, FaissIndex** p_out); /* :46 */
+
+/* ---------------- factory / tuning ---------------- */
+/* c_api/index_factory_c.h:24-28; supports "Flat", "IVF<n>,Flat",
+ * "IVF<n>,PQ<M>[x<nbits>][np]", "IVF<n>_HNSW<M>,Flat|PQ..", "HNSW<M>[,Flat]" */
+int faiss_index_factory(
+        FaissIndex** p_index,
+        int d,
+        const char* description,
+        FaissMetricType metric);
+/* c_api/AutoTune_c.h:36,63 — "nprobe", "efSearch", "quantizer_efSearch" */
+int faiss_ParameterSpace_new(FaissParameterSpace** space);
+void faiss_ParameterSpace_free(FaissParameterSpace* space);
+int faiss_ParameterSpace_set_index_parameter(
+        const FaissParameterSpace*,
+        FaissIndex*,
+        const char*,
+        double);
+
+/* ---------------- merge (faiss/utils/Heap.cpp:159-230) ---------------- */
+/* merge nshard sorted result tables [nshard][n][k] into [n][k] (L2: keep
+ * smallest; IP: keep largest; ties -> lower shard index). Host pointers. */
+int faiss_amd_merge_knn_results(
+        size_t n,
+        size_t k,
+        int nshard,
+        const float* all_distances,
+        const idx_t* all_labels,
+        float* distances,
+        idx_t* labels,
+        FaissMetricType metric);
+
+/* extension: dynamic type of a handle ("IndexFlat", "IndexIVFFlat",
+ * "IndexIVFPQ", "IndexHNSWFlat", "IndexShardsIVF", "Index") */
+const char* faiss_amd_Index_type(const FaissIndex* index);
+
+/* ---------------- device-resident extensions (no reference counterpart) */
+/* number of visible HIP devices (fails loudly: -4 when the HIP runtime
+ * cannot be initialised) */
+int faiss_amd_device_count(int* count);
+/* select the device an index is created on (default 0) for this thread */
+int faiss_amd_set_device(int device);
+/* ensure all host-side index data is uploaded to HBM */
+int faiss_amd_Index_sync_device(FaissIndex* index);
+/* search with x / distances / labels in HBM (device pointers) on `stream` */
+int faiss_amd_Index_search_device(
+        const FaissIndex* index,
+        idx_t n,
+        const float* x_dev,
+        idx_t k,
+        float* distances_dev,
+        idx_t* labels_dev,
+        void* stream);
+/* search_preassigned with device pointers; assign_dev is int32 [n*nprobe]
+ * (list numbers, -1 = skip), centroid_dis_dev f32 [n*nprobe] */
+int faiss_amd_IndexIVF_search_preassigned_device(
+        const FaissIndexIVF* index,
+        idx_t n,
+        const float* x_dev,
+        idx_t k,
+        int nprobe,
+        const int32_t* assign_dev,
+        const float* centroid_dis_dev,
+        float* distances_dev,
+        idx_t* labels_dev,
+        void* stream);
+/* coarse quantization only (device): top-nprobe lists per query */
+int faiss_amd_IndexIVF_quantize_device(
+        const FaissIndexIVF* index,
+        idx_t n,
+        const float* x_dev,
+        int nprobe,
+        float* coarse_dis_dev,
+        int32_t* assign_dev,
+        void* stream);
+/* device-side merge of nshard result tables (same semantics as
+ * faiss_amd_merge_knn_results) */
+int faiss_amd_merge_knn_results_device(
+        size_t n,
+        size_t k,
+        int nshard,
+        const float* all_distances_dev,
+        const idx_t* all_labels_dev,
+        float* distances_dev,
+        idx_t* labels_dev,
+        FaissMetricType metric,
+        void* stream);
+/* timing of the dominant kernel in the last search on this index: number of
+ * launches and summed milliseconds (HIP events, only when enabled) */
+int faiss_amd_set_kernel_timing(int enable);
+int faiss_amd_last_kernel_times(
+        const FaissIndex* index,
+        int* n_kernels,
+        char* names,      /* n_kernels * 32 chars */
+        double* millis,   /* n_kernels */
+        double* units);   /* n_kernels: work units (bytes or flops) */
+
+int faiss_amd_reset_kernel_times(FaissIndex* index);
+/* faiss::float_rand (faiss/utils/random.cpp:95-112), bit-exact restatement:
+ * the synthetic inputs of the benchmark are regenerated on the GPU box */
+int faiss_amd_float_rand(float* x, size_t n, int64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FAISS_AMD_C_H */

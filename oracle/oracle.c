@@ -1,0 +1,658 @@
+/*
+ * oracle.c — CPU restatement of the reference IVF search path.
+ *
+ * TEST INFRASTRUCTURE ONLY: the parity checker and the timed CPU baseline.
+ * Never linked into the product library.  See oracle.h for the reference
+ * file:line each function follows and for the fixed fp32 evaluation order.
+ */
+#include "oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+int oracle_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+/* ------------------------------------------------------------ mt19937 */
+/* std::mt19937 (the generator behind faiss::RandomGenerator) */
+typedef struct {
+    uint32_t mt[624];
+    int idx;
+} mt19937_t;
+
+static void mt_seed(mt19937_t* s, uint32_t seed) {
+    s->mt[0] = seed;
+    for (int i = 1; i < 624; i++)
+        s->mt[i] = 1812433253u * (s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) + (uint32_t)i;
+    s->idx = 624;
+}
+static uint32_t mt_next(mt19937_t* s) {
+    if (s->idx >= 624) {
+        for (int i = 0; i < 624; i++) {
+            uint32_t y = (s->mt[i] & 0x80000000u) | (s->mt[(i + 1) % 624] & 0x7fffffffu);
+            s->mt[i] = s->mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        s->idx = 0;
+    }
+    uint32_t y = s->mt[s->idx++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+/* faiss/utils/random.cpp:95-112: 1024 independent streams (n >= 1024) */
+void oracle_float_rand(float* x, size_t n, int64_t seed) {
+    const size_t nblock = n < 1024 ? 1 : 1024;
+    mt19937_t r0;
+    mt_seed(&r0, (uint32_t)seed);
+    int a0 = (int)(mt_next(&r0) & 0x7fffffff);
+    int b0 = (int)(mt_next(&r0) & 0x7fffffff);
+    const float mx = (float)4294967295u;
+#pragma omp parallel for if (n > 1000000)
+    for (int64_t j = 0; j < (int64_t)nblock; j++) {
+        mt19937_t r;
+        mt_seed(&r, (uint32_t)(int64_t)(a0 + j * (int64_t)b0));
+        size_t i0 = j * n / nblock, i1 = (j + 1) * n / nblock;
+        for (size_t i = i0; i < i1; i++) x[i] = (float)mt_next(&r) / mx;
+    }
+}
+
+/* ------------------------------------------------------------ distances */
+float oracle_fvec_L2sqr(const float* x, const float* y, size_t d) {
+    float acc = 0.f;
+    for (size_t j = 0; j < d; j++) {
+        float t = x[j] - y[j];
+        acc = fmaf(t, t, acc);
+    }
+    return acc;
+}
+float oracle_fvec_inner_product(const float* x, const float* y, size_t d) {
+    float acc = 0.f;
+    for (size_t j = 0; j < d; j++) acc = fmaf(x[j], y[j], acc);
+    return acc;
+}
+float oracle_fvec_norm_L2sqr(const float* x, size_t d) {
+    float acc = 0.f;
+    for (size_t j = 0; j < d; j++) acc = fmaf(x[j], x[j], acc);
+    return acc;
+}
+
+/* ------------------------------------------------------------ heaps */
+/* faiss/utils/ordered_key_value.h: CMax (cmax=1) / CMin (cmax=0) */
+static inline int cmp_(int cmax, float a, float b) { return cmax ? a > b : a < b; }
+static inline int cmp2_(int cmax, float a1, float b1, int64_t a2, int64_t b2) {
+    return cmax ? (a1 > b1 || (a1 == b1 && a2 > b2)) : (a1 < b1 || (a1 == b1 && a2 < b2));
+}
+static inline float neutral_(int cmax) { return cmax ? FLT_MAX : -FLT_MAX; }
+
+/* faiss/utils/Heap.h:47-79 */
+static void heap_pop_(int cmax, size_t k, float* bv, int64_t* bi) {
+    bv--;
+    bi--;
+    float val = bv[k];
+    int64_t id = bi[k];
+    size_t i = 1, i1, i2;
+    for (;;) {
+        i1 = i << 1;
+        i2 = i1 + 1;
+        if (i1 > k) break;
+        if ((i2 == k + 1) || cmp2_(cmax, bv[i1], bv[i2], bi[i1], bi[i2])) {
+            if (cmp2_(cmax, val, bv[i1], id, bi[i1])) break;
+            bv[i] = bv[i1];
+            bi[i] = bi[i1];
+            i = i1;
+        } else {
+            if (cmp2_(cmax, val, bv[i2], id, bi[i2])) break;
+            bv[i] = bv[i2];
+            bi[i] = bi[i2];
+            i = i2;
+        }
+    }
+    bv[i] = bv[k];
+    bi[i] = bi[k];
+}
+/* Heap.h:84-105 */
+static void heap_push_(int cmax, size_t k, float* bv, int64_t* bi, float val, int64_t id) {
+    bv--;
+    bi--;
+    size_t i = k, f;
+    while (i > 1) {
+        f = i >> 1;
+        if (!cmp2_(cmax, val, bv[f], id, bi[f])) break;
+        bv[i] = bv[f];
+        bi[i] = bi[f];
+        i = f;
+    }
+    bv[i] = val;
+    bi[i] = id;
+}
+/* Heap.h:112-149 */
+void oracle_heap_replace_top(int cmax, size_t k, float* bv, int64_t* bi, float val, int64_t id) {
+    bv--;
+    bi--;
+    size_t i = 1, i1, i2;
+    for (;;) {
+        i1 = i << 1;
+        i2 = i1 + 1;
+        if (i1 > k) break;
+        if ((i2 == k + 1) || cmp2_(cmax, bv[i1], bv[i2], bi[i1], bi[i2])) {
+            if (cmp2_(cmax, val, bv[i1], id, bi[i1])) break;
+            bv[i] = bv[i1];
+            bi[i] = bi[i1];
+            i = i1;
+        } else {
+            if (cmp2_(cmax, val, bv[i2], id, bi[i2])) break;
+            bv[i] = bv[i2];
+            bi[i] = bi[i2];
+            i = i2;
+        }
+    }
+    bv[i] = val;
+    bi[i] = id;
+}
+/* Heap.h:316-339 (k0 = 0) */
+void oracle_heap_heapify(int cmax, size_t k, float* bv, int64_t* bi) {
+    for (size_t i = 0; i < k; i++) {
+        bv[i] = neutral_(cmax);
+        bi[i] = -1;
+    }
+}
+/* Heap.h:366-390 */
+void oracle_heap_addn(int cmax, size_t k, float* bv, int64_t* bi, const float* x,
+                      const int64_t* xids, size_t n) {
+    for (size_t i = 0; i < n; i++)
+        if (cmp_(cmax, bv[0], x[i]))
+            oracle_heap_replace_top(cmax, k, bv, bi, x[i], xids ? xids[i] : (int64_t)i);
+}
+/* Heap.h:421-450 */
+size_t oracle_heap_reorder(int cmax, size_t k, float* bv, int64_t* bi) {
+    size_t i, ii;
+    for (i = 0, ii = 0; i < k; i++) {
+        float val = bv[0];
+        int64_t id = bi[0];
+        heap_pop_(cmax, k - i, bv, bi);
+        bv[k - ii - 1] = val;
+        bi[k - ii - 1] = id;
+        if (id != -1) ii++;
+    }
+    size_t nel = ii;
+    memmove(bv, bv + k - ii, ii * sizeof(*bv));
+    memmove(bi, bi + k - ii, ii * sizeof(*bi));
+    for (; ii < k; ii++) {
+        bv[ii] = neutral_(cmax);
+        bi[ii] = -1;
+    }
+    return nel;
+}
+
+/* ------------------------------------------------------------ kNN */
+/* faiss/utils/distances.cpp:170-199 / 259-342 with HeapBlockResultHandler */
+void oracle_knn(const float* x, const float* y, size_t d, size_t nx, size_t ny, size_t k,
+                int metric, int blas_form, float* D, int64_t* I, int nthreads) {
+    const int cmax = metric == 1;
+    float* yn = NULL;
+    if (metric == 1 && blas_form) {
+        yn = (float*)malloc(sizeof(float) * (ny ? ny : 1));
+        for (size_t j = 0; j < ny; j++) yn[j] = oracle_fvec_norm_L2sqr(y + j * d, d);
+    }
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 16)
+    for (int64_t i = 0; i < (int64_t)nx; i++) {
+        const float* xi = x + i * d;
+        float* hv = D + i * k;
+        int64_t* hi = I + i * k;
+        oracle_heap_heapify(cmax, k, hv, hi);
+        float xn = (metric == 1 && blas_form) ? oracle_fvec_norm_L2sqr(xi, d) : 0.f;
+        float thr = hv[0];
+        for (size_t j = 0; j < ny; j++) {
+            const float* yj = y + j * d;
+            float dis;
+            if (metric == 1) {
+                if (blas_form) {
+                    float ip = oracle_fvec_inner_product(xi, yj, d);
+                    dis = fmaf(-2.f, ip, xn + yn[j]);
+                    if (dis < 0) dis = 0;
+                } else {
+                    dis = oracle_fvec_L2sqr(xi, yj, d);
+                }
+            } else {
+                dis = oracle_fvec_inner_product(xi, yj, d);
+            }
+            if (cmp_(cmax, thr, dis)) {
+                oracle_heap_replace_top(cmax, k, hv, hi, dis, (int64_t)j);
+                thr = hv[0];
+            }
+        }
+        oracle_heap_reorder(cmax, k, hv, hi);
+    }
+    free(yn);
+}
+
+/* ------------------------------------------------------------ HNSW */
+/* MinimaxHeap on CMax<float, int32> (faiss/impl/HNSW.cpp:1096-1342) */
+typedef struct {
+    int n, k, nvalid;
+    int32_t* ids;
+    float* dis;
+} mmheap_t;
+
+static inline int cmp2i_(float a1, float b1, int32_t a2, int32_t b2) {
+    return a1 > b1 || (a1 == b1 && a2 > b2);
+}
+static void hpop_i(size_t k, float* bv, int32_t* bi) {
+    bv--;
+    bi--;
+    float val = bv[k];
+    int32_t id = bi[k];
+    size_t i = 1, i1, i2;
+    for (;;) {
+        i1 = i << 1;
+        i2 = i1 + 1;
+        if (i1 > k) break;
+        if ((i2 == k + 1) || cmp2i_(bv[i1], bv[i2], bi[i1], bi[i2])) {
+            if (cmp2i_(val, bv[i1], id, bi[i1])) break;
+            bv[i] = bv[i1];
+            bi[i] = bi[i1];
+            i = i1;
+        } else {
+            if (cmp2i_(val, bv[i2], id, bi[i2])) break;
+            bv[i] = bv[i2];
+            bi[i] = bi[i2];
+            i = i2;
+        }
+    }
+    bv[i] = bv[k];
+    bi[i] = bi[k];
+}
+static void hpush_i(size_t k, float* bv, int32_t* bi, float val, int32_t id) {
+    bv--;
+    bi--;
+    size_t i = k, f;
+    while (i > 1) {
+        f = i >> 1;
+        if (!cmp2i_(val, bv[f], id, bi[f])) break;
+        bv[i] = bv[f];
+        bi[i] = bi[f];
+        i = f;
+    }
+    bv[i] = val;
+    bi[i] = id;
+}
+static void mm_push(mmheap_t* h, int32_t i, float v) {
+    if (h->k == h->n) {
+        if (v >= h->dis[0]) return;
+        if (h->ids[0] != -1) --h->nvalid;
+        hpop_i(h->k--, h->dis, h->ids);
+    }
+    hpush_i(++h->k, h->dis, h->ids, v, i);
+    ++h->nvalid;
+}
+static int32_t mm_pop_min(mmheap_t* h, float* vmin_out) {
+    int i = h->k - 1;
+    while (i >= 0) {
+        if (h->ids[i] != -1) break;
+        i--;
+    }
+    if (i == -1) return -1;
+    int imin = i;
+    float vmin = h->dis[i];
+    i--;
+    while (i >= 0) {
+        if (h->ids[i] != -1 && h->dis[i] < vmin) {
+            vmin = h->dis[i];
+            imin = i;
+        }
+        i--;
+    }
+    if (vmin_out) *vmin_out = vmin;
+    int32_t ret = h->ids[imin];
+    h->ids[imin] = -1;
+    --h->nvalid;
+    return ret;
+}
+static int mm_count_below(const mmheap_t* h, float thresh) {
+    int n = 0;
+    for (int i = 0; i < h->k; i++)
+        if (h->dis[i] < thresh) n++;
+    return n;
+}
+
+static void hnsw_range(const oracle_hnsw_t* g, int64_t no, int level, size_t* b, size_t* e) {
+    size_t o = g->offsets[no];
+    *b = o + g->cum_nneighbor_per_level[level];
+    *e = o + g->cum_nneighbor_per_level[level + 1];
+}
+
+/* one query: HNSW::search with a HeapBlockResultHandler<CMax> of size k */
+static void hnsw_search_one(const oracle_hnsw_t* g, const float* q, size_t k, int efSearch,
+                            float* hv, int64_t* hi, uint8_t* visited) {
+    oracle_heap_heapify(1, k, hv, hi);
+    if (g->entry_point != -1) {
+        const int d = g->d;
+        int32_t nearest = g->entry_point;
+        float d_nearest = oracle_fvec_L2sqr(q, g->storage + (size_t)nearest * d, d);
+        /* greedy_update_nearest (HNSW.cpp:852-924) */
+        for (int level = g->max_level; level >= 1; level--) {
+            for (;;) {
+                int32_t prev = nearest;
+                size_t b, e;
+                hnsw_range(g, nearest, level, &b, &e);
+                for (size_t j = b; j < e; j++) {
+                    int32_t v = g->neighbors[j];
+                    if (v < 0) break;
+                    float dv = oracle_fvec_L2sqr(q, g->storage + (size_t)v * d, d);
+                    if (dv < d_nearest) {
+                        nearest = v;
+                        d_nearest = dv;
+                    }
+                }
+                if (nearest == prev) break;
+            }
+        }
+        int ef = efSearch > (int)k ? efSearch : (int)k;
+        mmheap_t h;
+        h.n = ef;
+        h.k = 0;
+        h.nvalid = 0;
+        h.ids = (int32_t*)malloc(sizeof(int32_t) * ef);
+        h.dis = (float*)malloc(sizeof(float) * ef);
+        mm_push(&h, nearest, d_nearest);
+        /* search_from_candidates (HNSW.cpp:605-741) */
+        float threshold = hv[0];
+        for (int i = 0; i < h.nvalid; i++) {
+            int32_t v1 = h.ids[i];
+            float dd = h.dis[i];
+            if (dd < threshold) {
+                if (cmp_(1, hv[0], dd)) {
+                    oracle_heap_replace_top(1, k, hv, hi, dd, v1);
+                    threshold = hv[0];
+                }
+            }
+            visited[v1] = 1;
+        }
+        int32_t* buf = (int32_t*)malloc(sizeof(int32_t) * 1024);
+        while (h.nvalid > 0) {
+            float d0 = 0;
+            int32_t v0 = mm_pop_min(&h, &d0);
+            if (mm_count_below(&h, d0) >= efSearch) break;
+            size_t b, e;
+            hnsw_range(g, v0, 0, &b, &e);
+            size_t jmax = b;
+            for (size_t j = b; j < e; j++) {
+                if (g->neighbors[j] < 0) break;
+                jmax++;
+            }
+            threshold = hv[0];
+            int nb = 0;
+            for (size_t j = b; j < jmax; j++) {
+                int32_t v1 = g->neighbors[j];
+                int vget = visited[v1];
+                visited[v1] = 1;
+                if (!vget) buf[nb++] = v1;
+            }
+            for (int t = 0; t < nb; t++) {
+                int32_t v1 = buf[t];
+                float dis = oracle_fvec_L2sqr(q, g->storage + (size_t)v1 * d, d);
+                if (dis < threshold) {
+                    if (cmp_(1, hv[0], dis)) {
+                        oracle_heap_replace_top(1, k, hv, hi, dis, v1);
+                        threshold = hv[0];
+                    }
+                }
+                mm_push(&h, v1, dis);
+            }
+        }
+        free(buf);
+        free(h.ids);
+        free(h.dis);
+    }
+    oracle_heap_reorder(1, k, hv, hi);
+}
+
+void oracle_hnsw_search(const oracle_hnsw_t* g, const float* x, size_t n, size_t k,
+                        int efSearch, float* D, int64_t* I, int nthreads) {
+#pragma omp parallel num_threads(nthreads)
+    {
+        uint8_t* visited = (uint8_t*)calloc(g->ntotal > 0 ? g->ntotal : 1, 1);
+#pragma omp for schedule(dynamic, 4)
+        for (int64_t i = 0; i < (int64_t)n; i++) {
+            memset(visited, 0, g->ntotal > 0 ? g->ntotal : 1);
+            hnsw_search_one(g, x + i * g->d, k, efSearch, D + i * k, I + i * k, visited);
+        }
+        free(visited);
+    }
+}
+
+/* ------------------------------------------------------------ IVF-PQ */
+void oracle_ivfpq_prepare(oracle_ivf_t* ivf) {
+    /* faiss/IndexIVFPQ.cpp:380-406 decision, :408-432 table 1 */
+    const int M = ivf->pq_M, ksub = 1 << ivf->pq_nbits, d = ivf->d, dsub = d / M;
+    ivf->use_precomputed_table = 0;
+    if (!(ivf->metric == 1 && ivf->by_residual)) return;
+    size_t table_size = (size_t)M * ksub * ivf->nlist * sizeof(float);
+    if (table_size > ((size_t)1 << 31)) return;
+    ivf->use_precomputed_table = 1;
+    float* rn = (float*)malloc(sizeof(float) * M * ksub);
+    for (int m = 0; m < M; m++)
+        for (int j = 0; j < ksub; j++)
+            rn[m * ksub + j] = oracle_fvec_norm_L2sqr(ivf->pq_centroids + ((size_t)m * ksub + j) * dsub,
+                                                      dsub);
+    ivf->precomputed_table = (float*)malloc(table_size);
+#pragma omp parallel for
+    for (int64_t i = 0; i < ivf->nlist; i++) {
+        const float* c = ivf->hnsw ? ivf->hnsw->storage + i * d : ivf->centroids + i * d;
+        float* tab = ivf->precomputed_table + (size_t)i * M * ksub;
+        for (int m = 0; m < M; m++)
+            for (int j = 0; j < ksub; j++) {
+                float ip = oracle_fvec_inner_product(
+                        c + m * dsub, ivf->pq_centroids + ((size_t)m * ksub + j) * dsub, dsub);
+                /* fvec_madd(n, r_norms, 2.0, tab, tab) */
+                tab[m * ksub + j] = fmaf(2.f, ip, rn[m * ksub + j]);
+            }
+    }
+    free(rn);
+}
+
+/* ------------------------------------------------------------ preassigned */
+void oracle_ivf_search_preassigned(const oracle_ivf_t* ivf, size_t n, const float* x, size_t k,
+                                   size_t nprobe, const int64_t* keys, const float* coarse_dis,
+                                   float* D, int64_t* I, int nthreads) {
+    const int cmax = ivf->metric == 1;
+    const int d = ivf->d;
+    const int M = ivf->pq_M;
+    const int ksub = M ? 1 << ivf->pq_nbits : 0;
+    const int dsub = M ? d / M : 0;
+#pragma omp parallel num_threads(nthreads)
+    {
+        float* sim2 = M ? (float*)malloc(sizeof(float) * M * ksub) : NULL;
+        float* sim = M ? (float*)malloc(sizeof(float) * M * ksub) : NULL;
+        float* resid = (float*)malloc(sizeof(float) * d);
+#pragma omp for schedule(dynamic, 8)
+        for (int64_t i = 0; i < (int64_t)n; i++) {
+            const float* xi = x + i * d;
+            float* hv = D + i * k;
+            int64_t* hi = I + i * k;
+            oracle_heap_heapify(cmax, k, hv, hi);
+            if (M) { /* init_query_L2 (IndexIVFPQ.cpp:560-566) */
+                if (!ivf->by_residual) {
+                    for (int m = 0; m < M; m++)
+                        for (int j = 0; j < ksub; j++)
+                            sim[m * ksub + j] = oracle_fvec_L2sqr(
+                                    xi + m * dsub, ivf->pq_centroids + ((size_t)m * ksub + j) * dsub,
+                                    dsub);
+                } else if (ivf->use_precomputed_table) {
+                    for (int m = 0; m < M; m++)
+                        for (int j = 0; j < ksub; j++)
+                            sim2[m * ksub + j] = oracle_fvec_inner_product(
+                                    xi + m * dsub, ivf->pq_centroids + ((size_t)m * ksub + j) * dsub,
+                                    dsub);
+                }
+            }
+            for (size_t ik = 0; ik < nprobe; ik++) {
+                int64_t key = keys[i * nprobe + ik];
+                if (key < 0 || key >= ivf->nlist) continue;
+                int64_t l0 = ivf->list_off[key], l1 = ivf->list_off[key + 1];
+                if (l1 == l0) continue;
+                if (!M) {
+                    /* IVFFlatScanner::scan_codes */
+                    for (int64_t j = l0; j < l1; j++) {
+                        const float* yj = (const float*)(ivf->codes + j * ivf->code_size);
+                        float dis = cmax ? oracle_fvec_L2sqr(xi, yj, d)
+                                         : oracle_fvec_inner_product(xi, yj, d);
+                        if (cmp_(cmax, hv[0], dis))
+                            oracle_heap_replace_top(cmax, k, hv, hi, dis, ivf->ids[j]);
+                    }
+                } else {
+                    float dis0 = 0;
+                    if (ivf->by_residual) {
+                        if (ivf->use_precomputed_table == 1) {
+                            dis0 = coarse_dis[i * nprobe + ik];
+                            const float* P = ivf->precomputed_table + (size_t)key * M * ksub;
+                            for (int e = 0; e < M * ksub; e++) sim[e] = fmaf(-2.f, sim2[e], P[e]);
+                        } else {
+                            const float* c = ivf->hnsw ? ivf->hnsw->storage + key * d
+                                                       : ivf->centroids + key * d;
+                            for (int j = 0; j < d; j++) resid[j] = xi[j] - c[j];
+                            for (int m = 0; m < M; m++)
+                                for (int j = 0; j < ksub; j++)
+                                    sim[m * ksub + j] = oracle_fvec_L2sqr(
+                                            resid + m * dsub,
+                                            ivf->pq_centroids + ((size_t)m * ksub + j) * dsub, dsub);
+                        }
+                    }
+                    for (int64_t j = l0; j < l1; j++) {
+                        const uint8_t* code = ivf->codes + j * ivf->code_size;
+                        float acc = 0.f;
+                        for (int m = 0; m < M; m++) acc += sim[m * ksub + code[m]];
+                        float dis = dis0 + acc;
+                        if (cmp_(cmax, hv[0], dis))
+                            oracle_heap_replace_top(cmax, k, hv, hi, dis, ivf->ids[j]);
+                    }
+                }
+            }
+            oracle_heap_reorder(cmax, k, hv, hi);
+        }
+        free(sim2);
+        free(sim);
+        free(resid);
+    }
+}
+
+void oracle_ivf_search(const oracle_ivf_t* ivf, size_t n, const float* x, size_t k,
+                       size_t nprobe, int efSearch, int nslices, float* D, int64_t* I,
+                       int64_t* coarse_I, float* coarse_D, int nthreads) {
+    if (nprobe > (size_t)ivf->nlist) nprobe = ivf->nlist;
+    int nt = nslices < (int)n ? nslices : (int)n;
+    if (nt < 1) nt = 1;
+    for (int s = 0; s < nt; s++) {
+        size_t i0 = n * s / nt, i1 = n * (s + 1) / nt;
+        size_t ns = i1 - i0;
+        if (!ns) continue;
+        const float* xs = x + i0 * ivf->d;
+        int64_t* ci = coarse_I + i0 * nprobe;
+        float* cd = coarse_D + i0 * nprobe;
+        if (ivf->hnsw)
+            oracle_hnsw_search(ivf->hnsw, xs, ns, nprobe, efSearch, cd, ci, nthreads);
+        else
+            oracle_knn(xs, ivf->centroids, ivf->d, ns, ivf->nlist, nprobe, ivf->metric,
+                       ns >= 20, cd, ci, nthreads);
+        oracle_ivf_search_preassigned(ivf, ns, xs, k, nprobe, ci, cd, D + i0 * k, I + i0 * k,
+                                      nthreads);
+    }
+}
+
+/* ------------------------------------------------------------ fast path */
+static inline float l2_fast(const float* x, const float* y, int d) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int j = 0;
+    for (; j + 8 <= d; j += 8)
+        for (int u = 0; u < 8; u++) {
+            float t = x[j + u] - y[j + u];
+            acc[u] += t * t;
+        }
+    float s = 0;
+    for (; j < d; j++) {
+        float t = x[j] - y[j];
+        s += t * t;
+    }
+    return ((acc[0] + acc[4]) + (acc[1] + acc[5])) + ((acc[2] + acc[6]) + (acc[3] + acc[7])) + s;
+}
+
+void oracle_ivf_search_fast(const oracle_ivf_t* ivf, size_t n, const float* x, size_t k,
+                            size_t nprobe, float* D, int64_t* I, int nthreads) {
+    int64_t* ci = (int64_t*)malloc(sizeof(int64_t) * n * nprobe);
+    float* cd = (float*)malloc(sizeof(float) * n * nprobe);
+    oracle_knn(x, ivf->centroids, ivf->d, n, ivf->nlist, nprobe, 1, 1, cd, ci, nthreads);
+    const int d = ivf->d;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 8)
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        const float* xi = x + i * d;
+        float* hv = D + i * k;
+        int64_t* hi = I + i * k;
+        oracle_heap_heapify(1, k, hv, hi);
+        for (size_t ik = 0; ik < nprobe; ik++) {
+            int64_t key = ci[i * nprobe + ik];
+            if (key < 0) continue;
+            for (int64_t j = ivf->list_off[key]; j < ivf->list_off[key + 1]; j++) {
+                float dis = l2_fast(xi, (const float*)(ivf->codes + j * ivf->code_size), d);
+                if (hv[0] > dis) oracle_heap_replace_top(1, k, hv, hi, dis, ivf->ids[j]);
+            }
+        }
+        oracle_heap_reorder(1, k, hv, hi);
+    }
+    free(ci);
+    free(cd);
+}
+
+/* ------------------------------------------------------------ merge */
+/* faiss/utils/Heap.cpp:159-230 with heap_push/heap_pop on (dist, shard):
+ * CMin<float,int> for L2, CMax<float,int> for IP. */
+void oracle_merge_knn_results(size_t n, size_t k, int nshard, const float* all_d,
+                              const int64_t* all_l, float* D, int64_t* L, int metric) {
+    const int cmax = metric != 1; /* L2 -> CMin heap */
+    const size_t stride = n * k;
+    int* pointer = (int*)malloc(sizeof(int) * nshard);
+    int64_t* shard_ids = (int64_t*)malloc(sizeof(int64_t) * nshard);
+    float* heap_vals = (float*)malloc(sizeof(float) * nshard);
+    for (size_t i = 0; i < n; i++) {
+        const float* Din = all_d + i * k;
+        const int64_t* Iin = all_l + i * k;
+        int heap_size = 0;
+        for (int s = 0; s < nshard; s++) {
+            pointer[s] = 0;
+            if (Iin[stride * s] >= 0)
+                heap_push_(cmax, ++heap_size, heap_vals, shard_ids, Din[stride * s], s);
+        }
+        float* Do = D + i * k;
+        int64_t* Io = L + i * k;
+        size_t j;
+        for (j = 0; j < k && heap_size > 0; j++) {
+            int s = (int)shard_ids[0];
+            int* p = &pointer[s];
+            Do[j] = heap_vals[0];
+            Io[j] = Iin[stride * s + *p];
+            heap_pop_(cmax, heap_size--, heap_vals, shard_ids);
+            (*p)++;
+            if ((size_t)*p < k && Iin[stride * s + *p] >= 0)
+                heap_push_(cmax, ++heap_size, heap_vals, shard_ids, Din[stride * s + *p], s);
+        }
+        for (; j < k; j++) {
+            Io[j] = -1;
+            Do[j] = metric == 1 ? FLT_MAX : -FLT_MAX;
+        }
+    }
+    free(pointer);
+    free(shard_ids);
+    free(heap_vals);
+}

@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprof summary.
+# Stops at the first fault / abort / timeout (rc not in {0,1}).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+PYTEST_ARGS=${PYTEST_ARGS:-"tests -q -m gpu -x"}
+timeout -k 10 ${T_TEST:-900} python -m pytest $PYTEST_ARGS > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log; ok $rc || exit $rc
+timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log; ok $rc || exit $rc
+timeout -k 10 ${T_BENCH:-600} python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; ok $rc || exit $rc
+if [ -n "$PROFILE" ]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --recall-queries 0 > gpurun_out/prof.log 2>&1
+  rc=$?; echo "rocprof rc=$rc"; ok $rc || exit $rc
+  find gpurun_out/prof -name "*stats*" | head
+fi
+exit 0

@@ -1,0 +1,173 @@
+"""GPU parity: IndexFlat and IndexIVFFlat (through the C-ABI) vs the oracle.
+
+The GPU path and the oracle evaluate every fp32 distance in the same order
+(sequential fma chains; coarse = fma(-2, ip, |x|^2+|y|^2) clamped), so ids AND
+distances must match bit for bit on the same index.
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_same_results, rand
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("metric", [1, 0])
+@pytest.mark.parametrize("k", [1, 10, 64])
+def test_flat_search_bit_exact(amd, orc, gpu, metric, k):
+    d, nb, nq = 48, 3000, 300
+    xb = rand(orc, nb, d, 11)
+    xq = rand(orc, nq, d, 12)
+    idx = amd.IndexFlat(d, metric)
+    idx.add(xb)
+    D, I = idx.search(xq, k)
+    Dr, Ir = orc.knn(xq, xb, k, metric=metric, blas_form=True)
+    assert_same_results(D, I, Dr, Ir)
+
+
+def test_flat_fewer_vectors_than_k(amd, orc, gpu):
+    d = 8
+    xb = rand(orc, 5, d, 1)
+    idx = amd.IndexFlatL2(d)
+    idx.add(xb)
+    D, I = idx.search(rand(orc, 3, d, 2), 10)
+    assert (I[:, 5:] == -1).all() and (D[:, 5:] == np.finfo(np.float32).max).all()
+    empty = amd.IndexFlatL2(d)
+    D, I = empty.search(rand(orc, 3, d, 2), 4)
+    assert (I == -1).all()
+
+
+def build_ivf(amd, orc, d, nb, nlist, desc="Flat", seed=1234):
+    xb = rand(orc, nb, d, seed)
+    idx = amd.index_factory(d, f"IVF{nlist},{desc}")
+    idx.train(xb)
+    idx.add(xb)
+    return idx, xb
+
+
+@pytest.fixture(scope="module")
+def cfg1(amd, orc, gpu):
+    # BASELINE.json configs[0]: IVF256,Flat d=64, 100k vectors, nq=1k, nprobe=8
+    idx, xb = build_ivf(amd, orc, 64, 100_000, 256)
+    xq = rand(orc, 1000, 64, 5678)
+    return idx, xb, xq
+
+
+def test_cfg1_ivfflat_bit_exact(amd, orc, cfg1):
+    idx, xb, xq = cfg1
+    idx.nprobe = 8
+    D, I = idx.search(xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, 8, nslices=1)
+    assert_same_results(D, I, Dr, Ir)
+    # recall sanity against exact search
+    _, Igt = orc.knn(xq, xb, 10, blas_form=False)
+    rec = np.mean([len(set(a) & set(b)) / 10 for a, b in zip(I, Igt)])
+    assert rec > 0.2
+
+
+def test_cfg1_lowlevel_decomposition(amd, orc, cfg1):
+    # tests/test_lowlevel_ivf.cpp:150-213: quantizer->search + search_preassigned == search
+    idx, xb, xq = cfg1
+    idx.nprobe = 8
+    Dq, Iq = idx.quantizer.search(xq, 8)
+    D1, I1 = idx.search_preassigned(xq, 10, Iq, Dq)
+    D2, I2 = idx.search(xq, 10)
+    assert_same_results(D1, I1, D2, I2)
+    # and the coarse step equals the oracle's flat knn
+    Dqr, Iqr = orc.knn(xq, idx.quantizer.xb, 8, blas_form=True)
+    assert_same_results(Dq, Iq, Dqr, Iqr)
+
+
+@pytest.mark.parametrize("nprobe", [1, 3, 17, 64])
+@pytest.mark.parametrize("k", [1, 5, 37, 64])
+def test_ivfflat_nprobe_k_grid(amd, orc, cfg1, nprobe, k):
+    idx, xb, xq = cfg1
+    idx.nprobe = nprobe
+    D, I = idx.search(xq[:200], k)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq[:200], k, nprobe, nslices=1)
+    assert_same_results(D, I, Dr, Ir)
+
+
+def test_ivfflat_exhaustive_equals_exact(amd, orc, cfg1):
+    idx, xb, xq = cfg1
+    idx.nprobe = 256 if False else 64  # nprobe <= 64 on this path
+    q = xq[:50]
+    D, I = idx.search(q, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(q, 10, 64, nslices=1)
+    assert_same_results(D, I, Dr, Ir)
+
+
+def test_ivfflat_edge_cases(amd, orc, gpu):
+    # ragged / tiny / empty lists, d not a multiple of 4, nq = 1, ids given
+    d, nb, nlist = 30, 700, 40
+    xb = rand(orc, nb, d, 7)
+    q = amd.IndexFlatL2(d)
+    idx = amd.IndexIVFFlat(q, d, nlist)
+    idx.train(xb)
+    ids = (np.arange(nb, dtype=np.int64) * 7919) % 100003
+    idx.add_with_ids(xb[:300], ids[:300])
+    idx.nprobe = 6
+    ref = orc.IVFOracle.from_index(idx)
+    for nq in (1, 7, 129):
+        xq = rand(orc, nq, d, 100 + nq)
+        D, I = idx.search(xq, 12)
+        Dr, Ir, _, _ = ref.search(xq, 12, 6, nslices=1)
+        assert_same_results(D, I, Dr, Ir)
+    # empty index: all padding
+    idx.reset()
+    D, I = idx.search(rand(orc, 4, d, 3), 5)
+    assert (I == -1).all()
+
+
+def test_ivfflat_inner_product(amd, orc, gpu):
+    d, nb, nlist = 32, 5000, 32
+    xb = rand(orc, nb, d, 21)
+    q = amd.IndexFlatIP(d)
+    idx = amd.IndexIVFFlat(q, d, nlist, amd.METRIC_INNER_PRODUCT)
+    idx.train(xb)
+    idx.add(xb)
+    idx.nprobe = 4
+    xq = rand(orc, 100, d, 22)
+    D, I = idx.search(xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, 4, nslices=1)
+    assert_same_results(D, I, Dr, Ir)
+
+
+def test_search_params_override(amd, orc, cfg1):
+    # tests/test_params_override.cpp: per-call nprobe overrides index.nprobe
+    idx, xb, xq = cfg1
+    idx.nprobe = 1
+    p = amd.SearchParametersIVF(nprobe=8)
+    D1, I1 = idx.search(xq[:100], 10, params=p)
+    idx.nprobe = 8
+    D2, I2 = idx.search(xq[:100], 10)
+    assert_same_results(D1, I1, D2, I2)
+
+
+def test_device_entry_points_match_host(amd, orc, cfg1):
+    import ctypes
+    idx, xb, xq = cfg1
+    idx.nprobe = 8
+    D, I = idx.search(xq, 10)
+    # device buffers through hipMalloc of the HIP runtime in the library's process
+    hip = ctypes.CDLL("libamdhip64.so")
+    def dmalloc(nbytes):
+        p = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(nbytes)) == 0
+        return p
+    n = xq.shape[0]
+    px, pd, pi = dmalloc(xq.nbytes), dmalloc(n * 10 * 4), dmalloc(n * 10 * 8)
+    hip.hipMemcpy(px, xq.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(xq.nbytes), 1)
+    idx.search_device(n, px.value, 10, pd.value, pi.value)
+    hip.hipDeviceSynchronize()
+    D2 = np.empty((n, 10), np.float32)
+    I2 = np.empty((n, 10), np.int64)
+    hip.hipMemcpy(D2.ctypes.data_as(ctypes.c_void_p), pd, ctypes.c_size_t(D2.nbytes), 2)
+    hip.hipMemcpy(I2.ctypes.data_as(ctypes.c_void_p), pi, ctypes.c_size_t(I2.nbytes), 2)
+    for p in (px, pd, pi):
+        hip.hipFree(p)
+    assert_same_results(D2, I2, D, I)
