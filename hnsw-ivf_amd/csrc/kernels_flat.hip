@@ -152,35 +152,96 @@ void pairwise_distances(const float* x, int64_t nx, int ldx, const float* xn, co
 }
 
 // ---------------------------------------------------------------- select
-// One wave per row; candidates streamed in chunks of 64 columns.
+// One wave per row.  Pass 1: every lane keeps the minimum key of its strided
+// columns; the K-th smallest lane minimum T0 bounds the K-th smallest key of
+// the row (K lanes each hold an element <= T0).  Pass 2: the columns with
+// key <= T0 (typically 1-3 K of them) are compacted into LDS and folded into
+// the wave queue, so a row costs two streaming passes, one 64-lane sort and a
+// couple of merges instead of one sort-merge per 64 columns.
+constexpr int SEL_CAP = 512;
+
 __global__ __launch_bounds__(256) void k_select_rows(const float* __restrict__ D, int64_t nx,
                                                      int64_t ny, int64_t ldD, int k,
                                                      int metric_l2, int64_t col0,
                                                      float* __restrict__ out_d,
                                                      int32_t* __restrict__ out_i32,
                                                      int64_t* __restrict__ out_i64, int64_t ldo) {
+    __shared__ float bufd[4][SEL_CAP];
+    __shared__ int32_t bufi[4][SEL_CAP];
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= nx) return;
-    const float* Dr = D + row * ldD;
+    const int w = threadIdx.x >> 6;
+    const int64_t row = (int64_t)blockIdx.x * 4 + w;
+    const bool valid_row = row < nx;  // every wave reaches the barrier below
+    ny = valid_row ? ny : 0;
+    const float* Dr = D + (valid_row ? row : 0) * ldD;
+    auto key_of = [&](int64_t col, float& k1, long long& k2) {
+        to_key(metric_l2, Dr[col], (long long)col, k1, k2);
+        if (!key_admissible(k1)) {
+            k1 = WS_INF;
+            k2 = WS_NOID;
+        }
+    };
+    // pass 1
+    float md = WS_INF;
+    long long mi = WS_NOID;
+    for (int64_t c = lane; c < ny; c += 64) {
+        float k1;
+        long long k2;
+        key_of(c, k1, k2);
+        if (key_less(k1, k2, md, mi)) {
+            md = k1;
+            mi = k2;
+        }
+    }
+    wave_sort64(md, mi, lane);
+    const float t_d = __shfl(md, k - 1);
+    const long long t_i = shfl_ll(mi, k - 1);
+    // pass 2: compact keys <= T0
+    int count = 0;
+    bool overflow = false;
+    for (int64_t c0 = 0; c0 < ny; c0 += 64) {
+        const int64_t c = c0 + lane;
+        float k1 = WS_INF;
+        long long k2 = WS_NOID;
+        if (c < ny) key_of(c, k1, k2);
+        const bool pass = k2 != WS_NOID && !key_less(t_d, t_i, k1, k2);
+        const unsigned long long m = __ballot(pass);
+        if (m) {
+            const int pos = count + __popcll(m & ((1ull << lane) - 1ull));
+            if (pass && pos < SEL_CAP) {
+                bufd[w][pos] = k1;
+                bufi[w][pos] = (int32_t)c;
+            }
+            count += __popcll(m);
+        }
+    }
+    if (count > SEL_CAP) overflow = true;
+    __syncthreads();  // one wave per region; also orders the LDS writes
     float qd = WS_INF;
     long long qi = WS_NOID;
     float thr_d = WS_INF;
     long long thr_i = WS_NOID;
-    for (int64_t c = 0; c < ny; c += 64) {
-        int64_t col = c + lane;
-        float k1 = WS_INF;
-        long long k2 = WS_NOID;
-        if (col < ny) {
-            to_key(metric_l2, Dr[col], (long long)col, k1, k2);
-            if (!key_admissible(k1)) {
-                k1 = WS_INF;
-                k2 = WS_NOID;
+    if (!overflow) {
+        for (int b0 = 0; b0 < count; b0 += 64) {
+            float k1 = WS_INF;
+            long long k2 = WS_NOID;
+            if (b0 + lane < count) {
+                k1 = bufd[w][b0 + lane];
+                const long long col = bufi[w][b0 + lane];
+                k2 = metric_l2 ? col : -col;
             }
+            wave_offer(qd, qi, k1, k2, thr_d, thr_i, k, lane);
         }
-        wave_offer(qd, qi, k1, k2, thr_d, thr_i, k, lane);
+    } else {
+        for (int64_t c0 = 0; c0 < ny; c0 += 64) {
+            const int64_t c = c0 + lane;
+            float k1 = WS_INF;
+            long long k2 = WS_NOID;
+            if (c < ny) key_of(c, k1, k2);
+            wave_offer(qd, qi, k1, k2, thr_d, thr_i, k, lane);
+        }
     }
-    if (lane < k) {
+    if (valid_row && lane < k) {
         float dis;
         long long id;
         from_key(metric_l2, qd, qi, dis, id);

@@ -115,7 +115,9 @@ constexpr int SVT = 64;   // codes per tile
 constexpr int SDC = 128;  // dims per LDS chunk
 constexpr int SSD = SDC + 4;  // LDS row stride (floats): 528 B, 16-B aligned
 
-template <bool L2>
+// KQ > 0: thread-queue selection (4 threads per query, k <= KQ);
+// KQ == 0: wave64 bitonic queues (16 queries per wave, any k <= 64).
+template <bool L2, int KQ>
 __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
         const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
         const int64_t* __restrict__ ids, const uint32_t* __restrict__ list_off,
@@ -168,12 +170,19 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
     };
     if (one_chunk) load_x(0);
 
-    float qd[16];
-    long long qi[16];
+    // selection state
+    constexpr int NQW = KQ > 0 ? 1 : 16;  // wave path: 16 queues per lane
+    float qd[NQW];
+    long long qi[NQW];
+    ThreadQueue<(KQ > 0 ? KQ : 1)> tq;
+    if constexpr (KQ > 0) {
+        tq.init();
+    } else {
 #pragma unroll
-    for (int qq = 0; qq < 16; qq++) {
-        qd[qq] = WS_INF;
-        qi[qq] = WS_NOID;
+        for (int qq = 0; qq < NQW; qq++) {
+            qd[qq] = WS_INF;
+            qi[qq] = WS_NOID;
+        }
     }
     const int qg = t >> 4, vg = t & 15;
 
@@ -232,43 +241,115 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
             }
             __syncthreads();
         }
-        // distance tile -> LDS (aliases the Y tile), ids of this tile
+        // distance tile -> LDS (aliases the Y tile)
         float* Ds = Ys;
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int j = 0; j < 4; j++) Ds[(qg + 16 * i) * (SVT + 1) + vg + 16 * j] = acc[i][j];
-        if (t < SVT) ids_s[t] = t < nv ? (long long)ids[row0 + v0 + t] : 0ll;
+        if constexpr (KQ == 0) {
+            if (t < SVT) ids_s[t] = t < nv ? (long long)ids[row0 + v0 + t] : 0ll;
+        }
         __syncthreads();
-        // selection: wave w owns queries w*16 .. w*16+15
-        const bool lane_ok = lane < nv;
-        const long long my_id = ids_s[lane];
-#pragma unroll
-        for (int qq = 0; qq < 16; qq++) {
-            const int q = w * 16 + qq;
+        if constexpr (KQ > 0) {
+            // thread (q = t>>2, s = t&3) owns codes s, s+4, ... of query q
+            const int q = t >> 2, s4 = t & 3;
             if (q < nQ) {
-                float dis = Ds[q * (SVT + 1) + lane];
-                float k1;
-                long long k2;
-                to_key(L2 ? 1 : 0, dis, my_id, k1, k2);
-                if (!lane_ok || !key_admissible(k1)) {
-                    k1 = WS_INF;
-                    k2 = WS_NOID;
+#pragma unroll 4
+                for (int j = s4; j < nv; j += 4) {
+                    float dis = Ds[q * (SVT + 1) + j];
+                    float k1 = L2 ? dis : -dis;
+                    if (k1 < FLT_MAX) {
+                        const uint32_t r = (uint32_t)(v0 + j);
+                        unsigned long long key =
+                                ((unsigned long long)ordered_f32(k1) << 32) | (L2 ? r : ~r);
+                        tq.push(key, k);
+                    }
                 }
-                wave_offer_q(qd[qq], qi[qq], k1, k2, k, lane);
+            }
+        } else {
+            // wave w owns queries w*16 .. w*16+15
+            const bool lane_ok = lane < nv;
+            const long long my_id = ids_s[lane];
+#pragma unroll
+            for (int qq = 0; qq < NQW; qq++) {
+                const int q = w * 16 + qq;
+                if (q < nQ) {
+                    float dis = Ds[q * (SVT + 1) + lane];
+                    float k1;
+                    long long k2;
+                    to_key(L2 ? 1 : 0, dis, my_id, k1, k2);
+                    if (!lane_ok || !key_admissible(k1)) {
+                        k1 = WS_INF;
+                        k2 = WS_NOID;
+                    }
+                    wave_offer_q(qd[qq], qi[qq], k1, k2, k, lane);
+                }
             }
         }
         __syncthreads();
     }
+    if constexpr (KQ > 0) {
+        // merge the 4 thread queues of each query through LDS
+        unsigned long long* M = (unsigned long long*)Xs;  // [64][4][KQ] fits Xs+Ys
+        const int q = t >> 2, s4 = t & 3;
 #pragma unroll
-    for (int qq = 0; qq < 16; qq++) {
-        const int q = w * 16 + qq;
-        if (q < nQ && lane < k) {
-            const int64_t e = ent_s[q];
-            part_k1[e * k + lane] = qd[qq];
-            part_k2[e * k + lane] = qi[qq];
+        for (int i = 0; i < KQ; i++) M[(q * 4 + s4) * KQ + i] = tq.q[i];
+        __syncthreads();
+        if (t < nQ) {
+            const unsigned long long* Mq = M + t * 4 * KQ;
+            int p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+            const int64_t e = ent_s[t];
+            for (int j = 0; j < k; j++) {
+                unsigned long long h0 = p0 < KQ ? Mq[p0] : ~0ull;
+                unsigned long long h1 = p1 < KQ ? Mq[KQ + p1] : ~0ull;
+                unsigned long long h2 = p2 < KQ ? Mq[2 * KQ + p2] : ~0ull;
+                unsigned long long h3 = p3 < KQ ? Mq[3 * KQ + p3] : ~0ull;
+                unsigned long long m01 = h0 < h1 ? h0 : h1, m23 = h2 < h3 ? h2 : h3;
+                unsigned long long m = m01 < m23 ? m01 : m23;
+                if (m == h0) p0++;
+                else if (m == h1) p1++;
+                else if (m == h2) p2++;
+                else p3++;
+                float k1 = WS_INF;
+                long long k2 = WS_NOID;
+                if (m != ~0ull) {
+                    k1 = unordered_f32((uint32_t)(m >> 32));
+                    uint32_t r = (uint32_t)m;
+                    if (!L2) r = ~r;
+                    const long long id = ids[row0 + r];
+                    k2 = L2 ? id : -id;
+                }
+                part_k1[e * k + j] = k1;
+                part_k2[e * k + j] = k2;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int qq = 0; qq < NQW; qq++) {
+            const int q = w * 16 + qq;
+            if (q < nQ && lane < k) {
+                const int64_t e = ent_s[q];
+                part_k1[e * k + lane] = qd[qq];
+                part_k2[e * k + lane] = qi[qq];
+            }
         }
     }
+}
+
+template <int KQ>
+static void launch_scan(bool l2, int64_t grid, hipStream_t s, const float* x, int ldx,
+                        const float* codes, int ldc, const int64_t* ids, const uint32_t* list_off,
+                        const uint32_t* list_len, int nlist, int dp, int nprobe, int k,
+                        IVFBuckets b, float* pk1, long long* pk2) {
+    if (l2)
+        k_ivf_flat_scan<true, KQ><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
+                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, nprobe, k, b.bucket_off,
+                b.item_off, b.entries, pk1, pk2);
+    else
+        k_ivf_flat_scan<false, KQ><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
+                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, nprobe, k, b.bucket_off,
+                b.item_off, b.entries, pk1, pk2);
 }
 
 void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const int64_t* ids,
@@ -279,14 +360,19 @@ void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const i
     FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
     FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldc % 4 == 0 && dp % 4 == 0);
     FAISS_THROW_IF_NOT(max_items < (1ll << 31));
-    if (metric_l2)
-        k_ivf_flat_scan<true><<<dim3((unsigned)max_items), dim3(256), 0, s>>>(
-                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, nprobe, k, b.bucket_off,
-                b.item_off, b.entries, part_k1, part_k2);
+    const bool l2 = metric_l2 != 0;
+    if (k <= 10)
+        launch_scan<10>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
+                        nprobe, k, b, part_k1, part_k2);
+    else if (k <= 16)
+        launch_scan<16>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
+                        nprobe, k, b, part_k1, part_k2);
+    else if (k <= 32)
+        launch_scan<32>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
+                        nprobe, k, b, part_k1, part_k2);
     else
-        k_ivf_flat_scan<false><<<dim3((unsigned)max_items), dim3(256), 0, s>>>(
-                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, nprobe, k, b.bucket_off,
-                b.item_off, b.entries, part_k1, part_k2);
+        launch_scan<0>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
+                       nprobe, k, b, part_k1, part_k2);
     HIP_LAUNCH_CHECK();
 }
 

@@ -143,3 +143,46 @@ __device__ __forceinline__ void from_key(int metric_l2, float k1, long long k2, 
 }
 
 }  // namespace faiss_amd
+
+namespace faiss_amd {
+// ---------------------------------------------------------------------------
+// Per-thread sorted queue of KQ 64-bit keys (ascending).  key = ordered
+// float bits << 32 | tie-breaker, so one unsigned compare orders (dist, tie).
+// Used where many candidates per query stream through a few threads (the
+// list-centric scan): a candidate costs one compare unless it enters the
+// queue; entering costs KQ predicated moves.  The union of the per-thread
+// top-k sets of a query contains its top-k, so k <= KQ entries per thread
+// suffice.
+__device__ __forceinline__ uint32_t ordered_f32(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unordered_f32(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+template <int KQ>
+struct ThreadQueue {
+    unsigned long long q[KQ];
+    unsigned long long thr;  // q[k-1]
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int i = 0; i < KQ; i++) q[i] = ~0ull;
+        thr = ~0ull;
+    }
+    __device__ __forceinline__ void push(unsigned long long c, int k) {
+        if (c < thr) {
+#pragma unroll
+            for (int i = KQ - 1; i > 0; i--) {
+                unsigned long long prev = q[i - 1];
+                q[i] = c < prev ? prev : (c < q[i] ? c : q[i]);
+            }
+            q[0] = c < q[0] ? c : q[0];
+            unsigned long long t = q[0];
+#pragma unroll
+            for (int i = 1; i < KQ; i++) t = (i == k - 1) ? q[i] : t;
+            thr = t;
+        }
+    }
+};
+}  // namespace faiss_amd

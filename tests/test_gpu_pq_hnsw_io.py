@@ -1,0 +1,157 @@
+"""GPU parity: IVF-PQ, HNSW (standalone and as IVF coarse quantizer), on-disk
+format round trips, and IndexShardsIVF, all through the C-ABI."""
+import numpy as np
+import pytest
+
+from conftest import assert_same_results, rand
+
+pytestmark = pytest.mark.gpu
+
+
+def recall(I, Igt, k):
+    return float(np.mean([len(set(a[:k]) & set(b[:k])) / k for a, b in zip(I, Igt)]))
+
+
+@pytest.fixture(scope="module")
+def pq_index(amd, orc, gpu):
+    d, nb, nlist, M = 64, 30000, 64, 16
+    xb = rand(orc, nb, d, 31)
+    idx = amd.index_factory(d, f"IVF{nlist},PQ{M}x8")
+    idx.train(xb)
+    idx.add(xb)
+    return idx, xb
+
+
+def test_ivfpq_recall_parity_with_oracle(amd, orc, pq_index):
+    idx, xb = pq_index
+    xq = rand(orc, 500, 64, 32)
+    idx.nprobe = 8
+    D, I = idx.search(xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    assert ref.use_precomputed_table == 1
+    Dr, Ir, _, _ = ref.search(xq, 10, 8)
+    _, Igt = orc.knn(xq, xb, 10, blas_form=False)
+    r_gpu, r_ref = recall(I, Igt, 10), recall(Ir, Igt, 10)
+    assert abs(r_gpu - r_ref) <= 0.01, (r_gpu, r_ref)
+    same = (I == Ir)
+    assert same.mean() > 0.97, same.mean()
+    # fp32 distances of the same codes agree to 1e-4 relative
+    np.testing.assert_allclose(D[same], Dr[same], rtol=1e-4, atol=1e-5)
+
+
+def test_ivfpq_table0_equals_table1_ids(amd, orc, pq_index):
+    # tests/test_index_accuracy.py:496-498: use_precomputed_table 0 vs 1 -> same I
+    idx, xb = pq_index
+    xq = rand(orc, 300, 64, 33)
+    ref1 = orc.IVFOracle.from_index(idx)
+    ref0 = orc.IVFOracle.from_index(idx)
+    ref0.s.use_precomputed_table = 0
+    _, I1, _, _ = ref1.search(xq, 10, 8)
+    _, I0, _, _ = ref0.search(xq, 10, 8)
+    assert (I1 == I0).mean() > 0.99
+    idx.nprobe = 8
+    _, Ig = idx.search(xq, 10)
+    assert (Ig == I0).mean() > 0.97
+
+
+@pytest.fixture(scope="module")
+def hnsw_index(amd, orc, gpu):
+    d, nb = 32, 6000
+    xb = rand(orc, nb, d, 41)
+    h = amd.IndexHNSWFlat(d, 16)
+    h.add(xb)
+    return h, xb
+
+
+@pytest.mark.parametrize("ef", [16, 64, 128])
+@pytest.mark.parametrize("k", [1, 10, 32])
+def test_hnsw_search_bit_exact(amd, orc, hnsw_index, ef, k):
+    h, xb = hnsw_index
+    h.efSearch = ef
+    xq = rand(orc, 300, 32, 42)
+    D, I = h.search(xq, k)
+    g = orc.HNSWGraph.from_index(h)
+    Dr, Ir = g.search(xq, k, ef)
+    assert_same_results(D, I, Dr, Ir)
+
+
+def test_hnsw_graph_quality(amd, orc, hnsw_index):
+    # tests/test_graph_based.py:17-75 style recall floor
+    h, xb = hnsw_index
+    h.efSearch = 64
+    xq = rand(orc, 200, 32, 43)
+    _, I = h.search(xq, 1)
+    _, Igt = orc.knn(xq, xb, 1, blas_form=False)
+    assert (I[:, 0] == Igt[:, 0]).mean() > 0.9
+
+
+@pytest.mark.parametrize("ef", [16, 64])
+def test_ivf_hnsw_quantizer_bit_exact(amd, orc, gpu, ef):
+    d, nb, nlist = 32, 20000, 128
+    xb = rand(orc, nb, d, 51)
+    idx = amd.index_factory(d, f"IVF{nlist}_HNSW16,Flat")
+    idx.train(xb)
+    idx.add(xb)
+    idx.nprobe = 16
+    amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", ef)
+    xq = rand(orc, 300, d, 52)
+    D, I = idx.search(xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, 16, efSearch=ef)
+    assert_same_results(D, I, Dr, Ir)
+
+
+@pytest.mark.parametrize("desc", ["IVF32,Flat", "IVF32,PQ8", "IVF32_HNSW8,Flat", "Flat"])
+def test_write_read_roundtrip(amd, orc, gpu, tmp_path, desc):
+    d, nb = 32, 4000
+    xb = rand(orc, nb, d, 61)
+    idx = amd.index_factory(d, desc)
+    idx.train(xb)
+    idx.add(xb)
+    if hasattr(idx, "nprobe"):
+        idx.nprobe = 4
+    xq = rand(orc, 100, d, 62)
+    D, I = idx.search(xq, 5)
+    fn = tmp_path / "x.index"
+    amd.write_index(idx, fn)
+    idx2 = amd.read_index(fn)
+    assert type(idx2).__name__ == type(idx).__name__
+    assert idx2.ntotal == nb
+    D2, I2 = idx2.search(xq, 5)
+    assert_same_results(D2, I2, D, I)
+    # writing the re-read index gives the same bytes
+    fn2 = tmp_path / "y.index"
+    amd.write_index(idx2, fn2)
+    assert fn.read_bytes() == fn2.read_bytes()
+
+
+def test_shards_ivf_equals_unsharded(amd, orc, gpu):
+    # tests/test_meta_index.py:128-148 (test_shards_ivf): exact I, close D
+    d, nb, nlist = 32, 9000, 40
+    xb = rand(orc, nb, d, 71)
+    q = amd.IndexFlatL2(d)
+    ref = amd.IndexIVFFlat(q, d, nlist)
+    ref.train(xb)
+    ref.add(xb)
+    ref.nprobe = 6
+    sh = amd.IndexShardsIVF(q, nlist, False, True)
+    parts = [amd.IndexIVFFlat(q, d, nlist) for _ in range(3)]
+    for p in parts:
+        sh.add_shard(p)
+    sh.add(xb)
+    sh.nprobe = 6
+    xq = rand(orc, 200, d, 72)
+    D1, I1 = ref.search(xq, 10)
+    D2, I2 = sh.search(xq, 10)
+    assert_same_results(D2, I2, D1, I1)
+
+
+def test_merge_knn_results_device_and_host(amd, orc, gpu):
+    rng = np.random.default_rng(3)
+    ns, n, k = 5, 200, 10
+    Dall = np.sort(rng.integers(0, 50, size=(ns, n, k)).astype(np.float32), axis=2)
+    Iall = rng.integers(0, 10**6, size=(ns, n, k)).astype(np.int64)
+    Iall[2, :, 6:] = -1
+    Dr, Ir = orc.merge_knn_results(Dall, Iall)
+    D, I = amd.merge_knn_results(Dall, Iall)
+    assert np.array_equal(I, Ir) and np.array_equal(D, Dr)
