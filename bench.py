@@ -197,13 +197,21 @@ def main():
         ref.search_fast(xq[:probe], k, nprobe, nthreads=ncores)
         tp = time.perf_counter() - tc
         ns = int(min(nq, max(probe, probe * args.cpu_seconds / max(tp, 1e-3))))
-        tc = time.perf_counter()
-        Dc, Ic = ref.search_fast(xq[:ns], k, nprobe, nthreads=ncores)
-        tcpu = time.perf_counter() - tc
+        # repeat passes over the sample until ~cpu_seconds of wall time
+        passes, tcpu = 0, 0.0
+        while True:
+            tc = time.perf_counter()
+            Dc, Ic = ref.search_fast(xq[:ns], k, nprobe, nthreads=ncores)
+            tcpu += time.perf_counter() - tc
+            passes += 1
+            if tcpu >= args.cpu_seconds or passes >= 50:
+                break
         agree = float(np.mean(Ic == I_t.cpu().numpy()[:ns]))
-        cpu = {"value": ns / tcpu, "unit": "queries/s", "cores": ncores, "kind": "port",
-               "sample": f"{ns} of the {nq} queries, same index, IVF-Flat scan with 8-way "
-                         f"vectorisable partial sums (oracle search_fast), {tcpu:.1f}s",
+        cpu = {"value": ns * passes / tcpu, "unit": "queries/s", "cores": ncores,
+               "kind": "port",
+               "sample": f"{passes} pass(es) over {ns} of the {nq} queries, same index, "
+                         f"IVF-Flat scan with 8-way vectorisable partial sums (oracle "
+                         f"search_fast), {tcpu:.1f}s wall on {ncores} threads",
                "id_agreement_vs_gpu": agree}
 
     if rank == 0:

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/faiss_amd.h"
@@ -284,12 +285,24 @@ void IndexIVFFlat::reconstruct(idx_t key, float* recons) const {
     FAISS_THROW_MSG("key not found");
 }
 
+void IndexIVFFlat::upload_extra() const {
+    hipStream_t s = stream();
+    const int l = (int)roundup((size_t)d, 4);
+    d_ynorm_.reserve(sizeof(float) * std::max<size_t>(arena_rows_, 1));
+    d_ynmax_.reserve(sizeof(float) * std::max<size_t>(nlist, 1));
+    if (arena_rows_ > 0)
+        kern::row_norms(d_codes_.as<float>(), arena_rows_, d, l, d_ynorm_.as<float>(), s);
+    kern::ivf_list_ynmax(d_ynorm_.as<float>(), d_list_off_.as<uint32_t>(),
+                         d_list_len_.as<uint32_t>(), (int)nlist, d_ynmax_.as<float>(), s);
+}
+
 void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
                                              const int32_t* assign, const float*,
                                              float* distances, idx_t* labels,
                                              hipStream_t s) const {
     if (n <= 0) return;
     sync_device();
+    std::lock_guard<std::recursive_mutex> g(mu_);
     const int QT = 64;
     const int l = (int)roundup((size_t)d, 4);
     s_counts_.reserve(sizeof(uint32_t) * nlist);
@@ -297,22 +310,57 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     s_boff_.reserve(sizeof(uint32_t) * (nlist + 1));
     s_ioff_.reserve(sizeof(uint32_t) * (nlist + 1));
     s_ent_.reserve(sizeof(uint32_t) * n * np);
-    s_pk1_.reserve(sizeof(float) * n * np * k);
-    s_pk2_.reserve(sizeof(long long) * n * np * k);
     kern::IVFBuckets b{s_counts_.as<uint32_t>(), s_boff_.as<uint32_t>(), s_ioff_.as<uint32_t>(),
                        s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
     kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), (int)nlist, QT, b, s);
     const int64_t max_items = kern::ivf_max_items(n, np, (int)nlist, QT);
+    const char* env = getenv("FAISS_AMD_IVF_SCAN");
+    int mode = scan_mode;
+    if (env && !strcmp(env, "exact")) mode = 1;
+    if (env && !strcmp(env, "mfma")) mode = 0;
+    const int KQ = kern::ivf_mfma_kq((int)k, l);
+    const bool l2 = metric_type == METRIC_L2;
+    s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(n, 4));
+    if (mode == 0 && KQ > 0) {
+        s_part_.reserve(sizeof(unsigned long long) * n * np * KQ);
+        s_pk1_.reserve(sizeof(float) * n * np * KQ);  // upper bounds
+        s_pk2_.reserve(sizeof(float) * n * np);       // dropped-candidate bounds
+        const bool dbg = getenv("FAISS_AMD_IVF_STATS") != nullptr;
+        if (dbg) HIP_CHECK(hipMemsetAsync(s_flags_.ptr, 0, 4 * sizeof(uint32_t), s));
+        kern::ivf_flat_scan_mfma(x, ldx, d_codes_.as<float>(), l, d_ids_.as<int64_t>(),
+                                 d_ynorm_.as<float>(), d_ynmax_.as<float>(),
+                                 d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(),
+                                 (int)nlist, d, l, n, np, (int)k, l2, b, max_items, assign,
+                                 s_part_.as<unsigned long long>(), s_pk1_.as<float>(),
+                                 s_pk2_.as<float>(), dbg ? s_flags_.as<uint32_t>() : nullptr,
+                                 distances, labels, &ktimes, s);
+        if (dbg) {
+            uint32_t st[4];
+            HIP_CHECK(hipMemcpyAsync(st, s_flags_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            fprintf(stderr,
+                    "[faiss_amd] ivf mfma scan: nq=%lld survivors/q=%.2f failing probes/q=%.4f "
+                    "overflow queries=%u\n",
+                    (long long)n, st[0] / (double)n, st[1] / (double)n, st[2]);
+        }
+        return;
+    }
+    s_pk1_.reserve(sizeof(float) * n * np * k);
+    s_pk2_.reserve(sizeof(long long) * n * np * k);
     {
         ScopedKernelTimer tm(&ktimes, "ivf_flat_scan", 0.0, s);
         kern::ivf_flat_scan(x, ldx, d_codes_.as<float>(), l, d_ids_.as<int64_t>(),
                             d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(), (int)nlist, l,
-                            n, np, (int)k, metric_type == METRIC_L2, b, max_items,
-                            s_pk1_.as<float>(), s_pk2_.as<long long>(), s);
+                            n, np, (int)k, l2, b, max_items, s_pk1_.as<float>(),
+                            s_pk2_.as<long long>(), s);
     }
     kern::ivf_merge(s_pk1_.as<float>(), s_pk2_.as<long long>(), assign,
-                    d_list_len_.as<uint32_t>(), (int)nlist, n, np, (int)k,
-                    metric_type == METRIC_L2, distances, labels, s);
+                    d_list_len_.as<uint32_t>(), (int)nlist, n, np, (int)k, l2, distances, labels,
+                    s_flags_.as<uint32_t>(), s);
+    kern::ivf_exact_fallback(s_flags_.as<uint32_t>(), assign, d_list_off_.as<uint32_t>(),
+                             d_list_len_.as<uint32_t>(), (int)nlist, x, ldx,
+                             d_codes_.as<float>(), l, d_ids_.as<int64_t>(), d, n, np, (int)k, l2,
+                             distances, labels, s);
 }
 
 // ---------------------------------------------------------------- PQ

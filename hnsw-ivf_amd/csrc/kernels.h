@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "common.h"
+
 namespace faiss_amd {
 namespace kern {
 
@@ -69,11 +71,32 @@ void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const i
                    int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b, int64_t max_items,
                    float* part_k1, long long* part_k2, hipStream_t s);
 
+// fp32-MFMA filter + exact re-rank variant (kernels_ivf_mfma.hip); results
+// are identical to ivf_flat_scan + ivf_merge.  ivf_mfma_kq = entries kept
+// per (query, list) (part/pub stride); 0 = not eligible (k > 32 or d > 128).
+int ivf_mfma_kq(int k, int dp);
+void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* list_len,
+                    int nlist, float* out, hipStream_t s);
+void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc,
+                        const int64_t* ids, const float* ynorm, const float* ynmax,
+                        const uint32_t* list_off, const uint32_t* list_len, int nlist, int d,
+                        int dp, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
+                        int64_t max_items, const int32_t* assign, unsigned long long* part,
+                        float* pub, float* pbound, uint32_t* stats, float* D, int64_t* I,
+                        KernelTimes* kt, hipStream_t s);
+// exact re-scan (reference tie rule) of the queries with flags[q] != 0
+void ivf_exact_fallback(const uint32_t* flags, const int32_t* assign, const uint32_t* list_off,
+                        const uint32_t* list_len, int nlist, const float* x, int ldx,
+                        const float* codes, int ldc, const int64_t* ids, int d, int64_t n,
+                        int nprobe, int k, int metric_l2, float* D, int64_t* I, hipStream_t s);
+
 // per-query merge of the nprobe partial top-k, reference
 // faiss/IndexIVF.cpp:595-631 (heap over probes) + Heap.h:421-450 (reorder)
+// flags[q] = 1 when a tie may cross the k boundary (resolve with
+// ivf_exact_fallback, which applies the reference's arrival-order rule)
 void ivf_merge(const float* part_k1, const long long* part_k2, const int32_t* assign,
                const uint32_t* list_len, int nlist, int64_t n, int nprobe, int k, int metric_l2,
-               float* D, int64_t* I, hipStream_t s);
+               float* D, int64_t* I, uint32_t* flags, hipStream_t s);
 
 // ---------------- IVF-PQ ----------------
 // query-centric PQ scan with the LUT in LDS, reference

@@ -125,8 +125,10 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
         const uint32_t* __restrict__ bucket_off, const uint32_t* __restrict__ item_off,
         const uint32_t* __restrict__ entries, float* __restrict__ part_k1,
         long long* __restrict__ part_k2) {
-    __shared__ __attribute__((aligned(16))) float Xs[SQT * SSD];
-    __shared__ __attribute__((aligned(16))) float Ys[SVT * SSD];
+    // one array: the end-of-kernel queue merge reuses both tiles (64 KB at KQ=32)
+    __shared__ __attribute__((aligned(16))) float smem_xy[(SQT + SVT) * SSD];
+    float* Xs = smem_xy;
+    float* Ys = smem_xy + SQT * SSD;
     __shared__ long long ids_s[SVT];
     __shared__ uint32_t ent_s[SQT];
     __shared__ int32_t qrow_s[SQT];
@@ -134,7 +136,12 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int w = t >> 6;
-    const uint32_t item = blockIdx.x;
+    // XCD-aware order: blocks b and b+8 share an XCD (dispatch round-robin),
+    // so groups of 4 consecutive work items (chunks of the same list) are
+    // placed on one XCD and re-read the list from its L2.  Bijective on the
+    // grid (a multiple of 32); affects speed only.
+    const uint32_t xcd = blockIdx.x & 7u, rest = blockIdx.x >> 3;
+    const uint32_t item = 4u * ((rest >> 2) * 8u + xcd) + (rest & 3u);
     const uint32_t total_items = item_off[nlist];
     if (item >= total_items) return;
     // list owning this item: largest l with item_off[l] <= item
@@ -186,6 +193,22 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
     }
     const int qg = t >> 4, vg = t & 15;
 
+    // register prefetch of the next code tile (d <= 128): its HBM latency
+    // overlaps the current tile's compute and selection
+    float4 pf[SVT * (SDC / 4) / 256];
+    auto fetch = [&](int v0n) {
+        const int nvn = min(SVT, len - v0n);
+#pragma unroll
+        for (int s = 0; s < SVT * (SDC / 4) / 256; s++) {
+            const int e = t + 256 * s;
+            const int r = e >> 5, kc = 4 * (e & 31);
+            pf[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r < nvn && kc < dp)
+                pf[s] = *(const float4*)(codes + (row0 + v0n + r) * (int64_t)ldc + kc);
+        }
+    };
+    if (one_chunk && len > 0) fetch(0);
+
     for (int v0 = 0; v0 < len; v0 += SVT) {
         const int nv = min(SVT, len - v0);
         float acc[4][4];
@@ -196,16 +219,26 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
 
         for (int dc = 0; dc < dp; dc += SDC) {
             const int dl = min(SDC, dp - dc);
-            if (!one_chunk) load_x(dc);
-            for (int e = t; e < SVT * (SDC / 4); e += 256) {
-                int r = e >> 5, c4 = e & 31;
-                int kc = 4 * c4;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (r < nv && kc < dl)
-                    v = *(const float4*)(codes + (row0 + v0 + r) * (int64_t)ldc + dc + kc);
-                *(float4*)(Ys + r * SSD + kc) = v;
+            if (one_chunk) {
+#pragma unroll
+                for (int s = 0; s < SVT * (SDC / 4) / 256; s++) {
+                    const int e = t + 256 * s;
+                    *(float4*)(Ys + (e >> 5) * SSD + 4 * (e & 31)) = pf[s];
+                }
+                __syncthreads();
+                if (v0 + SVT < len) fetch(v0 + SVT);
+            } else {
+                load_x(dc);
+                for (int e = t; e < SVT * (SDC / 4); e += 256) {
+                    int r = e >> 5, c4 = e & 31;
+                    int kc = 4 * c4;
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (r < nv && kc < dl)
+                        v = *(const float4*)(codes + (row0 + v0 + r) * (int64_t)ldc + dc + kc);
+                    *(float4*)(Ys + r * SSD + kc) = v;
+                }
+                __syncthreads();
             }
-            __syncthreads();
 #pragma unroll 2
             for (int dd = 0; dd < dl; dd += 4) {
                 float4 xa[4], yb[4];
@@ -361,6 +394,7 @@ void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const i
     FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldc % 4 == 0 && dp % 4 == 0);
     FAISS_THROW_IF_NOT(max_items < (1ll << 31));
     const bool l2 = metric_l2 != 0;
+    max_items = (int64_t)roundup((size_t)max_items, 32);  // XCD remap needs a multiple of 32
     if (k <= 10)
         launch_scan<10>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
                         nprobe, k, b, part_k1, part_k2);
@@ -377,16 +411,21 @@ void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const i
 }
 
 // ---------------------------------------------------------------- merge
+// Per query: lexicographic top-k of the nprobe per-list partial top-k.  A
+// boundary tie (the (k+1)-th merged key, or the last key of a full per-list
+// partial, equal to the k-th value) flags the query for the exact re-scan.
 __global__ __launch_bounds__(256) void k_ivf_merge(const float* __restrict__ part_k1,
                                                    const long long* __restrict__ part_k2,
                                                    const int32_t* __restrict__ assign,
                                                    const uint32_t* __restrict__ list_len,
                                                    int64_t n, int nprobe, int nlist, int k,
                                                    int metric_l2, float* __restrict__ D,
-                                                   int64_t* __restrict__ I) {
+                                                   int64_t* __restrict__ I,
+                                                   uint32_t* __restrict__ flags) {
     const int lane = threadIdx.x & 63;
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= n) return;
+    const int K1 = k < 64 ? k + 1 : 64;
     float qd = WS_INF;
     long long qi = WS_NOID;
     float thr_d = WS_INF;
@@ -405,7 +444,28 @@ __global__ __launch_bounds__(256) void k_ivf_merge(const float* __restrict__ par
                 k2 = part_k2[p];
             }
         }
-        wave_offer(qd, qi, k1, k2, thr_d, thr_i, k, lane);
+        wave_offer(qd, qi, k1, k2, thr_d, thr_i, K1, lane);
+    }
+    const float v = __shfl(qd, k - 1);
+    const long long vi = shfl_ll(qi, k - 1);
+    bool amb = false;
+    if (vi != WS_NOID) {
+        int cnt = 0;
+        bool tail = false;
+        for (int c = 0; c < total; c += 64) {
+            int e = c + lane;
+            bool eq = false;
+            if (e < total) {
+                int lst = assign[q * nprobe + e / k];
+                if (lst >= 0 && lst < nlist && list_len[lst] > 0) {
+                    int64_t p = (q * nprobe) * (int64_t)k + e;
+                    eq = part_k2[p] != WS_NOID && part_k1[p] == v;
+                    if (eq && e % k == k - 1) tail = true;
+                }
+            }
+            cnt += __popcll(__ballot(eq));
+        }
+        amb = __ballot(tail) != 0ull || cnt > __popcll(__ballot(lane < k && qd == v));
     }
     if (lane < k) {
         float dis;
@@ -414,14 +474,15 @@ __global__ __launch_bounds__(256) void k_ivf_merge(const float* __restrict__ par
         D[q * k + lane] = dis;
         I[q * k + lane] = id;
     }
+    if (lane == 0) flags[q] = amb ? 1u : 0u;
 }
 
 void ivf_merge(const float* part_k1, const long long* part_k2, const int32_t* assign,
                const uint32_t* list_len, int nlist, int64_t n, int nprobe, int k, int metric_l2,
-               float* D, int64_t* I, hipStream_t s) {
+               float* D, int64_t* I, uint32_t* flags, hipStream_t s) {
     if (n <= 0) return;
     k_ivf_merge<<<dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s>>>(
-            part_k1, part_k2, assign, list_len, n, nprobe, nlist, k, metric_l2, D, I);
+            part_k1, part_k2, assign, list_len, n, nprobe, nlist, k, metric_l2, D, I, flags);
     HIP_LAUNCH_CHECK();
 }
 

@@ -1,0 +1,553 @@
+// kernels_ivf_mfma.hip — IVF-Flat scan on fp32 MFMA with an exact re-rank.
+//
+// Reference hot loop: faiss/IndexIVFFlat.cpp:155-179 (exact sum (x-y)^2 per
+// code, strict heap admission) driven by faiss/IndexIVF.cpp:595-631.
+//
+// Three kernels, all results EXACT (bit-identical to the direct sequential
+// fma chain the CPU oracle evaluates):
+//  A  k_ivf_mfma_filter: list-centric (list x 64 queries per workgroup).
+//     <x,y> for a 64x64 tile on v_mfma_f32_32x32x2_f32 (one 32x32 block per
+//     wave), approx = |x|^2 + |y|^2 - 2<x,y>; per (query, list) the KQ best
+//     approx keys survive (4 threads per query, register queues).
+//  B  k_ivf_rerank: one wave per query.  With B(c) a rigorous bound on
+//     |approx - exact| (fp32 error analysis below), U = k-th smallest
+//     approx+B over the kept candidates bounds the exact k-th distance;
+//     every kept candidate with approx-B <= U gets its exact distance
+//     (sequential fma chain, fp32 rows from HBM) and the exact top-k by
+//     (dist, id) is emitted.  A list whose KQ-th kept candidate still has
+//     approx - Bmax(list) <= U may have dropped a member: the query is
+//     flagged.
+//  C  k_ivf_exact_fallback: exact scan of the flagged queries only.
+//
+// Error bound (d terms, u = 2^-24, g = d u / (1 - d u)):
+//   |ip_mfma - ip| <= g sum|x_i y_i| <= g (|x|^2 + |y|^2) / 2
+//   |approx - true| <= (2g + 3u)(|x|^2 + |y|^2)
+//   |exact  - true| <= (g + 2u) * 2 (|x|^2 + |y|^2)
+//   => |approx - exact| <= (4g + 7u)(|x|^2 + |y|^2); we use twice that.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "common.h"
+#include "kernels.h"
+#include "wave_select.h"
+#include "exact_select.h"
+
+namespace faiss_amd {
+namespace kern {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int MQT = 64;       // queries per work item
+constexpr int MVT = 64;       // codes per tile
+constexpr int MSD = 132;      // LDS row stride (floats)
+
+__device__ __forceinline__ float seq_l2(const float* __restrict__ a, const float* __restrict__ b,
+                                        int d) {
+    float acc = 0.f;
+    int j = 0;
+    for (; j + 4 <= d; j += 4) {
+        float4 av = *(const float4*)(a + j);
+        float4 bv = *(const float4*)(b + j);
+        float t0 = av.x - bv.x, t1 = av.y - bv.y, t2 = av.z - bv.z, t3 = av.w - bv.w;
+        acc = fmaf(t0, t0, acc);
+        acc = fmaf(t1, t1, acc);
+        acc = fmaf(t2, t2, acc);
+        acc = fmaf(t3, t3, acc);
+    }
+    for (; j < d; j++) {
+        float t = a[j] - b[j];
+        acc = fmaf(t, t, acc);
+    }
+    return acc;
+}
+__device__ __forceinline__ float seq_ip(const float* __restrict__ a, const float* __restrict__ b,
+                                        int d) {
+    float acc = 0.f;
+    int j = 0;
+    for (; j + 4 <= d; j += 4) {
+        float4 av = *(const float4*)(a + j);
+        float4 bv = *(const float4*)(b + j);
+        acc = fmaf(av.x, bv.x, acc);
+        acc = fmaf(av.y, bv.y, acc);
+        acc = fmaf(av.z, bv.z, acc);
+        acc = fmaf(av.w, bv.w, acc);
+    }
+    for (; j < d; j++) acc = fmaf(a[j], b[j], acc);
+    return acc;
+}
+
+// ---------------------------------------------------------------- A
+// Per (query, list) output, 4*KT entries (4 threads x KT keys each):
+//   part[e][i] = ordered_f32(lb) << 32 | row   (lb = approx - B, ~0 = empty)
+//   pub[e][i]  = approx + B                     (upper bound of the exact key)
+//   pbound[e]  = lower bound of the exact key of every candidate of the list
+//                that was dropped (min over the 4 threads of their KT-th
+//                approx, minus the list's largest margin); +inf if none.
+constexpr int DSS = MVT + 4;  // approx tile stride: 16 queries x 4 threads hit 64 banks
+
+template <bool L2, int KT>
+__global__ __launch_bounds__(256, 2) void k_ivf_mfma_filter(
+        const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
+        const float* __restrict__ ynorm, const float* __restrict__ ynmax,
+        const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
+        int dp, int nprobe, float coef, const uint32_t* __restrict__ bucket_off,
+        const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ entries,
+        unsigned long long* __restrict__ part, float* __restrict__ pub,
+        float* __restrict__ pbound) {
+    __shared__ __attribute__((aligned(16))) float smem_xy[(MQT + MVT) * MSD];
+    float* Xs = smem_xy;
+    float* Ys = smem_xy + MQT * MSD;
+    __shared__ float xn_s[MQT];
+    __shared__ float yn_s[MVT];
+    __shared__ uint32_t ent_s[MQT];
+    __shared__ int32_t qrow_s[MQT];
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t xcd = blockIdx.x & 7u, rest = blockIdx.x >> 3;
+    const uint32_t item = 4u * ((rest >> 2) * 8u + xcd) + (rest & 3u);
+    if (item >= item_off[nlist]) return;
+    int lo = 0, hi = nlist;
+    while (hi - lo > 1) {
+        int mid = (lo + hi) >> 1;
+        if (item_off[mid] <= item) lo = mid; else hi = mid;
+    }
+    const int l = lo;
+    const uint32_t qb = bucket_off[l] + (item - item_off[l]) * MQT;
+    const int nQ = (int)min((uint32_t)MQT, bucket_off[l + 1] - qb);
+    if (t < MQT) {
+        uint32_t e = t < nQ ? entries[qb + t] : 0u;
+        ent_s[t] = e;
+        qrow_s[t] = t < nQ ? (int32_t)(e / (uint32_t)nprobe) : -1;
+    }
+    const int len = (int)list_len[l];
+    const int64_t row0 = list_off[l];
+    __syncthreads();
+    for (int e = t; e < MQT * 32; e += 256) {
+        const int r = e >> 5, kc = 4 * (e & 31);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int qr = qrow_s[r];
+        if (qr >= 0 && kc < dp) v = *(const float4*)(x + (int64_t)qr * ldx + kc);
+        *(float4*)(Xs + r * MSD + kc) = v;
+    }
+    __syncthreads();
+    if (t < MQT) {
+        float s = 0.f;
+        for (int j = 0; j < dp; j++) s = fmaf(Xs[t * MSD + j], Xs[t * MSD + j], s);
+        xn_s[t] = s;
+    }
+
+    float4 pf[8];
+    auto fetch = [&](int v0n) {
+        const int nvn = min(MVT, len - v0n);
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const int e = t + 256 * s;
+            const int r = e >> 5, kc = 4 * (e & 31);
+            pf[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r < nvn && kc < dp)
+                pf[s] = *(const float4*)(codes + (row0 + v0n + r) * (int64_t)ldc + kc);
+        }
+    };
+    fetch(0);
+
+    ThreadQueue<KT> tq;
+    tq.init();
+    const int bi = w >> 1, bj = w & 1;
+    const int li = lane & 31, lh = lane >> 5;
+    const int dsteps = (dp + 7) >> 3;
+    const int q = t >> 2, s4 = t & 3;
+
+    for (int v0 = 0; v0 < len; v0 += MVT) {
+        const int nv = min(MVT, len - v0);
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const int e = t + 256 * s;
+            *(float4*)(Ys + (e >> 5) * MSD + 4 * (e & 31)) = pf[s];
+        }
+        if (t < MVT) yn_s[t] = t < nv ? ynorm[row0 + v0 + t] : 0.f;
+        __syncthreads();
+        if (v0 + MVT < len) fetch(v0 + MVT);
+        floatx16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc[r] = 0.f;
+        const float* ap = Xs + (32 * bi + li) * MSD + 4 * lh;
+        const float* bp = Ys + (32 * bj + li) * MSD + 4 * lh;
+        for (int s = 0; s < dsteps; s++) {
+            const float4 a = *(const float4*)(ap + 8 * s);
+            const float4 b = *(const float4*)(bp + 8 * s);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+        }
+        __syncthreads();
+        // approx tile -> LDS (aliases the code tile)
+        float* Ds = Ys;
+        const int col = 32 * bj + li;
+        const float ynv = yn_s[col];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int row = 32 * bi + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            float v;
+            if (L2) {
+                v = fmaf(-2.f, acc[r], xn_s[row] + ynv);
+                v = v < 0.f ? 0.f : v;
+            } else {
+                v = -acc[r];
+            }
+            Ds[row * DSS + col] = v;
+        }
+        __syncthreads();
+        if (q < nQ) {
+            if (nv == MVT) {
+#pragma unroll
+                for (int i = 0; i < MVT / 4; i++) {
+                    const int j = s4 + 4 * i;
+                    const float a = Ds[q * DSS + j];
+                    tq.push(((unsigned long long)ordered_f32(a) << 32) | (uint32_t)(v0 + j), KT);
+                }
+            } else {
+                for (int j = s4; j < nv; j += 4) {
+                    const float a = Ds[q * DSS + j];
+                    tq.push(((unsigned long long)ordered_f32(a) << 32) | (uint32_t)(v0 + j), KT);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // thread queue -> (lb key, ub) entries; dropped-candidate bound
+    const float xn = xn_s[q];
+    float bnd = tq.q[KT - 1] != ~0ull ? unordered_f32((uint32_t)(tq.q[KT - 1] >> 32)) : WS_INF;
+    bnd = fminf(bnd, __shfl_xor(bnd, 1));
+    bnd = fminf(bnd, __shfl_xor(bnd, 2));
+    if (q < nQ) {
+        const int64_t e = ent_s[q];
+        unsigned long long* po = part + e * (4 * KT) + s4 * KT;
+        float* pu = pub + e * (4 * KT) + s4 * KT;
+#pragma unroll
+        for (int i = 0; i < KT; i++) {
+            const unsigned long long key = tq.q[i];
+            if (key != ~0ull) {
+                const float a = unordered_f32((uint32_t)(key >> 32));
+                const uint32_t row = (uint32_t)key;
+                const float m = coef * (xn + ynorm[row0 + row]);
+                po[i] = ((unsigned long long)ordered_f32(a - m) << 32) | row;
+                pu[i] = a + m;
+            } else {
+                po[i] = ~0ull;
+                pu[i] = WS_INF;
+            }
+        }
+        if (s4 == 0) pbound[e] = bnd < WS_INF ? bnd - coef * (xn + ynmax[l]) : WS_INF;
+    }
+}
+
+// per-list max row norm (margin of dropped candidates)
+__global__ void k_list_max(const float* __restrict__ yn, const uint32_t* __restrict__ off,
+                           const uint32_t* __restrict__ len, int nlist, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (l >= nlist) return;
+    float m = 0.f;
+    for (uint32_t i = lane; i < len[l]; i += 64) m = fmaxf(m, yn[off[l] + i]);
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) m = fmaxf(m, __shfl_xor(m, s));
+    if (lane == 0) out[l] = m;
+}
+
+// ---------------------------------------------------------------- B
+// One wave per query.  U = k-th smallest upper bound over the kept entries
+// bounds the exact k-th key.  A probe whose dropped bound is <= U "fails":
+// all of its rows are re-ranked.  Every other probe contributes its kept
+// entries with lb <= U.  The exact top-k over that candidate stream (with the
+// reference tie rule, exact_select.h) is the reference result.
+constexpr int RR_CAP = 512;
+
+template <bool L2, int KE>
+struct RerankStream {
+    const unsigned long long* part;  // this query's [nprobe][KE]
+    const float* pub;
+    const int32_t* asg;  // this query's [nprobe]
+    const uint32_t* list_off;
+    const uint32_t* list_len;
+    int nlist, nprobe, d, ldc, lane, nsv;
+    bool overflow;
+    unsigned long long fmask;
+    float U;
+    const uint32_t* surv;
+    const float* xq;
+    const float* codes;
+    const int64_t* ids;
+
+    __device__ __forceinline__ bool entry_ok(int r) const {
+        const int lst = asg[r];
+        return lst >= 0 && lst < nlist && list_len[lst] > 0;
+    }
+    __device__ __forceinline__ bool survivor(int c) const {
+        const int r = c / KE;
+        if ((fmask >> r) & 1ull) return false;
+        if (!entry_ok(r)) return false;
+        const unsigned long long key = part[c];
+        return key != ~0ull && unordered_f32((uint32_t)(key >> 32)) <= U;
+    }
+    __device__ __forceinline__ void eval(int r, uint32_t row, float& k1, long long& k2, long long& rank) const {
+        const int64_t grow = (int64_t)list_off[asg[r]] + row;
+        const float* yr = codes + grow * ldc;
+        const float dis = L2 ? seq_l2(xq, yr, d) : seq_ip(xq, yr, d);
+        to_key(L2 ? 1 : 0, dis, (long long)ids[grow], k1, k2);
+        rank = ((long long)r << 32) | row;
+    }
+    template <class F>
+    __device__ __forceinline__ void for_each(F f) const {
+        // (1) surviving kept entries of the non-failing probes
+        if (!overflow) {
+            for (int s0 = 0; s0 < nsv; s0 += 64) {
+                float k1 = WS_INF;
+                long long k2 = WS_NOID, rank = 0;
+                bool ok = s0 + lane < nsv;
+                if (ok) {
+                    const int c = (int)surv[s0 + lane];
+                    eval(c / KE, (uint32_t)part[c], k1, k2, rank);
+                    ok = key_admissible(k1);
+                }
+                f(ok, k1, k2, rank);
+            }
+        } else {
+            const int total = nprobe * KE;
+            for (int c0 = 0; c0 < total; c0 += 64) {
+                const int c = c0 + lane;
+                float k1 = WS_INF;
+                long long k2 = WS_NOID, rank = 0;
+                bool ok = c < total && survivor(c);
+                if (__ballot(ok) == 0ull) continue;
+                if (ok) {
+                    eval(c / KE, (uint32_t)part[c], k1, k2, rank);
+                    ok = key_admissible(k1);
+                }
+                f(ok, k1, k2, rank);
+            }
+        }
+        // (2) every row of the failing probes
+        unsigned long long m = fmask;
+        while (m) {
+            const int r = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const int len = (int)list_len[asg[r]];
+            for (int v0 = 0; v0 < len; v0 += 64) {
+                float k1 = WS_INF;
+                long long k2 = WS_NOID, rank = 0;
+                bool ok = v0 + lane < len;
+                if (ok) {
+                    eval(r, (uint32_t)(v0 + lane), k1, k2, rank);
+                    ok = key_admissible(k1);
+                }
+                f(ok, k1, k2, rank);
+            }
+        }
+    }
+};
+
+template <bool L2, int KE>
+__global__ __launch_bounds__(256) void k_ivf_rerank(
+        const unsigned long long* __restrict__ part, const float* __restrict__ pub,
+        const float* __restrict__ pbound, const int32_t* __restrict__ assign,
+        const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
+        const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
+        const int64_t* __restrict__ ids, int d, int64_t n, int nprobe, int k,
+        float* __restrict__ D, int64_t* __restrict__ I, uint32_t* __restrict__ stats) {
+    __shared__ uint32_t surv[4][RR_CAP];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t q0 = (int64_t)blockIdx.x * 4 + w;
+    const bool valid = q0 < n;
+    const int64_t q = valid ? q0 : 0;
+    RerankStream<L2, KE> st;
+    st.part = part + q * nprobe * KE;
+    st.pub = pub + q * nprobe * KE;
+    st.asg = assign + q * nprobe;
+    st.list_off = list_off;
+    st.list_len = list_len;
+    st.nlist = nlist;
+    st.nprobe = valid ? nprobe : 0;
+    st.d = d;
+    st.ldc = ldc;
+    st.lane = lane;
+    st.xq = x + q * ldx;
+    st.codes = codes;
+    st.ids = ids;
+    st.fmask = 0ull;
+    st.U = WS_INF;
+    const int total = st.nprobe * KE;
+    // U: k-th smallest upper bound
+    float qd = WS_INF, td = WS_INF;
+    long long qi = WS_NOID, ti = WS_NOID;
+    for (int c0 = 0; c0 < total; c0 += 64) {
+        const int c = c0 + lane;
+        const bool ok = c < total && st.entry_ok(c / KE);
+        wave_offer(qd, qi, ok ? st.pub[c] : WS_INF, ok ? (long long)c : WS_NOID, td, ti, k,
+                   lane);
+    }
+    const float U = __shfl(qd, k - 1);
+    st.U = U;
+    // failing probes (nprobe <= 64: one ballot)
+    {
+        bool fl = false;
+        if (lane < st.nprobe && st.entry_ok(lane)) {
+            const float pb = pbound[q * nprobe + lane];
+            fl = pb < WS_INF && pb <= U;
+        }
+        st.fmask = __ballot(fl);
+    }
+    // compact the surviving entries
+    int ns = 0;
+    for (int c0 = 0; c0 < total; c0 += 64) {
+        const int c = c0 + lane;
+        const bool sv = c < total && st.survivor(c);
+        const unsigned long long m = __ballot(sv);
+        const int pos = ns + __popcll(m & ((1ull << lane) - 1ull));
+        if (sv && pos < RR_CAP) surv[w][pos] = (uint32_t)c;
+        ns += __popcll(m);
+    }
+    st.overflow = ns > RR_CAP;
+    st.nsv = ns;
+    st.surv = surv[w];
+    exact_topk_resolve(st, k, L2 ? 1 : 0, lane, valid, D + q * k, I + q * k);
+    if (stats && valid && lane == 0) {
+        atomicAdd(&stats[0], (uint32_t)min(ns, RR_CAP));
+        atomicAdd(&stats[1], (uint32_t)__popcll(st.fmask));
+        atomicAdd(&stats[2], st.overflow ? 1u : 0u);
+    }
+}
+
+// ---------------------------------------------------------------- C
+// Exact re-scan of flagged queries: every row of every probed list.
+template <bool L2>
+struct FullStream {
+    const int32_t* asg;
+    const uint32_t* list_off;
+    const uint32_t* list_len;
+    int nlist, nprobe, d, ldc, lane;
+    const float* xq;
+    const float* codes;
+    const int64_t* ids;
+    template <class F>
+    __device__ __forceinline__ void for_each(F f) const {
+        for (int r = 0; r < nprobe; r++) {
+            const int lst = asg[r];
+            if (lst < 0 || lst >= nlist) continue;
+            const int len = (int)list_len[lst];
+            for (int v0 = 0; v0 < len; v0 += 64) {
+                float k1 = WS_INF;
+                long long k2 = WS_NOID, rank = 0;
+                bool ok = v0 + lane < len;
+                if (ok) {
+                    const int64_t grow = (int64_t)list_off[lst] + v0 + lane;
+                    const float* yr = codes + grow * ldc;
+                    const float dis = L2 ? seq_l2(xq, yr, d) : seq_ip(xq, yr, d);
+                    to_key(L2 ? 1 : 0, dis, (long long)ids[grow], k1, k2);
+                    ok = key_admissible(k1);
+                    rank = ((long long)r << 32) | (uint32_t)(v0 + lane);
+                }
+                f(ok, k1, k2, rank);
+            }
+        }
+    }
+};
+
+template <bool L2>
+__global__ __launch_bounds__(64) void k_ivf_exact_fallback(
+        const uint32_t* __restrict__ flags, const int32_t* __restrict__ assign,
+        const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
+        const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
+        const int64_t* __restrict__ ids, int d, int nprobe, int k, float* __restrict__ D,
+        int64_t* __restrict__ I) {
+    const int64_t q = blockIdx.x;
+    if (flags[q] == 0u) return;
+    FullStream<L2> st{assign + q * nprobe, list_off, list_len, nlist, nprobe, d, ldc,
+                      (int)threadIdx.x, x + q * ldx, codes, ids};
+    exact_topk_resolve(st, k, L2 ? 1 : 0, (int)threadIdx.x, true, D + q * k, I + q * k);
+}
+
+void ivf_exact_fallback(const uint32_t* flags, const int32_t* assign, const uint32_t* list_off,
+                        const uint32_t* list_len, int nlist, const float* x, int ldx,
+                        const float* codes, int ldc, const int64_t* ids, int d, int64_t n,
+                        int nprobe, int k, int metric_l2, float* D, int64_t* I, hipStream_t s) {
+    if (n <= 0) return;
+    if (metric_l2)
+        k_ivf_exact_fallback<true><<<dim3((unsigned)n), dim3(64), 0, s>>>(
+                flags, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, nprobe, k,
+                D, I);
+    else
+        k_ivf_exact_fallback<false><<<dim3((unsigned)n), dim3(64), 0, s>>>(
+                flags, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, nprobe, k,
+                D, I);
+    HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------- host
+void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* list_len,
+                    int nlist, float* out, hipStream_t s) {
+    if (nlist <= 0) return;
+    k_list_max<<<dim3((unsigned)cdiv(nlist, 4)), dim3(256), 0, s>>>(yn, list_off, list_len,
+                                                                    nlist, out);
+    HIP_LAUNCH_CHECK();
+}
+
+int ivf_mfma_kq(int k, int dp) {
+    // entries kept per (query, list) = 4 threads x KT
+    if (dp > 128 || k > 32) return 0;
+    return 4 * (k <= 2 ? 2 : k <= 12 ? 4 : 8);
+}
+
+void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc,
+                        const int64_t* ids, const float* ynorm, const float* ynmax,
+                        const uint32_t* list_off, const uint32_t* list_len, int nlist, int d,
+                        int dp, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
+                        int64_t max_items, const int32_t* assign, unsigned long long* part,
+                        float* pub, float* pbound, uint32_t* stats, float* D, int64_t* I,
+                        KernelTimes* kt, hipStream_t s) {
+    if (n <= 0) return;
+    const int KE = ivf_mfma_kq(k, dp);
+    FAISS_THROW_IF_NOT(KE > 0);
+    FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldc % 4 == 0);
+    FAISS_THROW_IF_NOT(nprobe <= 64);
+    const int64_t grid = (int64_t)roundup((size_t)max_items, 32);
+    FAISS_THROW_IF_NOT(grid < (1ll << 31));
+    const bool l2 = metric_l2 != 0;
+    // margin coefficient (2x the derived bound)
+    const double u = 1.0 / 16777216.0;
+    const double g = d * u / (1.0 - d * u);
+    const float coef = (float)(2.0 * (l2 ? (4 * g + 7 * u) : (2 * g + 2 * u)));
+    {
+        ScopedKernelTimer tm(kt, "ivf_flat_scan", 0.0, s);
+#define LAUNCH_A(L2V, KTV)                                                                    \
+    k_ivf_mfma_filter<L2V, KTV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(                   \
+            x, ldx, codes, ldc, ynorm, ynmax, list_off, list_len, nlist, dp, nprobe, coef,    \
+            b.bucket_off, b.item_off, b.entries, part, pub, pbound)
+#define DISPATCH(M, L2V)                  \
+    do {                                  \
+        if (KE == 8) M(L2V, 2);           \
+        else if (KE == 16) M(L2V, 4);     \
+        else M(L2V, 8);                   \
+    } while (0)
+        if (l2) DISPATCH(LAUNCH_A, true);
+        else DISPATCH(LAUNCH_A, false);
+        HIP_LAUNCH_CHECK();
+    }
+    {
+        ScopedKernelTimer tm(kt, "ivf_rerank", 0.0, s);
+#define LAUNCH_B(L2V, KTV)                                                                    \
+    k_ivf_rerank<L2V, 4 * KTV><<<dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s>>>(              \
+            part, pub, pbound, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, \
+            n, nprobe, k, D, I, stats)
+        if (l2) DISPATCH(LAUNCH_B, true);
+        else DISPATCH(LAUNCH_B, false);
+        HIP_LAUNCH_CHECK();
+#undef LAUNCH_A
+#undef LAUNCH_B
+#undef DISPATCH
+    }
+}
+
+}  // namespace kern
+}  // namespace faiss_amd

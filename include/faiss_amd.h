@@ -239,6 +239,9 @@ struct IndexIVF : Index {
 
 struct IndexIVFFlat : IndexIVF {
     IndexIVFFlat(Index* quantizer, size_t d, size_t nlist, MetricType metric = METRIC_L2);
+    // scan algorithm: 0 = auto (MFMA filter + exact re-rank when eligible),
+    // 1 = direct exact VALU scan.  Both give identical results.
+    int scan_mode = 0;
     void encode_vectors(idx_t n, const float* x, const idx_t* list_nos,
                         uint8_t* codes) const override;
     void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
@@ -246,6 +249,10 @@ struct IndexIVFFlat : IndexIVF {
                                    float* distances, idx_t* labels,
                                    hipStream_t stream) const override;
     void reconstruct(idx_t key, float* recons) const override;
+
+   protected:
+    void upload_extra() const override;
+    mutable DeviceBuffer d_ynorm_, d_ynmax_, s_part_, s_flags_;
 };
 
 // faiss/impl/ProductQuantizer.h:29-186

@@ -171,3 +171,63 @@ def test_device_entry_points_match_host(amd, orc, cfg1):
     for p in (px, pd, pi):
         hip.hipFree(p)
     assert_same_results(D2, I2, D, I)
+
+
+# --- the two IVF-Flat scan algorithms (direct exact VALU scan, fp32-MFMA
+# filter + exact re-rank + flagged fallback) must give identical results.
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 10, 16, 24])
+@pytest.mark.parametrize("nprobe", [8, 32])
+def test_scan_modes_identical(amd, orc, cfg1, monkeypatch, k, nprobe):
+    idx, xb, xq = cfg1
+    idx.nprobe = nprobe
+    q = xq[:300]
+    monkeypatch.setenv("FAISS_AMD_IVF_SCAN", "mfma")
+    Dm, Im = idx.search(q, k)
+    monkeypatch.setenv("FAISS_AMD_IVF_SCAN", "exact")
+    De, Ie = idx.search(q, k)
+    assert_same_results(Dm, Im, De, Ie)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(q, k, nprobe, nslices=1)
+    assert_same_results(Dm, Im, Dr, Ir)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("metric", ["l2", "ip"])
+@pytest.mark.parametrize("mode", ["mfma", "exact"])
+def test_scan_duplicates_reference_tie_rule(amd, orc, gpu, monkeypatch, metric, mode):
+    # 25 copies of every vector: long runs of equal distances cross the k
+    # boundary.  The reference heap (strict admission, eviction by (dis, id))
+    # keeps an arrival-order-dependent subset of the tied candidates (for IP
+    # not the lexicographic one); both scan paths must reproduce it.
+    d, nu, copies, nlist = 64, 160, 25, 8
+    base = rand(orc, nu, d, 31)
+    perm = np.random.default_rng(0).permutation(nu * copies)
+    xb = np.ascontiguousarray(np.repeat(base, copies, axis=0)[perm])
+    if metric == "l2":
+        quant, mt = amd.IndexFlatL2(d), amd.METRIC_L2
+    else:
+        quant, mt = amd.IndexFlatIP(d), amd.METRIC_INNER_PRODUCT
+    idx = amd.IndexIVFFlat(quant, d, nlist, mt)
+    idx.train(xb)
+    idx.add(xb)
+    idx.nprobe = 3
+    xq = np.ascontiguousarray(np.concatenate([base[:40], rand(orc, 40, d, 32)]))
+    ref = orc.IVFOracle.from_index(idx)
+    monkeypatch.setenv("FAISS_AMD_IVF_SCAN", mode)
+    for k in (5, 10, 20, 40):
+        D, I = idx.search(xq, k)
+        Dr, Ir, _, _ = ref.search(xq, k, 3, nslices=1)
+        assert_same_results(D, I, Dr, Ir)
+
+
+@pytest.mark.gpu
+def test_mfma_scan_d128_bench_shape(amd, orc, gpu):
+    # the bench's shape (d=128, k=10, nprobe=32) at a size the oracle finishes fast
+    idx, xb = build_ivf(amd, orc, 128, 200_000, 1024)
+    idx.nprobe = 32
+    xq = rand(orc, 2000, 128, 5678)
+    D, I = idx.search(xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, 32, nslices=1)
+    assert_same_results(D, I, Dr, Ir)
