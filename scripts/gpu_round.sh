@@ -19,11 +19,15 @@ if [ -n "$PROFILE" ]; then
 fi
 if [ -n "$PMC" ]; then
   BA="--steps 2 --warmup 1 --no-cpu-baseline --recall-queries 0 ${PMC_BENCH_ARGS:-}"
+  KR=${PMC_KERNEL:-ivf}
   i=0
-  for ctrs in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"; do
+  for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
+      "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS" \
+      "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_INST_LDS"; do
     i=$((i+1))
-    timeout -k 10 600 rocprofv3 --pmc $ctrs --output-format csv -d gpurun_out/pmc$i -o pmc -- python bench.py $BA > gpurun_out/pmc$i.log 2>&1
+    timeout -k 10 600 rocprofv3 --pmc $ctrs --kernel-include-regex "$KR" --output-format csv -d gpurun_out/pmc$i -o pmc -- python bench.py $BA > gpurun_out/pmc$i.log 2>&1
     rc=$?; echo "pmc$i rc=$rc"; ok $rc || exit $rc
   done
+  python scripts/pmc_summary.py gpurun_out > gpurun_out/pmc_summary.txt 2>&1; cat gpurun_out/pmc_summary.txt
 fi
 exit 0
