@@ -207,7 +207,7 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     sync_device();
     const double t0 = now_ms();
     // bound the partial-result scratch to ~1 GiB per chunk
-    const size_t per_q = np * (size_t)k * 12 + np * 12;
+    const size_t per_q = np * (size_t)std::max<idx_t>(k, 32) * 12 + np * 16;
     idx_t qchunk = std::max<idx_t>(1, (idx_t)(((size_t)1 << 30) / per_q));
     qchunk = std::min<idx_t>(qchunk, n);
     std::lock_guard<std::recursive_mutex> g(mu_);
@@ -294,6 +294,15 @@ void IndexIVFFlat::upload_extra() const {
         kern::row_norms(d_codes_.as<float>(), arena_rows_, d, l, d_ynorm_.as<float>(), s);
     kern::ivf_list_ynmax(d_ynorm_.as<float>(), d_list_off_.as<uint32_t>(),
                          d_list_len_.as<uint32_t>(), (int)nlist, d_ynmax_.as<float>(), s);
+    // bf16 hi/lo image of the arena for the MFMA filter (same bytes as f32)
+    if (kern::ivf_mfma_kq(1, d) > 0) {
+        const int DB = (int)roundup((size_t)d, 16);
+        d_cbf_.reserve(std::max<size_t>(arena_rows_, 1) * 2 * DB * 2);
+        kern::split_bf16(d_codes_.as<float>(), arena_rows_, d, l, DB, d_cbf_.ptr, s);
+        size_t mx = 0;
+        for (size_t li = 0; li < nlist; li++) mx = std::max(mx, invlists->list_size(li));
+        obits_ = kern::ivf_bf3_obits((uint32_t)std::min<size_t>(mx, 0xffffffffu));
+    }
 }
 
 void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
@@ -318,7 +327,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     int mode = scan_mode;
     if (env && !strcmp(env, "exact")) mode = 1;
     if (env && !strcmp(env, "mfma")) mode = 0;
-    const int KQ = kern::ivf_mfma_kq((int)k, l);
+    const int KQ = obits_ <= 14 ? kern::ivf_mfma_kq((int)k, d) : 0;
     const bool l2 = metric_type == METRIC_L2;
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(n, 4));
     if (mode == 0 && KQ > 0) {
@@ -327,10 +336,10 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
         s_pk2_.reserve(sizeof(float) * n * np);       // dropped-candidate bounds
         const bool dbg = getenv("FAISS_AMD_IVF_STATS") != nullptr;
         if (dbg) HIP_CHECK(hipMemsetAsync(s_flags_.ptr, 0, 4 * sizeof(uint32_t), s));
-        kern::ivf_flat_scan_mfma(x, ldx, d_codes_.as<float>(), l, d_ids_.as<int64_t>(),
-                                 d_ynorm_.as<float>(), d_ynmax_.as<float>(),
+        kern::ivf_flat_scan_mfma(x, ldx, d_codes_.as<float>(), l, d_cbf_.ptr,
+                                 d_ids_.as<int64_t>(), d_ynorm_.as<float>(), d_ynmax_.as<float>(),
                                  d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(),
-                                 (int)nlist, d, l, n, np, (int)k, l2, b, max_items, assign,
+                                 (int)nlist, d, obits_, n, np, (int)k, l2, b, max_items, assign,
                                  s_part_.as<unsigned long long>(), s_pk1_.as<float>(),
                                  s_pk2_.as<float>(), dbg ? s_flags_.as<uint32_t>() : nullptr,
                                  distances, labels, &ktimes, s);

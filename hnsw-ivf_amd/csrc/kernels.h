@@ -71,16 +71,22 @@ void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const i
                    int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b, int64_t max_items,
                    float* part_k1, long long* part_k2, hipStream_t s);
 
-// fp32-MFMA filter + exact re-rank variant (kernels_ivf_mfma.hip); results
-// are identical to ivf_flat_scan + ivf_merge.  ivf_mfma_kq = entries kept
-// per (query, list) (part/pub stride); 0 = not eligible (k > 32 or d > 128).
-int ivf_mfma_kq(int k, int dp);
+// bf16x3-MFMA filter + certified exact re-rank (kernels_ivf_mfma.hip);
+// results are identical to ivf_flat_scan + ivf_merge (+ ivf_exact_fallback).
+// ivf_mfma_kq = entries kept per (query, list); 0 = not eligible
+// (k > 32 or roundup(d, 16) > 128).
+int ivf_mfma_kq(int k, int d);
+int ivf_bf3_obits(uint32_t max_list_len);  // ordinal bits of the 32-bit keys
+double ivf_bf3_coef(int d);                // margin coefficient
+// f32 arena [rows][ldc] -> bf16 hi/lo arena [rows][2 * roundup(d, 16)]
+void split_bf16(const float* codes, int64_t rows, int d, int ldc, int DB, void* out,
+                hipStream_t s);
 void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* list_len,
                     int nlist, float* out, hipStream_t s);
-void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc,
+void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, const void* cbf,
                         const int64_t* ids, const float* ynorm, const float* ynmax,
                         const uint32_t* list_off, const uint32_t* list_len, int nlist, int d,
-                        int dp, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
+                        int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
                         int64_t max_items, const int32_t* assign, unsigned long long* part,
                         float* pub, float* pbound, uint32_t* stats, float* D, int64_t* I,
                         KernelTimes* kt, hipStream_t s);

@@ -26,6 +26,7 @@
 //   => |approx - exact| <= (4g + 7u)(|x|^2 + |y|^2); we use twice that.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 
 #include "common.h"
@@ -36,11 +37,6 @@
 namespace faiss_amd {
 namespace kern {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-constexpr int MQT = 64;       // queries per work item
-constexpr int MVT = 64;       // codes per tile
-constexpr int MSD = 132;      // LDS row stride (floats)
 
 __device__ __forceinline__ float seq_l2(const float* __restrict__ a, const float* __restrict__ b,
                                         int d) {
@@ -78,30 +74,89 @@ __device__ __forceinline__ float seq_ip(const float* __restrict__ a, const float
 }
 
 // ---------------------------------------------------------------- A
+// Filter on bf16x3 MFMA (v_mfma_f32_32x32x16_bf16).  Every f32 value is
+// split x = xh + xl (+ xr), xh = bf16(x), xl = bf16(x - xh), |xr| <= 2^-16|x|;
+// <x,y> ~ xh.yh + xh.yl + xl.yh (products exact in f32, accumulated in f32).
+//   |ip_approx - ip| <= (3.1 * 2^-16 + 3 d u) sum|x_i y_i|
+// so with the f32 rounding of the norms, of the approx formula and of the
+// exact sequential evaluation (same analysis as above):
+//   |approx - exact| <= (3.1 * 2^-16 + (6d + 8) u) (|x|^2 + |y|^2)
+// The kernel uses twice that (host: ivf_bf3_coef) plus 1e-30 absolute.
+//
+// Roles: A = codes (rows = 32 codes per wave), B = queries (columns = 32
+// queries per wave, held in registers for the whole work item).  A lane's 16
+// accumulators are ONE query against 16 codes, so the per-thread queues are
+// fed straight from the MFMA result: 4 threads (2 waves x 2 lane halves) per
+// query, no LDS transpose.
+//
+// Keys are 32 bit: ordered_f32(approx) with the low `obits` bits replaced by
+// the thread-local candidate ordinal (tile << 4 | r).  The truncation only
+// widens the [lb, ub] interval (decoded with the low bits cleared / set).
+//
 // Per (query, list) output, 4*KT entries (4 threads x KT keys each):
-//   part[e][i] = ordered_f32(lb) << 32 | row   (lb = approx - B, ~0 = empty)
-//   pub[e][i]  = approx + B                     (upper bound of the exact key)
-//   pbound[e]  = lower bound of the exact key of every candidate of the list
-//                that was dropped (min over the 4 threads of their KT-th
-//                approx, minus the list's largest margin); +inf if none.
-constexpr int DSS = MVT + 4;  // approx tile stride: 16 queries x 4 threads hit 64 banks
+//   part[e][i] = ordered_f32(lb) << 32 | row   (~0 = empty)
+//   pub[e][i]  = ub                             (upper bound of the exact key)
+//   pbound[e]  = lower bound of the exact key of every dropped candidate of
+//                the list (min over the 4 threads of their KT-th key, minus
+//                the list's largest margin); +inf if none was dropped.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int BQ = 64;    // queries per work item
+constexpr int BV = 64;    // codes per tile
+constexpr int BDM = 128;  // max padded dim (multiple of 16)
+
+template <int KT>
+struct ThreadQueue32 {
+    uint32_t q[KT];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int i = 0; i < KT; i++) q[i] = 0xffffffffu;
+    }
+    // branchless insertion, keeps the KT smallest
+    __device__ __forceinline__ void push(uint32_t c) {
+#pragma unroll
+        for (int i = KT - 1; i > 0; i--) q[i] = c < q[i - 1] ? q[i - 1] : min(c, q[i]);
+        q[0] = min(c, q[0]);
+    }
+};
+
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& l) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const __bf16 hb = (__bf16)v[j];
+        h[j] = hb;
+        l[j] = (__bf16)(v[j] - (float)hb);
+    }
+}
+
+// f32 arena -> bf16 hi/lo arena: row r = hi[DB] | lo[DB], zero beyond d
+__global__ void k_split_bf16(const float* __restrict__ codes, int64_t rows, int d, int ldc, int DB,
+                             __bf16* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * DB) return;
+    const int64_t r = i / DB;
+    const int j = (int)(i - r * DB);
+    const float v = j < d ? codes[r * ldc + j] : 0.f;
+    const __bf16 h = (__bf16)v;
+    out[r * 2 * DB + j] = h;
+    out[r * 2 * DB + DB + j] = (__bf16)(v - (float)h);
+}
 
 template <bool L2, int KT>
-__global__ __launch_bounds__(256, 2) void k_ivf_mfma_filter(
-        const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
+__global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
+        const float* __restrict__ x, int ldx, int d, const __bf16* __restrict__ cbf, int DB,
         const float* __restrict__ ynorm, const float* __restrict__ ynmax,
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
-        int dp, int nprobe, float coef, const uint32_t* __restrict__ bucket_off,
+        int nprobe, float coef, int obits, const uint32_t* __restrict__ bucket_off,
         const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ entries,
         unsigned long long* __restrict__ part, float* __restrict__ pub,
         float* __restrict__ pbound) {
-    __shared__ __attribute__((aligned(16))) float smem_xy[(MQT + MVT) * MSD];
-    float* Xs = smem_xy;
-    float* Ys = smem_xy + MQT * MSD;
-    __shared__ float xn_s[MQT];
-    __shared__ float yn_s[MVT];
-    __shared__ uint32_t ent_s[MQT];
-    __shared__ int32_t qrow_s[MQT];
+    // two code tiles (double buffer), row stride CSB bytes = 4*DB + 16
+    __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * (4 * BDM + 16)];
+    __shared__ uint32_t ent_s[BQ];
+    __shared__ int32_t qrow_s[BQ];
+    __shared__ float bnd_s[BQ][4];
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t xcd = blockIdx.x & 7u, rest = blockIdx.x >> 3;
@@ -109,137 +164,163 @@ __global__ __launch_bounds__(256, 2) void k_ivf_mfma_filter(
     if (item >= item_off[nlist]) return;
     int lo = 0, hi = nlist;
     while (hi - lo > 1) {
-        int mid = (lo + hi) >> 1;
+        const int mid = (lo + hi) >> 1;
         if (item_off[mid] <= item) lo = mid; else hi = mid;
     }
     const int l = lo;
-    const uint32_t qb = bucket_off[l] + (item - item_off[l]) * MQT;
-    const int nQ = (int)min((uint32_t)MQT, bucket_off[l + 1] - qb);
-    if (t < MQT) {
-        uint32_t e = t < nQ ? entries[qb + t] : 0u;
+    const uint32_t qb = bucket_off[l] + (item - item_off[l]) * BQ;
+    const int nQ = (int)min((uint32_t)BQ, bucket_off[l + 1] - qb);
+    if (t < BQ) {
+        const uint32_t e = t < nQ ? entries[qb + t] : 0u;
         ent_s[t] = e;
         qrow_s[t] = t < nQ ? (int32_t)(e / (uint32_t)nprobe) : -1;
     }
     const int len = (int)list_len[l];
     const int64_t row0 = list_off[l];
+    const int CSB = 4 * DB + 16;     // LDS row stride (bytes)
+    const int RU = DB / 4;           // uint4 per code row (hi + lo)
+    const int nsteps = DB / 16;
+    const int bi = w >> 1, bj = w & 1;
+    const int li = lane & 31, lh = lane >> 5;
+    const int slot = 2 * bi + lh;    // this thread's share of its query's codes
+    const int qloc = 32 * bj + li;   // this thread's query (0..63)
     __syncthreads();
-    for (int e = t; e < MQT * 32; e += 256) {
-        const int r = e >> 5, kc = 4 * (e & 31);
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int qr = qrow_s[r];
-        if (qr >= 0 && kc < dp) v = *(const float4*)(x + (int64_t)qr * ldx + kc);
-        *(float4*)(Xs + r * MSD + kc) = v;
-    }
-    __syncthreads();
-    if (t < MQT) {
-        float s = 0.f;
-        for (int j = 0; j < dp; j++) s = fmaf(Xs[t * MSD + j], Xs[t * MSD + j], s);
-        xn_s[t] = s;
+
+    // ---- query fragments (B operand): registers for the whole work item
+    bf16x8 bh[BDM / 16], bl[BDM / 16];
+    float xn = 0.f;
+    {
+        const int qr = qrow_s[qloc];
+        const float* xr = x + (int64_t)(qr < 0 ? 0 : qr) * ldx;
+#pragma unroll
+        for (int s = 0; s < BDM / 16; s++) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int kk = 16 * s + 8 * lh + j;
+                v[j] = (qr >= 0 && s < nsteps && kk < d) ? xr[kk] : 0.f;
+            }
+            split8(v, bh[s], bl[s]);
+#pragma unroll
+            for (int j = 0; j < 8; j++) xn = fmaf(v[j], v[j], xn);
+        }
+        // |x|^2 over both lane halves (any summation order: the margin
+        // covers its rounding)
+        xn += __shfl_xor(xn, 32);
     }
 
-    float4 pf[8];
+    // ---- code tiles: global -> registers -> LDS
+    uint4 pf[8];
     auto fetch = [&](int v0n) {
-        const int nvn = min(MVT, len - v0n);
+        const int nvn = min(BV, len - v0n);
 #pragma unroll
         for (int s = 0; s < 8; s++) {
             const int e = t + 256 * s;
-            const int r = e >> 5, kc = 4 * (e & 31);
-            pf[s] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r < nvn && kc < dp)
-                pf[s] = *(const float4*)(codes + (row0 + v0n + r) * (int64_t)ldc + kc);
+            const int r = e / RU, c = e - r * RU;
+            pf[s] = make_uint4(0u, 0u, 0u, 0u);
+            if (e < BV * RU && r < nvn)
+                pf[s] = *(const uint4*)(cbf + (row0 + v0n + r) * (int64_t)(2 * DB) + 8 * c);
+        }
+    };
+    auto stash = [&](int buf) {
+        uint8_t* T = tiles + buf * BV * CSB;
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const int e = t + 256 * s;
+            const int r = e / RU, c = e - r * RU;
+            if (e < BV * RU) *(uint4*)(T + r * CSB + 16 * c) = pf[s];
         }
     };
     fetch(0);
+    stash(0);
+    if (BV < len) fetch(BV);
+    __syncthreads();
 
-    ThreadQueue<KT> tq;
+    ThreadQueue32<KT> tq;
     tq.init();
-    const int bi = w >> 1, bj = w & 1;
-    const int li = lane & 31, lh = lane >> 5;
-    const int dsteps = (dp + 7) >> 3;
-    const int q = t >> 2, s4 = t & 3;
+    const uint32_t lowmask = (1u << obits) - 1u;
+    const float* ynl = ynorm + row0;
 
-    for (int v0 = 0; v0 < len; v0 += MVT) {
-        const int nv = min(MVT, len - v0);
-#pragma unroll
-        for (int s = 0; s < 8; s++) {
-            const int e = t + 256 * s;
-            *(float4*)(Ys + (e >> 5) * MSD + 4 * (e & 31)) = pf[s];
+    for (int v0 = 0, tile = 0; v0 < len; v0 += BV, tile++) {
+        const int buf = tile & 1;
+        // next tile into the other buffer (its readers finished before the
+        // barrier that ended the previous iteration), then prefetch the one after
+        if (v0 + BV < len) {
+            stash(buf ^ 1);
+            if (v0 + 2 * BV < len) fetch(v0 + 2 * BV);
         }
-        if (t < MVT) yn_s[t] = t < nv ? ynorm[row0 + v0 + t] : 0.f;
-        __syncthreads();
-        if (v0 + MVT < len) fetch(v0 + MVT);
+        // code norms of this lane's 16 rows: rows 32bi + 4lh + 8g + (0..3)
+        float4 yq[4];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const int cr = v0 + 32 * bi + 4 * lh + 8 * g;
+            yq[g] = cr < len ? *(const float4*)(ynl + cr) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         floatx16 acc;
 #pragma unroll
         for (int r = 0; r < 16; r++) acc[r] = 0.f;
-        const float* ap = Xs + (32 * bi + li) * MSD + 4 * lh;
-        const float* bp = Ys + (32 * bj + li) * MSD + 4 * lh;
-        for (int s = 0; s < dsteps; s++) {
-            const float4 a = *(const float4*)(ap + 8 * s);
-            const float4 b = *(const float4*)(bp + 8 * s);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+        const uint8_t* Arow = tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh;
+#pragma unroll
+        for (int s = 0; s < BDM / 16; s++) {
+            if (s < nsteps) {
+                const bf16x8 ah = *(const bf16x8*)(Arow + 32 * s);
+                const bf16x8 al = *(const bf16x8*)(Arow + 2 * DB + 32 * s);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
+            }
         }
-        __syncthreads();
-        // approx tile -> LDS (aliases the code tile)
-        float* Ds = Ys;
-        const int col = 32 * bj + li;
-        const float ynv = yn_s[col];
+        // approx -> 32-bit keys -> thread queue
+        const uint32_t ordbase = (uint32_t)tile << 4;
+        const bool full = v0 + BV <= len;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
-            const int row = 32 * bi + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            float v;
-            if (L2) {
-                v = fmaf(-2.f, acc[r], xn_s[row] + ynv);
-                v = v < 0.f ? 0.f : v;
-            } else {
-                v = -acc[r];
+            const int g = r >> 2, c = r & 3;
+            const float yv = c == 0 ? yq[g].x : c == 1 ? yq[g].y : c == 2 ? yq[g].z : yq[g].w;
+            const float a = L2 ? fmaf(-2.f, acc[r], xn + yv) : -acc[r];
+            uint32_t key = (ordered_f32(a) & ~lowmask) | (ordbase | (uint32_t)r);
+            if (!full) {
+                const int cr = v0 + 32 * bi + 4 * lh + 8 * g + c;
+                key = cr < len ? key : 0xffffffffu;
             }
-            Ds[row * DSS + col] = v;
-        }
-        __syncthreads();
-        if (q < nQ) {
-            if (nv == MVT) {
-#pragma unroll
-                for (int i = 0; i < MVT / 4; i++) {
-                    const int j = s4 + 4 * i;
-                    const float a = Ds[q * DSS + j];
-                    tq.push(((unsigned long long)ordered_f32(a) << 32) | (uint32_t)(v0 + j), KT);
-                }
-            } else {
-                for (int j = s4; j < nv; j += 4) {
-                    const float a = Ds[q * DSS + j];
-                    tq.push(((unsigned long long)ordered_f32(a) << 32) | (uint32_t)(v0 + j), KT);
-                }
-            }
+            tq.push(key);
         }
         __syncthreads();
     }
-    // thread queue -> (lb key, ub) entries; dropped-candidate bound
-    const float xn = xn_s[q];
-    float bnd = tq.q[KT - 1] != ~0ull ? unordered_f32((uint32_t)(tq.q[KT - 1] >> 32)) : WS_INF;
-    bnd = fminf(bnd, __shfl_xor(bnd, 1));
-    bnd = fminf(bnd, __shfl_xor(bnd, 2));
-    if (q < nQ) {
-        const int64_t e = ent_s[q];
-        unsigned long long* po = part + e * (4 * KT) + s4 * KT;
-        float* pu = pub + e * (4 * KT) + s4 * KT;
+
+    // ---- outputs
+    const bool qvalid = qloc < nQ;
+    const float bnd = tq.q[KT - 1] != 0xffffffffu
+                              ? unordered_f32(tq.q[KT - 1] & ~lowmask)
+                              : WS_INF;
+    bnd_s[qloc][slot] = bnd;
+    __syncthreads();
+    if (qvalid) {
+        const int64_t e = ent_s[qloc];
+        unsigned long long* po = part + e * (4 * KT) + slot * KT;
+        float* pu = pub + e * (4 * KT) + slot * KT;
 #pragma unroll
         for (int i = 0; i < KT; i++) {
-            const unsigned long long key = tq.q[i];
-            if (key != ~0ull) {
-                const float a = unordered_f32((uint32_t)(key >> 32));
-                const uint32_t row = (uint32_t)key;
-                const float m = coef * (xn + ynorm[row0 + row]);
-                po[i] = ((unsigned long long)ordered_f32(a - m) << 32) | row;
-                pu[i] = a + m;
+            const uint32_t key = tq.q[i];
+            if (key != 0xffffffffu) {
+                const uint32_t ord = key & lowmask;
+                const int r = (int)(ord & 15u);
+                const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
+                const float m = coef * (xn + ynl[row]) + 1e-30f;
+                const float alo = unordered_f32(key & ~lowmask);
+                const float ahi = unordered_f32(key | lowmask);
+                po[i] = ((unsigned long long)ordered_f32(alo - m) << 32) | row;
+                pu[i] = ahi + m;
             } else {
                 po[i] = ~0ull;
                 pu[i] = WS_INF;
             }
         }
-        if (s4 == 0) pbound[e] = bnd < WS_INF ? bnd - coef * (xn + ynmax[l]) : WS_INF;
+        if (slot == 0) {
+            const float b4 = fminf(fminf(bnd_s[qloc][0], bnd_s[qloc][1]),
+                                   fminf(bnd_s[qloc][2], bnd_s[qloc][3]));
+            pbound[e] = b4 < WS_INF ? b4 - (coef * (xn + ynmax[l]) + 1e-30f) : WS_INF;
+        }
     }
 }
 
@@ -495,35 +576,58 @@ void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* l
 
 int ivf_mfma_kq(int k, int dp) {
     // entries kept per (query, list) = 4 threads x KT
-    if (dp > 128 || k > 32) return 0;
+    if (roundup((size_t)dp, 16) > (size_t)BDM || k > 32) return 0;
     return 4 * (k <= 2 ? 2 : k <= 12 ? 4 : 8);
 }
 
-void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc,
+int ivf_bf3_obits(uint32_t max_list_len) {
+    const uint32_t tiles = std::max<uint32_t>(1u, (max_list_len + BV - 1) / BV);
+    int b = 0;
+    while ((1u << b) < tiles) b++;
+    return 4 + b;
+}
+
+double ivf_bf3_coef(int d) {
+    const double u = 1.0 / 16777216.0;
+    return 2.0 * (3.1 / 65536.0 + (6.0 * d + 8.0) * u);
+}
+
+void split_bf16(const float* codes, int64_t rows, int d, int ldc, int DB, void* out,
+                hipStream_t s) {
+    if (rows <= 0) return;
+    const int64_t n = rows * DB;
+    k_split_bf16<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s>>>(codes, rows, d, ldc, DB,
+                                                                    (__bf16*)out);
+    HIP_LAUNCH_CHECK();
+}
+
+void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, const void* cbf,
                         const int64_t* ids, const float* ynorm, const float* ynmax,
                         const uint32_t* list_off, const uint32_t* list_len, int nlist, int d,
-                        int dp, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
+                        int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
                         int64_t max_items, const int32_t* assign, unsigned long long* part,
                         float* pub, float* pbound, uint32_t* stats, float* D, int64_t* I,
                         KernelTimes* kt, hipStream_t s) {
     if (n <= 0) return;
-    const int KE = ivf_mfma_kq(k, dp);
+    const int KE = ivf_mfma_kq(k, d);
     FAISS_THROW_IF_NOT(KE > 0);
-    FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldc % 4 == 0);
+    FAISS_THROW_IF_NOT(ldc % 4 == 0);
     FAISS_THROW_IF_NOT(nprobe <= 64);
+    FAISS_THROW_IF_NOT(obits >= 4 && obits <= 14);
+    const int DB = (int)roundup((size_t)d, 16);
     const int64_t grid = (int64_t)roundup((size_t)max_items, 32);
     FAISS_THROW_IF_NOT(grid < (1ll << 31));
     const bool l2 = metric_l2 != 0;
-    // margin coefficient (2x the derived bound)
-    const double u = 1.0 / 16777216.0;
-    const double g = d * u / (1.0 - d * u);
-    const float coef = (float)(2.0 * (l2 ? (4 * g + 7 * u) : (2 * g + 2 * u)));
+    // margin of the approximate keys: the bf16 split plus the relative
+    // truncation of the 32-bit keys (2^(obits-23)) on |approx|, which the
+    // decode (low bits cleared / set) already brackets
+    const float coef = (float)ivf_bf3_coef(d);
     {
         ScopedKernelTimer tm(kt, "ivf_flat_scan", 0.0, s);
 #define LAUNCH_A(L2V, KTV)                                                                    \
-    k_ivf_mfma_filter<L2V, KTV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(                   \
-            x, ldx, codes, ldc, ynorm, ynmax, list_off, list_len, nlist, dp, nprobe, coef,    \
-            b.bucket_off, b.item_off, b.entries, part, pub, pbound)
+    k_ivf_bf3_filter<L2V, KTV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(                    \
+            x, ldx, d, (const __bf16*)cbf, DB, ynorm, ynmax, list_off, list_len, nlist,       \
+            nprobe, coef, obits, b.bucket_off, b.item_off, b.entries, part, pub, pbound)
 #define DISPATCH(M, L2V)                  \
     do {                                  \
         if (KE == 8) M(L2V, 2);           \

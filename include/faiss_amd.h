@@ -252,7 +252,8 @@ struct IndexIVFFlat : IndexIVF {
 
    protected:
     void upload_extra() const override;
-    mutable DeviceBuffer d_ynorm_, d_ynmax_, s_part_, s_flags_;
+    mutable DeviceBuffer d_ynorm_, d_ynmax_, d_cbf_, s_part_, s_flags_;
+    mutable int obits_ = 4;
 };
 
 // faiss/impl/ProductQuantizer.h:29-186
