@@ -195,7 +195,12 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
         const float* xq = x + q0 * ldx;
         const float* xn = s_xn_.as<float>() + q0;
         if (nyc == 1) {
-            if (ny > 0)
+            // faiss/utils/distances.cpp:807-823: blocks of fewer than
+            // distance_compute_blas_threshold (20) queries take the direct form
+            if (ny > 0 && n < 20)
+                kern::direct_distances(xq, nq, ldx, d_xb_.as<float>(), ny, l, d, metric_l2,
+                                       s_tile_.as<float>(), ny, s);
+            else if (ny > 0)
                 kern::pairwise_distances(xq, nq, ldx, xn, d_xb_.as<float>(), ny, l,
                                          d_norms_.as<float>(), l, metric_l2,
                                          s_tile_.as<float>(), ny, s);
@@ -205,9 +210,13 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
         } else {
             for (idx_t c = 0; c < nyc; c++) {
                 const idx_t y0 = c * Yc, nyy = std::min(Yc, ny - y0);
-                kern::pairwise_distances(xq, nq, ldx, xn, d_xb_.as<float>() + y0 * l, nyy, l,
-                                         d_norms_.as<float>() + y0, l, metric_l2,
-                                         s_tile_.as<float>(), nyy, s);
+                if (n < 20)
+                    kern::direct_distances(xq, nq, ldx, d_xb_.as<float>() + y0 * l, nyy, l, d,
+                                           metric_l2, s_tile_.as<float>(), nyy, s);
+                else
+                    kern::pairwise_distances(xq, nq, ldx, xn, d_xb_.as<float>() + y0 * l, nyy,
+                                             l, d_norms_.as<float>() + y0, l, metric_l2,
+                                             s_tile_.as<float>(), nyy, s);
                 kern::select_rows(s_tile_.as<float>(), nq, nyy, nyy, k, metric_l2, y0,
                                   s_cand_d_.as<float>() + c * nq * k, nullptr,
                                   s_cand_i_.as<int64_t>() + c * nq * k, k, s);

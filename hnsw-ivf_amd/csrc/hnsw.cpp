@@ -32,14 +32,33 @@ struct DevGuard2 {
     }
 };
 
-// sequential fma chain, the evaluation order shared with the GPU kernels
+// fvec_L2sqr in the reference's evaluation order (see ref_arith.h: 8 fma
+// lanes, (j,j+4),(j,j+2),(0,1) reduction, 4-term epilogue, fma tail)
 inline float l2_seq(const float* a, const float* b, int d) {
-    float acc = 0.f;
-    for (int j = 0; j < d; j++) {
-        float t = a[j] - b[j];
-        acc = fmaf(t, t, acc);
+    float c[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int n8 = d & ~7;
+    for (int i = 0; i < n8; i += 8)
+        for (int j = 0; j < 8; j++) {
+            const float t = a[i + j] - b[i + j];
+            c[j] = std::fma(t, t, c[j]);
+        }
+    const float x0 = c[0] + c[4], x1 = c[1] + c[5], x2 = c[2] + c[6], x3 = c[3] + c[7];
+    float r = (x0 + x2) + (x1 + x3);
+    int i = n8;
+    if (d - n8 >= 4) {
+        float e[4];
+        for (int j = 0; j < 4; j++) {
+            const float t = a[n8 + j] - b[n8 + j];
+            e[j] = t * t;
+        }
+        r = r + ((e[0] + e[2]) + (e[1] + e[3]));
+        i += 4;
     }
-    return acc;
+    for (; i < d; i++) {
+        const float t = a[i] - b[i];
+        r = std::fma(t, t, r);
+    }
+    return r;
 }
 
 struct NodeDistCloser {  // faiss/impl/HNSW.h NodeDistCloser

@@ -360,7 +360,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
         ScopedKernelTimer tm(&ktimes, "ivf_flat_scan", 0.0, s);
         kern::ivf_flat_scan(x, ldx, d_codes_.as<float>(), l, d_ids_.as<int64_t>(),
                             d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(), (int)nlist, l,
-                            n, np, (int)k, l2, b, max_items, s_pk1_.as<float>(),
+                            d, n, np, (int)k, l2, b, max_items, s_pk1_.as<float>(),
                             s_pk2_.as<long long>(), s);
     }
     kern::ivf_merge(s_pk1_.as<float>(), s_pk2_.as<long long>(), assign,

@@ -31,6 +31,11 @@ void pairwise_distances(const float* x, int64_t nx, int ldx, const float* xn,
                         const float* y, int64_t ny, int ldy, const float* yn, int dp,
                         int metric_l2, float* D, int64_t ldD, hipStream_t s);
 
+// Direct per-pair distances in the reference order (faiss' path for query
+// blocks below distance_compute_blas_threshold = 20)
+void direct_distances(const float* x, int64_t nx, int ldx, const float* y, int64_t ny, int ldy,
+                      int d, int metric_l2, float* D, int64_t ldD, hipStream_t s);
+
 // k smallest (L2) / largest (IP) per row of D, ties by column index,
 // reference faiss/impl/ResultHandler.h:187-287 (HeapBlockResultHandler).
 // Outputs are sorted; missing slots are (+-FLT_MAX, -1).  Either of out_i32 /
@@ -67,7 +72,7 @@ inline int64_t ivf_max_items(int64_t n, int nprobe, int nlist, int QT) {
 // exact per-(query, list) top-k of sum (x - y)^2 (or <x,y>) written as
 // internal keys to part_k1/part_k2 [n*nprobe][k].
 void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const int64_t* ids,
-                   const uint32_t* list_off, const uint32_t* list_len, int nlist, int dp,
+                   const uint32_t* list_off, const uint32_t* list_len, int nlist, int dp, int d,
                    int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b, int64_t max_items,
                    float* part_k1, long long* part_k2, hipStream_t s);
 

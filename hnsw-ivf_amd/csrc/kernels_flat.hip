@@ -12,6 +12,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "ref_arith.h"
 #include "wave_select.h"
 
 namespace faiss_amd {
@@ -27,17 +28,33 @@ __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, 
     int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (row >= n) return;
     const float* xr = x + row * ld;
-    float s = 0.f;
-    int j = 0;
-    for (; j + 4 <= d; j += 4) {
-        float4 v = *(const float4*)(xr + j);
-        s = fmaf(v.x, v.x, s);
-        s = fmaf(v.y, v.y, s);
-        s = fmaf(v.z, v.z, s);
-        s = fmaf(v.w, v.w, s);
-    }
-    for (; j < d; j++) s = fmaf(xr[j], xr[j], s);
+    // reference order (fvec_norm_L2sqr, see ref_arith.h)
+    const float s = ref_norm(xr, d);
     out[row] = s;
+}
+
+// Direct form for query blocks below faiss' BLAS threshold
+// (faiss/utils/distances.cpp:170-199, 807-823: nx < 20 uses fvec_L2sqr /
+// fvec_inner_product per pair).  One thread per (query, row).
+__global__ __launch_bounds__(256) void k_direct_dist(const float* __restrict__ x, int64_t nx,
+                                                     int ldx, const float* __restrict__ y,
+                                                     int64_t ny, int ldy, int d, int metric_l2,
+                                                     float* __restrict__ D, int64_t ldD) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= nx * ny) return;
+    const int64_t i = p / ny, j = p - i * ny;
+    const float* a = x + i * ldx;
+    const float* b = y + j * ldy;
+    D[i * ldD + j] = metric_l2 ? ref_l2(a, b, d) : ref_ip(a, b, d);
+}
+
+void direct_distances(const float* x, int64_t nx, int ldx, const float* y, int64_t ny, int ldy,
+                      int d, int metric_l2, float* D, int64_t ldD, hipStream_t s) {
+    if (nx <= 0 || ny <= 0) return;
+    FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldy % 4 == 0);
+    k_direct_dist<<<dim3((unsigned)cdiv(nx * ny, 256)), dim3(256), 0, s>>>(x, nx, ldx, y, ny, ldy,
+                                                                          d, metric_l2, D, ldD);
+    HIP_LAUNCH_CHECK();
 }
 
 void row_norms(const float* x, int64_t n, int d, int ld, float* out, hipStream_t s) {

@@ -26,29 +26,17 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "ref_arith.h"
 #include "wave_select.h"
 
 namespace faiss_amd {
 namespace kern {
 
+// faiss FlatL2Dis (faiss/IndexFlat.cpp:111-170): fvec_L2sqr and
+// fvec_L2sqr_batch_4 evaluate in the same reference order (ref_arith.h)
 __device__ __forceinline__ float l2_row(const float* __restrict__ qs, const float* __restrict__ y,
                                         int d) {
-    float acc = 0.f;
-    int j = 0;
-    for (; j + 4 <= d; j += 4) {
-        float4 yv = *(const float4*)(y + j);
-        float4 qv = *(const float4*)(qs + j);
-        float t0 = qv.x - yv.x, t1 = qv.y - yv.y, t2 = qv.z - yv.z, t3 = qv.w - yv.w;
-        acc = fmaf(t0, t0, acc);
-        acc = fmaf(t1, t1, acc);
-        acc = fmaf(t2, t2, acc);
-        acc = fmaf(t3, t3, acc);
-    }
-    for (; j < d; j++) {
-        float t = qs[j] - y[j];
-        acc = fmaf(t, t, acc);
-    }
-    return acc;
+    return ref_l2(qs, y, d);
 }
 
 // merge a sorted 64-batch into a sorted 128-queue (c0: positions 0..63,

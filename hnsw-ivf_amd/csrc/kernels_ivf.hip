@@ -19,6 +19,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "ref_arith.h"
 #include "wave_select.h"
 
 namespace faiss_amd {
@@ -111,7 +112,7 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
 
 // ---------------------------------------------------------------- scan
 constexpr int SQT = 64;   // queries per work item
-constexpr int SVT = 64;   // codes per tile
+constexpr int SVT = 32;   // codes per tile (8 reference-order partial sums per pair)
 constexpr int SDC = 128;  // dims per LDS chunk
 constexpr int SSD = SDC + 4;  // LDS row stride (floats): 528 B, 16-B aligned
 
@@ -121,15 +122,15 @@ template <bool L2, int KQ>
 __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
         const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
         const int64_t* __restrict__ ids, const uint32_t* __restrict__ list_off,
-        const uint32_t* __restrict__ list_len, int nlist, int dp, int nprobe, int k,
-        const uint32_t* __restrict__ bucket_off, const uint32_t* __restrict__ item_off,
+        const uint32_t* __restrict__ list_len, int nlist, int dp, int dp_true, int nprobe,
+        int k, const uint32_t* __restrict__ bucket_off, const uint32_t* __restrict__ item_off,
         const uint32_t* __restrict__ entries, float* __restrict__ part_k1,
         long long* __restrict__ part_k2) {
-    // one array: the end-of-kernel queue merge reuses both tiles (64 KB at KQ=32)
-    __shared__ __attribute__((aligned(16))) float smem_xy[(SQT + SVT) * SSD];
+    // one array: the end-of-kernel queue merge reuses it (64 KB at KQ=32)
+    __shared__ __attribute__((aligned(16))) float smem_xy[(SQT + 64) * SSD];
     float* Xs = smem_xy;
     float* Ys = smem_xy + SQT * SSD;
-    __shared__ long long ids_s[SVT];
+    __shared__ long long ids_s[64];
     __shared__ uint32_t ent_s[SQT];
     __shared__ int32_t qrow_s[SQT];
 
@@ -209,13 +210,18 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
     };
     if (one_chunk && len > 0) fetch(0);
 
+    // dims evaluated in the reference order (ref_arith.h): lanes over
+    // i < n8, then the 4-term epilogue and the tail in the last chunk
+    const int d = dp_true;
+    const int n8 = d & ~7;
     for (int v0 = 0; v0 < len; v0 += SVT) {
         const int nv = min(SVT, len - v0);
-        float acc[4][4];
+        RefAcc8 acc[4][2];
+        float res[4][2];
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
-            for (int j = 0; j < 4; j++) acc[i][j] = 0.f;
+            for (int j = 0; j < 2; j++) acc[i][j].init();
 
         for (int dc = 0; dc < dp; dc += SDC) {
             const int dl = min(SDC, dp - dc);
@@ -239,38 +245,56 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
                 }
                 __syncthreads();
             }
-#pragma unroll 2
-            for (int dd = 0; dd < dl; dd += 4) {
-                float4 xa[4], yb[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) xa[i] = *(const float4*)(Xs + (qg + 16 * i) * SSD + dd);
-#pragma unroll
-                for (int j = 0; j < 4; j++) yb[j] = *(const float4*)(Ys + (vg + 16 * j) * SSD + dd);
+            const int dmain = min(dl, max(0, n8 - dc));
+            for (int dd = 0; dd < dmain; dd += 8) {
+                float4 xa[4][2], yb[2][2];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        if (L2) {
-                            float d0 = xa[i].x - yb[j].x;
-                            float d1 = xa[i].y - yb[j].y;
-                            float d2 = xa[i].z - yb[j].z;
-                            float d3 = xa[i].w - yb[j].w;
-                            float a = acc[i][j];
-                            a = fmaf(d0, d0, a);
-                            a = fmaf(d1, d1, a);
-                            a = fmaf(d2, d2, a);
-                            a = fmaf(d3, d3, a);
-                            acc[i][j] = a;
-                        } else {
-                            float a = acc[i][j];
-                            a = fmaf(xa[i].x, yb[j].x, a);
-                            a = fmaf(xa[i].y, yb[j].y, a);
-                            a = fmaf(xa[i].z, yb[j].z, a);
-                            a = fmaf(xa[i].w, yb[j].w, a);
-                            acc[i][j] = a;
-                        }
-                    }
+                    xa[i][0] = *(const float4*)(Xs + (qg + 16 * i) * SSD + dd);
+                    xa[i][1] = *(const float4*)(Xs + (qg + 16 * i) * SSD + dd + 4);
                 }
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    yb[j][0] = *(const float4*)(Ys + (vg + 16 * j) * SSD + dd);
+                    yb[j][1] = *(const float4*)(Ys + (vg + 16 * j) * SSD + dd + 4);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        float* c = acc[i][j].c;
+                        c[0] = ref_term_fma<L2>(xa[i][0].x, yb[j][0].x, c[0]);
+                        c[1] = ref_term_fma<L2>(xa[i][0].y, yb[j][0].y, c[1]);
+                        c[2] = ref_term_fma<L2>(xa[i][0].z, yb[j][0].z, c[2]);
+                        c[3] = ref_term_fma<L2>(xa[i][0].w, yb[j][0].w, c[3]);
+                        c[4] = ref_term_fma<L2>(xa[i][1].x, yb[j][1].x, c[4]);
+                        c[5] = ref_term_fma<L2>(xa[i][1].y, yb[j][1].y, c[5]);
+                        c[6] = ref_term_fma<L2>(xa[i][1].z, yb[j][1].z, c[6]);
+                        c[7] = ref_term_fma<L2>(xa[i][1].w, yb[j][1].w, c[7]);
+                    }
+            }
+            if (dc + dl >= dp) {
+                // last chunk: reduce, epilogue, tail (dims n8 .. d-1 are here)
+                const int e0 = n8 - dc;
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const float* xr = Xs + (qg + 16 * i) * SSD;
+                        const float* yr = Ys + (vg + 16 * j) * SSD;
+                        float r = acc[i][j].reduce();
+                        int ii = e0;
+                        if (d - n8 >= 4) {
+                            const float t0 = ref_term<L2>(xr[e0], yr[e0]);
+                            const float t1 = ref_term<L2>(xr[e0 + 1], yr[e0 + 1]);
+                            const float t2 = ref_term<L2>(xr[e0 + 2], yr[e0 + 2]);
+                            const float t3 = ref_term<L2>(xr[e0 + 3], yr[e0 + 3]);
+                            r = r + ((t0 + t2) + (t1 + t3));
+                            ii += 4;
+                        }
+                        for (; ii < d - dc; ii++) r = ref_term_fma<L2>(xr[ii], yr[ii], r);
+                        res[i][j] = r;
+                    }
             }
             __syncthreads();
         }
@@ -279,7 +303,7 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
-            for (int j = 0; j < 4; j++) Ds[(qg + 16 * i) * (SVT + 1) + vg + 16 * j] = acc[i][j];
+            for (int j = 0; j < 2; j++) Ds[(qg + 16 * i) * (SVT + 1) + vg + 16 * j] = res[i][j];
         if constexpr (KQ == 0) {
             if (t < SVT) ids_s[t] = t < nv ? (long long)ids[row0 + v0 + t] : 0ll;
         }
@@ -373,20 +397,20 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
 template <int KQ>
 static void launch_scan(bool l2, int64_t grid, hipStream_t s, const float* x, int ldx,
                         const float* codes, int ldc, const int64_t* ids, const uint32_t* list_off,
-                        const uint32_t* list_len, int nlist, int dp, int nprobe, int k,
+                        const uint32_t* list_len, int nlist, int dp, int d, int nprobe, int k,
                         IVFBuckets b, float* pk1, long long* pk2) {
     if (l2)
         k_ivf_flat_scan<true, KQ><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
-                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, nprobe, k, b.bucket_off,
+                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, d, nprobe, k, b.bucket_off,
                 b.item_off, b.entries, pk1, pk2);
     else
         k_ivf_flat_scan<false, KQ><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
-                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, nprobe, k, b.bucket_off,
+                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, d, nprobe, k, b.bucket_off,
                 b.item_off, b.entries, pk1, pk2);
 }
 
 void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const int64_t* ids,
-                   const uint32_t* list_off, const uint32_t* list_len, int nlist, int dp,
+                   const uint32_t* list_off, const uint32_t* list_len, int nlist, int dp, int d,
                    int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b, int64_t max_items,
                    float* part_k1, long long* part_k2, hipStream_t s) {
     if (n <= 0) return;
@@ -397,16 +421,13 @@ void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const i
     max_items = (int64_t)roundup((size_t)max_items, 32);  // XCD remap needs a multiple of 32
     if (k <= 10)
         launch_scan<10>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
-                        nprobe, k, b, part_k1, part_k2);
+                        d, nprobe, k, b, part_k1, part_k2);
     else if (k <= 16)
         launch_scan<16>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
-                        nprobe, k, b, part_k1, part_k2);
-    else if (k <= 32)
-        launch_scan<32>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
-                        nprobe, k, b, part_k1, part_k2);
+                        d, nprobe, k, b, part_k1, part_k2);
     else
         launch_scan<0>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
-                       nprobe, k, b, part_k1, part_k2);
+                       d, nprobe, k, b, part_k1, part_k2);
     HIP_LAUNCH_CHECK();
 }
 

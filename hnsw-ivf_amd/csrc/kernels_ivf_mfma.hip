@@ -3,8 +3,9 @@
 // Reference hot loop: faiss/IndexIVFFlat.cpp:155-179 (exact sum (x-y)^2 per
 // code, strict heap admission) driven by faiss/IndexIVF.cpp:595-631.
 //
-// Three kernels, all results EXACT (bit-identical to the direct sequential
-// fma chain the CPU oracle evaluates):
+// Results are EXACT: bit-identical to the reference's fvec_L2sqr /
+// fvec_inner_product evaluation order (ref_arith.h), which the CPU oracle
+// restates:
 //  A  k_ivf_mfma_filter: list-centric (list x 64 queries per workgroup).
 //     <x,y> for a 64x64 tile on v_mfma_f32_32x32x2_f32 (one 32x32 block per
 //     wave), approx = |x|^2 + |y|^2 - 2<x,y>; per (query, list) the KQ best
@@ -33,45 +34,11 @@
 #include "kernels.h"
 #include "wave_select.h"
 #include "exact_select.h"
+#include "ref_arith.h"
 
 namespace faiss_amd {
 namespace kern {
 
-
-__device__ __forceinline__ float seq_l2(const float* __restrict__ a, const float* __restrict__ b,
-                                        int d) {
-    float acc = 0.f;
-    int j = 0;
-    for (; j + 4 <= d; j += 4) {
-        float4 av = *(const float4*)(a + j);
-        float4 bv = *(const float4*)(b + j);
-        float t0 = av.x - bv.x, t1 = av.y - bv.y, t2 = av.z - bv.z, t3 = av.w - bv.w;
-        acc = fmaf(t0, t0, acc);
-        acc = fmaf(t1, t1, acc);
-        acc = fmaf(t2, t2, acc);
-        acc = fmaf(t3, t3, acc);
-    }
-    for (; j < d; j++) {
-        float t = a[j] - b[j];
-        acc = fmaf(t, t, acc);
-    }
-    return acc;
-}
-__device__ __forceinline__ float seq_ip(const float* __restrict__ a, const float* __restrict__ b,
-                                        int d) {
-    float acc = 0.f;
-    int j = 0;
-    for (; j + 4 <= d; j += 4) {
-        float4 av = *(const float4*)(a + j);
-        float4 bv = *(const float4*)(b + j);
-        acc = fmaf(av.x, bv.x, acc);
-        acc = fmaf(av.y, bv.y, acc);
-        acc = fmaf(av.z, bv.z, acc);
-        acc = fmaf(av.w, bv.w, acc);
-    }
-    for (; j < d; j++) acc = fmaf(a[j], b[j], acc);
-    return acc;
-}
 
 // ---------------------------------------------------------------- A
 // Filter on bf16x3 MFMA (v_mfma_f32_32x32x16_bf16).  Every f32 value is
@@ -375,7 +342,7 @@ struct RerankStream {
     __device__ __forceinline__ void eval(int r, uint32_t row, float& k1, long long& k2, long long& rank) const {
         const int64_t grow = (int64_t)list_off[asg[r]] + row;
         const float* yr = codes + grow * ldc;
-        const float dis = L2 ? seq_l2(xq, yr, d) : seq_ip(xq, yr, d);
+        const float dis = L2 ? ref_l2(xq, yr, d) : ref_ip(xq, yr, d);
         to_key(L2 ? 1 : 0, dis, (long long)ids[grow], k1, k2);
         rank = ((long long)r << 32) | row;
     }
@@ -524,7 +491,7 @@ struct FullStream {
                 if (ok) {
                     const int64_t grow = (int64_t)list_off[lst] + v0 + lane;
                     const float* yr = codes + grow * ldc;
-                    const float dis = L2 ? seq_l2(xq, yr, d) : seq_ip(xq, yr, d);
+                    const float dis = L2 ? ref_l2(xq, yr, d) : ref_ip(xq, yr, d);
                     to_key(L2 ? 1 : 0, dis, (long long)ids[grow], k1, k2);
                     ok = key_admissible(k1);
                     rank = ((long long)r << 32) | (uint32_t)(v0 + lane);

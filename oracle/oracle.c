@@ -70,22 +70,62 @@ void oracle_float_rand(float* x, size_t n, int64_t seed) {
 }
 
 /* ------------------------------------------------------------ distances */
-float oracle_fvec_L2sqr(const float* x, const float* y, size_t d) {
-    float acc = 0.f;
-    for (size_t j = 0; j < d; j++) {
-        float t = x[j] - y[j];
-        acc = fmaf(t, t, acc);
+/* faiss/utils/distances_simd.cpp:220-230 (fvec_L2sqr) and its inner-product
+ * and norm siblings, as GCC compiles them under the reference's
+ * FAISS_PRAGMA_IMPRECISE_FUNCTION_BEGIN (associative-math) + AVX2/FMA flags:
+ * 8 fma accumulators over i < d & ~7, reduced (j,j+4),(j,j+2),(0,1); a
+ * 4-term epilogue rounded alone and reduced (0,2),(1,3),(0,1), then added;
+ * the last d % 4 terms fma'd in order.  Pinned bit-for-bit against the
+ * reference sources compiled by oracle/ref (tests/test_oracle_golden.py). */
+static float ref_dist_(const float* x, const float* y, size_t d, int l2) {
+    float c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const size_t n8 = d & ~(size_t)7;
+    for (size_t i = 0; i < n8; i += 8)
+        for (int j = 0; j < 8; j++) {
+            if (l2) {
+                const float t = x[i + j] - y[i + j];
+                c[j] = fmaf(t, t, c[j]);
+            } else {
+                c[j] = fmaf(x[i + j], y[i + j], c[j]);
+            }
+        }
+    const float x0 = c[0] + c[4], x1 = c[1] + c[5], x2 = c[2] + c[6], x3 = c[3] + c[7];
+    float r = (x0 + x2) + (x1 + x3);
+    size_t i = n8;
+    if (d - n8 >= 4) {
+        float e[4];
+        for (int j = 0; j < 4; j++) {
+            if (l2) {
+                const float t = x[n8 + j] - y[n8 + j];
+                e[j] = t * t;
+            } else {
+                e[j] = x[n8 + j] * y[n8 + j];
+            }
+        }
+        r = r + ((e[0] + e[2]) + (e[1] + e[3]));
+        i += 4;
     }
-    return acc;
+    for (; i < d; i++) {
+        if (l2) {
+            const float t = x[i] - y[i];
+            r = fmaf(t, t, r);
+        } else {
+            r = fmaf(x[i], y[i], r);
+        }
+    }
+    return r;
 }
+float oracle_fvec_L2sqr(const float* x, const float* y, size_t d) { return ref_dist_(x, y, d, 1); }
 float oracle_fvec_inner_product(const float* x, const float* y, size_t d) {
+    return ref_dist_(x, y, d, 0);
+}
+float oracle_fvec_norm_L2sqr(const float* x, size_t d) { return ref_dist_(x, x, d, 0); }
+/* The BLAS-form inner product <x, c> of the coarse quantizer comes from
+ * sgemm (MKL / OpenBLAS order, not reproducible); the restatement fixes it
+ * to the sequential fma chain, which is what the fp32 MFMA tile computes. */
+float oracle_ip_seq(const float* x, const float* y, size_t d) {
     float acc = 0.f;
     for (size_t j = 0; j < d; j++) acc = fmaf(x[j], y[j], acc);
-    return acc;
-}
-float oracle_fvec_norm_L2sqr(const float* x, size_t d) {
-    float acc = 0.f;
-    for (size_t j = 0; j < d; j++) acc = fmaf(x[j], x[j], acc);
     return acc;
 }
 
@@ -220,14 +260,14 @@ void oracle_knn(const float* x, const float* y, size_t d, size_t nx, size_t ny, 
             float dis;
             if (metric == 1) {
                 if (blas_form) {
-                    float ip = oracle_fvec_inner_product(xi, yj, d);
+                    float ip = oracle_ip_seq(xi, yj, d);
                     dis = fmaf(-2.f, ip, xn + yn[j]);
                     if (dis < 0) dis = 0;
                 } else {
                     dis = oracle_fvec_L2sqr(xi, yj, d);
                 }
             } else {
-                dis = oracle_fvec_inner_product(xi, yj, d);
+                dis = blas_form ? oracle_ip_seq(xi, yj, d) : oracle_fvec_inner_product(xi, yj, d);
             }
             if (cmp_(cmax, thr, dis)) {
                 oracle_heap_replace_top(cmax, k, hv, hi, dis, (int64_t)j);
