@@ -77,7 +77,7 @@ void oracle_float_rand(float* x, size_t n, int64_t seed) {
  * 4-term epilogue rounded alone and reduced (0,2),(1,3),(0,1), then added;
  * the last d % 4 terms fma'd in order.  Pinned bit-for-bit against the
  * reference sources compiled by oracle/ref (tests/test_oracle_golden.py). */
-static float ref_dist_(const float* x, const float* y, size_t d, int l2) {
+static inline float ref_dist_(const float* x, const float* y, size_t d, int l2) {
     float c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const size_t n8 = d & ~(size_t)7;
     for (size_t i = 0; i < n8; i += 8)
@@ -613,20 +613,10 @@ void oracle_ivf_search(const oracle_ivf_t* ivf, size_t n, const float* x, size_t
 }
 
 /* ------------------------------------------------------------ fast path */
+/* the reference order (ref_dist_: 8 independent fma lanes) vectorises as
+ * the reference's own compiled loop does */
 static inline float l2_fast(const float* x, const float* y, int d) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int j = 0;
-    for (; j + 8 <= d; j += 8)
-        for (int u = 0; u < 8; u++) {
-            float t = x[j + u] - y[j + u];
-            acc[u] += t * t;
-        }
-    float s = 0;
-    for (; j < d; j++) {
-        float t = x[j] - y[j];
-        s += t * t;
-    }
-    return ((acc[0] + acc[4]) + (acc[1] + acc[5])) + ((acc[2] + acc[6]) + (acc[3] + acc[7])) + s;
+    return ref_dist_(x, y, (size_t)d, 1);
 }
 
 void oracle_ivf_search_fast(const oracle_ivf_t* ivf, size_t n, const float* x, size_t k,
