@@ -1,0 +1,96 @@
+// bf3.h — shared pieces of the bf16x3 MFMA filters (IVF-Flat list scan and
+// coarse quantizer).
+//
+// Every f32 operand is split x = xh + xl (+ xr) with xh = bf16(x),
+// xl = bf16(x - xh), |xr| <= 2^-16 |x|; <x,y> ~ xh.yh + xh.yl + xl.yh on
+// v_mfma_f32_32x32x16_bf16 (products exact in f32, f32 accumulation).
+//   |ip_approx - ip| <= (3.1 * 2^-16 + 3 d u) sum |x_i y_i|,   u = 2^-24.
+// Callers turn that into a certified margin (bf3_coef) and re-rank the
+// candidates the margin cannot separate with the exact f32 evaluation.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace faiss_amd {
+namespace kern {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int BQ = 64;    // queries per work item
+constexpr int BV = 64;    // database rows per tile
+constexpr int BDM = 128;  // max padded dim (multiple of 16)
+
+// Per-thread sorted queue of the KT smallest 32-bit keys (branchless).
+template <int KT>
+struct ThreadQueue32 {
+    uint32_t q[KT];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int i = 0; i < KT; i++) q[i] = 0xffffffffu;
+    }
+    __device__ __forceinline__ void push(uint32_t c) {
+#pragma unroll
+        for (int i = KT - 1; i > 0; i--) q[i] = c < q[i - 1] ? q[i - 1] : min(c, q[i]);
+        q[0] = min(c, q[0]);
+    }
+};
+
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& l) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const __bf16 hb = (__bf16)v[j];
+        h[j] = hb;
+        l[j] = (__bf16)(v[j] - (float)hb);
+    }
+}
+
+// The B operand (32 query columns per wave) for one work item: lane holds
+// query column `li` dims [16 s + 8 lh, +8) split into hi / lo, and |x|^2
+// (any order; margins only).  qr < 0: zero column.
+__device__ __forceinline__ void load_query_frags(const float* __restrict__ x, int ldx, int d,
+                                                 int nsteps, int qr, int lh, bf16x8 (&bh)[BDM / 16],
+                                                 bf16x8 (&bl)[BDM / 16], float& xn) {
+    const float* xr = x + (int64_t)(qr < 0 ? 0 : qr) * ldx;
+    xn = 0.f;
+#pragma unroll
+    for (int s = 0; s < BDM / 16; s++) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int kk = 16 * s + 8 * lh + j;
+            v[j] = (qr >= 0 && s < nsteps && kk < d) ? xr[kk] : 0.f;
+        }
+        split8(v, bh[s], bl[s]);
+#pragma unroll
+        for (int j = 0; j < 8; j++) xn = fmaf(v[j], v[j], xn);
+    }
+    xn += __shfl_xor(xn, 32);
+}
+
+// One 32x32 block: A = 32 database rows (hi/lo image in LDS, row stride CSB
+// bytes, this lane's row pointer `arow` already offset by 16 * lh bytes),
+// B = the register query fragments.  acc[r] = row (r&3)+8(r>>2)+4lh, col li.
+__device__ __forceinline__ floatx16 bf3_block(const uint8_t* arow, int DB, int nsteps,
+                                              const bf16x8 (&bh)[BDM / 16],
+                                              const bf16x8 (&bl)[BDM / 16]) {
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < BDM / 16; s++) {
+        if (s < nsteps) {
+            const bf16x8 ah = *(const bf16x8*)(arow + 32 * s);
+            const bf16x8 al = *(const bf16x8*)(arow + 2 * DB + 32 * s);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
+        }
+    }
+    return acc;
+}
+
+}  // namespace kern
+}  // namespace faiss_amd

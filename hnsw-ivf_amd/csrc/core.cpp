@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -149,6 +150,14 @@ void IndexFlat::sync_device() const {
         HIP_CHECK(hipMemcpy2DAsync(d_xb_.ptr, sizeof(float) * l, xb.data(), sizeof(float) * d,
                                    sizeof(float) * d, ntotal, hipMemcpyHostToDevice, s));
         kern::row_norms(d_xb_.as<float>(), ntotal, d, l, d_norms_.as<float>(), s);
+        // bf16 hi/lo image + largest norm for the bf16x3 coarse filter
+        if (roundup((size_t)d, 16) <= 128) {
+            const int DB = (int)roundup((size_t)d, 16);
+            d_cbf_.reserve((size_t)ntotal * 2 * DB * 2);
+            d_cnmax_.reserve(sizeof(float));
+            kern::split_bf16(d_xb_.as<float>(), ntotal, d, l, DB, d_cbf_.ptr, s);
+            kern::array_max(d_norms_.as<float>(), ntotal, d_cnmax_.as<float>(), s);
+        }
     }
     HIP_CHECK(hipStreamSynchronize(s));
     dirty_ = false;
@@ -176,6 +185,33 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
     int64_t* o64 = i32 ? nullptr : (int64_t*)labels;
     const idx_t ny = ntotal;
     s_xn_.reserve(sizeof(float) * std::max<idx_t>(n, 1));
+    // bf16x3 MFMA filter + certified exact re-rank: identical results to the
+    // f32 tile + select below (FAISS_AMD_COARSE=f32 forces the latter)
+    const char* cenv = getenv("FAISS_AMD_COARSE");
+    const kern::CoarsePlan plan =
+            (cenv && !strcmp(cenv, "f32")) || ny > (1 << 20) || d_cbf_.ptr == nullptr
+                    ? kern::CoarsePlan{}
+                    : kern::coarse_bf3_plan(n, (int)ny, d, k);
+    if (plan.ok) {
+        kern::row_norms(x, n, d, ldx, s_xn_.as<float>(), s);
+        const size_t per_q = (size_t)plan.entries * 12 + plan.nsplit * 4;
+        const idx_t qchunk = std::max<idx_t>(64, (idx_t)(((size_t)256 << 20) / per_q) / 64 * 64);
+        const idx_t qc = std::min<idx_t>(qchunk, n);
+        s_cand_i_.reserve(sizeof(unsigned long long) * qc * plan.entries);
+        s_cand_d_.reserve(sizeof(float) * qc * plan.entries);
+        s_tile_.reserve(sizeof(float) * qc * plan.nsplit);
+        ScopedKernelTimer tm(&ktimes, "coarse_bf3", 2.0 * n * ny * d, s);
+        for (idx_t q0 = 0; q0 < n; q0 += qc) {
+            const idx_t nq = std::min(qc, n - q0);
+            kern::coarse_bf3_knn(plan, x + q0 * ldx, nq, ldx, s_xn_.as<float>() + q0,
+                                 d_xb_.as<float>(), l, d_cbf_.ptr, d_norms_.as<float>(),
+                                 d_cnmax_.as<float>(), (int)ny, d, k, metric_l2,
+                                 s_cand_i_.as<unsigned long long>(), s_cand_d_.as<float>(),
+                                 s_tile_.as<float>(), distances + q0 * k,
+                                 o32 ? o32 + q0 * k : nullptr, o64 ? o64 + q0 * k : nullptr, s);
+        }
+        return;
+    }
     if (metric_l2) kern::row_norms(x, n, d, ldx, s_xn_.as<float>(), s);
     const idx_t Yc = std::min<idx_t>(std::max<idx_t>(ny, 1), 1 << 20);
     const idx_t nyc = (idx_t)cdiv(std::max<idx_t>(ny, 1), Yc);

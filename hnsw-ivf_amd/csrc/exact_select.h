@@ -30,10 +30,10 @@
 namespace faiss_amd {
 namespace kern {
 
-template <class Stream>
+template <class Stream, class OutIdx = int64_t>
 __device__ __forceinline__ void exact_topk_resolve(Stream& st, int k, int metric_l2, int lane,
                                                    bool write, float* __restrict__ Dq,
-                                                   int64_t* __restrict__ Iq) {
+                                                   OutIdx* __restrict__ Iq) {
     // pass A: lexicographic top-(k+1) (the extra slot detects a boundary tie)
     const int K1 = k < 64 ? k + 1 : 64;
     float fd = WS_INF, td = WS_INF;
@@ -92,7 +92,7 @@ __device__ __forceinline__ void exact_topk_resolve(Stream& st, int k, int metric
         long long id;
         from_key(metric_l2, od, oi, dis, id);
         Dq[lane] = dis;
-        Iq[lane] = id;
+        Iq[lane] = (OutIdx)id;
     }
 }
 

@@ -36,6 +36,21 @@ void pairwise_distances(const float* x, int64_t nx, int ldx, const float* xn,
 void direct_distances(const float* x, int64_t nx, int ldx, const float* y, int64_t ny, int ldy,
                       int d, int metric_l2, float* D, int64_t ldD, hipStream_t s);
 
+// Coarse top-k on bf16x3 MFMA + certified exact re-rank (kernels_coarse.hip);
+// identical results to pairwise_distances + select_rows for blocks of >= 20
+// queries.  plan.ok == false: not eligible (fall back to the f32 tile path).
+struct CoarsePlan {
+    bool ok = false;
+    int nsplit = 0, split_len = 0, kt = 0, obits = 0, entries = 0;  // entries per query
+};
+CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k);
+void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, const float* xnorm,
+                    const float* cent, int ldc, const void* cbf, const float* cnorm,
+                    const float* cnmax, int nlist, int d, int k, int metric_l2,
+                    unsigned long long* part, float* pub, float* pbound, float* D, int32_t* I32,
+                    int64_t* I64, hipStream_t s);
+void array_max(const float* a, int64_t n, float* out, hipStream_t s);
+
 // k smallest (L2) / largest (IP) per row of D, ties by column index,
 // reference faiss/impl/ResultHandler.h:187-287 (HeapBlockResultHandler).
 // Outputs are sorted; missing slots are (+-FLT_MAX, -1).  Either of out_i32 /

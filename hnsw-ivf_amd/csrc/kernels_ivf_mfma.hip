@@ -35,6 +35,7 @@
 #include "wave_select.h"
 #include "exact_select.h"
 #include "ref_arith.h"
+#include "bf3.h"
 
 namespace faiss_amd {
 namespace kern {
@@ -66,37 +67,6 @@ namespace kern {
 //   pbound[e]  = lower bound of the exact key of every dropped candidate of
 //                the list (min over the 4 threads of their KT-th key, minus
 //                the list's largest margin); +inf if none was dropped.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-constexpr int BQ = 64;    // queries per work item
-constexpr int BV = 64;    // codes per tile
-constexpr int BDM = 128;  // max padded dim (multiple of 16)
-
-template <int KT>
-struct ThreadQueue32 {
-    uint32_t q[KT];
-    __device__ __forceinline__ void init() {
-#pragma unroll
-        for (int i = 0; i < KT; i++) q[i] = 0xffffffffu;
-    }
-    // branchless insertion, keeps the KT smallest
-    __device__ __forceinline__ void push(uint32_t c) {
-#pragma unroll
-        for (int i = KT - 1; i > 0; i--) q[i] = c < q[i - 1] ? q[i - 1] : min(c, q[i]);
-        q[0] = min(c, q[0]);
-    }
-};
-
-__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& l) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const __bf16 hb = (__bf16)v[j];
-        h[j] = hb;
-        l[j] = (__bf16)(v[j] - (float)hb);
-    }
-}
-
 // f32 arena -> bf16 hi/lo arena: row r = hi[DB] | lo[DB], zero beyond d
 __global__ void k_split_bf16(const float* __restrict__ codes, int64_t rows, int d, int ldc, int DB,
                              __bf16* __restrict__ out) {
@@ -155,26 +125,8 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
 
     // ---- query fragments (B operand): registers for the whole work item
     bf16x8 bh[BDM / 16], bl[BDM / 16];
-    float xn = 0.f;
-    {
-        const int qr = qrow_s[qloc];
-        const float* xr = x + (int64_t)(qr < 0 ? 0 : qr) * ldx;
-#pragma unroll
-        for (int s = 0; s < BDM / 16; s++) {
-            float v[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int kk = 16 * s + 8 * lh + j;
-                v[j] = (qr >= 0 && s < nsteps && kk < d) ? xr[kk] : 0.f;
-            }
-            split8(v, bh[s], bl[s]);
-#pragma unroll
-            for (int j = 0; j < 8; j++) xn = fmaf(v[j], v[j], xn);
-        }
-        // |x|^2 over both lane halves (any summation order: the margin
-        // covers its rounding)
-        xn += __shfl_xor(xn, 32);
-    }
+    float xn;
+    load_query_frags(x, ldx, d, nsteps, qrow_s[qloc], lh, bh, bl, xn);
 
     // ---- code tiles: global -> registers -> LDS
     uint4 pf[8];
@@ -223,20 +175,8 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
             const int cr = v0 + 32 * bi + 4 * lh + 8 * g;
             yq[g] = cr < len ? *(const float4*)(ynl + cr) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        floatx16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; r++) acc[r] = 0.f;
-        const uint8_t* Arow = tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh;
-#pragma unroll
-        for (int s = 0; s < BDM / 16; s++) {
-            if (s < nsteps) {
-                const bf16x8 ah = *(const bf16x8*)(Arow + 32 * s);
-                const bf16x8 al = *(const bf16x8*)(Arow + 2 * DB + 32 * s);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[s], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
-            }
-        }
+        const floatx16 acc = bf3_block(tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh,
+                                       DB, nsteps, bh, bl);
         // approx -> 32-bit keys -> thread queue
         const uint32_t ordbase = (uint32_t)tile << 4;
         const bool full = v0 + BV <= len;

@@ -105,7 +105,7 @@ struct IndexFlat : Index {
     template <class OutIdx>
     void knn_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
                     hipStream_t stream) const;
-    mutable DeviceBuffer d_xb_, d_norms_;
+    mutable DeviceBuffer d_xb_, d_norms_, d_cbf_, d_cnmax_;
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
     mutable DeviceBuffer s_xn_, s_tile_, s_cand_d_, s_cand_i_;

@@ -231,3 +231,24 @@ def test_mfma_scan_d128_bench_shape(amd, orc, gpu):
     ref = orc.IVFOracle.from_index(idx)
     Dr, Ir, _, _ = ref.search(xq, 10, 32, nslices=1)
     assert_same_results(D, I, Dr, Ir)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("metric", [1, 0])
+@pytest.mark.parametrize("ny,k", [(256, 8), (1024, 32), (4096, 32), (4096, 64), (5000, 1)])
+def test_coarse_bf3_equals_f32_tile_and_oracle(amd, orc, gpu, monkeypatch, metric, ny, k):
+    # bf16x3 filter + exact re-rank vs the f32 MFMA tile + select; duplicated
+    # rows make exact distance ties at the k boundary
+    d = 64
+    y = rand(orc, ny, d, 41)
+    y[ny // 2: ny // 2 + 40] = y[:40]
+    x = np.ascontiguousarray(np.concatenate([rand(orc, 180, d, 42), y[:20]]))
+    idx = amd.IndexFlat(d, metric)
+    idx.add(y)
+    monkeypatch.setenv("FAISS_AMD_COARSE", "f32")
+    Df, If = idx.search(x, k)
+    monkeypatch.setenv("FAISS_AMD_COARSE", "bf3")
+    Db, Ib = idx.search(x, k)
+    assert_same_results(Db, Ib, Df, If)
+    Dr, Ir = orc.knn(x, y, k, metric=metric, blas_form=True)
+    assert_same_results(Db, Ib, Dr, Ir)
