@@ -50,18 +50,19 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& l
 // The B operand (32 query columns per wave) for one work item: lane holds
 // query column `li` dims [16 s + 8 lh, +8) split into hi / lo, and |x|^2
 // (any order; margins only).  qr < 0: zero column.
+template <int NS>
 __device__ __forceinline__ void load_query_frags(const float* __restrict__ x, int ldx, int d,
-                                                 int nsteps, int qr, int lh, bf16x8 (&bh)[BDM / 16],
-                                                 bf16x8 (&bl)[BDM / 16], float& xn) {
+                                                 int qr, int lh, bf16x8 (&bh)[NS],
+                                                 bf16x8 (&bl)[NS], float& xn) {
     const float* xr = x + (int64_t)(qr < 0 ? 0 : qr) * ldx;
     xn = 0.f;
 #pragma unroll
-    for (int s = 0; s < BDM / 16; s++) {
+    for (int s = 0; s < NS; s++) {
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const int kk = 16 * s + 8 * lh + j;
-            v[j] = (qr >= 0 && s < nsteps && kk < d) ? xr[kk] : 0.f;
+            v[j] = (qr >= 0 && kk < d) ? xr[kk] : 0.f;
         }
         split8(v, bh[s], bl[s]);
 #pragma unroll
@@ -70,27 +71,33 @@ __device__ __forceinline__ void load_query_frags(const float* __restrict__ x, in
     xn += __shfl_xor(xn, 32);
 }
 
-// One 32x32 block: A = 32 database rows (hi/lo image in LDS, row stride CSB
-// bytes, this lane's row pointer `arow` already offset by 16 * lh bytes),
-// B = the register query fragments.  acc[r] = row (r&3)+8(r>>2)+4lh, col li.
-__device__ __forceinline__ floatx16 bf3_block(const uint8_t* arow, int DB, int nsteps,
-                                              const bf16x8 (&bh)[BDM / 16],
-                                              const bf16x8 (&bl)[BDM / 16]) {
+// One 32x32 block: A = 32 database rows (hi/lo image in LDS, this lane's row
+// pointer `arow` already offset by 16 * lh bytes), B = the register query
+// fragments.  acc[r] = row (r&3)+8(r>>2)+4lh, col li.
+template <int NS>
+__device__ __forceinline__ floatx16 bf3_block(const uint8_t* arow, const bf16x8 (&bh)[NS],
+                                              const bf16x8 (&bl)[NS]) {
+    constexpr int DB = 16 * NS;
+    bf16x8 ah[NS], al[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        ah[s] = *(const bf16x8*)(arow + 32 * s);
+        al[s] = *(const bf16x8*)(arow + 2 * DB + 32 * s);
+    }
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; r++) acc[r] = 0.f;
 #pragma unroll
-    for (int s = 0; s < BDM / 16; s++) {
-        if (s < nsteps) {
-            const bf16x8 ah = *(const bf16x8*)(arow + 32 * s);
-            const bf16x8 al = *(const bf16x8*)(arow + 2 * DB + 32 * s);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
-        }
+    for (int s = 0; s < NS; s++) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], bh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
     }
     return acc;
 }
+
+// padded dim of the bf16 hi/lo images: a multiple of 32 (NS = DB/16 even)
+inline int bf3_db(int d) { return (d + 31) / 32 * 32; }
 
 }  // namespace kern
 }  // namespace faiss_amd

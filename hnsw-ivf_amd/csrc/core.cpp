@@ -151,8 +151,8 @@ void IndexFlat::sync_device() const {
                                    sizeof(float) * d, ntotal, hipMemcpyHostToDevice, s));
         kern::row_norms(d_xb_.as<float>(), ntotal, d, l, d_norms_.as<float>(), s);
         // bf16 hi/lo image + largest norm for the bf16x3 coarse filter
-        if (roundup((size_t)d, 16) <= 128) {
-            const int DB = (int)roundup((size_t)d, 16);
+        if (kern::bf3_db_host(d) <= 128) {
+            const int DB = kern::bf3_db_host(d);
             d_cbf_.reserve((size_t)ntotal * 2 * DB * 2);
             d_cnmax_.reserve(sizeof(float));
             kern::split_bf16(d_xb_.as<float>(), ntotal, d, l, DB, d_cbf_.ptr, s);
@@ -243,6 +243,10 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
             kern::select_rows(s_tile_.as<float>(), nq, ny, ny, k, metric_l2, 0,
                               distances + q0 * k, o32 ? o32 + q0 * k : nullptr,
                               o64 ? o64 + q0 * k : nullptr, k, s);
+            if (!metric_l2 && ny > 0)
+                kern::select_fix_ip(s_tile_.as<float>(), nq, ny, ny, k, distances + q0 * k,
+                                    o32 ? o32 + q0 * k : nullptr, o64 ? o64 + q0 * k : nullptr,
+                                    k, s);
         } else {
             for (idx_t c = 0; c < nyc; c++) {
                 const idx_t y0 = c * Yc, nyy = std::min(Yc, ny - y0);

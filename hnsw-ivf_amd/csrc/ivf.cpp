@@ -296,7 +296,7 @@ void IndexIVFFlat::upload_extra() const {
                          d_list_len_.as<uint32_t>(), (int)nlist, d_ynmax_.as<float>(), s);
     // bf16 hi/lo image of the arena for the MFMA filter (same bytes as f32)
     if (kern::ivf_mfma_kq(1, d) > 0) {
-        const int DB = (int)roundup((size_t)d, 16);
+        const int DB = kern::bf3_db_host(d);
         d_cbf_.reserve(std::max<size_t>(arena_rows_, 1) * 2 * DB * 2);
         kern::split_bf16(d_codes_.as<float>(), arena_rows_, d, l, DB, d_cbf_.ptr, s);
         size_t mx = 0;

@@ -59,6 +59,11 @@ void select_rows(const float* D, int64_t nx, int64_t ny, int64_t ldD, int k, int
                  int64_t col0, float* out_d, int32_t* out_i32, int64_t* out_i64,
                  int64_t ldo, hipStream_t s);
 
+// Inner product only: re-select rows whose k-th value ties with an unselected
+// column using the reference heap's arrival-order rule (col0 == 0 tables).
+void select_fix_ip(const float* D, int64_t nx, int64_t ny, int64_t ldD, int k, float* out_d,
+                   int32_t* out_i32, int64_t* out_i64, int64_t ldo, hipStream_t s);
+
 // Merge `nin` sorted candidate tables per row: cand_d/cand_i [n][nin*kin]
 // (already final (dis,label) form, label -1 = empty) -> [n][k].
 void merge_rows(const float* cand_d, const int64_t* cand_i, int64_t n, int nin_x_kin, int k,
@@ -96,7 +101,9 @@ void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const i
 // ivf_mfma_kq = entries kept per (query, list); 0 = not eligible
 // (k > 32 or roundup(d, 16) > 128).
 int ivf_mfma_kq(int k, int d);
-int ivf_bf3_obits(uint32_t max_list_len);  // ordinal bits of the 32-bit keys
+int ivf_bf3_obits(uint32_t max_list_len);
+// padded dim of the bf16 hi/lo images (multiple of 32)
+inline int bf3_db_host(int d) { return (d + 31) / 32 * 32; }  // ordinal bits of the 32-bit keys
 double ivf_bf3_coef(int d);                // margin coefficient
 // f32 arena [rows][ldc] -> bf16 hi/lo arena [rows][2 * roundup(d, 16)]
 void split_bf16(const float* codes, int64_t rows, int d, int ldc, int DB, void* out,

@@ -50,14 +50,14 @@ __device__ __forceinline__ float ip_seq(const float* __restrict__ a, const float
     return acc;
 }
 
-template <bool L2, int KT>
+template <bool L2, int KT, int NS>
 __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
         const float* __restrict__ x, int ldx, int64_t n, int d, const __bf16* __restrict__ cbf,
-        int DB, const float* __restrict__ cnorm, const float* __restrict__ xnorm, int nlist,
+        const float* __restrict__ cnorm, const float* __restrict__ xnorm, int nlist,
         int nsplit, int split_len, float coef, const float* __restrict__ cnmax_p, int obits,
         unsigned long long* __restrict__ part, float* __restrict__ pub,
         float* __restrict__ pbound) {
-    __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * (4 * BDM + 16)];
+    __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * (4 * 16 * NS + 16)];
     __shared__ float bnd_s[BQ][4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     // blocks b and b+8 share an XCD: consecutive splits of one query block
@@ -66,13 +66,13 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
     const int sp = (int)(blockIdx.x % nsplit);
     const int c0 = sp * split_len;
     const int len = min(split_len, nlist - c0);
-    const int CSB = 4 * DB + 16, RU = DB / 4, nsteps = DB / 16;
+    constexpr int DB = 16 * NS, CSB = 4 * DB + 16, RU = DB / 4;
     const int bi = w >> 1, bj = w & 1, li = lane & 31, lh = lane >> 5;
     const int slot = 2 * bi + lh, qloc = 32 * bj + li;
     const int64_t q = qb * BQ + qloc;
-    bf16x8 bh[BDM / 16], bl[BDM / 16];
+    bf16x8 bh[NS], bl[NS];
     float xn_approx;
-    load_query_frags(x, ldx, d, nsteps, q < n ? (int)q : -1, lh, bh, bl, xn_approx);
+    load_query_frags<NS>(x, ldx, d, q < n ? (int)q : -1, lh, bh, bl, xn_approx);
     const float xn = q < n ? xnorm[q] : 0.f;  // the reference-order norm (exact side)
     const float cnmax = *cnmax_p;
 
@@ -120,8 +120,8 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
                 const int cr = v0 + 32 * bi + 4 * lh + 8 * g + c;
                 yv[4 * g + c] = cr < len ? cn[cr] : 0.f;
             }
-        const floatx16 acc = bf3_block(tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh,
-                                       DB, nsteps, bh, bl);
+        const floatx16 acc =
+                bf3_block<NS>(tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh, bh, bl);
         const uint32_t ordbase = (uint32_t)tile << 4;
         const bool full = v0 + BV <= len;
 #pragma unroll
@@ -333,7 +333,7 @@ __global__ void k_array_max(const float* __restrict__ a, int64_t n, float* __res
 // ---------------------------------------------------------------- host
 CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k) {
     CoarsePlan p{};
-    if (n < 20 || nlist <= 0 || k < 1 || k > kMaxK || roundup((size_t)d, 16) > (size_t)BDM)
+    if (n < 20 || nlist <= 0 || k < 1 || k > kMaxK || bf3_db(d) > BDM)
         return p;
     int nsplit = nlist >= 2048 ? 4 : nlist >= 1024 ? 2 : 1;
     const int per = (int)cdiv((size_t)k, (size_t)(4 * nsplit));
@@ -363,15 +363,22 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(p.ok);
     FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldc % 4 == 0);
-    const int DB = (int)roundup((size_t)d, 16);
+    const int NS = bf3_db(d) / 16;
     const float coef = (float)ivf_bf3_coef(d);
     const int64_t nqb = (int64_t)cdiv((size_t)n, BQ);
     const int64_t grid = nqb * p.nsplit;
     FAISS_THROW_IF_NOT(grid < (1ll << 31));
-#define LAUNCH_A(L2V, KTV)                                                                     \
-    k_coarse_bf3_filter<L2V, KTV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(                  \
-            x, ldx, n, d, (const __bf16*)cbf, DB, cnorm, xnorm, nlist, p.nsplit, p.split_len, \
+#define LAUNCH_NS(L2V, KTV, NSV)                                                              \
+    k_coarse_bf3_filter<L2V, KTV, NSV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(            \
+            x, ldx, n, d, (const __bf16*)cbf, cnorm, xnorm, nlist, p.nsplit, p.split_len,     \
             coef, cnmax, p.obits, part, pub, pbound)
+#define LAUNCH_A(L2V, KTV)                     \
+    do {                                       \
+        if (NS == 2) LAUNCH_NS(L2V, KTV, 2);   \
+        else if (NS == 4) LAUNCH_NS(L2V, KTV, 4); \
+        else if (NS == 6) LAUNCH_NS(L2V, KTV, 6); \
+        else LAUNCH_NS(L2V, KTV, 8);           \
+    } while (0)
 #define DISPATCH(L2V)                      \
     do {                                   \
         if (p.kt == 4) LAUNCH_A(L2V, 4);   \
@@ -382,6 +389,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     else DISPATCH(false);
 #undef DISPATCH
 #undef LAUNCH_A
+#undef LAUNCH_NS
     HIP_LAUNCH_CHECK();
     const dim3 g2((unsigned)cdiv((size_t)n, 4)), b2(256);
     const int E1 = 4 * p.kt;

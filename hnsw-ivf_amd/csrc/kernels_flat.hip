@@ -14,6 +14,7 @@
 #include "kernels.h"
 #include "ref_arith.h"
 #include "wave_select.h"
+#include "exact_select.h"
 
 namespace faiss_amd {
 namespace kern {
@@ -276,6 +277,65 @@ void select_rows(const float* D, int64_t nx, int64_t ny, int64_t ldD, int k, int
     FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
     k_select_rows<<<dim3((unsigned)cdiv(nx, 4)), dim3(256), 0, s>>>(
             D, nx, ny, ldD, k, metric_l2, col0, out_d, out_i32, out_i64, ldo);
+    HIP_LAUNCH_CHECK();
+}
+
+// Inner-product rows whose k-th value is tied with a column that was not
+// selected: the lexicographic (-ip, -j) choice of k_select_rows differs from
+// the reference heap (CMin, strict admission, columns arriving in id
+// order), so such rows are re-selected with the arrival-order rule
+// (exact_select.h).  One wave per row; rows without a boundary tie exit
+// after one counting pass.
+struct RowStream {
+    const float* row;
+    int64_t ny;
+    int lane;
+    template <class F>
+    __device__ __forceinline__ void for_each(F f) const {
+        for (int64_t j0 = 0; j0 < ny; j0 += 64) {
+            const int64_t j = j0 + lane;
+            float k1 = WS_INF;
+            long long k2 = WS_NOID;
+            bool ok = j < ny;
+            if (ok) {
+                to_key(0, row[j], (long long)j, k1, k2);
+                ok = key_admissible(k1);
+            }
+            f(ok, k1, k2, (long long)j);
+        }
+    }
+};
+
+template <class OutIdx>
+__global__ __launch_bounds__(256) void k_select_fix_ip(const float* __restrict__ D, int64_t nx,
+                                                       int64_t ny, int64_t ldD, int k,
+                                                       float* __restrict__ out_d,
+                                                       OutIdx* __restrict__ out_i, int64_t ldo) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= nx) return;
+    const float v = out_d[r * ldo + k - 1];
+    if ((int64_t)out_i[r * ldo + k - 1] < 0) return;  // fewer than k results: no boundary
+    const float* row = D + r * ldD;
+    int cnt = 0;
+    for (int64_t j0 = 0; j0 < ny; j0 += 64) {
+        const int64_t j = j0 + lane;
+        cnt += __popcll(__ballot(j < ny && row[j] == v));
+    }
+    const int in = __popcll(__ballot(lane < k && out_d[r * ldo + (lane < k ? lane : 0)] == v));
+    if (cnt <= in) return;
+    RowStream st{row, ny, lane};
+    exact_topk_resolve(st, k, 0, lane, true, out_d + r * ldo, out_i + r * ldo);
+}
+
+void select_fix_ip(const float* D, int64_t nx, int64_t ny, int64_t ldD, int k, float* out_d,
+                   int32_t* out_i32, int64_t* out_i64, int64_t ldo, hipStream_t s) {
+    if (nx <= 0) return;
+    const dim3 g((unsigned)cdiv(nx, 4)), b(256);
+    if (out_i32)
+        k_select_fix_ip<int32_t><<<g, b, 0, s>>>(D, nx, ny, ldD, k, out_d, out_i32, ldo);
+    else
+        k_select_fix_ip<int64_t><<<g, b, 0, s>>>(D, nx, ny, ldD, k, out_d, out_i64, ldo);
     HIP_LAUNCH_CHECK();
 }
 

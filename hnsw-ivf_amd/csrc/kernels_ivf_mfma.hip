@@ -80,9 +80,9 @@ __global__ void k_split_bf16(const float* __restrict__ codes, int64_t rows, int 
     out[r * 2 * DB + DB + j] = (__bf16)(v - (float)h);
 }
 
-template <bool L2, int KT>
+template <bool L2, int KT, int NS>
 __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
-        const float* __restrict__ x, int ldx, int d, const __bf16* __restrict__ cbf, int DB,
+        const float* __restrict__ x, int ldx, int d, const __bf16* __restrict__ cbf,
         const float* __restrict__ ynorm, const float* __restrict__ ynmax,
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
         int nprobe, float coef, int obits, const uint32_t* __restrict__ bucket_off,
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
         unsigned long long* __restrict__ part, float* __restrict__ pub,
         float* __restrict__ pbound) {
     // two code tiles (double buffer), row stride CSB bytes = 4*DB + 16
-    __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * (4 * BDM + 16)];
+    __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * (4 * 16 * NS + 16)];
     __shared__ uint32_t ent_s[BQ];
     __shared__ int32_t qrow_s[BQ];
     __shared__ float bnd_s[BQ][4];
@@ -114,9 +114,9 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
     }
     const int len = (int)list_len[l];
     const int64_t row0 = list_off[l];
-    const int CSB = 4 * DB + 16;     // LDS row stride (bytes)
-    const int RU = DB / 4;           // uint4 per code row (hi + lo)
-    const int nsteps = DB / 16;
+    constexpr int DB = 16 * NS;
+    constexpr int CSB = 4 * DB + 16;  // LDS row stride (bytes)
+    constexpr int RU = DB / 4;        // uint4 per code row (hi + lo)
     const int bi = w >> 1, bj = w & 1;
     const int li = lane & 31, lh = lane >> 5;
     const int slot = 2 * bi + lh;    // this thread's share of its query's codes
@@ -124,9 +124,9 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
     __syncthreads();
 
     // ---- query fragments (B operand): registers for the whole work item
-    bf16x8 bh[BDM / 16], bl[BDM / 16];
+    bf16x8 bh[NS], bl[NS];
     float xn;
-    load_query_frags(x, ldx, d, nsteps, qrow_s[qloc], lh, bh, bl, xn);
+    load_query_frags<NS>(x, ldx, d, qrow_s[qloc], lh, bh, bl, xn);
 
     // ---- code tiles: global -> registers -> LDS
     uint4 pf[8];
@@ -175,8 +175,8 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
             const int cr = v0 + 32 * bi + 4 * lh + 8 * g;
             yq[g] = cr < len ? *(const float4*)(ynl + cr) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        const floatx16 acc = bf3_block(tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh,
-                                       DB, nsteps, bh, bl);
+        const floatx16 acc =
+                bf3_block<NS>(tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh, bh, bl);
         // approx -> 32-bit keys -> thread queue
         const uint32_t ordbase = (uint32_t)tile << 4;
         const bool full = v0 + BV <= len;
@@ -483,7 +483,7 @@ void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* l
 
 int ivf_mfma_kq(int k, int dp) {
     // entries kept per (query, list) = 4 threads x KT
-    if (roundup((size_t)dp, 16) > (size_t)BDM || k > 32) return 0;
+    if (bf3_db(dp) > BDM || k > 32) return 0;
     return 4 * (k <= 2 ? 2 : k <= 12 ? 4 : 8);
 }
 
@@ -521,7 +521,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     FAISS_THROW_IF_NOT(ldc % 4 == 0);
     FAISS_THROW_IF_NOT(nprobe <= 64);
     FAISS_THROW_IF_NOT(obits >= 4 && obits <= 14);
-    const int DB = (int)roundup((size_t)d, 16);
+    const int NS = bf3_db(d) / 16;
     const int64_t grid = (int64_t)roundup((size_t)max_items, 32);
     FAISS_THROW_IF_NOT(grid < (1ll << 31));
     const bool l2 = metric_l2 != 0;
@@ -531,10 +531,17 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     const float coef = (float)ivf_bf3_coef(d);
     {
         ScopedKernelTimer tm(kt, "ivf_flat_scan", 0.0, s);
-#define LAUNCH_A(L2V, KTV)                                                                    \
-    k_ivf_bf3_filter<L2V, KTV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(                    \
-            x, ldx, d, (const __bf16*)cbf, DB, ynorm, ynmax, list_off, list_len, nlist,       \
-            nprobe, coef, obits, b.bucket_off, b.item_off, b.entries, part, pub, pbound)
+#define LAUNCH_NS(L2V, KTV, NSV)                                                              \
+    k_ivf_bf3_filter<L2V, KTV, NSV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(               \
+            x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, list_off, list_len, nlist, nprobe,   \
+            coef, obits, b.bucket_off, b.item_off, b.entries, part, pub, pbound)
+#define LAUNCH_A(L2V, KTV)                     \
+    do {                                       \
+        if (NS == 2) LAUNCH_NS(L2V, KTV, 2);   \
+        else if (NS == 4) LAUNCH_NS(L2V, KTV, 4); \
+        else if (NS == 6) LAUNCH_NS(L2V, KTV, 6); \
+        else LAUNCH_NS(L2V, KTV, 8);           \
+    } while (0)
 #define DISPATCH(M, L2V)                  \
     do {                                  \
         if (KE == 8) M(L2V, 2);           \
@@ -555,6 +562,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         else DISPATCH(LAUNCH_B, false);
         HIP_LAUNCH_CHECK();
 #undef LAUNCH_A
+#undef LAUNCH_NS
 #undef LAUNCH_B
 #undef DISPATCH
     }
