@@ -216,7 +216,7 @@ struct CoarseStream {
                 long long k2 = WS_NOID, rank = 0;
                 bool ok = s0 + lane < nsv;
                 if (ok) {
-                    eval((int)(uint32_t)part[surv[s0 + lane]], k1, k2, rank);
+                    eval((int)surv[s0 + lane], k1, k2, rank);
                     ok = key_admissible(k1);
                 }
                 f(ok, k1, k2, rank);
@@ -254,7 +254,7 @@ struct CoarseStream {
     }
 };
 
-template <bool L2, class OutIdx>
+template <bool L2, class OutIdx, int V>
 __global__ __launch_bounds__(256) void k_coarse_rerank(
         const unsigned long long* __restrict__ part, const float* __restrict__ pub,
         const float* __restrict__ pbound, const float* __restrict__ x, int ldx,
@@ -283,14 +283,14 @@ __global__ __launch_bounds__(256) void k_coarse_rerank(
     st.U = WS_INF;
     const int total = valid ? st.E : 0;
     const float* pu = pub + q * st.E;
-    float qd = WS_INF, td = WS_INF;
-    long long qi = WS_NOID, ti = WS_NOID;
-    for (int c0 = 0; c0 < total; c0 += 64) {
-        const int c = c0 + lane;
-        const bool ok = c < total;
-        wave_offer(qd, qi, ok ? pu[c] : WS_INF, ok ? (long long)c : WS_NOID, td, ti, k, lane);
+    float ub[V];
+#pragma unroll
+    for (int i = 0; i < V; i++) {
+        const int c = i * 64 + lane;
+        ub[i] = c < total ? pu[c] : WS_INF;
     }
-    const float U = __shfl(qd, k - 1);
+    float U = wave_kth_smallest<V>(ub, k);
+    if (!(U <= WS_INF)) U = WS_INF;
     st.U = U;
     {
         bool fl = false;
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256) void k_coarse_rerank(
         const bool sv = c < total && st.survivor(c);
         const unsigned long long m = __ballot(sv);
         const int pos = ns + __popcll(m & ((1ull << lane) - 1ull));
-        if (sv && pos < CR_CAP) surv[w][pos] = (uint32_t)c;
+        if (sv && pos < CR_CAP) surv[w][pos] = (uint32_t)st.part[c];  // centroid id
         ns += __popcll(m);
     }
     st.overflow = ns > CR_CAP;
@@ -393,27 +393,29 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     HIP_LAUNCH_CHECK();
     const dim3 g2((unsigned)cdiv((size_t)n, 4)), b2(256);
     const int E1 = 4 * p.kt;
+    const int E = p.nsplit * E1;
+    const int V = E <= 128 ? 2 : E <= 256 ? 4 : E <= 512 ? 8 : 16;
+    FAISS_THROW_IF_NOT(E <= 1024);
+#define LAUNCH_R(L2V, OT, OUT, VV)                                                              \
+    k_coarse_rerank<L2V, OT, VV><<<g2, b2, 0, s>>>(part, pub, pbound, x, ldx, xnorm, cent, ldc, \
+                                                   cnorm, n, d, nlist, p.nsplit, p.split_len,   \
+                                                   E1, k, D, OUT)
+#define LAUNCH_RV(L2V, OT, OUT)                  \
+    do {                                         \
+        if (V == 2) LAUNCH_R(L2V, OT, OUT, 2);   \
+        else if (V == 4) LAUNCH_R(L2V, OT, OUT, 4); \
+        else if (V == 8) LAUNCH_R(L2V, OT, OUT, 8); \
+        else LAUNCH_R(L2V, OT, OUT, 16);         \
+    } while (0)
     if (metric_l2) {
-        if (I32)
-            k_coarse_rerank<true, int32_t><<<g2, b2, 0, s>>>(part, pub, pbound, x, ldx, xnorm,
-                                                             cent, ldc, cnorm, n, d, nlist,
-                                                             p.nsplit, p.split_len, E1, k, D, I32);
-        else
-            k_coarse_rerank<true, int64_t><<<g2, b2, 0, s>>>(part, pub, pbound, x, ldx, xnorm,
-                                                             cent, ldc, cnorm, n, d, nlist,
-                                                             p.nsplit, p.split_len, E1, k, D, I64);
+        if (I32) LAUNCH_RV(true, int32_t, I32);
+        else LAUNCH_RV(true, int64_t, I64);
     } else {
-        if (I32)
-            k_coarse_rerank<false, int32_t><<<g2, b2, 0, s>>>(part, pub, pbound, x, ldx, xnorm,
-                                                              cent, ldc, cnorm, n, d, nlist,
-                                                              p.nsplit, p.split_len, E1, k, D,
-                                                              I32);
-        else
-            k_coarse_rerank<false, int64_t><<<g2, b2, 0, s>>>(part, pub, pbound, x, ldx, xnorm,
-                                                              cent, ldc, cnorm, n, d, nlist,
-                                                              p.nsplit, p.split_len, E1, k, D,
-                                                              I64);
+        if (I32) LAUNCH_RV(false, int32_t, I32);
+        else LAUNCH_RV(false, int64_t, I64);
     }
+#undef LAUNCH_RV
+#undef LAUNCH_R
     HIP_LAUNCH_CHECK();
 }
 

@@ -250,84 +250,85 @@ __global__ void k_list_max(const float* __restrict__ yn, const uint32_t* __restr
 // all of its rows are re-ranked.  Every other probe contributes its kept
 // entries with lb <= U.  The exact top-k over that candidate stream (with the
 // reference tie rule, exact_select.h) is the reference result.
+//
+// Latency layout: lane r < nprobe holds probe r's list (offset, length,
+// dropped bound); the kept entries' upper bounds are loaded V per lane in one
+// round trip; U comes from a ballot radix select (no shuffles); survivors are
+// compacted to LDS as global arena rows.
 constexpr int RR_CAP = 512;
 
-template <bool L2, int KE>
+template <bool L2>
 struct RerankStream {
-    const unsigned long long* part;  // this query's [nprobe][KE]
-    const float* pub;
-    const int32_t* asg;  // this query's [nprobe]
-    const uint32_t* list_off;
-    const uint32_t* list_len;
-    int nlist, nprobe, d, ldc, lane, nsv;
-    bool overflow;
-    unsigned long long fmask;
-    float U;
-    const uint32_t* surv;
+    const uint32_t* surv;  // global arena rows of the survivors
+    const uint16_t* sprobe;  // their probe rank
+    const int64_t* ids;
     const float* xq;
     const float* codes;
-    const int64_t* ids;
+    int ldc, d, lane, nsv;
+    // overflow mode: re-scan the survivor predicate from global memory
+    bool overflow;
+    const unsigned long long* part;
+    int E, KE;
+    float U;
+    unsigned long long okmask, fmask;
+    uint32_t my_off, my_len;  // lane r: probe r
 
-    __device__ __forceinline__ bool entry_ok(int r) const {
-        const int lst = asg[r];
-        return lst >= 0 && lst < nlist && list_len[lst] > 0;
-    }
-    __device__ __forceinline__ bool survivor(int c) const {
-        const int r = c / KE;
-        if ((fmask >> r) & 1ull) return false;
-        if (!entry_ok(r)) return false;
-        const unsigned long long key = part[c];
-        return key != ~0ull && unordered_f32((uint32_t)(key >> 32)) <= U;
-    }
-    __device__ __forceinline__ void eval(int r, uint32_t row, float& k1, long long& k2, long long& rank) const {
-        const int64_t grow = (int64_t)list_off[asg[r]] + row;
-        const float* yr = codes + grow * ldc;
+    __device__ __forceinline__ uint32_t off_of(int r) const { return __shfl(my_off, r); }
+    __device__ __forceinline__ void eval_row(int r, uint32_t grow, uint32_t rank_row, float& k1,
+                                             long long& k2, long long& rank) const {
+        const float* yr = codes + (int64_t)grow * ldc;
         const float dis = L2 ? ref_l2(xq, yr, d) : ref_ip(xq, yr, d);
         to_key(L2 ? 1 : 0, dis, (long long)ids[grow], k1, k2);
-        rank = ((long long)r << 32) | row;
+        rank = ((long long)r << 32) | rank_row;
     }
     template <class F>
     __device__ __forceinline__ void for_each(F f) const {
-        // (1) surviving kept entries of the non-failing probes
         if (!overflow) {
             for (int s0 = 0; s0 < nsv; s0 += 64) {
                 float k1 = WS_INF;
                 long long k2 = WS_NOID, rank = 0;
                 bool ok = s0 + lane < nsv;
                 if (ok) {
-                    const int c = (int)surv[s0 + lane];
-                    eval(c / KE, (uint32_t)part[c], k1, k2, rank);
+                    const uint32_t grow = surv[s0 + lane];
+                    const int r = sprobe[s0 + lane];
+                    eval_row(r, grow, grow, k1, k2, rank);
                     ok = key_admissible(k1);
                 }
                 f(ok, k1, k2, rank);
             }
         } else {
-            const int total = nprobe * KE;
-            for (int c0 = 0; c0 < total; c0 += 64) {
+            for (int c0 = 0; c0 < E; c0 += 64) {
                 const int c = c0 + lane;
+                const int r = c / KE;
+                const uint32_t roff = off_of(r < 64 ? r : 0);
                 float k1 = WS_INF;
                 long long k2 = WS_NOID, rank = 0;
-                bool ok = c < total && survivor(c);
-                if (__ballot(ok) == 0ull) continue;
-                if (ok) {
-                    eval(c / KE, (uint32_t)part[c], k1, k2, rank);
-                    ok = key_admissible(k1);
+                bool ok = false;
+                if (c < E && ((okmask >> r) & 1ull) && !((fmask >> r) & 1ull)) {
+                    const unsigned long long key = part[c];
+                    ok = key != ~0ull && unordered_f32((uint32_t)(key >> 32)) <= U;
+                    if (ok) {
+                        eval_row(r, roff + (uint32_t)key, roff + (uint32_t)key, k1, k2, rank);
+                        ok = key_admissible(k1);
+                    }
                 }
+                if (__ballot(ok) == 0ull) continue;
                 f(ok, k1, k2, rank);
             }
         }
-        // (2) every row of the failing probes
+        // every row of the failing probes (rank = list row; the arena row
+        // order within a list is the list order)
         unsigned long long m = fmask;
         while (m) {
             const int r = __ffsll((long long)m) - 1;
             m &= m - 1ull;
-            const int len = (int)list_len[asg[r]];
-            for (int v0 = 0; v0 < len; v0 += 64) {
+            const uint32_t o = off_of(r), len = __shfl(my_len, r);
+            for (uint32_t v0 = 0; v0 < len; v0 += 64) {
                 float k1 = WS_INF;
                 long long k2 = WS_NOID, rank = 0;
                 bool ok = v0 + lane < len;
                 if (ok) {
-                    eval(r, (uint32_t)(v0 + lane), k1, k2, rank);
+                    eval_row(r, o + v0 + lane, o + v0 + lane, k1, k2, rank);
                     ok = key_admissible(k1);
                 }
                 f(ok, k1, k2, rank);
@@ -336,73 +337,92 @@ struct RerankStream {
     }
 };
 
-template <bool L2, int KE>
+template <bool L2, int V>
 __global__ __launch_bounds__(256) void k_ivf_rerank(
         const unsigned long long* __restrict__ part, const float* __restrict__ pub,
         const float* __restrict__ pbound, const int32_t* __restrict__ assign,
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
         const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
-        const int64_t* __restrict__ ids, int d, int64_t n, int nprobe, int k,
+        const int64_t* __restrict__ ids, int d, int64_t n, int nprobe, int KE, int k,
         float* __restrict__ D, int64_t* __restrict__ I, uint32_t* __restrict__ stats) {
     __shared__ uint32_t surv[4][RR_CAP];
+    __shared__ uint16_t sprobe[4][RR_CAP];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t q0 = (int64_t)blockIdx.x * 4 + w;
     const bool valid = q0 < n;
     const int64_t q = valid ? q0 : 0;
-    RerankStream<L2, KE> st;
-    st.part = part + q * nprobe * KE;
-    st.pub = pub + q * nprobe * KE;
-    st.asg = assign + q * nprobe;
-    st.list_off = list_off;
-    st.list_len = list_len;
-    st.nlist = nlist;
-    st.nprobe = valid ? nprobe : 0;
-    st.d = d;
-    st.ldc = ldc;
-    st.lane = lane;
-    st.xq = x + q * ldx;
-    st.codes = codes;
-    st.ids = ids;
-    st.fmask = 0ull;
-    st.U = WS_INF;
-    const int total = st.nprobe * KE;
-    // U: k-th smallest upper bound
-    float qd = WS_INF, td = WS_INF;
-    long long qi = WS_NOID, ti = WS_NOID;
-    for (int c0 = 0; c0 < total; c0 += 64) {
-        const int c = c0 + lane;
-        const bool ok = c < total && st.entry_ok(c / KE);
-        wave_offer(qd, qi, ok ? st.pub[c] : WS_INF, ok ? (long long)c : WS_NOID, td, ti, k,
-                   lane);
-    }
-    const float U = __shfl(qd, k - 1);
-    st.U = U;
-    // failing probes (nprobe <= 64: one ballot)
-    {
-        bool fl = false;
-        if (lane < st.nprobe && st.entry_ok(lane)) {
-            const float pb = pbound[q * nprobe + lane];
-            fl = pb < WS_INF && pb <= U;
+    const int E = valid ? nprobe * KE : 0;
+    // per-probe state, lane r = probe r
+    uint32_t my_off = 0, my_len = 0;
+    float my_pb = WS_INF;
+    bool my_ok = false;
+    if (valid && lane < nprobe) {
+        const int lst = assign[q * nprobe + lane];
+        if (lst >= 0 && lst < nlist) {
+            my_len = list_len[lst];
+            my_off = list_off[lst];
+            my_ok = my_len > 0;
+            if (my_ok) my_pb = pbound[q * nprobe + lane];
         }
-        st.fmask = __ballot(fl);
     }
-    // compact the surviving entries
+    const unsigned long long okmask = __ballot(my_ok);
+    // upper bounds, V per lane, one round trip
+    const float* pu = pub + q * (int64_t)nprobe * KE;
+    float ub[V];
+#pragma unroll
+    for (int i = 0; i < V; i++) {
+        const int c = i * 64 + lane;
+        ub[i] = (c < E && ((okmask >> (c / KE)) & 1ull)) ? pu[c] : WS_INF;
+    }
+    float U = wave_kth_smallest<V>(ub, k);
+    if (!(U <= WS_INF)) U = WS_INF;  // NaN guard
+    const unsigned long long fmask = __ballot(my_ok && my_pb < WS_INF && my_pb <= U);
+    // survivors -> LDS (global arena row + probe rank)
+    const unsigned long long* pp = part + q * (int64_t)nprobe * KE;
     int ns = 0;
-    for (int c0 = 0; c0 < total; c0 += 64) {
-        const int c = c0 + lane;
-        const bool sv = c < total && st.survivor(c);
+#pragma unroll
+    for (int i = 0; i < V; i++) {
+        const int c = i * 64 + lane;
+        const int r = c / KE;
+        const uint32_t roff = __shfl(my_off, r < 64 ? r : 0);
+        bool sv = false;
+        uint32_t grow = 0;
+        if (ub[i] < WS_INF && !((fmask >> r) & 1ull)) {
+            const unsigned long long key = pp[c];
+            sv = key != ~0ull && unordered_f32((uint32_t)(key >> 32)) <= U;
+            grow = roff + (uint32_t)key;
+        }
         const unsigned long long m = __ballot(sv);
         const int pos = ns + __popcll(m & ((1ull << lane) - 1ull));
-        if (sv && pos < RR_CAP) surv[w][pos] = (uint32_t)c;
+        if (sv && pos < RR_CAP) {
+            surv[w][pos] = grow;
+            sprobe[w][pos] = (uint16_t)r;
+        }
         ns += __popcll(m);
     }
-    st.overflow = ns > RR_CAP;
-    st.nsv = ns;
+    RerankStream<L2> st;
     st.surv = surv[w];
+    st.sprobe = sprobe[w];
+    st.ids = ids;
+    st.xq = x + q * ldx;
+    st.codes = codes;
+    st.ldc = ldc;
+    st.d = d;
+    st.lane = lane;
+    st.nsv = ns;
+    st.overflow = ns > RR_CAP;
+    st.part = pp;
+    st.E = E;
+    st.KE = KE;
+    st.U = U;
+    st.okmask = okmask;
+    st.fmask = fmask;
+    st.my_off = my_off;
+    st.my_len = my_len;
     exact_topk_resolve(st, k, L2 ? 1 : 0, lane, valid, D + q * k, I + q * k);
     if (stats && valid && lane == 0) {
         atomicAdd(&stats[0], (uint32_t)min(ns, RR_CAP));
-        atomicAdd(&stats[1], (uint32_t)__popcll(st.fmask));
+        atomicAdd(&stats[1], (uint32_t)__popcll(fmask));
         atomicAdd(&stats[2], st.overflow ? 1u : 0u);
     }
 }
@@ -554,13 +574,24 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     }
     {
         ScopedKernelTimer tm(kt, "ivf_rerank", 0.0, s);
-#define LAUNCH_B(L2V, KTV)                                                                    \
-    k_ivf_rerank<L2V, 4 * KTV><<<dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s>>>(              \
+        const int E = nprobe * KE;
+        const int V = E <= 128 ? 2 : E <= 256 ? 4 : E <= 512 ? 8 : E <= 1024 ? 16 : 32;
+#define LAUNCH_B(L2V, VV)                                                                     \
+    k_ivf_rerank<L2V, VV><<<dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s>>>(                  \
             part, pub, pbound, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, \
-            n, nprobe, k, D, I, stats)
-        if (l2) DISPATCH(LAUNCH_B, true);
-        else DISPATCH(LAUNCH_B, false);
+            n, nprobe, KE, k, D, I, stats)
+#define DISPATCH_V(L2V)                      \
+    do {                                     \
+        if (V == 2) LAUNCH_B(L2V, 2);        \
+        else if (V == 4) LAUNCH_B(L2V, 4);   \
+        else if (V == 8) LAUNCH_B(L2V, 8);   \
+        else if (V == 16) LAUNCH_B(L2V, 16); \
+        else LAUNCH_B(L2V, 32);              \
+    } while (0)
+        if (l2) DISPATCH_V(true);
+        else DISPATCH_V(false);
         HIP_LAUNCH_CHECK();
+#undef DISPATCH_V
 #undef LAUNCH_A
 #undef LAUNCH_NS
 #undef LAUNCH_B

@@ -186,3 +186,27 @@ struct ThreadQueue {
     }
 };
 }  // namespace faiss_amd
+
+namespace faiss_amd {
+// k-th smallest (1-based k) of the V*64 values held V per lane, by a 32-step
+// radix descent on the ordered bit patterns: every step is V compares whose
+// ballots are popcounted on the scalar unit — no cross-lane shuffles.  +inf
+// (or NaN-free padding) sorts last.  Returns +inf when fewer than k values
+// are finite... (precisely: the k-th smallest key, whatever it is).
+template <int V>
+__device__ __forceinline__ float wave_kth_smallest(const float (&v)[V], int k) {
+    uint32_t key[V];
+#pragma unroll
+    for (int i = 0; i < V; i++) key[i] = ordered_f32(v[i]);
+    uint32_t prefix = 0u;
+#pragma unroll 4
+    for (int bit = 31; bit >= 0; bit--) {
+        const uint32_t cand = prefix | (1u << bit);
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < V; i++) cnt += __popcll(__ballot(key[i] < cand));
+        if (cnt < k) prefix = cand;
+    }
+    return unordered_f32(prefix);
+}
+}  // namespace faiss_amd
