@@ -23,6 +23,8 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cstdio>
+#include <cstdlib>
 
 #include "bf3.h"
 #include "common.h"
@@ -34,11 +36,27 @@
 namespace faiss_amd {
 namespace kern {
 
-// sequential fma chain (the fixed order of the BLAS-form inner product)
+// sequential fma chain (the fixed order of the BLAS-form inner product);
+// operands are fetched 32 floats at a time so a lane has 16 loads in flight
 __device__ __forceinline__ float ip_seq(const float* __restrict__ a, const float* __restrict__ b,
                                         int d) {
     float acc = 0.f;
     int j = 0;
+    for (; j + 32 <= d; j += 32) {
+        float4 av[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            av[u] = *(const float4*)(a + j + 4 * u);
+            bv[u] = *(const float4*)(b + j + 4 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            acc = fmaf(av[u].x, bv[u].x, acc);
+            acc = fmaf(av[u].y, bv[u].y, acc);
+            acc = fmaf(av[u].z, bv[u].z, acc);
+            acc = fmaf(av[u].w, bv[u].w, acc);
+        }
+    }
     for (; j + 4 <= d; j += 4) {
         const float4 av = *(const float4*)(a + j), bv = *(const float4*)(b + j);
         acc = fmaf(av.x, bv.x, acc);
@@ -58,7 +76,6 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
         unsigned long long* __restrict__ part, float* __restrict__ pub,
         float* __restrict__ pbound) {
     __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * (4 * 16 * NS + 16)];
-    __shared__ float bnd_s[BQ][4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     // blocks b and b+8 share an XCD: consecutive splits of one query block
     // stay together
@@ -144,8 +161,6 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
     }
     const float bnd = tq.q[KT - 1] != 0xffffffffu ? unordered_f32(tq.q[KT - 1] & ~lowmask)
                                                  : WS_INF;
-    bnd_s[qloc][slot] = bnd;
-    __syncthreads();
     if (q < n) {
         const int64_t e = q * nsplit + sp;
         unsigned long long* po = part + e * (4 * KT) + slot * KT;
@@ -168,11 +183,8 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
                 pu[i] = WS_INF;
             }
         }
-        if (slot == 0) {
-            const float b4 = fminf(fminf(bnd_s[qloc][0], bnd_s[qloc][1]),
-                                   fminf(bnd_s[qloc][2], bnd_s[qloc][3]));
-            pbound[e] = b4 < WS_INF ? b4 - (coef * (xn + cnmax) + 1e-30f) : WS_INF;
-        }
+        // per-thread stream bound: a failing stream is re-scanned alone
+        pbound[e * 4 + slot] = bnd < WS_INF ? bnd - (coef * (xn + cnmax) + 1e-30f) : WS_INF;
     }
 }
 
@@ -185,14 +197,14 @@ struct CoarseStream {
     const float* cent;
     const float* cnorm;
     float xn;
-    int ldc, d, nlist, nsplit, split_len, E, lane, nsv;
+    int ldc, d, nlist, nsplit, split_len, E, KT, lane, nsv;
     bool overflow;
-    uint32_t fmask;
+    unsigned long long fmask;  // failing streams: bit 4 * split + slot
     float U;
     const uint32_t* surv;
 
     __device__ __forceinline__ bool survivor(int c) const {
-        if ((fmask >> (c / (E / nsplit))) & 1u) return false;
+        if ((fmask >> (c / KT)) & 1ull) return false;  // entries of stream c / KT
         const unsigned long long key = part[c];
         return key != ~0ull && unordered_f32((uint32_t)(key >> 32)) <= U;
     }
@@ -235,17 +247,24 @@ struct CoarseStream {
                 f(ok, k1, k2, rank);
             }
         }
-        uint32_t m = fmask;
+        // failing streams: thread slot (bi, lh) of split s saw, per 64-row
+        // tile, rows 32 bi + 4 lh + 8 g + c (g, c < 4)
+        unsigned long long m = fmask;
         while (m) {
-            const int s = __ffs((int)m) - 1;
-            m &= m - 1u;
+            const int sidx = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const int s = sidx >> 2, slot = sidx & 3, bi = slot >> 1, lh = slot & 1;
             const int j0 = s * split_len, j1 = min(nlist, j0 + split_len);
-            for (int v0 = j0; v0 < j1; v0 += 64) {
+            const int ntile = (j1 - j0 + BV - 1) / BV;
+            for (int t0 = 0; t0 < ntile * 16; t0 += 64) {
+                const int e = t0 + lane;  // tile e >> 4, register e & 15
+                const int r = e & 15;
+                const int j = j0 + (e >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
                 float k1 = WS_INF;
                 long long k2 = WS_NOID, rank = 0;
-                bool ok = v0 + lane < j1;
+                bool ok = e < ntile * 16 && j < j1;
                 if (ok) {
-                    eval(v0 + lane, k1, k2, rank);
+                    eval(j, k1, k2, rank);
                     ok = key_admissible(k1);
                 }
                 f(ok, k1, k2, rank);
@@ -260,7 +279,8 @@ __global__ __launch_bounds__(256) void k_coarse_rerank(
         const float* __restrict__ pbound, const float* __restrict__ x, int ldx,
         const float* __restrict__ xnorm, const float* __restrict__ cent, int ldc,
         const float* __restrict__ cnorm, int64_t n, int d, int nlist, int nsplit, int split_len,
-        int E1, int k, float* __restrict__ D, OutIdx* __restrict__ I) {
+        int E1, int k, float* __restrict__ D, OutIdx* __restrict__ I,
+        uint32_t* __restrict__ stats) {
     __shared__ uint32_t surv[4][CR_CAP];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t q0 = (int64_t)blockIdx.x * 4 + w;
@@ -278,6 +298,7 @@ __global__ __launch_bounds__(256) void k_coarse_rerank(
     st.nlist = nlist;
     st.nsplit = nsplit;
     st.split_len = split_len;
+    st.KT = E1 / 4;
     st.lane = lane;
     st.fmask = 0u;
     st.U = WS_INF;
@@ -294,11 +315,11 @@ __global__ __launch_bounds__(256) void k_coarse_rerank(
     st.U = U;
     {
         bool fl = false;
-        if (valid && lane < nsplit) {
-            const float pb = pbound[q * nsplit + lane];
+        if (valid && lane < 4 * nsplit) {
+            const float pb = pbound[q * 4 * nsplit + lane];
             fl = pb < WS_INF && pb <= U;
         }
-        st.fmask = (uint32_t)__ballot(fl);
+        st.fmask = __ballot(fl);
     }
     int ns = 0;
     for (int c0 = 0; c0 < total; c0 += 64) {
@@ -313,6 +334,11 @@ __global__ __launch_bounds__(256) void k_coarse_rerank(
     st.nsv = ns;
     st.surv = surv[w];
     exact_topk_resolve(st, k, L2 ? 1 : 0, lane, valid, D + q * k, I + q * k);
+    if (stats && valid && lane == 0) {
+        atomicAdd(&stats[0], (uint32_t)min(ns, CR_CAP));
+        atomicAdd(&stats[1], (uint32_t)__popcll(st.fmask));
+        atomicAdd(&stats[2], st.overflow ? 1u : 0u);
+    }
 }
 
 __global__ void k_array_max(const float* __restrict__ a, int64_t n, float* __restrict__ out) {
@@ -362,6 +388,10 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
                     int64_t* I64, hipStream_t s) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(p.ok);
+    static uint32_t* stats = nullptr;  // FAISS_AMD_IVF_STATS debug counters
+    const bool dbg = getenv("FAISS_AMD_IVF_STATS") != nullptr;
+    if (dbg && !stats) HIP_CHECK(hipMalloc(&stats, 16));
+    if (dbg) HIP_CHECK(hipMemsetAsync(stats, 0, 16, s));
     FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldc % 4 == 0);
     const int NS = bf3_db(d) / 16;
     const float coef = (float)ivf_bf3_coef(d);
@@ -399,7 +429,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
 #define LAUNCH_R(L2V, OT, OUT, VV)                                                              \
     k_coarse_rerank<L2V, OT, VV><<<g2, b2, 0, s>>>(part, pub, pbound, x, ldx, xnorm, cent, ldc, \
                                                    cnorm, n, d, nlist, p.nsplit, p.split_len,   \
-                                                   E1, k, D, OUT)
+                                                   E1, k, D, OUT, st_ptr)
 #define LAUNCH_RV(L2V, OT, OUT)                  \
     do {                                         \
         if (V == 2) LAUNCH_R(L2V, OT, OUT, 2);   \
@@ -407,6 +437,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
         else if (V == 8) LAUNCH_R(L2V, OT, OUT, 8); \
         else LAUNCH_R(L2V, OT, OUT, 16);         \
     } while (0)
+    uint32_t* const st_ptr = dbg ? stats : nullptr;
     if (metric_l2) {
         if (I32) LAUNCH_RV(true, int32_t, I32);
         else LAUNCH_RV(true, int64_t, I64);
@@ -416,6 +447,13 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     }
 #undef LAUNCH_RV
 #undef LAUNCH_R
+    if (dbg) {
+        uint32_t h[4];
+        HIP_CHECK(hipMemcpyAsync(h, stats, 16, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        fprintf(stderr, "[faiss_amd] coarse bf3: nq=%lld k=%d survivors/q=%.2f failing streams/q=%.4f "
+                "overflow=%u\n", (long long)n, k, h[0] / (double)n, h[1] / (double)n, h[2]);
+    }
     HIP_LAUNCH_CHECK();
 }
 

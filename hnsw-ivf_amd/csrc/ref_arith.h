@@ -43,6 +43,7 @@ __device__ __forceinline__ float ref_dist(const float* __restrict__ a,
                                           const float* __restrict__ b, int d) {
     float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, c4 = 0.f, c5 = 0.f, c6 = 0.f, c7 = 0.f;
     const int n8 = d & ~7;
+#pragma unroll 4
     for (int i = 0; i < n8; i += 8) {
         const float4 a0 = *(const float4*)(a + i), a1 = *(const float4*)(a + i + 4);
         const float4 b0 = *(const float4*)(b + i), b1 = *(const float4*)(b + i + 4);
