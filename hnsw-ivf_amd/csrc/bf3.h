@@ -13,6 +13,8 @@
 
 #include <cstdint>
 
+#include "wave_select.h"
+
 namespace faiss_amd {
 namespace kern {
 
@@ -23,6 +25,12 @@ constexpr int BQ = 64;    // queries per work item
 constexpr int BV = 64;    // database rows per tile
 constexpr int BDM = 128;  // max padded dim (multiple of 16)
 
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // Per-thread sorted queue of the KT smallest 32-bit keys (branchless).
 template <int KT>
 struct ThreadQueue32 {
@@ -31,12 +39,34 @@ struct ThreadQueue32 {
 #pragma unroll
         for (int i = 0; i < KT; i++) q[i] = 0xffffffffu;
     }
+    // q[i] <- median(q[i-1], c, q[i]) (= max(q[i-1], min(c, q[i])) on a sorted
+    // queue): one v_med3_u32 per slot
     __device__ __forceinline__ void push(uint32_t c) {
 #pragma unroll
-        for (int i = KT - 1; i > 0; i--) q[i] = c < q[i - 1] ? q[i - 1] : min(c, q[i]);
+        for (int i = KT - 1; i > 0; i--) q[i] = med3_u32(q[i - 1], c, q[i]);
         q[0] = min(c, q[0]);
     }
 };
+
+// 32-bit candidate keys: the approx value with its low `obits` bits replaced
+// by the thread-local candidate ordinal.  L2 approx values are clamped at 0
+// (the exact distance is >= 0 and max(0, .) is 1-Lipschitz, so the
+// certification bound still holds) and their raw bits are already ordered;
+// IP keys (-ip) use the sign-folded ordering.  decode_lo / decode_hi bracket
+// the approx value whatever the ordinal.
+template <bool L2>
+__device__ __forceinline__ uint32_t key_encode(float a, uint32_t lowmask, uint32_t ord) {
+    const uint32_t bits = L2 ? __float_as_uint(fmaxf(a, 0.f)) : ordered_f32(a);
+    return (bits & ~lowmask) | ord;
+}
+template <bool L2>
+__device__ __forceinline__ float key_decode_lo(uint32_t key, uint32_t lowmask) {
+    return L2 ? __uint_as_float(key & ~lowmask) : unordered_f32(key & ~lowmask);
+}
+template <bool L2>
+__device__ __forceinline__ float key_decode_hi(uint32_t key, uint32_t lowmask) {
+    return L2 ? __uint_as_float(key | lowmask) : unordered_f32(key | lowmask);
+}
 
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& l) {
 #pragma unroll

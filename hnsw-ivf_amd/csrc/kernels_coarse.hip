@@ -143,14 +143,9 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
         const bool full = v0 + BV <= len;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
-            float a;
-            if (L2) {
-                a = fmaf(-2.f, acc[r], xn + yv[r]);
-                a = a < 0.f ? 0.f : a;  // the reference clamps; max(0, .) is 1-Lipschitz
-            } else {
-                a = -acc[r];
-            }
-            uint32_t key = (ordered_f32(a) & ~lowmask) | (ordbase | (uint32_t)r);
+            // L2: clamped at 0 inside key_encode, as the reference clamps
+            const float a = L2 ? fmaf(-2.f, acc[r], xn + yv[r]) : -acc[r];
+            uint32_t key = key_encode<L2>(a, lowmask, ordbase | (uint32_t)r);
             if (!full) {
                 const int cr = v0 + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
                 key = cr < len ? key : 0xffffffffu;
@@ -159,7 +154,7 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
         }
         __syncthreads();
     }
-    const float bnd = tq.q[KT - 1] != 0xffffffffu ? unordered_f32(tq.q[KT - 1] & ~lowmask)
+    const float bnd = tq.q[KT - 1] != 0xffffffffu ? key_decode_lo<L2>(tq.q[KT - 1], lowmask)
                                                  : WS_INF;
     if (q < n) {
         const int64_t e = q * nsplit + sp;
@@ -174,8 +169,8 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
                 const uint32_t row =
                         (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
                 const float m = coef * (xn + cn[row]) + 1e-30f;
-                const float alo = unordered_f32(key & ~lowmask);
-                const float ahi = unordered_f32(key | lowmask);
+                const float alo = key_decode_lo<L2>(key, lowmask);
+                const float ahi = key_decode_hi<L2>(key, lowmask);
                 po[i] = ((unsigned long long)ordered_f32(alo - m) << 32) | (uint32_t)(c0 + row);
                 pu[i] = ahi + m;
             } else {

@@ -185,7 +185,7 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
             const int g = r >> 2, c = r & 3;
             const float yv = c == 0 ? yq[g].x : c == 1 ? yq[g].y : c == 2 ? yq[g].z : yq[g].w;
             const float a = L2 ? fmaf(-2.f, acc[r], xn + yv) : -acc[r];
-            uint32_t key = (ordered_f32(a) & ~lowmask) | (ordbase | (uint32_t)r);
+            uint32_t key = key_encode<L2>(a, lowmask, ordbase | (uint32_t)r);
             if (!full) {
                 const int cr = v0 + 32 * bi + 4 * lh + 8 * g + c;
                 key = cr < len ? key : 0xffffffffu;
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
     // ---- outputs
     const bool qvalid = qloc < nQ;
     const float bnd = tq.q[KT - 1] != 0xffffffffu
-                              ? unordered_f32(tq.q[KT - 1] & ~lowmask)
+                              ? key_decode_lo<L2>(tq.q[KT - 1], lowmask)
                               : WS_INF;
     bnd_s[qloc][slot] = bnd;
     __syncthreads();
@@ -214,8 +214,8 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
                 const int r = (int)(ord & 15u);
                 const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
                 const float m = coef * (xn + ynl[row]) + 1e-30f;
-                const float alo = unordered_f32(key & ~lowmask);
-                const float ahi = unordered_f32(key | lowmask);
+                const float alo = key_decode_lo<L2>(key, lowmask);
+                const float ahi = key_decode_hi<L2>(key, lowmask);
                 po[i] = ((unsigned long long)ordered_f32(alo - m) << 32) | row;
                 pu[i] = ahi + m;
             } else {
