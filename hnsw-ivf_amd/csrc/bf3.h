@@ -126,6 +126,24 @@ __device__ __forceinline__ floatx16 bf3_block(const uint8_t* arow, const bf16x8 
     return acc;
 }
 
+// bf16x2: codes' hi part only (A), queries hi + lo (B)
+template <int NS>
+__device__ __forceinline__ floatx16 bf2_block(const uint8_t* arow, const bf16x8 (&bh)[NS],
+                                              const bf16x8 (&bl)[NS]) {
+    bf16x8 ah[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) ah[s] = *(const bf16x8*)(arow + 32 * s);
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
 // padded dim of the bf16 hi/lo images: a multiple of 32 (NS = DB/16 even)
 inline int bf3_db(int d) { return (d + 31) / 32 * 32; }
 

@@ -315,7 +315,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     const int QT = 64;
     const int l = (int)roundup((size_t)d, 4);
     s_counts_.reserve(sizeof(uint32_t) * nlist);
-    s_cur_.reserve(sizeof(uint32_t) * nlist);
+    s_cur_.reserve(sizeof(uint32_t) * std::max<idx_t>(n * np, 1));
     s_boff_.reserve(sizeof(uint32_t) * (nlist + 1));
     s_ioff_.reserve(sizeof(uint32_t) * (nlist + 1));
     s_ent_.reserve(sizeof(uint32_t) * n * np);

@@ -78,7 +78,7 @@ struct IVFBuckets {
     uint32_t* counts;      // [nlist]
     uint32_t* bucket_off;  // [nlist + 1]
     uint32_t* item_off;    // [nlist + 1]
-    uint32_t* cursor;      // [nlist]
+    uint32_t* cursor;      // [n * nprobe]: slot of each entry in its bucket
     uint32_t* entries;     // [n * nprobe], entry = q * nprobe + rank
 };
 void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,

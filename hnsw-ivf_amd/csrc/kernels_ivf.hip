@@ -26,13 +26,15 @@ namespace faiss_amd {
 namespace kern {
 
 // ---------------------------------------------------------------- bucketing
+// counts per list; the value returned by the atomic is the entry's slot in
+// its bucket, so the fill needs no second round of atomics
 __global__ void k_bucket_count(const int32_t* __restrict__ assign, int64_t total,
                                const uint32_t* __restrict__ list_len, int nlist,
-                               uint32_t* __restrict__ counts) {
+                               uint32_t* __restrict__ counts, uint32_t* __restrict__ pos) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
     int l = assign[e];
-    if (l >= 0 && l < nlist && list_len[l] > 0) atomicAdd(&counts[l], 1u);
+    if (l >= 0 && l < nlist && list_len[l] > 0) pos[e] = atomicAdd(&counts[l], 1u);
 }
 
 // single-workgroup exclusive scan of counts -> bucket_off, ceil(counts/QT)
@@ -80,14 +82,11 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
 __global__ void k_bucket_fill(const int32_t* __restrict__ assign, int64_t total,
                               const uint32_t* __restrict__ list_len, int nlist,
                               const uint32_t* __restrict__ bucket_off,
-                              uint32_t* __restrict__ cursor, uint32_t* __restrict__ entries) {
+                              const uint32_t* __restrict__ pos, uint32_t* __restrict__ entries) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
     int l = assign[e];
-    if (l >= 0 && l < nlist && list_len[l] > 0) {
-        uint32_t pos = bucket_off[l] + atomicAdd(&cursor[l], 1u);
-        entries[pos] = (uint32_t)e;
-    }
+    if (l >= 0 && l < nlist && list_len[l] > 0) entries[bucket_off[l] + pos[e]] = (uint32_t)e;
 }
 
 void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
@@ -95,10 +94,9 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
     int64_t total = n * nprobe;
     FAISS_THROW_IF_NOT_MSG(total < (1ll << 32), "n * nprobe must fit in 32 bits");
     HIP_CHECK(hipMemsetAsync(b.counts, 0, sizeof(uint32_t) * nlist, s));
-    HIP_CHECK(hipMemsetAsync(b.cursor, 0, sizeof(uint32_t) * nlist, s));
     if (total > 0) {
         k_bucket_count<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
-                assign, total, list_len, nlist, b.counts);
+                assign, total, list_len, nlist, b.counts, b.cursor);
         HIP_LAUNCH_CHECK();
     }
     k_bucket_scan<<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off, b.item_off);

@@ -29,6 +29,8 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "kernels.h"
@@ -80,8 +82,12 @@ __global__ void k_split_bf16(const float* __restrict__ codes, int64_t rows, int 
     out[r * 2 * DB + DB + j] = (__bf16)(v - (float)h);
 }
 
-template <bool L2, int KT, int NS>
-__global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
+// Y3: bf16x3 (codes split hi + lo, three MFMAs per k-step);  !Y3: bf16x2
+// (codes rounded to bf16, queries split: two MFMAs per k-step, half the code
+// bytes streamed; wider margin, ivf_bf2_coef).  Both read the same hi|lo
+// image; !Y3 touches only the hi half of every row.
+template <bool L2, int KT, int NS, bool Y3>
+__global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         const float* __restrict__ x, int ldx, int d, const __bf16* __restrict__ cbf,
         const float* __restrict__ ynorm, const float* __restrict__ ynmax,
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
@@ -89,8 +95,8 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
         const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ entries,
         unsigned long long* __restrict__ part, float* __restrict__ pub,
         float* __restrict__ pbound) {
-    // two code tiles (double buffer), row stride CSB bytes = 4*DB + 16
-    __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * (4 * 16 * NS + 16)];
+    // two code tiles (double buffer), row stride CSB bytes = (Y3 ? 4 : 2) * DB + 16
+    __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * ((Y3 ? 4 : 2) * 16 * NS + 16)];
     __shared__ uint32_t ent_s[BQ];
     __shared__ int32_t qrow_s[BQ];
     __shared__ float bnd_s[BQ][4];
@@ -115,8 +121,9 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
     const int len = (int)list_len[l];
     const int64_t row0 = list_off[l];
     constexpr int DB = 16 * NS;
-    constexpr int CSB = 4 * DB + 16;  // LDS row stride (bytes)
-    constexpr int RU = DB / 4;        // uint4 per code row (hi + lo)
+    constexpr int CSB = (Y3 ? 4 : 2) * DB + 16;  // LDS row stride (bytes)
+    constexpr int RU = (Y3 ? DB / 4 : DB / 8);   // uint4 staged per code row
+    constexpr int PF = (BV * RU + 255) / 256;    // uint4 per thread per tile
     const int bi = w >> 1, bj = w & 1;
     const int li = lane & 31, lh = lane >> 5;
     const int slot = 2 * bi + lh;    // this thread's share of its query's codes
@@ -129,11 +136,11 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
     load_query_frags<NS>(x, ldx, d, qrow_s[qloc], lh, bh, bl, xn);
 
     // ---- code tiles: global -> registers -> LDS
-    uint4 pf[8];
+    uint4 pf[PF];
     auto fetch = [&](int v0n) {
         const int nvn = min(BV, len - v0n);
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
+        for (int s = 0; s < PF; s++) {
             const int e = t + 256 * s;
             const int r = e / RU, c = e - r * RU;
             pf[s] = make_uint4(0u, 0u, 0u, 0u);
@@ -144,7 +151,7 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
     auto stash = [&](int buf) {
         uint8_t* T = tiles + buf * BV * CSB;
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
+        for (int s = 0; s < PF; s++) {
             const int e = t + 256 * s;
             const int r = e / RU, c = e - r * RU;
             if (e < BV * RU) *(uint4*)(T + r * CSB + 16 * c) = pf[s];
@@ -175,8 +182,8 @@ __global__ __launch_bounds__(256, 2) void k_ivf_bf3_filter(
             const int cr = v0 + 32 * bi + 4 * lh + 8 * g;
             yq[g] = cr < len ? *(const float4*)(ynl + cr) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        const floatx16 acc =
-                bf3_block<NS>(tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh, bh, bl);
+        const uint8_t* arow = tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh;
+        const floatx16 acc = Y3 ? bf3_block<NS>(arow, bh, bl) : bf2_block<NS>(arow, bh, bl);
         // approx -> 32-bit keys -> thread queue
         const uint32_t ordbase = (uint32_t)tile << 4;
         const bool full = v0 + BV <= len;
@@ -519,6 +526,13 @@ double ivf_bf3_coef(int d) {
     return 2.0 * (3.1 / 65536.0 + (6.0 * d + 8.0) * u);
 }
 
+// bf16x2: |x.y - (xh + xl).yh| <= (2^-8 + 2^-16 (1 + 2^-8)) |x||y| per term
+// plus the f32 accumulation, norm and exact-side roundings (as above)
+double ivf_bf2_coef(int d) {
+    const double u = 1.0 / 16777216.0;
+    return 2.0 * (1.0 / 256.0 + 1.01 / 65536.0 + (6.0 * d + 8.0) * u);
+}
+
 void split_bf16(const float* codes, int64_t rows, int d, int ldc, int DB, void* out,
                 hipStream_t s) {
     if (rows <= 0) return;
@@ -548,13 +562,25 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     // margin of the approximate keys: the bf16 split plus the relative
     // truncation of the 32-bit keys (2^(obits-23)) on |approx|, which the
     // decode (low bits cleared / set) already brackets
-    const float coef = (float)ivf_bf3_coef(d);
+    // precision of the filter: bf16x3 (default) or bf16x2 (FAISS_AMD_IVF_PREC)
+    const char* prec = getenv("FAISS_AMD_IVF_PREC");
+    const bool y3 = !(prec && !strcmp(prec, "bf16x2"));
+    const float coef = (float)(y3 ? ivf_bf3_coef(d) : ivf_bf2_coef(d));
     {
         ScopedKernelTimer tm(kt, "ivf_flat_scan", 0.0, s);
 #define LAUNCH_NS(L2V, KTV, NSV)                                                              \
-    k_ivf_bf3_filter<L2V, KTV, NSV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(               \
-            x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, list_off, list_len, nlist, nprobe,   \
-            coef, obits, b.bucket_off, b.item_off, b.entries, part, pub, pbound)
+    do {                                                                                      \
+        if (y3)                                                                               \
+            k_ivf_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+                    x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, list_off, list_len, nlist,   \
+                    nprobe, coef, obits, b.bucket_off, b.item_off, b.entries, part, pub,      \
+                    pbound);                                                                  \
+        else                                                                                  \
+            k_ivf_bf3_filter<L2V, KTV, NSV, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(\
+                    x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, list_off, list_len, nlist,   \
+                    nprobe, coef, obits, b.bucket_off, b.item_off, b.entries, part, pub,      \
+                    pbound);                                                                  \
+    } while (0)
 #define LAUNCH_A(L2V, KTV)                     \
     do {                                       \
         if (NS == 2) LAUNCH_NS(L2V, KTV, 2);   \
