@@ -299,6 +299,11 @@ void IndexIVFFlat::upload_extra() const {
         const int DB = kern::bf3_db_host(d);
         d_cbf_.reserve(std::max<size_t>(arena_rows_, 1) * 2 * DB * 2);
         kern::split_bf16(d_codes_.as<float>(), arena_rows_, d, l, DB, d_cbf_.ptr, s);
+        d_rres_.reserve(sizeof(float) * std::max<size_t>(arena_rows_, 1));
+        d_rmax_.reserve(sizeof(float) * std::max<size_t>(nlist, 1));
+        kern::row_resnorm_bf16(d_codes_.as<float>(), arena_rows_, d, l, d_rres_.as<float>(), s);
+        kern::ivf_list_ynmax(d_rres_.as<float>(), d_list_off_.as<uint32_t>(),
+                             d_list_len_.as<uint32_t>(), (int)nlist, d_rmax_.as<float>(), s);
         size_t mx = 0;
         for (size_t li = 0; li < nlist; li++) mx = std::max(mx, invlists->list_size(li));
         obits_ = kern::ivf_bf3_obits((uint32_t)std::min<size_t>(mx, 0xffffffffu));
@@ -338,6 +343,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
         if (dbg) HIP_CHECK(hipMemsetAsync(s_flags_.ptr, 0, 4 * sizeof(uint32_t), s));
         kern::ivf_flat_scan_mfma(x, ldx, d_codes_.as<float>(), l, d_cbf_.ptr,
                                  d_ids_.as<int64_t>(), d_ynorm_.as<float>(), d_ynmax_.as<float>(),
+                                 d_rres_.as<float>(), d_rmax_.as<float>(),
                                  d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(),
                                  (int)nlist, d, obits_, n, np, (int)k, l2, b, max_items, assign,
                                  s_part_.as<unsigned long long>(), s_pk1_.as<float>(),

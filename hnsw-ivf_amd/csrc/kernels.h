@@ -105,6 +105,10 @@ int ivf_bf3_obits(uint32_t max_list_len);
 // padded dim of the bf16 hi/lo images (multiple of 32)
 inline int bf3_db_host(int d) { return (d + 31) / 32 * 32; }  // ordinal bits of the 32-bit keys
 double ivf_bf3_coef(int d);                // margin coefficient
+double ivf_bf2_coef(int d);
+// |y - bf16(y)| per row (bf16x2 filter margins)
+void row_resnorm_bf16(const float* codes, int64_t rows, int d, int ldc, float* out,
+                      hipStream_t s);
 // f32 arena [rows][ldc] -> bf16 hi/lo arena [rows][2 * roundup(d, 16)]
 void split_bf16(const float* codes, int64_t rows, int d, int ldc, int DB, void* out,
                 hipStream_t s);
@@ -112,6 +116,7 @@ void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* l
                     int nlist, float* out, hipStream_t s);
 void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, const void* cbf,
                         const int64_t* ids, const float* ynorm, const float* ynmax,
+                        const float* rres, const float* rmax,
                         const uint32_t* list_off, const uint32_t* list_len, int nlist, int d,
                         int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
                         int64_t max_items, const int32_t* assign, unsigned long long* part,

@@ -90,6 +90,7 @@ template <bool L2, int KT, int NS, bool Y3>
 __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         const float* __restrict__ x, int ldx, int d, const __bf16* __restrict__ cbf,
         const float* __restrict__ ynorm, const float* __restrict__ ynmax,
+        const float* __restrict__ rres, const float* __restrict__ rmax,
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
         int nprobe, float coef, int obits, const uint32_t* __restrict__ bucket_off,
         const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ entries,
@@ -220,7 +221,11 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
                 const uint32_t ord = key & lowmask;
                 const int r = (int)(ord & 15u);
                 const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-                const float m = coef * (xn + ynl[row]) + 1e-30f;
+                // Y3: coef (x^2 + y^2); bf16x2: Cauchy-Schwarz on the code
+                // rounding residual, 2 (2 |x| |y - yh| + coef (x^2 + y^2))
+                const float m = Y3 ? coef * (xn + ynl[row]) + 1e-30f
+                                   : 2.f * (2.f * sqrtf(xn) * rres[row0 + row] +
+                                            coef * (xn + ynl[row])) + 1e-30f;
                 const float alo = key_decode_lo<L2>(key, lowmask);
                 const float ahi = key_decode_hi<L2>(key, lowmask);
                 po[i] = ((unsigned long long)ordered_f32(alo - m) << 32) | row;
@@ -233,7 +238,10 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         if (slot == 0) {
             const float b4 = fminf(fminf(bnd_s[qloc][0], bnd_s[qloc][1]),
                                    fminf(bnd_s[qloc][2], bnd_s[qloc][3]));
-            pbound[e] = b4 < WS_INF ? b4 - (coef * (xn + ynmax[l]) + 1e-30f) : WS_INF;
+            const float mmax = Y3 ? coef * (xn + ynmax[l]) + 1e-30f
+                                  : 2.f * (2.f * sqrtf(xn) * rmax[l] + coef * (xn + ynmax[l])) +
+                                            1e-30f;
+            pbound[e] = b4 < WS_INF ? b4 - mmax : WS_INF;
         }
     }
 }
@@ -526,11 +534,34 @@ double ivf_bf3_coef(int d) {
     return 2.0 * (3.1 / 65536.0 + (6.0 * d + 8.0) * u);
 }
 
-// bf16x2: |x.y - (xh + xl).yh| <= (2^-8 + 2^-16 (1 + 2^-8)) |x||y| per term
-// plus the f32 accumulation, norm and exact-side roundings (as above)
+// bf16x2: <x, y> - <xh + xl, yh> = <x, y - yh> + <xr, yh>: the first term is
+// bounded by |x| |y - yh| (Cauchy-Schwarz, |y - yh| stored per row), the
+// second by 2^-16 (1 + 2^-8) |x||y|; plus the f32 accumulation, norm and
+// exact-side roundings.  This is the (x^2 + y^2) coefficient of that bound.
 double ivf_bf2_coef(int d) {
     const double u = 1.0 / 16777216.0;
-    return 2.0 * (1.0 / 256.0 + 1.01 / 65536.0 + (6.0 * d + 8.0) * u);
+    return 1.02 / 65536.0 + (6.1 * d + 8.0) * u;
+}
+
+// |y - bf16(y)| per row (rounded up), the bf16x2 residual norms
+__global__ void k_row_resnorm(const float* __restrict__ codes, int64_t rows, int d, int ldc,
+                              float* __restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    double s = 0.0;
+    for (int j = 0; j < d; j++) {
+        const float v = codes[r * ldc + j];
+        const double e = (double)v - (double)(float)(__bf16)v;
+        s += e * e;
+    }
+    out[r] = (float)(sqrt(s) * (1.0 + 1e-6)) + 1e-38f;
+}
+
+void row_resnorm_bf16(const float* codes, int64_t rows, int d, int ldc, float* out,
+                      hipStream_t s) {
+    if (rows <= 0) return;
+    k_row_resnorm<<<dim3((unsigned)cdiv(rows, 256)), dim3(256), 0, s>>>(codes, rows, d, ldc, out);
+    HIP_LAUNCH_CHECK();
 }
 
 void split_bf16(const float* codes, int64_t rows, int d, int ldc, int DB, void* out,
@@ -544,6 +575,7 @@ void split_bf16(const float* codes, int64_t rows, int d, int ldc, int DB, void* 
 
 void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, const void* cbf,
                         const int64_t* ids, const float* ynorm, const float* ynmax,
+                        const float* rres, const float* rmax,
                         const uint32_t* list_off, const uint32_t* list_len, int nlist, int d,
                         int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
                         int64_t max_items, const int32_t* assign, unsigned long long* part,
@@ -572,12 +604,14 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     do {                                                                                      \
         if (y3)                                                                               \
             k_ivf_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
-                    x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, list_off, list_len, nlist,   \
+                    x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
+                    list_len, nlist,                                                          \
                     nprobe, coef, obits, b.bucket_off, b.item_off, b.entries, part, pub,      \
                     pbound);                                                                  \
         else                                                                                  \
             k_ivf_bf3_filter<L2V, KTV, NSV, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(\
-                    x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, list_off, list_len, nlist,   \
+                    x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
+                    list_len, nlist,                                                          \
                     nprobe, coef, obits, b.bucket_off, b.item_off, b.entries, part, pub,      \
                     pbound);                                                                  \
     } while (0)

@@ -252,7 +252,7 @@ struct IndexIVFFlat : IndexIVF {
 
    protected:
     void upload_extra() const override;
-    mutable DeviceBuffer d_ynorm_, d_ynmax_, d_cbf_, s_part_, s_flags_;
+    mutable DeviceBuffer d_ynorm_, d_ynmax_, d_cbf_, d_rres_, d_rmax_, s_part_, s_flags_;
     mutable int obits_ = 4;
 };
 
