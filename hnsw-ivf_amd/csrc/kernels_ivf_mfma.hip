@@ -594,9 +594,11 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     // margin of the approximate keys: the bf16 split plus the relative
     // truncation of the 32-bit keys (2^(obits-23)) on |approx|, which the
     // decode (low bits cleared / set) already brackets
-    // precision of the filter: bf16x3 (default) or bf16x2 (FAISS_AMD_IVF_PREC)
+    // precision of the filter: bf16x2 (default: half the code bytes, Cauchy-
+    // Schwarz margins) or bf16x3 (FAISS_AMD_IVF_PREC=bf16x3: tighter margins,
+    // fewer re-ranked candidates on data where bf16x2 keeps too many)
     const char* prec = getenv("FAISS_AMD_IVF_PREC");
-    const bool y3 = !(prec && !strcmp(prec, "bf16x2"));
+    const bool y3 = prec && !strcmp(prec, "bf16x3");
     const float coef = (float)(y3 ? ivf_bf3_coef(d) : ivf_bf2_coef(d));
     {
         ScopedKernelTimer tm(kt, "ivf_flat_scan", 0.0, s);
