@@ -252,3 +252,20 @@ def test_coarse_bf3_equals_f32_tile_and_oracle(amd, orc, gpu, monkeypatch, metri
     assert_same_results(Db, Ib, Df, If)
     Dr, Ir = orc.knn(x, y, k, metric=metric, blas_form=True)
     assert_same_results(Db, Ib, Dr, Ir)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 10, 32])
+def test_filter_precisions_identical(amd, orc, cfg1, monkeypatch, k):
+    # bf16x2 / bf16x3 filters and the direct exact scan return the same result
+    idx, xb, xq = cfg1
+    idx.nprobe = 16
+    q = xq[:256]
+    out = {}
+    for mode, prec in (("mfma", "bf16x2"), ("mfma", "bf16x3"), ("exact", "bf16x2")):
+        monkeypatch.setenv("FAISS_AMD_IVF_SCAN", mode)
+        monkeypatch.setenv("FAISS_AMD_IVF_PREC", prec)
+        out[(mode, prec)] = idx.search(q, k)
+    ref = out[("exact", "bf16x2")]
+    for key, (D, I) in out.items():
+        assert_same_results(D, I, *ref)
