@@ -49,6 +49,46 @@ _P = C.c_void_p
 _I64 = C.c_int64
 
 
+class IndexIVFStats(C.Structure):
+    """faiss/IndexIVF.h:567-583 (faiss.cvar.indexIVF_stats); aliases the
+    library's global, so reset() / field reads act on it directly."""
+    _fields_ = [("nq", C.c_size_t), ("nlist", C.c_size_t), ("ndis", C.c_size_t),
+                ("nheap_updates", C.c_size_t), ("quantization_time", C.c_double),
+                ("search_time", C.c_double)]
+
+    def reset(self):
+        lib().faiss_IndexIVFStats_reset(C.byref(self))
+
+
+class HNSWStats(C.Structure):
+    """faiss/impl/HNSW.h:234-253 (faiss.cvar.hnsw_stats), aliases the global."""
+    _fields_ = [("n1", C.c_size_t), ("n2", C.c_size_t), ("ndis", C.c_size_t),
+                ("nhops", C.c_size_t)]
+
+    def reset(self):
+        lib().faiss_amd_HNSWStats_reset()
+
+
+# faiss/IndexIVF.h:28-32 QueryLatencyStats, one record per query (microseconds)
+QUERY_LATENCY_DTYPE = np.dtype([("total_us", np.float64), ("quantization_us", np.float64),
+                                ("list_scan_us", np.float64)])
+
+
+class _CVar:
+    """faiss.cvar: the library's global statistics."""
+
+    @property
+    def indexIVF_stats(self):
+        return lib().faiss_get_indexIVF_stats().contents
+
+    @property
+    def hnsw_stats(self):
+        return lib().faiss_amd_get_hnsw_stats().contents
+
+
+cvar = _CVar()
+
+
 def _declare(L):
     sig = {
         "faiss_get_last_error": (C.c_char_p, []),
@@ -87,7 +127,13 @@ def _declare(L):
         "faiss_amd_IndexIVF_invlists_get_codes": (None, [_P, C.c_size_t, _P]),
         "faiss_amd_IndexIVF_code_size": (C.c_size_t, [_P]),
         "faiss_IndexIVFStats_reset": (None, [_P]),
-        "faiss_get_indexIVF_stats": (_P, []),
+        "faiss_get_indexIVF_stats": (C.POINTER(IndexIVFStats), []),
+        "faiss_amd_IndexIVF_search_stats": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P]),
+        "faiss_amd_IndexIVF_search_preassigned_stats": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, C.c_int, _P, _P, _P]),
+        "faiss_amd_IndexHNSW_search_stats": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P]),
+        "faiss_amd_get_hnsw_stats": (C.POINTER(HNSWStats), []),
+        "faiss_amd_HNSWStats_reset": (None, []),
+        "faiss_amd_fold_device_stats": (C.c_int, [_P]),
         "faiss_IndexIVFFlat_new_with": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t]),
         "faiss_IndexIVFFlat_new_with_metric": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t, C.c_int]),
         "faiss_amd_IndexIVFPQ_new_with": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int]),
@@ -241,6 +287,10 @@ class Index:
                                                    C.c_void_p(D_ptr), C.c_void_p(I_ptr),
                                                    C.c_void_p(stream or 0)))
 
+    def fold_device_stats(self):
+        """Fold device-side counters (hnsw_stats) of device-API searches."""
+        _check(lib().faiss_amd_fold_device_stats(self.h))
+
     def reset_kernel_times(self):
         _check(lib().faiss_amd_reset_kernel_times(self.h))
 
@@ -303,6 +353,17 @@ class IndexHNSW(Index):
     @efConstruction.setter
     def efConstruction(self, v):
         lib().faiss_amd_IndexHNSW_set_efConstruction(self.h, int(v))
+
+    def search_stats(self, x, k):
+        """IndexHNSW::search_stats: (D, I, per-query QueryLatencyStats records)."""
+        x = _f32(x)
+        n = x.shape[0]
+        D = np.empty((n, k), dtype=np.float32)
+        I = np.empty((n, k), dtype=np.int64)
+        st = np.zeros(n, dtype=QUERY_LATENCY_DTYPE)
+        _check(lib().faiss_amd_IndexHNSW_search_stats(self.h, n, _ptr(x), k, None, _ptr(D),
+                                                      _ptr(I), _ptr(st)))
+        return D, I, st
 
     def storage_vectors(self):
         h = lib().faiss_amd_IndexHNSW_storage(self.h)
@@ -387,6 +448,32 @@ class IndexIVF(Index):
                                                        _ptr(centroid_dis), _ptr(D), _ptr(I),
                                                        int(store_pairs)))
         return D, I
+
+    def search_stats(self, x, k, params=None):
+        """IndexIVF::search_stats: (D, I, per-query QueryLatencyStats records)."""
+        x = _f32(x)
+        n = x.shape[0]
+        D = np.empty((n, k), dtype=np.float32)
+        I = np.empty((n, k), dtype=np.int64)
+        st = np.zeros(n, dtype=QUERY_LATENCY_DTYPE)
+        _check(lib().faiss_amd_IndexIVF_search_stats(self.h, n, _ptr(x), k,
+                                                     params.h if params is not None else None,
+                                                     _ptr(D), _ptr(I), _ptr(st)))
+        return D, I, st
+
+    def search_preassigned_stats(self, x, k, assign, centroid_dis, ivf_stats=None):
+        """IndexIVF::search_preassigned_stats: (D, I, per-query records)."""
+        x = _f32(x)
+        n = x.shape[0]
+        assign = np.ascontiguousarray(assign, dtype=np.int64)
+        centroid_dis = np.ascontiguousarray(centroid_dis, dtype=np.float32)
+        D = np.empty((n, k), dtype=np.float32)
+        I = np.empty((n, k), dtype=np.int64)
+        st = np.zeros(n, dtype=QUERY_LATENCY_DTYPE)
+        _check(lib().faiss_amd_IndexIVF_search_preassigned_stats(
+            self.h, n, _ptr(x), k, _ptr(assign), _ptr(centroid_dis), _ptr(D), _ptr(I), 0, None,
+            C.byref(ivf_stats) if ivf_stats is not None else None, _ptr(st)))
+        return D, I, st
 
     def quantize_device(self, n, x_ptr, nprobe, cdis_ptr, assign_ptr, stream=None):
         _check(lib().faiss_amd_IndexIVF_quantize_device(self.h, n, C.c_void_p(x_ptr), nprobe,

@@ -238,16 +238,42 @@ size_t faiss_amd_IndexIVF_code_size(const FaissIndexIVF* index) {
     return v ? v->code_size : 0;
 }
 
-static FaissIndexIVFStats g_stats_c;
-void faiss_IndexIVFStats_reset(FaissIndexIVFStats* stats) { memset(stats, 0, sizeof(*stats)); }
+// IndexIVFStats is layout-identical to FaissIndexIVFStats (static_assert
+// below), so the C struct aliases the global like the reference C API does
+static_assert(sizeof(FaissIndexIVFStats) == sizeof(IndexIVFStats), "stats layout");
+static_assert(sizeof(FaissQueryLatencyStats) == sizeof(QueryLatencyStats), "latency layout");
+static_assert(sizeof(FaissHNSWStats) == sizeof(HNSWStats), "hnsw stats layout");
+void faiss_IndexIVFStats_reset(FaissIndexIVFStats* stats) {
+    reinterpret_cast<IndexIVFStats*>(stats)->reset();
+}
 FaissIndexIVFStats* faiss_get_indexIVF_stats(void) {
-    g_stats_c.nq = indexIVF_stats.nq;
-    g_stats_c.nlist = indexIVF_stats.nlist;
-    g_stats_c.ndis = indexIVF_stats.ndis;
-    g_stats_c.nheap_updates = indexIVF_stats.nheap_updates;
-    g_stats_c.quantization_time = indexIVF_stats.quantization_time;
-    g_stats_c.search_time = indexIVF_stats.search_time;
-    return &g_stats_c;
+    return reinterpret_cast<FaissIndexIVFStats*>(&indexIVF_stats);
+}
+
+int faiss_amd_IndexIVF_search_stats(const FaissIndexIVF* index, idx_t n, const float* x,
+                                    idx_t k, const FaissSearchParameters* params,
+                                    float* distances, idx_t* labels,
+                                    FaissQueryLatencyStats* per_query_stats) {
+    C_TRY IVF(index)->search_stats(n, x, k, distances, labels, resolve_params(params),
+                                   reinterpret_cast<QueryLatencyStats*>(per_query_stats));
+    C_CATCH
+}
+
+int faiss_amd_IndexIVF_search_preassigned_stats(
+        const FaissIndexIVF* index, idx_t n, const float* x, idx_t k, const idx_t* assign,
+        const float* centroid_dis, float* distances, idx_t* labels, int store_pairs,
+        const FaissSearchParameters* params, FaissIndexIVFStats* ivf_stats,
+        FaissQueryLatencyStats* per_query_stats) {
+    C_TRY const SearchParametersIVF* p = nullptr;
+    if (params) {
+        p = dynamic_cast<const SearchParametersIVF*>(resolve_params(params));
+        FAISS_THROW_IF_NOT_MSG(p, "IndexIVF params have incorrect type");
+    }
+    IVF(index)->search_preassigned_stats(n, x, k, assign, centroid_dis, distances, labels,
+                                         store_pairs != 0, p,
+                                         reinterpret_cast<IndexIVFStats*>(ivf_stats),
+                                         reinterpret_cast<QueryLatencyStats*>(per_query_stats));
+    C_CATCH
 }
 
 // ---------------- IndexIVFFlat
@@ -320,6 +346,31 @@ void faiss_amd_IndexHNSW_set_efConstruction(FaissIndexHNSW* p, int v) {
 FaissIndex* faiss_amd_IndexHNSW_storage(const FaissIndexHNSW* p) {
     auto h = HNnt(p);
     return h ? FX(h->storage) : nullptr;
+}
+int faiss_amd_IndexHNSW_search_stats(const FaissIndexHNSW* p, idx_t n, const float* x, idx_t k,
+                                     const FaissSearchParameters* params, float* distances,
+                                     idx_t* labels, FaissQueryLatencyStats* per_query_stats) {
+    C_TRY auto h = HNnt(p);
+    FAISS_THROW_IF_NOT_MSG(h, "index is not an IndexHNSW");
+    // the efSearch set with faiss_amd_SearchParametersIVF_set_quantizer_efSearch
+    const SearchParameters* sp = nullptr;
+    if (params) {
+        auto c = reinterpret_cast<const SearchParamsC*>(params);
+        if (c->ivf.quantizer_params) sp = &c->hnsw;
+    }
+    h->search_stats(n, x, k, distances, labels, sp,
+                    reinterpret_cast<QueryLatencyStats*>(per_query_stats));
+    C_CATCH
+}
+FaissHNSWStats* faiss_amd_get_hnsw_stats(void) {
+    return reinterpret_cast<FaissHNSWStats*>(&hnsw_stats);
+}
+void faiss_amd_HNSWStats_reset(void) { hnsw_stats.reset(); }
+int faiss_amd_fold_device_stats(const FaissIndex* index) {
+    C_TRY auto ix = IX(index);
+    ix->fold_device_stats();
+    if (auto v = dynamic_cast<const IndexIVF*>(ix)) v->quantizer->fold_device_stats();
+    C_CATCH
 }
 int faiss_amd_IndexHNSW_graph(const FaissIndexHNSW* p, int* entry_point, int* max_level,
                               size_t* n_neighbors, size_t* n_cum, const int32_t** levels,

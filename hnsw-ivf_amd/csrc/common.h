@@ -59,6 +59,13 @@ class FaissException : public std::exception {
         FAISS_THROW_MSG(__buf);                                       \
     } while (0)
 
+#define FAISS_THROW_IF_NOT_FMT(X, FMT, ...)                           \
+    do {                                                              \
+        if (!(X)) {                                                   \
+            FAISS_THROW_FMT("Error: '" #X "' failed: " FMT, __VA_ARGS__); \
+        }                                                             \
+    } while (0)
+
 #define HIP_CHECK(expr)                                                            \
     do {                                                                           \
         hipError_t __e = (expr);                                                   \

@@ -13,6 +13,7 @@
 namespace faiss_amd {
 
 IndexIVFStats indexIVF_stats;
+HNSWStats hnsw_stats;
 
 // ---------------------------------------------------------------- devices
 namespace {
@@ -112,6 +113,7 @@ void Index::search(idx_t n, const float* x, idx_t k, float* distances, idx_t* la
     HIP_CHECK(hipMemcpyAsync(distances, bd.ptr, sizeof(float) * n * k, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    fold_device_stats();
 }
 
 // ---------------------------------------------------------------- IndexFlat

@@ -388,9 +388,73 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
     const int64_t vwords = (int64_t)cdiv(std::max<idx_t>(ntotal, 1), 32);
     if (vwords * 4 > 64 * 1024) s_visited_.reserve(sizeof(uint32_t) * vwords * n);
     constexpr bool i32 = sizeof(OutIdx) == 4;
+    if (!d_stats_.ptr) {
+        d_stats_.reserve(4 * sizeof(unsigned long long));
+        HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, 4 * sizeof(unsigned long long), s));
+    }
     ScopedKernelTimer tm(&ktimes, "hnsw_search", 0.0, s);
     kern::hnsw_search(gd, x, ldx, n, k, efSearch, distances, i32 ? nullptr : (int64_t*)labels,
-                      i32 ? (int32_t*)labels : nullptr, s_visited_.as<uint32_t>(), vwords, s);
+                      i32 ? (int32_t*)labels : nullptr, s_visited_.as<uint32_t>(), vwords,
+                      d_stats_.as<unsigned long long>(), s);
+}
+
+// HNSWStats counted by the kernel -> the host global (faiss::hnsw_stats)
+void IndexHNSW::fold_device_stats() const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    if (!d_stats_.ptr) return;
+    DevGuard2 dg(device);
+    hipStream_t s = stream();
+    unsigned long long st[4];
+    HIP_CHECK(hipMemcpyAsync(st, d_stats_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, sizeof(st), s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    HNSWStats add;
+    add.n1 = st[0];
+    add.n2 = st[1];
+    add.ndis = st[2];
+    add.nhops = st[3];
+    hnsw_stats.combine(add);
+}
+
+void IndexHNSW::search_stats(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                             const SearchParameters* params,
+                             QueryLatencyStats* per_query_stats) const {
+    // faiss/IndexHNSW.cpp:345-366 + hnsw_search (:246-343)
+    FAISS_THROW_IF_NOT(k > 0);
+    if (per_query_stats) memset(per_query_stats, 0, sizeof(QueryLatencyStats) * n);
+    if (n == 0) return;
+    DevGuard2 dg(device);
+    sync_device();
+    hipStream_t s = stream();
+    const int ldx = ld();
+    DeviceBuffer bx, bd, bi;
+    bx.reserve(sizeof(float) * n * ldx);
+    bd.reserve(sizeof(float) * n * k);
+    bi.reserve(sizeof(idx_t) * n * k);
+    if (ldx != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * n * ldx, s));
+    HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ldx, x, sizeof(float) * d,
+                               sizeof(float) * d, n, hipMemcpyHostToDevice, s));
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    HIP_CHECK(hipEventRecord(e0, s));
+    hnsw_device<idx_t>(n, bx.as<float>(), ldx, (int)k, bd.as<float>(), bi.as<idx_t>(), params, s);
+    HIP_CHECK(hipEventRecord(e1, s));
+    HIP_CHECK(hipMemcpyAsync(distances, bd.ptr, sizeof(float) * n * k, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    fold_device_stats();
+    if (per_query_stats) {
+        // no quantization phase; the batch's traversal time is each query's
+        for (idx_t i = 0; i < n; i++) {
+            per_query_stats[i].total_us = ms * 1e3;
+            per_query_stats[i].list_scan_us = ms * 1e3;
+        }
+    }
 }
 
 void IndexHNSW::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,

@@ -28,11 +28,6 @@ struct DevGuard {
         if (cur != prev) hipSetDevice(prev);
     }
 };
-double now_ms() {
-    return std::chrono::duration<double, std::milli>(
-                   std::chrono::steady_clock::now().time_since_epoch())
-            .count();
-}
 }  // namespace
 
 // ---------------------------------------------------------------- invlists
@@ -188,6 +183,13 @@ void IndexIVF::quantize_device(idx_t n, const float* x, int ldx, int np, float* 
     quantizer->assign_device(n, x, ldx, np, coarse_dis, assign, qparams, s);
 }
 
+// queries per chunk: bounds the partial-result scratch to ~1 GiB
+idx_t IndexIVF::search_chunk(idx_t n, size_t np, idx_t k) const {
+    const size_t per_q = np * (size_t)std::max<idx_t>(k, 32) * 12 + np * 16;
+    idx_t qchunk = std::max<idx_t>(1, (idx_t)(((size_t)1 << 30) / per_q));
+    return std::max<idx_t>(1, std::min<idx_t>(qchunk, n));
+}
+
 void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
                              idx_t* labels, const SearchParameters* params_in,
                              hipStream_t s) const {
@@ -205,11 +207,9 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
     DevGuard dg(device);
     sync_device();
-    const double t0 = now_ms();
-    // bound the partial-result scratch to ~1 GiB per chunk
-    const size_t per_q = np * (size_t)std::max<idx_t>(k, 32) * 12 + np * 16;
-    idx_t qchunk = std::max<idx_t>(1, (idx_t)(((size_t)1 << 30) / per_q));
-    qchunk = std::min<idx_t>(qchunk, n);
+    // device API: asynchronous, so indexIVF_stats is maintained by the host
+    // entry points (search / search_stats / search_preassigned) only
+    const idx_t qchunk = search_chunk(n, np, k);
     std::lock_guard<std::recursive_mutex> g(mu_);
     s_cd_.reserve(sizeof(float) * qchunk * np);
     s_ci_.reserve(sizeof(int32_t) * qchunk * np);
@@ -220,23 +220,59 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
         search_preassigned_device(nq, x + q0 * ldx, ldx, k, (int)np, s_ci_.as<int32_t>(),
                                   s_cd_.as<float>(), distances + q0 * k, labels + q0 * k, s);
     }
-    indexIVF_stats.nq += n;
-    indexIVF_stats.search_time += now_ms() - t0;
 }
 
 void IndexIVF::search_preassigned(idx_t n, const float* x, idx_t k, const idx_t* assign,
                                   const float* centroid_dis, float* distances, idx_t* labels,
-                                  bool store_pairs, const SearchParametersIVF* params) const {
-    // faiss/IndexIVF.cpp:399-723 (parallel_mode 0 semantics)
+                                  bool store_pairs, const SearchParametersIVF* params,
+                                  IndexIVFStats* stats) const {
+    search_preassigned_stats(n, x, k, assign, centroid_dis, distances, labels, store_pairs,
+                             params, stats, nullptr);
+}
+
+namespace {
+// HIP events bracketing the stages of one host call (resolved after the
+// final synchronisation, so timing adds no host-device round trip)
+struct StageEvents {
+    std::vector<hipEvent_t> ev;
+    hipEvent_t mark(hipStream_t s) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e));
+        HIP_CHECK(hipEventRecord(e, s));
+        ev.push_back(e);
+        return e;
+    }
+    static double ms(hipEvent_t a, hipEvent_t b) {
+        float t = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&t, a, b));
+        return t;
+    }
+    ~StageEvents() {
+        for (auto e : ev) (void)hipEventDestroy(e);
+    }
+};
+}  // namespace
+
+void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const idx_t* assign,
+                                        const float* centroid_dis, float* distances,
+                                        idx_t* labels, bool store_pairs,
+                                        const SearchParametersIVF* params,
+                                        IndexIVFStats* ivf_stats,
+                                        QueryLatencyStats* per_query_stats) const {
+    // faiss/IndexIVF.cpp:399-723 / 870-1200 (parallel_mode 0 semantics)
     FAISS_THROW_IF_NOT(k > 0);
     FAISS_THROW_IF_NOT_MSG(!store_pairs, "store_pairs is not supported on the GPU path");
+    FAISS_THROW_IF_NOT_MSG(parallel_mode == 0, "only parallel_mode 0 runs on the GPU path");
     const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
+    FAISS_THROW_IF_NOT_MSG((params ? params->max_codes : max_codes) == 0,
+                           "max_codes is not supported on the GPU path");
     if (n == 0) return;
     std::vector<int32_t> a32((size_t)n * np);
     for (size_t i = 0; i < (size_t)n * np; i++) {
         idx_t key = assign[i];
-        FAISS_THROW_IF_NOT_MSG(key < (idx_t)nlist, "Invalid key");
+        FAISS_THROW_IF_NOT_FMT(key < (idx_t)nlist, "Invalid key=%lld nlist=%zd",
+                               (long long)key, nlist);
         a32[i] = (int32_t)(key < 0 ? -1 : key);
     }
     DevGuard dg(device);
@@ -256,11 +292,121 @@ void IndexIVF::search_preassigned(idx_t n, const float* x, idx_t k, const idx_t*
                              hipMemcpyHostToDevice, s));
     HIP_CHECK(hipMemcpyAsync(bc.ptr, centroid_dis, sizeof(float) * n * np,
                              hipMemcpyHostToDevice, s));
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    s_stats_.reserve(2 * sizeof(unsigned long long));
+    HIP_CHECK(hipMemsetAsync(s_stats_.ptr, 0, 2 * sizeof(unsigned long long), s));
+    StageEvents ev;
+    hipEvent_t e0 = ev.mark(s);
     search_preassigned_device(n, bx.as<float>(), ldx, k, (int)np, ba.as<int32_t>(),
                               bc.as<float>(), bd.as<float>(), bi.as<idx_t>(), s);
+    hipEvent_t e1 = ev.mark(s);
+    kern::ivf_visit_stats(ba.as<int32_t>(), n * (int64_t)np, d_list_len_.as<uint32_t>(),
+                          (int)nlist, s_stats_.as<unsigned long long>(), s);
+    unsigned long long st[2];
     HIP_CHECK(hipMemcpyAsync(distances, bd.ptr, sizeof(float) * n * k, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(st, s_stats_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    IndexIVFStats* out = ivf_stats ? ivf_stats : &indexIVF_stats;
+    out->nq += n;
+    out->nlist += st[0];
+    out->ndis += st[1];
+    if (per_query_stats) {
+        const double scan_us = StageEvents::ms(e0, e1) * 1e3;
+        for (idx_t i = 0; i < n; i++) per_query_stats[i].list_scan_us = scan_us;
+    }
+}
+
+void IndexIVF::search(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                      const SearchParameters* params) const {
+    search_host(n, x, k, distances, labels, params, nullptr, true);
+}
+
+void IndexIVF::search_stats(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                            const SearchParameters* params,
+                            QueryLatencyStats* per_query_stats) const {
+    search_host(n, x, k, distances, labels, params, per_query_stats, false);
+}
+
+// faiss/IndexIVF.cpp:303-397 and :725-867 on one slice (the whole batch):
+// coarse stage, scan stage, stats.  update_times: search() adds the stage
+// times to indexIVF_stats (search_stats() does not, like the reference).
+void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                           const SearchParameters* params_in,
+                           QueryLatencyStats* per_query_stats, bool update_times) const {
+    FAISS_THROW_IF_NOT(k > 0);
+    if (per_query_stats) memset(per_query_stats, 0, sizeof(QueryLatencyStats) * n);
+    const SearchParametersIVF* params = nullptr;
+    if (params_in) {
+        params = dynamic_cast<const SearchParametersIVF*>(params_in);
+        FAISS_THROW_IF_NOT_MSG(params, "IndexIVF params have incorrect type");
+    }
+    const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
+    FAISS_THROW_IF_NOT(np > 0);
+    FAISS_THROW_IF_NOT_MSG(parallel_mode == 0, "only parallel_mode 0 runs on the GPU path");
+    FAISS_THROW_IF_NOT_MSG((params ? params->max_codes : max_codes) == 0,
+                           "max_codes is not supported on the GPU path");
+    FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
+    if (n == 0) return;
+    DevGuard dg(device);
+    sync_device();
+    hipStream_t s = stream();
+    const int ldx = ld();
+    DeviceBuffer bx, bd, bi;
+    bx.reserve(sizeof(float) * n * ldx);
+    bd.reserve(sizeof(float) * n * k);
+    bi.reserve(sizeof(idx_t) * n * k);
+    if (ldx != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * n * ldx, s));
+    HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ldx, x, sizeof(float) * d,
+                               sizeof(float) * d, n, hipMemcpyHostToDevice, s));
+    const idx_t qchunk = search_chunk(n, np, k);
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    s_cd_.reserve(sizeof(float) * qchunk * np);
+    s_ci_.reserve(sizeof(int32_t) * qchunk * np);
+    s_stats_.reserve(2 * sizeof(unsigned long long));
+    HIP_CHECK(hipMemsetAsync(s_stats_.ptr, 0, 2 * sizeof(unsigned long long), s));
+    StageEvents ev;
+    std::vector<hipEvent_t> marks;
+    for (idx_t q0 = 0; q0 < n; q0 += qchunk) {
+        const idx_t nq = std::min(qchunk, n - q0);
+        marks.push_back(ev.mark(s));
+        quantize_device(nq, bx.as<float>() + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
+                        s_ci_.as<int32_t>(), params ? params->quantizer_params : nullptr, s);
+        marks.push_back(ev.mark(s));
+        search_preassigned_device(nq, bx.as<float>() + q0 * ldx, ldx, k, (int)np,
+                                  s_ci_.as<int32_t>(), s_cd_.as<float>(),
+                                  bd.as<float>() + q0 * k, bi.as<idx_t>() + q0 * k, s);
+        marks.push_back(ev.mark(s));
+        kern::ivf_visit_stats(s_ci_.as<int32_t>(), nq * (int64_t)np,
+                              d_list_len_.as<uint32_t>(), (int)nlist,
+                              s_stats_.as<unsigned long long>(), s);
+    }
+    unsigned long long st[2];
+    HIP_CHECK(hipMemcpyAsync(distances, bd.ptr, sizeof(float) * n * k, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(st, s_stats_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    quantizer->fold_device_stats();
+    double qms = 0, sms = 0;
+    for (size_t c = 0; c + 2 < marks.size(); c += 3) {
+        qms += StageEvents::ms(marks[c], marks[c + 1]);
+        sms += StageEvents::ms(marks[c + 1], marks[c + 2]);
+    }
+    indexIVF_stats.nq += n;
+    indexIVF_stats.nlist += st[0];
+    indexIVF_stats.ndis += st[1];
+    if (update_times) {
+        indexIVF_stats.quantization_time += qms;
+        indexIVF_stats.search_time += qms + sms;
+    }
+    if (per_query_stats) {
+        const double qus = qms * 1e3 / n, sus = sms * 1e3;
+        for (idx_t i = 0; i < n; i++) {
+            per_query_stats[i].quantization_us = qus;
+            per_query_stats[i].list_scan_us = sus;
+            per_query_stats[i].total_us = qus + sus;
+        }
+    }
 }
 
 // ---------------------------------------------------------------- IVFFlat

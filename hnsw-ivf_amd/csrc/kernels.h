@@ -83,6 +83,10 @@ struct IVFBuckets {
 };
 void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
                 int nlist, int QT, IVFBuckets b, hipStream_t s);
+// IndexIVFStats counters of a batch (faiss/IndexIVF.cpp:1184-1198):
+// stats[0] += non-empty lists visited, stats[1] += codes scanned (device)
+void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_len, int nlist,
+                     unsigned long long* stats, hipStream_t s);
 // upper bound on the number of work items (grid size without a host sync)
 inline int64_t ivf_max_items(int64_t n, int nprobe, int nlist, int QT) {
     return (n * nprobe + QT - 1) / QT + nlist;
@@ -178,7 +182,7 @@ struct HNSWDevice {
 // :605-741 (search_from_candidates), :1096-1342 (MinimaxHeap)
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
-                 int64_t visited_words_per_query, hipStream_t s);
+                 int64_t visited_words_per_query, unsigned long long* stats, hipStream_t s);
 
 }  // namespace kern
 }  // namespace faiss_amd

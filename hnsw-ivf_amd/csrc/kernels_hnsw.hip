@@ -69,7 +69,8 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
                                                     int64_t* __restrict__ I,
                                                     int32_t* __restrict__ I32,
                                                     uint32_t* __restrict__ vis_global,
-                                                    int64_t vwords) {
+                                                    int64_t vwords,
+                                                    unsigned long long* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* qs = sm;  // [ld]
     uint32_t* vis = LDS_VISITED ? (uint32_t*)(sm + g.ld) : vis_global + blockIdx.x * vwords;
@@ -82,6 +83,8 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
 
     float res_d = WS_INF;
     long long res_i = WS_NOID;
+    // HNSWStats (faiss/impl/HNSW.h:234-246): n1, n2, ndis, nhops of this query
+    uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0;
     if (g.entry_point >= 0) {
         // ---- greedy descent on the upper levels
         int nearest = g.entry_point;
@@ -96,6 +99,10 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
                 const int first_neg = neg ? __ffsll((long long)neg) - 1 : 64;
                 float dis = WS_INF;
                 if (lane < first_neg) dis = l2_row(qs, g.storage + (int64_t)v * g.ld, g.d);
+                // greedy_update_nearest (HNSW.cpp:883-918): every valid
+                // neighbour is a distance, every pass a hop
+                st_ndis += (uint32_t)min(first_neg, 64);
+                st_nhops += 1;
                 // min (dis, lane) over the wave
                 float md = dis;
                 int ml = lane;
@@ -140,7 +147,10 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
             const bool a0 = in0 && c0i != WS_NOID && (c0i & 1);
             const bool a1 = in1 && c1i != WS_NOID && (c1i & 1);
             unsigned long long m0 = __ballot(a0), m1 = __ballot(a1);
-            if (!m0 && !m1) break;  // candidates.size() == 0
+            if (!m0 && !m1) {  // candidates.size() == 0
+                st_n2 = 1;
+                break;
+            }
             // pop_min: smallest alive slot
             int pos;
             if (m0) pos = __ffsll((long long)m0) - 1;
@@ -157,7 +167,13 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
             const bool f0 = in0 && c0i != WS_NOID && c0d < d0v;
             const bool f1 = in1 && c1i != WS_NOID && c1d < d0v;
             const int n_below = __popcll(__ballot(f0)) + __popcll(__ballot(f1));
-            if (n_below >= efSearch) break;
+            if (n_below >= efSearch) {
+                // HNSW.cpp:732-735: n2 counts an exhausted candidate heap
+                const bool b0 = in0 && c0i != WS_NOID && (c0i & 1);
+                const bool b1 = in1 && c1i != WS_NOID && (c1i & 1);
+                st_n2 = (__ballot(b0) | __ballot(b1)) == 0ull ? 1u : 0u;
+                break;
+            }
             // neighbours of v0 at level 0
             const uint64_t o = g.offsets[v0];
             const int b = g.cum_nb[0], e = g.cum_nb[1];
@@ -173,7 +189,10 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
             }
             float dis = WS_INF;
             if (fresh) dis = l2_row(qs, g.storage + (int64_t)v * g.ld, g.d);
-            if (__ballot(fresh) == 0ull) continue;
+            const unsigned long long fm = __ballot(fresh);
+            st_ndis += (uint32_t)__popcll(fm);
+            st_nhops += 1;  // nstep
+            if (fm == 0ull) continue;
             // result heap: k smallest (dis, id) of the union, strict admission
             {
                 float cd = (fresh && dis < FLT_MAX) ? dis : WS_INF;
@@ -189,6 +208,12 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
             }
         }
     }
+    if (stats && lane == 0 && g.entry_point >= 0) {
+        atomicAdd(&stats[0], 1ull);
+        atomicAdd(&stats[1], (unsigned long long)st_n2);
+        atomicAdd(&stats[2], (unsigned long long)st_ndis);
+        atomicAdd(&stats[3], (unsigned long long)st_nhops);
+    }
     if (lane < k) {
         float dis;
         long long id;
@@ -201,7 +226,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
 
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
-                 int64_t visited_words_per_query, hipStream_t s) {
+                 int64_t visited_words_per_query, unsigned long long* stats, hipStream_t s) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
     const int ef = efSearch > k ? efSearch : k;
@@ -213,12 +238,12 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
     if (lds_vis) {
         size_t lds = lds_q + sizeof(uint32_t) * vwords;
         k_hnsw_search<true><<<dim3((unsigned)n), dim3(64), lds, s>>>(
-                g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords);
+                g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats);
     } else {
         FAISS_THROW_IF_NOT(visited_scratch != nullptr);
         HIP_CHECK(hipMemsetAsync(visited_scratch, 0, sizeof(uint32_t) * vwords * n, s));
         k_hnsw_search<false><<<dim3((unsigned)n), dim3(64), lds_q, s>>>(
-                g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords);
+                g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats);
     }
     HIP_LAUNCH_CHECK();
 }

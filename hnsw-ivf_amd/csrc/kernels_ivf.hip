@@ -89,6 +89,33 @@ __global__ void k_bucket_fill(const int32_t* __restrict__ assign, int64_t total,
     if (l >= 0 && l < nlist && list_len[l] > 0) entries[bucket_off[l] + pos[e]] = (uint32_t)e;
 }
 
+__global__ void k_ivf_visit_stats(const int32_t* __restrict__ assign, int64_t total,
+                                  const uint32_t* __restrict__ list_len, int nlist,
+                                  unsigned long long* __restrict__ stats) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t len = 0;
+    if (e < total) {
+        const int l = assign[e];
+        if (l >= 0 && l < nlist) len = list_len[l];
+    }
+    const unsigned long long nv = __popcll(__ballot(len > 0));
+    unsigned long long nd = len;
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) nd += __shfl_xor(nd, m);
+    if ((threadIdx.x & 63) == 0 && nv) {
+        atomicAdd(&stats[0], nv);
+        atomicAdd(&stats[1], nd);
+    }
+}
+
+void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_len, int nlist,
+                     unsigned long long* stats, hipStream_t s) {
+    if (total <= 0) return;
+    k_ivf_visit_stats<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(assign, total,
+                                                                            list_len, nlist, stats);
+    HIP_LAUNCH_CHECK();
+}
+
 void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
                 int nlist, int QT, IVFBuckets b, hipStream_t s) {
     int64_t total = n * nprobe;

@@ -36,13 +36,51 @@ struct SearchParametersIVF : SearchParameters {  // faiss/IndexIVF.h:77-85
     SearchParameters* quantizer_params = nullptr;
 };
 
-// faiss/IndexIVF.h:567-583
+// faiss/IndexIVF.h:567-583.  On the GPU path nheap_updates stays 0 (there is
+// no sequential heap); nq / nlist / ndis count exactly what the reference
+// counts (non-empty lists visited, codes scanned).
 struct IndexIVFStats {
     size_t nq = 0, nlist = 0, ndis = 0, nheap_updates = 0;
     double quantization_time = 0, search_time = 0;
     void reset() { *this = IndexIVFStats(); }
+    void add(const IndexIVFStats& o) {
+        nq += o.nq;
+        nlist += o.nlist;
+        ndis += o.ndis;
+        nheap_updates += o.nheap_updates;
+        quantization_time += o.quantization_time;
+        search_time += o.search_time;
+    }
 };
 extern IndexIVFStats indexIVF_stats;
+
+// faiss/IndexIVF.h:28-32 — this fork's per-query latency record filled by
+// IndexIVF::search_stats / IndexHNSW::search_stats (microseconds).
+// GPU semantics: a batch is one slice, so quantization_us is
+// the coarse stage's wall time / n (the reference's amortisation) and
+// list_scan_us the wall time of the batched scan stage that produced the
+// query's result; total_us = quantization_us + list_scan_us.
+struct QueryLatencyStats {
+    double total_us = 0.0;
+    double quantization_us = 0.0;
+    double list_scan_us = 0.0;
+};
+
+// faiss/impl/HNSW.h:234-253 (global faiss::hnsw_stats).  Counted on the
+// device by the search kernel; folded into the host struct at the end of
+// every synchronous host call (device-API searches fold at the next one, or
+// at fold_device_stats()).
+struct HNSWStats {
+    size_t n1 = 0, n2 = 0, ndis = 0, nhops = 0;
+    void reset() { n1 = n2 = ndis = nhops = 0; }
+    void combine(const HNSWStats& o) {
+        n1 += o.n1;
+        n2 += o.n2;
+        ndis += o.ndis;
+        nhops += o.nhops;
+    }
+};
+extern HNSWStats hnsw_stats;
 
 // ---------------------------------------------------------------- Index
 struct Index {
@@ -76,6 +114,8 @@ struct Index {
     virtual void reset() = 0;
     virtual void reconstruct(idx_t key, float* recons) const;
     virtual void sync_device() const {}
+    // fold device-side search counters (HNSWStats) into the host globals
+    virtual void fold_device_stats() const {}
 
     hipStream_t stream() const;
     int ld() const { return (int)roundup((size_t)d, 4); }
@@ -156,12 +196,18 @@ struct IndexHNSW : Index {
     void reset() override;
     void reconstruct(idx_t key, float* recons) const override;
     void sync_device() const override;
+    void fold_device_stats() const override;
+    // faiss/IndexHNSW.cpp:345-366: search with per-query latency statistics
+    // (quantization_us = 0, list_scan_us = total_us, like the reference)
+    void search_stats(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                      const SearchParameters* params = nullptr,
+                      QueryLatencyStats* per_query_stats = nullptr) const;
 
    private:
     template <class OutIdx>
     void hnsw_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
                      const SearchParameters* params, hipStream_t stream) const;
-    mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, s_visited_;
+    mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, s_visited_, d_stats_;
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
 };
@@ -191,6 +237,7 @@ struct IndexIVF : Index {
     size_t code_size = 0;
     bool by_residual = true;
     int niter = 25;  // k-means iterations (faiss ClusteringParameters::niter)
+    int parallel_mode = 0;  // faiss/IndexIVF.h:58-62; the GPU path runs mode 0 only
     std::unique_ptr<ArrayInvertedLists> invlists;
 
     IndexIVF(Index* quantizer, size_t d, size_t nlist, size_t code_size, MetricType metric);
@@ -202,10 +249,25 @@ struct IndexIVF : Index {
     void search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
                        idx_t* labels, const SearchParameters* params,
                        hipStream_t stream) const override;
+    // faiss/IndexIVF.cpp:303-397 (host pointers, synchronous): also updates
+    // indexIVF_stats (nq, nlist, ndis, quantization_time, search_time)
+    void search(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                const SearchParameters* params = nullptr) const override;
+    // faiss/IndexIVF.cpp:725-867: search with per-query latency statistics
+    void search_stats(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                      const SearchParameters* params = nullptr,
+                      QueryLatencyStats* per_query_stats = nullptr) const;
     // faiss/IndexIVF.h:120-130; assign = [n][nprobe] host list numbers
     void search_preassigned(idx_t n, const float* x, idx_t k, const idx_t* assign,
                             const float* centroid_dis, float* distances, idx_t* labels,
-                            bool store_pairs, const SearchParametersIVF* params = nullptr) const;
+                            bool store_pairs, const SearchParametersIVF* params = nullptr,
+                            IndexIVFStats* stats = nullptr) const;
+    // faiss/IndexIVF.cpp:870-1200 (per-query list_scan_us)
+    void search_preassigned_stats(idx_t n, const float* x, idx_t k, const idx_t* assign,
+                                  const float* centroid_dis, float* distances, idx_t* labels,
+                                  bool store_pairs, const SearchParametersIVF* params,
+                                  IndexIVFStats* ivf_stats,
+                                  QueryLatencyStats* per_query_stats) const;
     // device form (int32 assignments)
     virtual void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k,
                                            int nprobe, const int32_t* assign,
@@ -234,7 +296,13 @@ struct IndexIVF : Index {
     // scratch
     mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_counts_, s_boff_, s_ioff_, s_cur_, s_ent_,
             s_pk1_, s_pk2_, s_q_;
-    mutable DeviceBuffer s_as_, s_ad_;
+    mutable DeviceBuffer s_as_, s_ad_, s_stats_;
+
+   private:
+    idx_t search_chunk(idx_t n, size_t np, idx_t k) const;
+    void search_host(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                     const SearchParameters* params, QueryLatencyStats* per_query_stats,
+                     bool update_times) const;
 };
 
 struct IndexIVFFlat : IndexIVF {

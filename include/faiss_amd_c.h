@@ -177,6 +177,45 @@ typedef struct FaissIndexIVFStats {
 void faiss_IndexIVFStats_reset(FaissIndexIVFStats* stats);
 FaissIndexIVFStats* faiss_get_indexIVF_stats(void);
 
+/* reference faiss/IndexIVF.h:28-32 — this fork's per-query latency record
+ * (microseconds).  GPU semantics: quantization_us = coarse-stage wall time / n
+ * (the reference's amortisation over a slice; the batch is one slice),
+ * list_scan_us = wall time of the batched scan stage, total = their sum. */
+typedef struct FaissQueryLatencyStats {
+    double total_us;
+    double quantization_us;
+    double list_scan_us;
+} FaissQueryLatencyStats;
+/* extension, replaces IndexIVF::search_stats (faiss/IndexIVF.h:329-337,
+ * faiss/IndexIVF.cpp:725-867; the reference C API has no binding for it).
+ * params may be NULL or a FaissSearchParametersIVF; per_query_stats may be
+ * NULL or [n].  Updates indexIVF_stats nq / nlist / ndis. */
+int faiss_amd_IndexIVF_search_stats(
+        const FaissIndexIVF* index,
+        idx_t n,
+        const float* x,
+        idx_t k,
+        const FaissSearchParameters* params,
+        float* distances,
+        idx_t* labels,
+        FaissQueryLatencyStats* per_query_stats);
+/* extension, replaces IndexIVF::search_preassigned_stats
+ * (faiss/IndexIVF.h:306-317): sets list_scan_us of each query; ivf_stats NULL
+ * = the global indexIVF_stats */
+int faiss_amd_IndexIVF_search_preassigned_stats(
+        const FaissIndexIVF* index,
+        idx_t n,
+        const float* x,
+        idx_t k,
+        const idx_t* assign,
+        const float* centroid_dis,
+        float* distances,
+        idx_t* labels,
+        int store_pairs,
+        const FaissSearchParameters* params,
+        FaissIndexIVFStats* ivf_stats,
+        FaissQueryLatencyStats* per_query_stats);
+
 /* ---------------- IndexIVFFlat (c_api/IndexIVFFlat_c.h) ---------------- */
 /* IndexIVFFlat_c.h:47-51 */
 int faiss_IndexIVFFlat_new_with(
@@ -227,6 +266,30 @@ int faiss_amd_IndexHNSW_efConstruction(const FaissIndexHNSW*);
 void faiss_amd_IndexHNSW_set_efConstruction(FaissIndexHNSW*, int);
 /* the flat storage index of an IndexHNSW (owned by it) */
 FaissIndex* faiss_amd_IndexHNSW_storage(const FaissIndexHNSW* index);
+/* extension, replaces IndexHNSW::search_stats (faiss/IndexHNSW.h:68-76,
+ * faiss/IndexHNSW.cpp:345-366): total_us = list_scan_us = the batch's
+ * traversal time, quantization_us = 0 */
+int faiss_amd_IndexHNSW_search_stats(
+        const FaissIndexHNSW* index,
+        idx_t n,
+        const float* x,
+        idx_t k,
+        const FaissSearchParameters* params,
+        float* distances,
+        idx_t* labels,
+        FaissQueryLatencyStats* per_query_stats);
+/* faiss/impl/HNSW.h:234-253 — the global hnsw_stats (faiss.cvar.hnsw_stats
+ * in the reference's Python tests).  Device-API searches are folded in at the
+ * next synchronous call or by faiss_amd_fold_device_stats(index). */
+typedef struct FaissHNSWStats {
+    size_t n1;
+    size_t n2;
+    size_t ndis;
+    size_t nhops;
+} FaissHNSWStats;
+FaissHNSWStats* faiss_amd_get_hnsw_stats(void);
+void faiss_amd_HNSWStats_reset(void);
+int faiss_amd_fold_device_stats(const FaissIndex* index);
 /* graph export for tests: levels[ntotal], offsets[ntotal+1], neighbors[],
  * cum_nneighbor_per_level[]; pass NULL to query sizes only */
 int faiss_amd_IndexHNSW_graph(

@@ -40,7 +40,7 @@ L.ref_hnsw_sizes.argtypes = [P, P]
 L.ref_hnsw_copy.argtypes = [P, P, P, P, P, P, C.c_int64]
 L.ref_hnsw_free.argtypes = [P]
 L.ref_hnsw_search.argtypes = [P, SZ, SZ, P, P, SZ, P, SZ, P, SZ, C.c_int32, C.c_int32, C.c_int,
-                              P, SZ, SZ, P, P]
+                              P, SZ, SZ, P, P, P]
 
 
 def p(a):
@@ -197,10 +197,12 @@ def main():
         for k in (1, 10):
             D = np.empty((40, k), np.float32)
             I = np.empty((40, k), np.int64)
+            st = np.zeros(4, np.uint64)
             L.ref_hnsw_search(p(xh), nb, d, p(levels), p(offsets), len(offsets), p(neighbors),
                               len(neighbors), p(cum), len(cum), int(sz[4]), int(sz[5]), ef,
-                              p(xq), 40, k, p(D), p(I))
+                              p(xq), 40, k, p(D), p(I), p(st))
             fx[f"hnsw_{ef}_{k}_D"], fx[f"hnsw_{ef}_{k}_I"] = D, I
+            fx[f"hnsw_{ef}_{k}_stats"] = st  # HNSWStats n1, n2, ndis, nhops
     del nprob
 
     os.makedirs(os.path.dirname(OUT), exist_ok=True)

@@ -147,7 +147,8 @@ void ref_hnsw_search(const float* xb, size_t nb, size_t d, const int32_t* levels
                      const uint64_t* offsets, size_t n_offsets, const int32_t* neighbors,
                      size_t n_neighbors, const int32_t* cum_nneighbor_per_level,
                      size_t n_cum, int32_t entry_point, int32_t max_level, int ef_search,
-                     const float* xq, size_t nq, size_t k, float* D, int64_t* I) {
+                     const float* xq, size_t nq, size_t k, float* D, int64_t* I,
+                     uint64_t* stats /* n1, n2, ndis, nhops summed (HNSWStats), or NULL */) {
     faiss::HNSW h;
     h.levels.assign(levels, levels + nb);
     h.offsets.assign(offsets, offsets + n_offsets);
@@ -161,12 +162,19 @@ void ref_hnsw_search(const float* xb, size_t nb, size_t d, const int32_t* levels
     faiss::VisitedTable vt(nb);
     faiss::HeapBlockResultHandler<faiss::HNSW::C> bres(nq, D, I, k);
     faiss::HeapBlockResultHandler<faiss::HNSW::C>::SingleResultHandler res(bres);
+    faiss::HNSWStats tot;
     for (size_t i = 0; i < nq; i++) {
         res.begin(i);
         dis.set_query(xq + i * d);
-        h.search(dis, res, vt, nullptr);
+        tot.combine(h.search(dis, res, vt, nullptr));
         res.end();
         vt.advance();
+    }
+    if (stats) {
+        stats[0] = tot.n1;
+        stats[1] = tot.n2;
+        stats[2] = tot.ndis;
+        stats[3] = tot.nhops;
     }
 }
 
