@@ -42,6 +42,26 @@ CONFIGS = {
 }
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector == fp32 MFMA peak
 PEAK_HBM_GBS = 8000.0
+PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+# dominant kernel per workload (device symbol substring) for the PMC traffic
+DOMINANT = {"flat": "k_ivf_bf3_filter", "pq": "k_ivfpq_scan"}
+
+
+def pmc_traffic(config, kernel_sub):
+    """HBM bytes per launch of the dominant kernel from the newest committed
+    rocprofv3 --pmc summary for this workload (profiles/rNN_<config>_pmc.json,
+    written by scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950
+    correction + WRITE_SIZE, separate passes)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        summ = json.load(f)
+    for name, ent in summ.items():
+        if kernel_sub in name and "hbm_bytes" in ent:
+            return ent["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 def log(*a):
@@ -159,20 +179,40 @@ def main():
     sizes = np.array([index.get_list_size(l) for l in range(index.nlist)], dtype=np.int64)
     cand_per_q = float(sizes[ci_h.cpu().numpy().astype(np.int64)].sum()) / nq
     cands = cand_per_q * nq_launch
-    if "PQ" in cfg["desc"]:
+    is_pq = "PQ" in cfg["desc"]
+    traffic, traffic_src = pmc_traffic(args.config, DOMINANT["pq" if is_pq else "flat"])
+    if is_pq:
         M = index.pq_info()["M"]
         work = cands * M  # code bytes streamed (LUT-gather bound)
         achieved = work / (scan_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": None}
-    else:
-        work = cands * 3.0 * d  # flops: per candidate d x (sub + fma)
-        achieved = work / (scan_ms * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
-                    "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
+                    "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                     "kernel": scan_name, "kernel_ms": scan_ms,
+                    "algorithmic_bytes_per_launch": work}
+    else:
+        # The filter runs on bf16 MFMA: every fp32 operand pair is split
+        # (bf16x2: codes hi x queries hi+lo = 2 products; bf16x3: 3), so its
+        # algorithmic work is nprod x 2d bf16 flops per candidate, priced
+        # against the dense bf16 MFMA peak.  The fp32-equivalent figure
+        # (3d flops per candidate: sub + fma) is reported beside it.
+        nprod = 3 if os.environ.get("FAISS_AMD_IVF_PREC") == "bf16x3" else 2
+        dpad = -(-d // 32) * 32
+        work = cands * nprod * 2.0 * dpad
+        achieved = work / (scan_ms * 1e-3) / 1e12
+        fp32_eq = cands * 3.0 * d / (scan_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
+                    "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
+                    "kernel": scan_name, "kernel_ms": scan_ms, "mfma_dtype": "bf16",
                     "algorithmic_flops_per_launch": work,
+                    "flops_per_candidate": nprod * 2 * dpad,
+                    "fp32_equivalent_tflops": fp32_eq,
                     "streamed_bytes_per_launch": cands * d * 4.0}
+    if traffic is not None:
+        # HBM bytes per launch from rocprofv3 PMC (committed summary), and
+        # the bandwidth they imply at the live kernel time
+        roofline["traffic_source"] = traffic_src
+        roofline["traffic_unit"] = "bytes/launch"
+        roofline["traffic_gbs"] = traffic / (scan_ms * 1e-3) / 1e9
 
     # ---- recall@10 of this rank's queries vs exact search (subset)
     recall = None
@@ -187,21 +227,37 @@ def main():
 
     # ---- CPU baseline: the oracle restatement on the host cores, rank 0, N=1
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and "PQ" not in cfg["desc"] \
-            and "HNSW" not in cfg["desc"]:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         orc = ge.load_oracle()
         ncores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
         ref = orc.IVFOracle.from_index(index)
-        probe = min(500, nq)
+        fast = not is_pq and "HNSW" not in cfg["desc"]
+        ef = cfg.get("efSearch", 16)
+        if fast:
+            what = "IVF-Flat scan with 8-way vectorisable partial sums (oracle search_fast)"
+
+            def cpu_search(xs):
+                return ref.search_fast(xs, k, nprobe, nthreads=ncores)
+        else:
+            what = ("IndexIVF::search restated (oracle search: coarse "
+                    + ("HNSW" if "HNSW" in cfg["desc"] else "flat") + " quantizer, "
+                    + ("IVF-PQ table %d scan" % ref.use_precomputed_table if is_pq
+                       else "IVF-Flat scan") + f", {ncores} query slices)")
+
+            def cpu_search(xs):
+                D_, I_, _, _ = ref.search(xs, k, nprobe, efSearch=ef, nslices=ncores,
+                                          nthreads=ncores)
+                return D_, I_
+        probe = min(200, nq)
         tc = time.perf_counter()
-        ref.search_fast(xq[:probe], k, nprobe, nthreads=ncores)
+        cpu_search(xq[:probe])
         tp = time.perf_counter() - tc
         ns = int(min(nq, max(probe, probe * args.cpu_seconds / max(tp, 1e-3))))
         # repeat passes over the sample until ~cpu_seconds of wall time
         passes, tcpu = 0, 0.0
         while True:
             tc = time.perf_counter()
-            Dc, Ic = ref.search_fast(xq[:ns], k, nprobe, nthreads=ncores)
+            Dc, Ic = cpu_search(xq[:ns])
             tcpu += time.perf_counter() - tc
             passes += 1
             if tcpu >= args.cpu_seconds or passes >= 50:
@@ -210,8 +266,7 @@ def main():
         cpu = {"value": ns * passes / tcpu, "unit": "queries/s", "cores": ncores,
                "kind": "port",
                "sample": f"{passes} pass(es) over {ns} of the {nq} queries, same index, "
-                         f"IVF-Flat scan with 8-way vectorisable partial sums (oracle "
-                         f"search_fast), {tcpu:.1f}s wall on {ncores} threads",
+                         f"{what}, {tcpu:.1f}s wall on {ncores} threads",
                "id_agreement_vs_gpu": agree}
 
     if rank == 0:

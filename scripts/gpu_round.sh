@@ -32,6 +32,6 @@ if [ -n "$PMC" ]; then
     timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-include-regex "$KR" --output-format csv -d gpurun_out/pmc$i -o pmc -- python bench.py $BA > gpurun_out/pmc$i.log 2>&1
     rc=$?; echo "pmc$i rc=$rc"; ok $rc || exit $rc
   done
-  python scripts/pmc_summary.py gpurun_out > gpurun_out/pmc_summary.txt 2>&1; cat gpurun_out/pmc_summary.txt
+  python scripts/pmc_summary.py gpurun_out gpurun_out/pmc_summary.json > gpurun_out/pmc_summary.txt 2>&1; cat gpurun_out/pmc_summary.txt
 fi
 exit 0

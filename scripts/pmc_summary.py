@@ -7,10 +7,12 @@ MI355X_MICROARCH.md "HBM"); sizes are in KB as rocprofv3 reports them.
 import collections
 import csv
 import glob
+import json
 import os
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+json_out = sys.argv[2] if len(sys.argv) > 2 else None  # per-kernel HBM bytes / launch
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "pmc*", "**", "*counter_collection*.csv"),
                           recursive=True)):
@@ -19,6 +21,7 @@ for f in sorted(glob.glob(os.path.join(root, "pmc*", "**", "*counter_collection*
         per[(r["Kernel_Name"], r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     for (kn, _, cn), v in per.items():
         acc[kn][cn].append(v)
+summary = {}
 for kn, cs in acc.items():
     print(kn[:110])
     vals = {cn: sum(v) / len(v) for cn, v in cs.items()}
@@ -30,8 +33,21 @@ for kn, cs in acc.items():
         if cn == "WRITE_SIZE":
             extra = f"   -> HBM write {v / 1e3:.1f} MB/launch"
         print(f"  {cn:28s} {v:16.1f}  (n={len(cs[cn])}){extra}")
+    ent = {"launches": max(len(v) for v in cs.values())}
+    if "FETCH_SIZE" in vals:
+        ent["hbm_read_bytes"] = 2 * vals["FETCH_SIZE"] * 1e3   # KB, x2 (gfx950)
+    if "WRITE_SIZE" in vals:
+        ent["hbm_write_bytes"] = vals["WRITE_SIZE"] * 1e3
+    if "hbm_read_bytes" in ent and "hbm_write_bytes" in ent:
+        ent["hbm_bytes"] = ent["hbm_read_bytes"] + ent["hbm_write_bytes"]
+    ent["counters"] = vals
+    summary[kn] = ent
     if "SQ_WAVE_CYCLES" in vals and vals["SQ_WAVE_CYCLES"] > 0:
         wc = vals["SQ_WAVE_CYCLES"]
         for cn in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
             if cn in vals:
                 print(f"  {cn + ' / WAVE_CYCLES':40s} {vals[cn] / wc:.3f}")
+
+if json_out:
+    with open(json_out, "w") as f:
+        json.dump(summary, f, indent=1)
