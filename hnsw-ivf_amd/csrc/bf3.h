@@ -79,21 +79,30 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& l
 
 // The B operand (32 query columns per wave) for one work item: lane holds
 // query column `li` dims [16 s + 8 lh, +8) split into hi / lo, and |x|^2
-// (any order; margins only).  qr < 0: zero column.
+// (any order; margins only).  Rows are read as float4 (a row is readable up
+// to roundup(d, 4) <= ldx); dims >= d are zeroed.  qr < 0 (an unused column,
+// whose results are discarded) reads row 0.
 template <int NS>
 __device__ __forceinline__ void load_query_frags(const float* __restrict__ x, int ldx, int d,
                                                  int qr, int lh, bf16x8 (&bh)[NS],
                                                  bf16x8 (&bl)[NS], float& xn) {
     const float* xr = x + (int64_t)(qr < 0 ? 0 : qr) * ldx;
+    const int d4 = (d + 3) & ~3;
+    float4 raw[2 * NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int kk = 16 * s + 8 * lh + 4 * u;
+            raw[2 * s + u] = kk < d4 ? *(const float4*)(xr + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     xn = 0.f;
 #pragma unroll
     for (int s = 0; s < NS; s++) {
-        float v[8];
+        float v[8] = {raw[2 * s].x,     raw[2 * s].y,     raw[2 * s].z,     raw[2 * s].w,
+                      raw[2 * s + 1].x, raw[2 * s + 1].y, raw[2 * s + 1].z, raw[2 * s + 1].w};
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int kk = 16 * s + 8 * lh + j;
-            v[j] = (qr >= 0 && kk < d) ? xr[kk] : 0.f;
-        }
+        for (int j = 0; j < 8; j++) v[j] = 16 * s + 8 * lh + j < d ? v[j] : 0.f;
         split8(v, bh[s], bl[s]);
 #pragma unroll
         for (int j = 0; j < 8; j++) xn = fmaf(v[j], v[j], xn);

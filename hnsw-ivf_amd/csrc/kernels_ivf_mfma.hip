@@ -86,6 +86,14 @@ __global__ void k_split_bf16(const float* __restrict__ codes, int64_t rows, int 
 // (codes rounded to bf16, queries split: two MFMAs per k-step, half the code
 // bytes streamed; wider margin, ivf_bf2_coef).  Both read the same hi|lo
 // image; !Y3 touches only the hi half of every row.
+//
+// Pipeline (one barrier per 64-row tile): tile t+1 is stashed from registers
+// into the other LDS buffer while tile t is computed, and tile t+2 is fetched
+// into registers; the row norms travel with the tile (LDS), so the compute of
+// a tile never waits on a global load issued in the same iteration.  Rows
+// past the list end get norm +inf (L2) / bias +inf (IP): their keys sort
+// after every real candidate and the epilogue drops them by row index.
+// Waves whose 32 query columns are all unused skip the MFMA and selection.
 template <bool L2, int KT, int NS, bool Y3>
 __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         const float* __restrict__ x, int ldx, int d, const __bf16* __restrict__ cbf,
@@ -98,6 +106,7 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         float* __restrict__ pbound) {
     // two code tiles (double buffer), row stride CSB bytes = (Y3 ? 4 : 2) * DB + 16
     __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * ((Y3 ? 4 : 2) * 16 * NS + 16)];
+    __shared__ __attribute__((aligned(16))) float ynt[2][BV];  // row norm (L2) / bias (IP)
     __shared__ uint32_t ent_s[BQ];
     __shared__ int32_t qrow_s[BQ];
     __shared__ float bnd_s[BQ][4];
@@ -129,15 +138,18 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     const int li = lane & 31, lh = lane >> 5;
     const int slot = 2 * bi + lh;    // this thread's share of its query's codes
     const int qloc = 32 * bj + li;   // this thread's query (0..63)
+    const bool active = 32 * bj < nQ;  // wave-uniform
+    const float* ynl = ynorm + row0;
     __syncthreads();
 
     // ---- query fragments (B operand): registers for the whole work item
     bf16x8 bh[NS], bl[NS];
-    float xn;
-    load_query_frags<NS>(x, ldx, d, qrow_s[qloc], lh, bh, bl, xn);
+    float xn = 0.f;
+    if (active) load_query_frags<NS>(x, ldx, d, qrow_s[qloc], lh, bh, bl, xn);
 
-    // ---- code tiles: global -> registers -> LDS
+    // ---- code tiles: global -> registers -> LDS (+ the tile's row norms)
     uint4 pf[PF];
+    float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
     auto fetch = [&](int v0n) {
         const int nvn = min(BV, len - v0n);
 #pragma unroll
@@ -148,6 +160,16 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             if (e < BV * RU && r < nvn)
                 pf[s] = *(const uint4*)(cbf + (row0 + v0n + r) * (int64_t)(2 * DB) + 8 * c);
         }
+        if (t < BV / 4) {
+            const int r = 4 * t;
+            // rows < roundup(len, 16) are inside the list's arena slot
+            float4 v = r < nvn ? *(const float4*)(ynl + v0n + r) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!L2) v = make_float4(0.f, 0.f, 0.f, 0.f);
+            pn.x = r + 0 < nvn ? v.x : WS_INF;
+            pn.y = r + 1 < nvn ? v.y : WS_INF;
+            pn.z = r + 2 < nvn ? v.z : WS_INF;
+            pn.w = r + 3 < nvn ? v.w : WS_INF;
+        }
     };
     auto stash = [&](int buf) {
         uint8_t* T = tiles + buf * BV * CSB;
@@ -157,6 +179,7 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             const int r = e / RU, c = e - r * RU;
             if (e < BV * RU) *(uint4*)(T + r * CSB + 16 * c) = pf[s];
         }
+        if (t < BV / 4) *(float4*)(&ynt[buf][4 * t]) = pn;
     };
     fetch(0);
     stash(0);
@@ -166,7 +189,6 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     ThreadQueue32<KT> tq;
     tq.init();
     const uint32_t lowmask = (1u << obits) - 1u;
-    const float* ynl = ynorm + row0;
 
     for (int v0 = 0, tile = 0; v0 < len; v0 += BV, tile++) {
         const int buf = tile & 1;
@@ -176,38 +198,36 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             stash(buf ^ 1);
             if (v0 + 2 * BV < len) fetch(v0 + 2 * BV);
         }
-        // code norms of this lane's 16 rows: rows 32bi + 4lh + 8g + (0..3)
-        float4 yq[4];
+        if (active) {
+            // norms / biases of this lane's 16 rows: 32bi + 4lh + 8g + (0..3)
+            float4 yq[4];
 #pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const int cr = v0 + 32 * bi + 4 * lh + 8 * g;
-            yq[g] = cr < len ? *(const float4*)(ynl + cr) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        const uint8_t* arow = tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh;
-        const floatx16 acc = Y3 ? bf3_block<NS>(arow, bh, bl) : bf2_block<NS>(arow, bh, bl);
-        // approx -> 32-bit keys -> thread queue
-        const uint32_t ordbase = (uint32_t)tile << 4;
-        const bool full = v0 + BV <= len;
+            for (int g = 0; g < 4; g++) yq[g] = *(const float4*)(&ynt[buf][32 * bi + 4 * lh + 8 * g]);
+            const uint8_t* arow = tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh;
+            const floatx16 acc = Y3 ? bf3_block<NS>(arow, bh, bl) : bf2_block<NS>(arow, bh, bl);
+            const uint32_t ordbase = (uint32_t)tile << 4;
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const int g = r >> 2, c = r & 3;
-            const float yv = c == 0 ? yq[g].x : c == 1 ? yq[g].y : c == 2 ? yq[g].z : yq[g].w;
-            const float a = L2 ? fmaf(-2.f, acc[r], xn + yv) : -acc[r];
-            uint32_t key = key_encode<L2>(a, lowmask, ordbase | (uint32_t)r);
-            if (!full) {
-                const int cr = v0 + 32 * bi + 4 * lh + 8 * g + c;
-                key = cr < len ? key : 0xffffffffu;
+            for (int r = 0; r < 16; r++) {
+                const int g = r >> 2, c = r & 3;
+                const float yv = c == 0 ? yq[g].x : c == 1 ? yq[g].y : c == 2 ? yq[g].z : yq[g].w;
+                const float a = L2 ? fmaf(-2.f, acc[r], xn + yv) : yv - acc[r];
+                tq.push(key_encode<L2>(a, lowmask, ordbase | (uint32_t)r));
             }
-            tq.push(key);
         }
         __syncthreads();
     }
 
     // ---- outputs
     const bool qvalid = qloc < nQ;
-    const float bnd = tq.q[KT - 1] != 0xffffffffu
-                              ? key_decode_lo<L2>(tq.q[KT - 1], lowmask)
-                              : WS_INF;
+    const uint32_t last = tq.q[KT - 1];
+    float bnd = WS_INF;  // lower bound of every dropped candidate (none: +inf)
+    if (last != 0xffffffffu) {
+        const uint32_t ord = last & lowmask;
+        const int r = (int)(ord & 15u);
+        const int row = (int)((ord >> 4) * BV) + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
+        // a padding row in the last slot: every real row of this stream is kept
+        if (row < len) bnd = key_decode_lo<L2>(last, lowmask);
+    }
     bnd_s[qloc][slot] = bnd;
     __syncthreads();
     if (qvalid) {
@@ -217,10 +237,10 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
 #pragma unroll
         for (int i = 0; i < KT; i++) {
             const uint32_t key = tq.q[i];
-            if (key != 0xffffffffu) {
-                const uint32_t ord = key & lowmask;
-                const int r = (int)(ord & 15u);
-                const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
+            const uint32_t ord = key & lowmask;
+            const int r = (int)(ord & 15u);
+            const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
+            if (key != 0xffffffffu && row < (uint32_t)len) {
                 // Y3: coef (x^2 + y^2); bf16x2: Cauchy-Schwarz on the code
                 // rounding residual, 2 (2 |x| |y - yh| + coef (x^2 + y^2))
                 const float m = Y3 ? coef * (xn + ynl[row]) + 1e-30f
