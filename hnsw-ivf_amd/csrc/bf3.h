@@ -94,7 +94,8 @@ __device__ __forceinline__ void load_query_frags(const float* __restrict__ x, in
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const int kk = 16 * s + 8 * lh + 4 * u;
-            raw[2 * s + u] = kk < d4 ? *(const float4*)(xr + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+            // clamped address: every load is unconditional (no branches)
+            raw[2 * s + u] = *(const float4*)(xr + min(kk, d4 - 4));
         }
     xn = 0.f;
 #pragma unroll
@@ -102,7 +103,7 @@ __device__ __forceinline__ void load_query_frags(const float* __restrict__ x, in
         float v[8] = {raw[2 * s].x,     raw[2 * s].y,     raw[2 * s].z,     raw[2 * s].w,
                       raw[2 * s + 1].x, raw[2 * s + 1].y, raw[2 * s + 1].z, raw[2 * s + 1].w};
 #pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = 16 * s + 8 * lh + j < d ? v[j] : 0.f;
+        for (int j = 0; j < 8; j++) v[j] = 16 * s + 8 * lh + j < d ? v[j] : 0.f;  // also kk >= d4
         split8(v, bh[s], bl[s]);
 #pragma unroll
         for (int j = 0; j < 8; j++) xn = fmaf(v[j], v[j], xn);

@@ -96,5 +96,134 @@ __device__ __forceinline__ void exact_topk_resolve(Stream& st, int k, int metric
     }
 }
 
+// Fast path for a query whose whole candidate set fits NB 64-lane batches
+// (candidate 64 b + lane < ns holds key (k1[b], k2[b]); the others are
+// ignored): each candidate's rank by (k1, k2) (ties in both broken by
+// position, as duplicate (dist, id) pairs are kept twice by the reference
+// heap) from a broadcast loop, no sorting network.  Returns false and writes
+// nothing when the k-th key value is shared past the k boundary (the
+// arrival-order rule then needs exact_topk_resolve).
+template <int NB, class OutIdx = int64_t>
+__device__ __forceinline__ bool exact_topk_small(float (&k1)[NB], long long (&k2)[NB], int ns,
+                                                 int k, int metric_l2, int lane, bool write,
+                                                 float* __restrict__ Dq,
+                                                 OutIdx* __restrict__ Iq) {
+    int rank[NB], eq[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        rank[b] = 0;
+        eq[b] = 0;
+        if (64 * b + lane >= ns) {
+            k1[b] = WS_INF;
+            k2[b] = WS_NOID;
+        }
+    }
+    // rank by k1 alone (one broadcast per candidate); equal k1 values (rare:
+    // exact distance ties, or the +inf padding) are counted and, when any
+    // real candidate shares its k1, ranked again by (k1, k2, position)
+#pragma unroll
+    for (int bb = 0; bb < NB; bb++) {
+        const int nj = min(64, ns - 64 * bb);
+        for (int j = 0; j < nj; j++) {
+            const float a1 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(k1[bb]), j));
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                if (64 * b < ns) {  // uniform: batches past ns hold nothing
+                    rank[b] += a1 < k1[b] ? 1 : 0;
+                    eq[b] += a1 == k1[b] ? 1 : 0;
+                }
+            }
+        }
+    }
+    bool ties = false;
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+        ties |= __ballot(64 * b + lane < ns && eq[b] > 1 && k1[b] < WS_INF) != 0ull;
+    if (ties) {
+#pragma unroll
+        for (int b = 0; b < NB; b++) rank[b] = 0;
+#pragma unroll
+        for (int bb = 0; bb < NB; bb++) {
+            const int nj = min(64, ns - 64 * bb);
+            for (int j = 0; j < nj; j++) {
+                const float a1 =
+                        __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(k1[bb]), j));
+                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)(k2[bb] & 0xffffffffLL), j);
+                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(k2[bb] >> 32), j);
+                const long long a2 = (long long)(((unsigned long long)hi << 32) | lo);
+                const int pj = 64 * bb + j;
+#pragma unroll
+                for (int b = 0; b < NB; b++) {
+                    if (64 * b < ns) {
+                        const bool before =
+                                a1 < k1[b] ||
+                                (a1 == k1[b] && (a2 < k2[b] || (a2 == k2[b] && pj < 64 * b + lane)));
+                        rank[b] += before ? 1 : 0;
+                    }
+                }
+            }
+        }
+    } else {
+        // distinct k1 among real candidates; the +inf padding (all k1 equal)
+        // only ever fills output slots with (FLT_MAX / -FLT_MAX, -1), so its
+        // order among itself is immaterial: break it by position
+#pragma unroll
+        for (int bb = 0; bb < NB; bb++) {
+            if (64 * bb < ns) {
+                const unsigned long long inf_m = __ballot(64 * bb + lane < ns && k1[bb] == WS_INF);
+#pragma unroll
+                for (int b = 0; b < NB; b++) {
+                    // +inf candidates before this one in position order
+                    if (64 * b < ns && k1[b] == WS_INF) {
+                        if (bb < b) rank[b] += __popcll(inf_m);
+                        else if (bb == b) rank[b] += __popcll(inf_m & ((1ull << lane) - 1ull));
+                    }
+                }
+            }
+        }
+    }
+    // boundary tie: the key at rank k has the k1 of the key at rank k - 1
+    float v1 = WS_INF, n1 = WS_INF;
+    long long n2 = WS_NOID;
+    bool hv = false, hn = false;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const bool cand = 64 * b + lane < ns;
+        const unsigned long long mv = __ballot(cand && rank[b] == k - 1);
+        const unsigned long long mn = __ballot(cand && rank[b] == k);
+        if (mv) {
+            hv = true;
+            v1 = __shfl(k1[b], __ffsll((long long)mv) - 1);
+        }
+        if (mn) {
+            hn = true;
+            const int ln = __ffsll((long long)mn) - 1;
+            n1 = __shfl(k1[b], ln);
+            n2 = shfl_ll(k2[b], ln);
+        }
+    }
+    if (hv && hn && n2 != WS_NOID && n1 == v1) return false;
+    if (write) {
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            if (64 * b + lane < ns && rank[b] < k) {
+                float dis;
+                long long id;
+                from_key(metric_l2, k1[b], k2[b], dis, id);
+                Dq[rank[b]] = dis;
+                Iq[rank[b]] = (OutIdx)id;
+            }
+        }
+        if (lane >= ns && lane < k) {  // fewer than k candidates: padding slots
+            float dis;
+            long long id;
+            from_key(metric_l2, WS_INF, WS_NOID, dis, id);
+            Dq[lane] = dis;
+            Iq[lane] = (OutIdx)id;
+        }
+    }
+    return true;
+}
+
 }  // namespace kern
 }  // namespace faiss_amd

@@ -158,7 +158,8 @@ void IndexIVF::sync_device() const {
         }
         if (n) memcpy(hi.data() + off[l], invlists->ids[l].data(), sizeof(idx_t) * n);
     }
-    d_codes_.reserve(hc.size());
+    // + tail padding: the re-rank reads BDM floats from any row start
+    d_codes_.reserve(hc.size() + sizeof(float) * kern::BDM_HOST);
     d_ids_.reserve(sizeof(idx_t) * hi.size());
     d_row_list_.reserve(sizeof(uint32_t) * hl.size());
     d_list_off_.reserve(sizeof(uint32_t) * (nlist + 1));
@@ -472,37 +473,42 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     s_ent_.reserve(sizeof(uint32_t) * n * np);
     kern::IVFBuckets b{s_counts_.as<uint32_t>(), s_boff_.as<uint32_t>(), s_ioff_.as<uint32_t>(),
                        s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
-    kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), (int)nlist, QT, b, s);
-    const int64_t max_items = kern::ivf_max_items(n, np, (int)nlist, QT);
     const char* env = getenv("FAISS_AMD_IVF_SCAN");
     int mode = scan_mode;
     if (env && !strcmp(env, "exact")) mode = 1;
     if (env && !strcmp(env, "mfma")) mode = 0;
     const int KQ = obits_ <= 14 ? kern::ivf_mfma_kq((int)k, d) : 0;
+    const bool mfma = mode == 0 && KQ > 0;
+    if (mfma) {
+        s_part_.reserve(sizeof(uint32_t) * n * np * KQ);        // raw filter keys
+        s_pk2_.reserve(sizeof(kern::ProbeRec) * n * np);        // per-probe records
+        b.mark_keys = s_part_.as<uint32_t>();
+        b.mark_recs = s_pk2_.as<kern::ProbeRec>();
+        b.mark_ke = KQ;
+    }
+    kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), (int)nlist, QT, b, s);
+    const int64_t max_items = kern::ivf_max_items(n, np, (int)nlist, QT);
     const bool l2 = metric_type == METRIC_L2;
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(n, 4));
-    if (mode == 0 && KQ > 0) {
-        s_part_.reserve(sizeof(unsigned long long) * n * np * KQ);
-        s_pk1_.reserve(sizeof(float) * n * np * KQ);  // upper bounds
-        s_pk2_.reserve(sizeof(float) * n * np);       // dropped-candidate bounds
+    if (mfma) {
         const bool dbg = getenv("FAISS_AMD_IVF_STATS") != nullptr;
         if (dbg) HIP_CHECK(hipMemsetAsync(s_flags_.ptr, 0, 4 * sizeof(uint32_t), s));
         kern::ivf_flat_scan_mfma(x, ldx, d_codes_.as<float>(), l, d_cbf_.ptr,
                                  d_ids_.as<int64_t>(), d_ynorm_.as<float>(), d_ynmax_.as<float>(),
                                  d_rres_.as<float>(), d_rmax_.as<float>(),
                                  d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(),
-                                 (int)nlist, d, obits_, n, np, (int)k, l2, b, max_items, assign,
-                                 s_part_.as<unsigned long long>(), s_pk1_.as<float>(),
-                                 s_pk2_.as<float>(), dbg ? s_flags_.as<uint32_t>() : nullptr,
-                                 distances, labels, &ktimes, s);
+                                 (int)nlist, d, obits_, n, np, (int)k, l2, b, max_items,
+                                 s_part_.as<uint32_t>(), s_pk2_.as<kern::ProbeRec>(),
+                                 dbg ? s_flags_.as<uint32_t>() : nullptr, distances, labels,
+                                 &ktimes, s);
         if (dbg) {
             uint32_t st[4];
             HIP_CHECK(hipMemcpyAsync(st, s_flags_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
             HIP_CHECK(hipStreamSynchronize(s));
             fprintf(stderr,
                     "[faiss_amd] ivf mfma scan: nq=%lld survivors/q=%.2f failing probes/q=%.4f "
-                    "overflow queries=%u\n",
-                    (long long)n, st[0] / (double)n, st[1] / (double)n, st[2]);
+                    "overflow queries=%u general-resolve queries=%u\n",
+                    (long long)n, st[0] / (double)n, st[1] / (double)n, st[2], st[3]);
         }
         return;
     }

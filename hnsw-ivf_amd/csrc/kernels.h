@@ -74,12 +74,30 @@ void translate_labels(int64_t* labels, int64_t n, int64_t offset, hipStream_t s)
 
 // ---------------- IVF list-centric batching ----------------
 // Work item = (list, chunk of <= QT queries probing it).
+// Per (query, probe) record of the IVF-Flat MFMA filter, read by the re-rank:
+// per thread stream (4 per (query, list)) a lower bound of every candidate it
+// dropped (+inf: none dropped / empty probe), the list's largest
+// certification margin, and the list's arena geometry.
+struct alignas(16) ProbeRec {
+    float pb[4];
+    float mmax;
+    uint32_t off;
+    uint32_t len;
+    uint32_t pad;
+};
+
 struct IVFBuckets {
     uint32_t* counts;      // [nlist]
     uint32_t* bucket_off;  // [nlist + 1]
     uint32_t* item_off;    // [nlist + 1]
     uint32_t* cursor;      // [n * nprobe]: slot of each entry in its bucket
     uint32_t* entries;     // [n * nprobe], entry = q * nprobe + rank
+    // optional (MFMA filter path): entries whose list is invalid or empty get
+    // empty partials (part ~0, pub / pbound +inf), so the re-rank reads every
+    // entry without consulting the assignment
+    uint32_t* mark_keys = nullptr;
+    ProbeRec* mark_recs = nullptr;
+    int mark_ke = 0;
 };
 void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
                 int nlist, int QT, IVFBuckets b, hipStream_t s);
@@ -107,6 +125,7 @@ void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const i
 int ivf_mfma_kq(int k, int d);
 int ivf_bf3_obits(uint32_t max_list_len);
 // padded dim of the bf16 hi/lo images (multiple of 32)
+constexpr int BDM_HOST = 128;  // bf3.h BDM: max padded dim of the MFMA paths
 inline int bf3_db_host(int d) { return (d + 31) / 32 * 32; }  // ordinal bits of the 32-bit keys
 double ivf_bf3_coef(int d);                // margin coefficient
 double ivf_bf2_coef(int d);
@@ -123,9 +142,8 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         const float* rres, const float* rmax,
                         const uint32_t* list_off, const uint32_t* list_len, int nlist, int d,
                         int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
-                        int64_t max_items, const int32_t* assign, unsigned long long* part,
-                        float* pub, float* pbound, uint32_t* stats, float* D, int64_t* I,
-                        KernelTimes* kt, hipStream_t s);
+                        int64_t max_items, uint32_t* keys, ProbeRec* recs, uint32_t* stats,
+                        float* D, int64_t* I, KernelTimes* kt, hipStream_t s);
 // exact re-scan (reference tie rule) of the queries with flags[q] != 0
 void ivf_exact_fallback(const uint32_t* flags, const int32_t* assign, const uint32_t* list_off,
                         const uint32_t* list_len, int nlist, const float* x, int ldx,

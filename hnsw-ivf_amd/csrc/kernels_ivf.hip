@@ -82,11 +82,24 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
 __global__ void k_bucket_fill(const int32_t* __restrict__ assign, int64_t total,
                               const uint32_t* __restrict__ list_len, int nlist,
                               const uint32_t* __restrict__ bucket_off,
-                              const uint32_t* __restrict__ pos, uint32_t* __restrict__ entries) {
+                              const uint32_t* __restrict__ pos, uint32_t* __restrict__ entries,
+                              uint32_t* __restrict__ mkeys, ProbeRec* __restrict__ mrecs,
+                              int ke) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
     int l = assign[e];
-    if (l >= 0 && l < nlist && list_len[l] > 0) entries[bucket_off[l] + pos[e]] = (uint32_t)e;
+    if (l >= 0 && l < nlist && list_len[l] > 0) {
+        entries[bucket_off[l] + pos[e]] = (uint32_t)e;
+    } else if (mkeys) {
+        for (int i = 0; i < ke; i++) mkeys[e * ke + i] = 0xffffffffu;
+        ProbeRec pr;
+        for (int i = 0; i < 4; i++) pr.pb[i] = WS_INF;
+        pr.mmax = 0.f;
+        pr.off = 0u;
+        pr.len = 0u;
+        pr.pad = 0u;
+        mrecs[e] = pr;
+    }
 }
 
 __global__ void k_ivf_visit_stats(const int32_t* __restrict__ assign, int64_t total,
@@ -130,7 +143,8 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
     HIP_LAUNCH_CHECK();
     if (total > 0) {
         k_bucket_fill<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
-                assign, total, list_len, nlist, b.bucket_off, b.cursor, b.entries);
+                assign, total, list_len, nlist, b.bucket_off, b.cursor, b.entries, b.mark_keys,
+                b.mark_recs, b.mark_ke);
         HIP_LAUNCH_CHECK();
     }
 }

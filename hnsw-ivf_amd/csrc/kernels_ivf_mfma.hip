@@ -31,6 +31,8 @@
 #include <cfloat>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
+#include <vector>
 
 #include "common.h"
 #include "kernels.h"
@@ -64,7 +66,7 @@ namespace kern {
 // widens the [lb, ub] interval (decoded with the low bits cleared / set).
 //
 // Per (query, list) output, 4*KT entries (4 threads x KT keys each):
-//   part[e][i] = ordered_f32(lb) << 32 | row   (~0 = empty)
+//   part[e][i] = ordered_f32(lb) << 32 | arena row   (~0 = empty)
 //   pub[e][i]  = ub                             (upper bound of the exact key)
 //   pbound[e]  = lower bound of the exact key of every dropped candidate of
 //                the list (min over the 4 threads of their KT-th key, minus
@@ -102,8 +104,7 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
         int nprobe, float coef, int obits, const uint32_t* __restrict__ bucket_off,
         const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ entries,
-        unsigned long long* __restrict__ part, float* __restrict__ pub,
-        float* __restrict__ pbound) {
+        uint32_t* __restrict__ keys, ProbeRec* __restrict__ recs) {
     // two code tiles (double buffer), row stride CSB bytes = (Y3 ? 4 : 2) * DB + 16
     __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * ((Y3 ? 4 : 2) * 16 * NS + 16)];
     __shared__ __attribute__((aligned(16))) float ynt[2][BV];  // row norm (L2) / bias (IP)
@@ -231,37 +232,35 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     bnd_s[qloc][slot] = bnd;
     __syncthreads();
     if (qvalid) {
+        // raw 32-bit keys (the re-rank decodes the approx bracket and the row)
         const int64_t e = ent_s[qloc];
-        unsigned long long* po = part + e * (4 * KT) + slot * KT;
-        float* pu = pub + e * (4 * KT) + slot * KT;
+        uint32_t* ko = keys + e * (4 * KT) + slot * KT;
 #pragma unroll
         for (int i = 0; i < KT; i++) {
             const uint32_t key = tq.q[i];
             const uint32_t ord = key & lowmask;
             const int r = (int)(ord & 15u);
             const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-            if (key != 0xffffffffu && row < (uint32_t)len) {
-                // Y3: coef (x^2 + y^2); bf16x2: Cauchy-Schwarz on the code
-                // rounding residual, 2 (2 |x| |y - yh| + coef (x^2 + y^2))
-                const float m = Y3 ? coef * (xn + ynl[row]) + 1e-30f
-                                   : 2.f * (2.f * sqrtf(xn) * rres[row0 + row] +
-                                            coef * (xn + ynl[row])) + 1e-30f;
-                const float alo = key_decode_lo<L2>(key, lowmask);
-                const float ahi = key_decode_hi<L2>(key, lowmask);
-                po[i] = ((unsigned long long)ordered_f32(alo - m) << 32) | row;
-                pu[i] = ahi + m;
-            } else {
-                po[i] = ~0ull;
-                pu[i] = WS_INF;
-            }
+            ko[i] = (key != 0xffffffffu && row < (uint32_t)len) ? key : 0xffffffffu;
         }
         if (slot == 0) {
-            const float b4 = fminf(fminf(bnd_s[qloc][0], bnd_s[qloc][1]),
-                                   fminf(bnd_s[qloc][2], bnd_s[qloc][3]));
+            // the list's largest margin bounds every kept row's margin:
+            // Y3: coef (x^2 + y^2); bf16x2: Cauchy-Schwarz on the code
+            // rounding residual, 2 (2 |x| |y - yh| + coef (x^2 + y^2))
             const float mmax = Y3 ? coef * (xn + ynmax[l]) + 1e-30f
                                   : 2.f * (2.f * sqrtf(xn) * rmax[l] + coef * (xn + ynmax[l])) +
                                             1e-30f;
-            pbound[e] = b4 < WS_INF ? b4 - mmax : WS_INF;
+            ProbeRec pr;
+#pragma unroll
+            for (int sl = 0; sl < 4; sl++) {
+                const float b = bnd_s[qloc][sl];
+                pr.pb[sl] = b < WS_INF ? b - mmax : WS_INF;
+            }
+            pr.mmax = mmax;
+            pr.off = (uint32_t)row0;
+            pr.len = (uint32_t)len;
+            pr.pad = 0u;
+            recs[e] = pr;
         }
     }
 }
@@ -286,179 +285,413 @@ __global__ void k_list_max(const float* __restrict__ yn, const uint32_t* __restr
 // entries with lb <= U.  The exact top-k over that candidate stream (with the
 // reference tie rule, exact_select.h) is the reference result.
 //
-// Latency layout: lane r < nprobe holds probe r's list (offset, length,
-// dropped bound); the kept entries' upper bounds are loaded V per lane in one
-// round trip; U comes from a ballot radix select (no shuffles); survivors are
-// compacted to LDS as global arena rows.
+// Latency layout (two dependent global round trips on the common path):
+//   1. the kept entries' raw 32-bit keys (V per lane), the probes' records
+//      (dropped bound, largest margin M, arena offset / length) and the
+//      query, all independent;  ub' = approx_hi + M and lb' = approx_lo - M
+//      bracket each entry's exact key (M >= the entry's own margin);
+//   2. the survivors' rows and ids.
+// Invalid / empty probes carry empty entries (k_bucket_fill), so neither the
+// assignment nor the list geometry arrays are read.
+// Exact distances: 4 lanes per row (ref_arith.h order, see eval_rows64).
 constexpr int RR_CAP = 512;
+constexpr int RR_XM = BDM / 8;
+constexpr int RR_W = 1;  // waves (queries) per block: one, for fine-grained packing
+// (the re-rank's barriers sit in wave-uniform branches: one wave per block)
+static_assert(RR_W == 1, "k_ivf_rerank assumes one wave per block");
+
+__device__ __forceinline__ uint32_t cdiv_dev(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// list row of a filter key: thread slot (bi, lh) of its (query, list), tile
+// and register index from the ordinal (the 32x32 MFMA block layout)
+__device__ __forceinline__ uint32_t ivf_key_row(uint32_t key, uint32_t lowmask, int slot) {
+    const uint32_t ord = key & lowmask;
+    const uint32_t r = ord & 15u;
+    return (ord >> 4) * BV + 32 * (slot >> 1) + 4 * (slot & 1) + 8 * (r >> 2) + (r & 3);
+}
+
+// exact reference-order distance of the row `grow` each lane names (valid
+// lanes only); 16 rows per pass, 4 lanes per row: lane j' of a row owns the
+// reference's partial sums c[2j'] and c[2j'+1] (dims 8m + 2j' + {0,1}), so a
+// pass is one round trip of 16 float2 loads per lane
+constexpr int RR_RS = BDM + 4;  // LDS row stride (floats) of the staged rows
+
+// exact reference-order distance of the row `grow` each lane names (valid
+// lanes only), 16 rows per pass:
+//  1. the pass's rows are staged into LDS with coalesced 16-B loads (32
+//     lanes per 512-B row, whole cache lines per request);
+//  2. 4 lanes per row evaluate it: lane j' owns the reference's partial sums
+//     c[2j'] and c[2j'+1] (dims 8m + 2j' + {0,1}); x_j = c_j + c_{j+4},
+//     then (x0 + x2) + (x1 + x3) (ref_arith.h order), then the epilogue dims.
+template <bool L2>
+__device__ __forceinline__ float eval_rows64(const float* xr /* LDS copy of the query */,
+                                             float* stage /* LDS [16][RR_RS] */,
+                                             const float* __restrict__ xq,
+                                             const float* __restrict__ codes, int ldc, int d,
+                                             uint32_t grow, bool valid, int lane) {
+    const int g = lane >> 2, jp = lane & 3;
+    const int n8 = d & ~7, nm = n8 >> 3;
+    const int d4 = (d + 3) >> 2;  // float4 per row actually read
+    const unsigned long long vm = __ballot(valid);
+    float out = 0.f;
+#pragma unroll 1
+    for (int p = 0; p < 4; p++) {
+        if (((vm >> (16 * p)) & 0xffffull) == 0ull) continue;
+        // ---- stage: row 2t + (lane >> 5), float4 column lane & 31
+        float4 v[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int row = 2 * t + (lane >> 5), c4 = lane & 31;
+            const uint32_t rg = __shfl(grow, 16 * p + row);
+            const bool rv = (vm >> (16 * p + row)) & 1ull;
+            v[t] = (rv && c4 < d4) ? *(const float4*)(codes + (int64_t)rg * ldc + 4 * c4)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int row = 2 * t + (lane >> 5), c4 = lane & 31;
+            *(float4*)(stage + row * RR_RS + 4 * c4) = v[t];
+        }
+        __syncthreads();  // one wave per block: orders the staging before the reads
+        // ---- evaluate
+        const float* yj = stage + g * RR_RS + 2 * jp;
+        const float* xj = xr + 2 * jp;
+        float ca = 0.f, cb = 0.f;
+#pragma unroll
+        for (int m = 0; m < RR_XM; m++) {
+            const float2 xv = *(const float2*)(xj + 8 * m);
+            const float2 yv = *(const float2*)(yj + 8 * m);
+            const float ta = ref_term_fma<L2>(xv.x, yv.x, ca);
+            const float tb = ref_term_fma<L2>(xv.y, yv.y, cb);
+            ca = m < nm ? ta : ca;
+            cb = m < nm ? tb : cb;
+        }
+        ca += __shfl_xor(ca, 2);
+        cb += __shfl_xor(cb, 2);
+        ca += __shfl_xor(ca, 1);  // lane 0: x0 + x2
+        cb += __shfl_xor(cb, 1);  // lane 0: x1 + x3
+        float r = ca + cb;
+        if (n8 < d) {
+            const float* y = stage + g * RR_RS;
+            int i = n8;
+            if (d - n8 >= 4) {
+                const float e0 = ref_term<L2>(xq[n8], y[n8]), e1 = ref_term<L2>(xq[n8 + 1], y[n8 + 1]);
+                const float e2 = ref_term<L2>(xq[n8 + 2], y[n8 + 2]);
+                const float e3 = ref_term<L2>(xq[n8 + 3], y[n8 + 3]);
+                r = r + ((e0 + e2) + (e1 + e3));
+                i += 4;
+            }
+            for (; i < d; i++) r = ref_term_fma<L2>(xq[i], y[i], r);
+        }
+        const float got = __shfl(r, 4 * (lane & 15));
+        if ((lane >> 4) == p) out = got;
+        __syncthreads();  // the next pass overwrites the staging rows
+    }
+    return out;
+}
+
+// Rows of thread stream `slot` of a list of length len, enumerated as
+// e = tile * 16 + register (the filter's visiting order within the stream)
+__device__ __forceinline__ int ivf_stream_row(int e, int slot) {
+    const int r = e & 15;
+    return (e >> 4) * BV + 32 * (slot >> 1) + 4 * (slot & 1) + 8 * (r >> 2) + (r & 3);
+}
 
 template <bool L2>
 struct RerankStream {
-    const uint32_t* surv;  // global arena rows of the survivors
+    const uint32_t* surv;    // arena rows of the candidates (LDS)
     const uint16_t* sprobe;  // their probe rank
     const int64_t* ids;
     const float* xq;
     const float* codes;
-    int ldc, d, lane, nsv;
-    // overflow mode: re-scan the survivor predicate from global memory
-    bool overflow;
-    const unsigned long long* part;
-    int E, KE;
+    const float* xs;  // LDS copy of the query (first d & ~7 dims)
+    float* stage;     // LDS staging rows of the evaluator
+    int ldc, d, lane, nsv, KE, KT, E;
+    uint32_t lowmask;
+    bool overflow;  // candidate list did not fit: re-derive it from global
+    const uint32_t* keys;
     float U;
-    unsigned long long okmask, fmask;
-    uint32_t my_off, my_len;  // lane r: probe r
+    uint32_t my_fail;         // lane r: failing streams of probe r (4 bits)
+    float my_m;               // lane r: probe r's margin
+    uint32_t my_off, my_len;  // lane r: probe r's arena geometry
 
-    __device__ __forceinline__ uint32_t off_of(int r) const { return __shfl(my_off, r); }
-    __device__ __forceinline__ void eval_row(int r, uint32_t grow, uint32_t rank_row, float& k1,
-                                             long long& k2, long long& rank) const {
-        const float* yr = codes + (int64_t)grow * ldc;
-        const float dis = L2 ? ref_l2(xq, yr, d) : ref_ip(xq, yr, d);
-        to_key(L2 ? 1 : 0, dis, (long long)ids[grow], k1, k2);
-        rank = ((long long)r << 32) | rank_row;
+    __device__ __forceinline__ void emit(bool ok, uint32_t grow, float& k1, long long& k2) const {
+        // the id load is issued before the rows', so both share one round trip
+        const long long idv = ok ? (long long)ids[grow] : 0ll;
+        const float dis = eval_rows64<L2>(xs, stage, xq, codes, ldc, d, grow, ok, lane);
+        k1 = WS_INF;
+        k2 = WS_NOID;
+        if (ok) to_key(L2 ? 1 : 0, dis, idv, k1, k2);
     }
     template <class F>
     __device__ __forceinline__ void for_each(F f) const {
         if (!overflow) {
             for (int s0 = 0; s0 < nsv; s0 += 64) {
-                float k1 = WS_INF;
-                long long k2 = WS_NOID, rank = 0;
                 bool ok = s0 + lane < nsv;
-                if (ok) {
-                    const uint32_t grow = surv[s0 + lane];
-                    const int r = sprobe[s0 + lane];
-                    eval_row(r, grow, grow, k1, k2, rank);
-                    ok = key_admissible(k1);
-                }
-                f(ok, k1, k2, rank);
+                const uint32_t grow = ok ? surv[s0 + lane] : 0u;
+                const long long rank = ok ? (((long long)sprobe[s0 + lane] << 32) | grow) : 0;
+                float k1;
+                long long k2;
+                emit(ok, grow, k1, k2);
+                f(ok && key_admissible(k1), k1, k2, rank);
             }
-        } else {
-            for (int c0 = 0; c0 < E; c0 += 64) {
-                const int c = c0 + lane;
-                const int r = c / KE;
-                const uint32_t roff = off_of(r < 64 ? r : 0);
-                float k1 = WS_INF;
-                long long k2 = WS_NOID, rank = 0;
-                bool ok = false;
-                if (c < E && ((okmask >> r) & 1ull) && !((fmask >> r) & 1ull)) {
-                    const unsigned long long key = part[c];
-                    ok = key != ~0ull && unordered_f32((uint32_t)(key >> 32)) <= U;
-                    if (ok) {
-                        eval_row(r, roff + (uint32_t)key, roff + (uint32_t)key, k1, k2, rank);
-                        ok = key_admissible(k1);
-                    }
-                }
-                if (__ballot(ok) == 0ull) continue;
-                f(ok, k1, k2, rank);
-            }
+            return;
         }
-        // every row of the failing probes (rank = list row; the arena row
-        // order within a list is the list order)
-        unsigned long long m = fmask;
+        // kept entries under U of the streams that did not fail
+        for (int c0 = 0; c0 < E; c0 += 64) {
+            const int c = c0 + lane;
+            const int r = c < E ? c / KE : 0;
+            const int sl = (c - r * KE) / KT;
+            const float mr = __shfl(my_m, r);
+            const uint32_t orr = __shfl(my_off, r);
+            const uint32_t fl = __shfl(my_fail, r);
+            bool ok = false;
+            uint32_t grow = 0;
+            if (c < E && !((fl >> sl) & 1u)) {
+                const uint32_t key = keys[c];
+                ok = key != 0xffffffffu && key_decode_lo<L2>(key, lowmask) - mr <= U;
+                grow = orr + ivf_key_row(key, lowmask, sl);
+            }
+            if (__ballot(ok) == 0ull) continue;
+            const long long rank = ((long long)r << 32) | grow;
+            float k1;
+            long long k2;
+            emit(ok, grow, k1, k2);
+            f(ok && key_admissible(k1), k1, k2, rank);
+        }
+        // every row of the failing streams
+        unsigned long long m = __ballot(my_fail != 0u);
         while (m) {
             const int r = __ffsll((long long)m) - 1;
             m &= m - 1ull;
-            const uint32_t o = off_of(r), len = __shfl(my_len, r);
-            for (uint32_t v0 = 0; v0 < len; v0 += 64) {
-                float k1 = WS_INF;
-                long long k2 = WS_NOID, rank = 0;
-                bool ok = v0 + lane < len;
-                if (ok) {
-                    eval_row(r, o + v0 + lane, o + v0 + lane, k1, k2, rank);
-                    ok = key_admissible(k1);
+            const uint32_t o = __shfl(my_off, r), len = __shfl(my_len, r);
+            const uint32_t fl = __shfl(my_fail, r);
+            const int ne = (int)cdiv_dev(len, BV) * 16;
+            for (int sl = 0; sl < 4; sl++) {
+                if (!((fl >> sl) & 1u)) continue;
+                for (int e0 = 0; e0 < ne; e0 += 64) {
+                    const int row = ivf_stream_row(e0 + lane, sl);
+                    const bool ok = e0 + lane < ne && row < (int)len;
+                    const uint32_t grow = o + (uint32_t)(ok ? row : 0);
+                    const long long rank = ((long long)r << 32) | grow;
+                    float k1;
+                    long long k2;
+                    emit(ok, grow, k1, k2);
+                    f(ok && key_admissible(k1), k1, k2, rank);
                 }
-                f(ok, k1, k2, rank);
             }
         }
     }
 };
 
 template <bool L2, int V>
-__global__ __launch_bounds__(256) void k_ivf_rerank(
-        const unsigned long long* __restrict__ part, const float* __restrict__ pub,
-        const float* __restrict__ pbound, const int32_t* __restrict__ assign,
-        const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
+__global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
+        const uint32_t* __restrict__ keys, const ProbeRec* __restrict__ recs,
         const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
-        const int64_t* __restrict__ ids, int d, int64_t n, int nprobe, int KE, int k,
-        float* __restrict__ D, int64_t* __restrict__ I, uint32_t* __restrict__ stats) {
-    __shared__ uint32_t surv[4][RR_CAP];
-    __shared__ uint16_t sprobe[4][RR_CAP];
+        const int64_t* __restrict__ ids, int d, int64_t n, int nprobe, int KT, int obits, int k,
+        float* __restrict__ D, int64_t* __restrict__ I, uint32_t* __restrict__ stats,
+        unsigned long long* __restrict__ trace) {
+    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    __shared__ uint32_t surv[RR_W][RR_CAP];
+    __shared__ uint16_t sprobe[RR_W][RR_CAP];
+    __shared__ __attribute__((aligned(16))) float xsh[RR_W][BDM];
+    __shared__ __attribute__((aligned(16))) float stg[RR_W][16 * RR_RS];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t q0 = (int64_t)blockIdx.x * 4 + w;
+    const int64_t q0 = (int64_t)blockIdx.x * RR_W + w;
     const bool valid = q0 < n;
     const int64_t q = valid ? q0 : 0;
+    const int KE = 4 * KT;
     const int E = valid ? nprobe * KE : 0;
-    // per-probe state, lane r = probe r
-    uint32_t my_off = 0, my_len = 0;
-    float my_pb = WS_INF;
-    bool my_ok = false;
-    if (valid && lane < nprobe) {
-        const int lst = assign[q * nprobe + lane];
-        if (lst >= 0 && lst < nlist) {
-            my_len = list_len[lst];
-            my_off = list_off[lst];
-            my_ok = my_len > 0;
-            if (my_ok) my_pb = pbound[q * nprobe + lane];
+    const uint32_t lowmask = (1u << obits) - 1u;
+    // ---- round trip 1: keys, probe records, query.  Lane l holds the V
+    // consecutive entries l V .. l V + V - 1, all of probe lp = l V / KE
+    // (V <= KE, both powers of two).
+    const uint32_t* kq = keys + q * (int64_t)nprobe * KE;
+    uint32_t kv[V];
+    const bool has = lane * V < E;
+    if constexpr (V >= 4) {
+#pragma unroll
+        for (int i = 0; i < V; i += 4) {
+            const uint4 v4 = has ? *(const uint4*)(kq + lane * V + i)
+                                 : make_uint4(~0u, ~0u, ~0u, ~0u);
+            kv[i] = v4.x;
+            kv[i + 1] = v4.y;
+            kv[i + 2] = v4.z;
+            kv[i + 3] = v4.w;
         }
+    } else {
+#pragma unroll
+        for (int i = 0; i < V; i++) kv[i] = has ? kq[lane * V + i] : 0xffffffffu;
     }
-    const unsigned long long okmask = __ballot(my_ok);
-    // upper bounds, V per lane, one round trip
-    const float* pu = pub + q * (int64_t)nprobe * KE;
+    ProbeRec pr;
+#pragma unroll
+    for (int sl = 0; sl < 4; sl++) pr.pb[sl] = WS_INF;
+    pr.mmax = 0.f;
+    pr.off = 0u;
+    pr.len = 0u;
+    pr.pad = 0u;
+    if (valid && lane < nprobe) pr = recs[q * nprobe + lane];
+    const float* xq = x + q * ldx;
+    if (lane < BDM / 4 && 4 * lane < (d & ~3))
+        *(float4*)(&xsh[w][4 * lane]) = *(const float4*)(xq + 4 * lane);
+    const int lp = has ? lane * V / KE : 0;  // this lane's probe
+    const float lm = __shfl(pr.mmax, lp);
+    const uint32_t loff = __shfl(pr.off, lp);
+    // ---- U = k-th smallest ub' over the kept entries, in two stages: T =
+    // the k-th smallest lane minimum (>= U: the k lanes below it hold k
+    // values <= T), then the exact k-th among the values <= T when they fit
+    // one per lane
     float ub[V];
+    float lmin = WS_INF;
 #pragma unroll
     for (int i = 0; i < V; i++) {
-        const int c = i * 64 + lane;
-        ub[i] = (c < E && ((okmask >> (c / KE)) & 1ull)) ? pu[c] : WS_INF;
+        ub[i] = kv[i] != 0xffffffffu ? key_decode_hi<L2>(kv[i], lowmask) + lm : WS_INF;
+        lmin = fminf(lmin, ub[i]);
     }
-    float U = wave_kth_smallest<V>(ub, k);
+    float U;
+    {
+        const float lmv[1] = {lmin};
+        const float T = wave_kth_smallest<1>(lmv, k);
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < V; i++) cnt += __popcll(__ballot(ub[i] <= T));
+        if (T < WS_INF && cnt <= 64) {
+            // compact the values <= T to lanes 0..cnt-1 through LDS
+            float* cb = reinterpret_cast<float*>(surv[w]);
+            int pos = 0;
+#pragma unroll
+            for (int i = 0; i < V; i++) {
+                const bool in = ub[i] <= T;
+                const unsigned long long m = __ballot(in);
+                if (in) cb[pos + __popcll(m & ((1ull << lane) - 1ull))] = ub[i];
+                pos += __popcll(m);
+            }
+            __syncthreads();
+            const float cv[1] = {lane < cnt ? cb[lane] : WS_INF};
+            __syncthreads();
+            U = wave_kth_smallest<1>(cv, k);
+        } else {
+            U = wave_kth_smallest<V>(ub, k);
+        }
+    }
     if (!(U <= WS_INF)) U = WS_INF;  // NaN guard
-    const unsigned long long fmask = __ballot(my_ok && my_pb < WS_INF && my_pb <= U);
-    // survivors -> LDS (global arena row + probe rank)
-    const unsigned long long* pp = part + q * (int64_t)nprobe * KE;
+    const unsigned long long t_u = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    // failing streams: one that dropped a candidate that may be <= U
+    uint32_t my_fail = 0u;
+#pragma unroll
+    for (int sl = 0; sl < 4; sl++)
+        my_fail |= (pr.pb[sl] < WS_INF && pr.pb[sl] <= U) ? (1u << sl) : 0u;
+    const unsigned long long fmask = __ballot(my_fail != 0u);
+    const uint32_t lfail = __shfl(my_fail, lp);
+    // ---- candidates -> LDS as arena rows: kept entries with lb' <= U of the
+    // streams that did not fail, then every row of the failing streams
     int ns = 0;
 #pragma unroll
     for (int i = 0; i < V; i++) {
-        const int c = i * 64 + lane;
-        const int r = c / KE;
-        const uint32_t roff = __shfl(my_off, r < 64 ? r : 0);
+        const int sl = ((lane * V + i) % KE) / KT;
         bool sv = false;
         uint32_t grow = 0;
-        if (ub[i] < WS_INF && !((fmask >> r) & 1ull)) {
-            const unsigned long long key = pp[c];
-            sv = key != ~0ull && unordered_f32((uint32_t)(key >> 32)) <= U;
-            grow = roff + (uint32_t)key;
+        if (kv[i] != 0xffffffffu && !((lfail >> sl) & 1u)) {
+            sv = key_decode_lo<L2>(kv[i], lowmask) - lm <= U;
+            grow = loff + ivf_key_row(kv[i], lowmask, sl);
         }
         const unsigned long long m = __ballot(sv);
         const int pos = ns + __popcll(m & ((1ull << lane) - 1ull));
         if (sv && pos < RR_CAP) {
             surv[w][pos] = grow;
-            sprobe[w][pos] = (uint16_t)r;
+            sprobe[w][pos] = (uint16_t)lp;
         }
         ns += __popcll(m);
     }
+    const int nkept = ns;
+    {
+        unsigned long long m = fmask;
+        while (m) {
+            const int r = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const uint32_t o = __shfl(pr.off, r), len = __shfl(pr.len, r);
+            const uint32_t fl = __shfl(my_fail, r);
+            const int ne = (int)cdiv_dev(len, BV) * 16;
+            for (int sl = 0; sl < 4; sl++) {
+                if (!((fl >> sl) & 1u)) continue;
+                for (int e0 = 0; e0 < ne; e0 += 64) {
+                    const int row = ivf_stream_row(e0 + lane, sl);
+                    const bool in = e0 + lane < ne && row < (int)len;
+                    const unsigned long long bm = __ballot(in);
+                    const int pos = ns + __popcll(bm & ((1ull << lane) - 1ull));
+                    if (in && pos < RR_CAP) {
+                        surv[w][pos] = o + (uint32_t)row;
+                        sprobe[w][pos] = (uint16_t)r;
+                    }
+                    ns += __popcll(bm);
+                }
+            }
+        }
+    }
+    __syncthreads();  // the LDS query copy and candidate list (every wave gets here)
+    const unsigned long long t_c = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     RerankStream<L2> st;
     st.surv = surv[w];
     st.sprobe = sprobe[w];
     st.ids = ids;
-    st.xq = x + q * ldx;
+    st.xq = xq;
     st.codes = codes;
+    st.xs = xsh[w];
+    st.stage = stg[w];
     st.ldc = ldc;
     st.d = d;
     st.lane = lane;
     st.nsv = ns;
-    st.overflow = ns > RR_CAP;
-    st.part = pp;
-    st.E = E;
     st.KE = KE;
+    st.KT = KT;
+    st.E = E;
+    st.lowmask = lowmask;
+    st.overflow = ns > RR_CAP;
+    st.keys = kq;
     st.U = U;
-    st.okmask = okmask;
-    st.fmask = fmask;
-    st.my_off = my_off;
-    st.my_len = my_len;
-    exact_topk_resolve(st, k, L2 ? 1 : 0, lane, valid, D + q * k, I + q * k);
+    st.my_fail = my_fail;
+    st.my_m = pr.mmax;
+    st.my_off = pr.off;
+    st.my_len = pr.len;
+    // ---- round trip 2: candidate rows and ids; up to 4 batches are ranked
+    // directly, anything else goes through the general resolve
+    bool done = false;
+    unsigned long long t_e = 0ull;
+    auto small = [&](auto nbc) {
+        constexpr int NB = decltype(nbc)::value;
+        float k1[NB];
+        long long k2[NB];
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const bool ok = 64 * b + lane < ns;
+            st.emit(ok, ok ? surv[w][64 * b + lane] : 0u, k1[b], k2[b]);
+            if (!(ok && key_admissible(k1[b]))) {
+                k1[b] = WS_INF;
+                k2[b] = WS_NOID;
+            }
+        }
+        t_e = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        return exact_topk_small<NB>(k1, k2, ns, k, L2 ? 1 : 0, lane, valid, D + q * k,
+                                    I + q * k);
+    };
+    if (ns <= 64) done = small(std::integral_constant<int, 1>());
+    else if (ns <= 128) done = small(std::integral_constant<int, 2>());
+    else if (ns <= 256) done = small(std::integral_constant<int, 4>());
+    if (!done) exact_topk_resolve(st, k, L2 ? 1 : 0, lane, valid, D + q * k, I + q * k);
     if (stats && valid && lane == 0) {
-        atomicAdd(&stats[0], (uint32_t)min(ns, RR_CAP));
+        atomicAdd(&stats[0], (uint32_t)min(nkept, RR_CAP));
         atomicAdd(&stats[1], (uint32_t)__popcll(fmask));
         atomicAdd(&stats[2], st.overflow ? 1u : 0u);
+        atomicAdd(&stats[3], done ? 0u : 1u);
+    }
+    if (trace && valid && lane == 0) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        trace[8 * q + 0] = t_start;
+        trace[8 * q + 1] = t_end;
+        trace[8 * q + 2] = (unsigned long long)ns | ((unsigned long long)__popcll(fmask) << 32);
+        trace[8 * q + 3] = t_u;
+        trace[8 * q + 4] = t_c;
+        trace[8 * q + 5] = t_e;
     }
 }
 
@@ -598,9 +831,8 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         const float* rres, const float* rmax,
                         const uint32_t* list_off, const uint32_t* list_len, int nlist, int d,
                         int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
-                        int64_t max_items, const int32_t* assign, unsigned long long* part,
-                        float* pub, float* pbound, uint32_t* stats, float* D, int64_t* I,
-                        KernelTimes* kt, hipStream_t s) {
+                        int64_t max_items, uint32_t* keys, ProbeRec* recs, uint32_t* stats,
+                        float* D, int64_t* I, KernelTimes* kt, hipStream_t s) {
     if (n <= 0) return;
     const int KE = ivf_mfma_kq(k, d);
     FAISS_THROW_IF_NOT(KE > 0);
@@ -611,12 +843,11 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     const int64_t grid = (int64_t)roundup((size_t)max_items, 32);
     FAISS_THROW_IF_NOT(grid < (1ll << 31));
     const bool l2 = metric_l2 != 0;
-    // margin of the approximate keys: the bf16 split plus the relative
-    // truncation of the 32-bit keys (2^(obits-23)) on |approx|, which the
-    // decode (low bits cleared / set) already brackets
     // precision of the filter: bf16x2 (default: half the code bytes, Cauchy-
     // Schwarz margins) or bf16x3 (FAISS_AMD_IVF_PREC=bf16x3: tighter margins,
-    // fewer re-ranked candidates on data where bf16x2 keeps too many)
+    // fewer re-ranked candidates on data where bf16x2 keeps too many).  The
+    // 32-bit keys' truncation (2^(obits-23) relative) is bracketed by the
+    // decode (low bits cleared / set).
     const char* prec = getenv("FAISS_AMD_IVF_PREC");
     const bool y3 = prec && !strcmp(prec, "bf16x3");
     const float coef = (float)(y3 ? ivf_bf3_coef(d) : ivf_bf2_coef(d));
@@ -627,15 +858,13 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         if (y3)                                                                               \
             k_ivf_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
-                    list_len, nlist,                                                          \
-                    nprobe, coef, obits, b.bucket_off, b.item_off, b.entries, part, pub,      \
-                    pbound);                                                                  \
+                    list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
+                    b.entries, keys, recs);                                                   \
         else                                                                                  \
             k_ivf_bf3_filter<L2V, KTV, NSV, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(\
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
-                    list_len, nlist,                                                          \
-                    nprobe, coef, obits, b.bucket_off, b.item_off, b.entries, part, pub,      \
-                    pbound);                                                                  \
+                    list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
+                    b.entries, keys, recs);                                                   \
     } while (0)
 #define LAUNCH_A(L2V, KTV)                     \
     do {                                       \
@@ -658,10 +887,23 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         ScopedKernelTimer tm(kt, "ivf_rerank", 0.0, s);
         const int E = nprobe * KE;
         const int V = E <= 128 ? 2 : E <= 256 ? 4 : E <= 512 ? 8 : E <= 1024 ? 16 : 32;
-#define LAUNCH_B(L2V, VV)                                                                     \
-    k_ivf_rerank<L2V, VV><<<dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s>>>(                  \
-            part, pub, pbound, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, \
-            n, nprobe, KE, k, D, I, stats)
+        // FAISS_AMD_RERANK_TRACE=<file>: per-query wave timestamps (profiling)
+        static unsigned long long* trace_buf = nullptr;
+        static int64_t trace_n = 0;
+        const char* tr = getenv("FAISS_AMD_RERANK_TRACE");
+        unsigned long long* trace = nullptr;
+        if (tr) {
+            if (trace_n < n) {
+                if (trace_buf) HIP_CHECK(hipFree(trace_buf));
+                HIP_CHECK(hipMalloc(&trace_buf, 64 * n));
+                trace_n = n;
+            }
+            trace = trace_buf;
+        }
+#define LAUNCH_B(L2V, VV)                                                                      \
+    k_ivf_rerank<L2V, VV><<<dim3((unsigned)cdiv(n, RR_W)), dim3(64 * RR_W), 0, s>>>(           \
+            keys, recs, x, ldx, codes, ldc, ids, d, n, nprobe, KE / 4, obits, k, D, I, stats,   \
+            trace)
 #define DISPATCH_V(L2V)                      \
     do {                                     \
         if (V == 2) LAUNCH_B(L2V, 2);        \
@@ -673,6 +915,15 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         if (l2) DISPATCH_V(true);
         else DISPATCH_V(false);
         HIP_LAUNCH_CHECK();
+        if (trace) {
+            std::vector<unsigned long long> h(8 * n);
+            HIP_CHECK(hipMemcpyAsync(h.data(), trace, 64 * n, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            if (FILE* f = fopen(tr, "wb")) {
+                fwrite(h.data(), 64, n, f);
+                fclose(f);
+            }
+        }
 #undef DISPATCH_V
 #undef LAUNCH_A
 #undef LAUNCH_NS

@@ -153,12 +153,13 @@ namespace faiss_amd {
 // queue; entering costs KQ predicated moves.  The union of the per-thread
 // top-k sets of a query contains its top-k, so k <= KQ entries per thread
 // suffice.
+// (branch-free xor forms: negative floats flip every bit, others the sign)
 __device__ __forceinline__ uint32_t ordered_f32(float f) {
-    uint32_t u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    const uint32_t u = __float_as_uint(f);
+    return u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
 }
 __device__ __forceinline__ float unordered_f32(uint32_t u) {
-    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+    return __uint_as_float(u ^ (~(uint32_t)((int32_t)u >> 31) | 0x80000000u));
 }
 
 template <int KQ>
