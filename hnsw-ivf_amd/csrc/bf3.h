@@ -154,6 +154,23 @@ __device__ __forceinline__ floatx16 bf2_block(const uint8_t* arow, const bf16x8 
     return acc;
 }
 
+__device__ __forceinline__ uint32_t cdiv_dev(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// list row of a filter key: thread slot (bi, lh) of its (query, list), tile
+// and register index from the ordinal (the 32x32 MFMA block layout)
+__device__ __forceinline__ uint32_t ivf_key_row(uint32_t key, uint32_t lowmask, int slot) {
+    const uint32_t ord = key & lowmask;
+    const uint32_t r = ord & 15u;
+    return (ord >> 4) * BV + 32 * (slot >> 1) + 4 * (slot & 1) + 8 * (r >> 2) + (r & 3);
+}
+
+// Rows of thread stream `slot` of a list of length len, enumerated as
+// e = tile * 16 + register (the filter's visiting order within the stream)
+__device__ __forceinline__ int ivf_stream_row(int e, int slot) {
+    const int r = e & 15;
+    return (e >> 4) * BV + 32 * (slot >> 1) + 4 * (slot & 1) + 8 * (r >> 2) + (r & 3);
+}
+
 // padded dim of the bf16 hi/lo images: a multiple of 32 (NS = DB/16 even)
 inline int bf3_db(int d) { return (d + 31) / 32 * 32; }
 

@@ -196,20 +196,18 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
                     : kern::coarse_bf3_plan(n, (int)ny, d, k);
     if (plan.ok) {
         kern::row_norms(x, n, d, ldx, s_xn_.as<float>(), s);
-        const size_t per_q = (size_t)plan.entries * 12 + plan.nsplit * 16;
+        const size_t per_q = (size_t)plan.entries * 4 + plan.nsplit * 16;
         const idx_t qchunk = std::max<idx_t>(64, (idx_t)(((size_t)256 << 20) / per_q) / 64 * 64);
         const idx_t qc = std::min<idx_t>(qchunk, n);
-        s_cand_i_.reserve(sizeof(unsigned long long) * qc * plan.entries);
-        s_cand_d_.reserve(sizeof(float) * qc * plan.entries);
-        s_tile_.reserve(sizeof(float) * qc * plan.nsplit * 4);
+        s_cand_i_.reserve(sizeof(uint32_t) * qc * plan.entries);  // raw filter keys
+        s_tile_.reserve(sizeof(float) * qc * plan.nsplit * 4);    // per-stream dropped bounds
         ScopedKernelTimer tm(&ktimes, "coarse_bf3", 2.0 * n * ny * d, s);
         for (idx_t q0 = 0; q0 < n; q0 += qc) {
             const idx_t nq = std::min(qc, n - q0);
             kern::coarse_bf3_knn(plan, x + q0 * ldx, nq, ldx, s_xn_.as<float>() + q0,
                                  d_xb_.as<float>(), l, d_cbf_.ptr, d_norms_.as<float>(),
                                  d_cnmax_.as<float>(), (int)ny, d, k, metric_l2,
-                                 s_cand_i_.as<unsigned long long>(), s_cand_d_.as<float>(),
-                                 s_tile_.as<float>(), distances + q0 * k,
+                                 s_cand_i_.as<uint32_t>(), s_tile_.as<float>(), distances + q0 * k,
                                  o32 ? o32 + q0 * k : nullptr, o64 ? o64 + q0 * k : nullptr, s);
         }
         return;

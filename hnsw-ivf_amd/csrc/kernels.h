@@ -46,9 +46,8 @@ struct CoarsePlan {
 CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k);
 void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, const float* xnorm,
                     const float* cent, int ldc, const void* cbf, const float* cnorm,
-                    const float* cnmax, int nlist, int d, int k, int metric_l2,
-                    unsigned long long* part, float* pub, float* pbound, float* D, int32_t* I32,
-                    int64_t* I64, hipStream_t s);
+                    const float* cnmax, int nlist, int d, int k, int metric_l2, uint32_t* keys,
+                    float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s);
 void array_max(const float* a, int64_t n, float* out, hipStream_t s);
 
 // k smallest (L2) / largest (IP) per row of D, ties by column index,

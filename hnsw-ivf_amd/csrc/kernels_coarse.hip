@@ -25,6 +25,7 @@
 #include <cfloat>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "bf3.h"
 #include "common.h"
@@ -68,14 +69,25 @@ __device__ __forceinline__ float ip_seq(const float* __restrict__ a, const float
     return acc;
 }
 
+// Pipeline as in the IVF-Flat filter (kernels_ivf_mfma.hip): one barrier per
+// 64-centroid tile, tile t+1 stashed from registers while t is computed, the
+// centroid norms (L2) / a +inf bias for rows past the split (IP) travel with
+// the tile, so the compute never waits on a same-iteration global load and
+// padding rows need no per-candidate test (their keys sort last and are
+// dropped by index in the epilogue).
+//
+// Output per (query, split, thread stream): the KT raw 32-bit keys (~0 =
+// empty) and a lower bound of every candidate the stream dropped (+inf when
+// none), after subtracting the query's largest margin M = coef (|x|^2 +
+// max|c|^2) (the re-rank uses the same M for every entry of the query).
 template <bool L2, int KT, int NS>
 __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
         const float* __restrict__ x, int ldx, int64_t n, int d, const __bf16* __restrict__ cbf,
         const float* __restrict__ cnorm, const float* __restrict__ xnorm, int nlist,
         int nsplit, int split_len, float coef, const float* __restrict__ cnmax_p, int obits,
-        unsigned long long* __restrict__ part, float* __restrict__ pub,
-        float* __restrict__ pbound) {
+        uint32_t* __restrict__ keys, float* __restrict__ pbs) {
     __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * (4 * 16 * NS + 16)];
+    __shared__ __attribute__((aligned(16))) float ynt[2][BV];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     // blocks b and b+8 share an XCD: consecutive splits of one query block
     // stay together
@@ -92,8 +104,10 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
     load_query_frags<NS>(x, ldx, d, q < n ? (int)q : -1, lh, bh, bl, xn_approx);
     const float xn = q < n ? xnorm[q] : 0.f;  // the reference-order norm (exact side)
     const float cnmax = *cnmax_p;
+    const float* cn = cnorm + c0;
 
     uint4 pf[8];
+    float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
     auto fetch = [&](int v0n) {
         const int nvn = min(BV, len - v0n);
 #pragma unroll
@@ -104,6 +118,14 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
             if (e < BV * RU && r < nvn)
                 pf[s] = *(const uint4*)(cbf + (int64_t)(c0 + v0n + r) * (2 * DB) + 8 * c);
         }
+        if (t < BV / 4) {
+            const int r = 4 * t;
+            float v[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                v[c] = r + c < nvn ? (L2 ? cn[v0n + r + c] : 0.f) : WS_INF;
+            pn = make_float4(v[0], v[1], v[2], v[3]);
+        }
     };
     auto stash = [&](int buf) {
         uint8_t* T = tiles + buf * BV * CSB;
@@ -113,6 +135,7 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
             const int r = e / RU, c = e - r * RU;
             if (e < BV * RU) *(uint4*)(T + r * CSB + 16 * c) = pf[s];
         }
+        if (t < BV / 4) *(float4*)(&ynt[buf][4 * t]) = pn;
     };
     fetch(0);
     stash(0);
@@ -122,217 +145,252 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
     ThreadQueue32<KT> tq;
     tq.init();
     const uint32_t lowmask = (1u << obits) - 1u;
-    const float* cn = cnorm + c0;
     for (int v0 = 0, tile = 0; v0 < len; v0 += BV, tile++) {
         const int buf = tile & 1;
         if (v0 + BV < len) {
             stash(buf ^ 1);
             if (v0 + 2 * BV < len) fetch(v0 + 2 * BV);
         }
-        float yv[16];
+        float4 yq[4];
 #pragma unroll
-        for (int g = 0; g < 4; g++)
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const int cr = v0 + 32 * bi + 4 * lh + 8 * g + c;
-                yv[4 * g + c] = cr < len ? cn[cr] : 0.f;
-            }
+        for (int g = 0; g < 4; g++) yq[g] = *(const float4*)(&ynt[buf][32 * bi + 4 * lh + 8 * g]);
         const floatx16 acc =
                 bf3_block<NS>(tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh, bh, bl);
         const uint32_t ordbase = (uint32_t)tile << 4;
-        const bool full = v0 + BV <= len;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
+            const int g = r >> 2, c = r & 3;
+            const float yv = c == 0 ? yq[g].x : c == 1 ? yq[g].y : c == 2 ? yq[g].z : yq[g].w;
             // L2: clamped at 0 inside key_encode, as the reference clamps
-            const float a = L2 ? fmaf(-2.f, acc[r], xn + yv[r]) : -acc[r];
-            uint32_t key = key_encode<L2>(a, lowmask, ordbase | (uint32_t)r);
-            if (!full) {
-                const int cr = v0 + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-                key = cr < len ? key : 0xffffffffu;
-            }
-            tq.push(key);
+            const float a = L2 ? fmaf(-2.f, acc[r], xn + yv) : yv - acc[r];
+            tq.push(key_encode<L2>(a, lowmask, ordbase | (uint32_t)r));
         }
         __syncthreads();
     }
-    const float bnd = tq.q[KT - 1] != 0xffffffffu ? key_decode_lo<L2>(tq.q[KT - 1], lowmask)
-                                                 : WS_INF;
     if (q < n) {
-        const int64_t e = q * nsplit + sp;
-        unsigned long long* po = part + e * (4 * KT) + slot * KT;
-        float* pu = pub + e * (4 * KT) + slot * KT;
+        const float M = coef * (xn + cnmax) + 1e-30f;
+        const int E1 = 4 * KT;
+        uint32_t* ko = keys + (q * nsplit + sp) * E1 + slot * KT;
 #pragma unroll
         for (int i = 0; i < KT; i++) {
             const uint32_t key = tq.q[i];
-            if (key != 0xffffffffu) {
-                const uint32_t ord = key & lowmask;
-                const int r = (int)(ord & 15u);
-                const uint32_t row =
-                        (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-                const float m = coef * (xn + cn[row]) + 1e-30f;
-                const float alo = key_decode_lo<L2>(key, lowmask);
-                const float ahi = key_decode_hi<L2>(key, lowmask);
-                po[i] = ((unsigned long long)ordered_f32(alo - m) << 32) | (uint32_t)(c0 + row);
-                pu[i] = ahi + m;
-            } else {
-                po[i] = ~0ull;
-                pu[i] = WS_INF;
-            }
+            const uint32_t row = ivf_key_row(key, lowmask, slot);
+            ko[i] = (key != 0xffffffffu && row < (uint32_t)len) ? key : 0xffffffffu;
         }
-        // per-thread stream bound: a failing stream is re-scanned alone
-        pbound[e * 4 + slot] = bnd < WS_INF ? bnd - (coef * (xn + cnmax) + 1e-30f) : WS_INF;
+        const uint32_t last = tq.q[KT - 1];
+        float bnd = WS_INF;
+        if (last != 0xffffffffu && ivf_key_row(last, lowmask, slot) < (uint32_t)len)
+            bnd = key_decode_lo<L2>(last, lowmask);
+        pbs[(q * nsplit + sp) * 4 + slot] = bnd < WS_INF ? bnd - M : WS_INF;
     }
 }
 
 constexpr int CR_CAP = 512;
 
+// exact coarse distance of centroid j (the fixed BLAS-form order: sequential
+// fma chain for <x, c>, then fma(-2, ip, |x|^2 + |c|^2) clamped at 0 for L2),
+// query from LDS, centroid rows L2-resident (one lane per centroid)
+template <bool L2>
+__device__ __forceinline__ float coarse_exact(const float* xs, const float* __restrict__ cent,
+                                              int ldc, const float* __restrict__ cnorm, float xn,
+                                              int d, int j) {
+    const float ip = ip_seq(xs, cent + (int64_t)j * ldc, d);
+    if (!L2) return ip;
+    const float dis = fmaf(-2.f, ip, xn + cnorm[j]);
+    return dis < 0.f ? 0.f : dis;
+}
+
 template <bool L2>
 struct CoarseStream {
-    const unsigned long long* part;  // this query's [nsplit][E1]
-    const float* xq;
+    const uint32_t* surv;  // candidate centroids (LDS)
+    const uint32_t* keys;  // this query's [nsplit * 4 * KT] raw keys
+    const float* xs;       // LDS copy of the query
     const float* cent;
     const float* cnorm;
-    float xn;
+    float xn, M, U;
     int ldc, d, nlist, nsplit, split_len, E, KT, lane, nsv;
+    uint32_t lowmask;
     bool overflow;
     unsigned long long fmask;  // failing streams: bit 4 * split + slot
-    float U;
-    const uint32_t* surv;
 
-    __device__ __forceinline__ bool survivor(int c) const {
-        if ((fmask >> (c / KT)) & 1ull) return false;  // entries of stream c / KT
-        const unsigned long long key = part[c];
-        return key != ~0ull && unordered_f32((uint32_t)(key >> 32)) <= U;
-    }
-    __device__ __forceinline__ void eval(int j, float& k1, long long& k2, long long& rank) const {
-        const float ip = ip_seq(xq, cent + (int64_t)j * ldc, d);
-        float dis;
-        if (L2) {
-            dis = fmaf(-2.f, ip, xn + cnorm[j]);
-            dis = dis < 0.f ? 0.f : dis;
-        } else {
-            dis = ip;
-        }
-        to_key(L2 ? 1 : 0, dis, (long long)j, k1, k2);
-        rank = j;
+    __device__ __forceinline__ void emit(bool ok, int j, float& k1, long long& k2) const {
+        k1 = WS_INF;
+        k2 = WS_NOID;
+        if (ok) to_key(L2 ? 1 : 0, coarse_exact<L2>(xs, cent, ldc, cnorm, xn, d, j), j, k1, k2);
     }
     template <class F>
     __device__ __forceinline__ void for_each(F f) const {
         if (!overflow) {
             for (int s0 = 0; s0 < nsv; s0 += 64) {
-                float k1 = WS_INF;
-                long long k2 = WS_NOID, rank = 0;
-                bool ok = s0 + lane < nsv;
-                if (ok) {
-                    eval((int)surv[s0 + lane], k1, k2, rank);
-                    ok = key_admissible(k1);
-                }
-                f(ok, k1, k2, rank);
+                const bool ok = s0 + lane < nsv;
+                const int j = ok ? (int)surv[s0 + lane] : 0;
+                float k1;
+                long long k2;
+                emit(ok, j, k1, k2);
+                f(ok && key_admissible(k1), k1, k2, (long long)j);
             }
-        } else {
-            for (int c0 = 0; c0 < E; c0 += 64) {
-                const int c = c0 + lane;
-                float k1 = WS_INF;
-                long long k2 = WS_NOID, rank = 0;
-                bool ok = c < E && survivor(c);
-                if (__ballot(ok) == 0ull) continue;
-                if (ok) {
-                    eval((int)(uint32_t)part[c], k1, k2, rank);
-                    ok = key_admissible(k1);
-                }
-                f(ok, k1, k2, rank);
-            }
+            return;
         }
-        // failing streams: thread slot (bi, lh) of split s saw, per 64-row
-        // tile, rows 32 bi + 4 lh + 8 g + c (g, c < 4)
+        for (int c0 = 0; c0 < E; c0 += 64) {
+            const int c = c0 + lane;
+            const int st = c < E ? c / KT : 0;  // stream 4 * split + slot
+            bool ok = false;
+            int j = 0;
+            if (c < E && !((fmask >> st) & 1ull)) {
+                const uint32_t key = keys[c];
+                ok = key != 0xffffffffu && key_decode_lo<L2>(key, lowmask) - M <= U;
+                j = (st >> 2) * split_len + (int)ivf_key_row(key, lowmask, st & 3);
+            }
+            if (__ballot(ok) == 0ull) continue;
+            float k1;
+            long long k2;
+            emit(ok, j, k1, k2);
+            f(ok && key_admissible(k1), k1, k2, (long long)j);
+        }
         unsigned long long m = fmask;
         while (m) {
             const int sidx = __ffsll((long long)m) - 1;
             m &= m - 1ull;
-            const int s = sidx >> 2, slot = sidx & 3, bi = slot >> 1, lh = slot & 1;
-            const int j0 = s * split_len, j1 = min(nlist, j0 + split_len);
-            const int ntile = (j1 - j0 + BV - 1) / BV;
-            for (int t0 = 0; t0 < ntile * 16; t0 += 64) {
-                const int e = t0 + lane;  // tile e >> 4, register e & 15
-                const int r = e & 15;
-                const int j = j0 + (e >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-                float k1 = WS_INF;
-                long long k2 = WS_NOID, rank = 0;
-                bool ok = e < ntile * 16 && j < j1;
-                if (ok) {
-                    eval(j, k1, k2, rank);
-                    ok = key_admissible(k1);
-                }
-                f(ok, k1, k2, rank);
+            const int sp = sidx >> 2, slot = sidx & 3;
+            const int j0 = sp * split_len, j1 = min(nlist, j0 + split_len);
+            const int ne = (int)cdiv_dev((uint32_t)(j1 - j0), BV) * 16;
+            for (int e0 = 0; e0 < ne; e0 += 64) {
+                const int j = j0 + ivf_stream_row(e0 + lane, slot);
+                const bool ok = e0 + lane < ne && j < j1;
+                float k1;
+                long long k2;
+                emit(ok, j, k1, k2);
+                f(ok && key_admissible(k1), k1, k2, (long long)j);
             }
         }
     }
 };
 
+// One wave per query (block = one wave).  Same structure as k_ivf_rerank:
+// round trip 1 = the raw keys (V consecutive per lane, one stream per lane),
+// the streams' dropped bounds and the query; U = k-th smallest ub' = approx_hi
+// + M; candidates = entries with approx_lo - M <= U of the streams that did
+// not fail, plus every centroid of the failing streams; exact evaluation and a
+// rank-based top-k (exact_topk_resolve when a tie crosses the boundary).
 template <bool L2, class OutIdx, int V>
-__global__ __launch_bounds__(256) void k_coarse_rerank(
-        const unsigned long long* __restrict__ part, const float* __restrict__ pub,
-        const float* __restrict__ pbound, const float* __restrict__ x, int ldx,
-        const float* __restrict__ xnorm, const float* __restrict__ cent, int ldc,
-        const float* __restrict__ cnorm, int64_t n, int d, int nlist, int nsplit, int split_len,
-        int E1, int k, float* __restrict__ D, OutIdx* __restrict__ I,
+__global__ __launch_bounds__(64, 4) void k_coarse_rerank(
+        const uint32_t* __restrict__ keys, const float* __restrict__ pbs,
+        const float* __restrict__ x, int ldx, const float* __restrict__ xnorm,
+        const float* __restrict__ cent, int ldc, const float* __restrict__ cnorm,
+        const float* __restrict__ cnmax_p, float coef, int64_t n, int d, int nlist, int nsplit,
+        int split_len, int KT, int obits, int k, float* __restrict__ D, OutIdx* __restrict__ I,
         uint32_t* __restrict__ stats) {
-    __shared__ uint32_t surv[4][CR_CAP];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t q0 = (int64_t)blockIdx.x * 4 + w;
+    __shared__ uint32_t surv[CR_CAP];
+    __shared__ __attribute__((aligned(16))) float xsh[BDM];
+    const int lane = threadIdx.x;
+    const int64_t q0 = blockIdx.x;
     const bool valid = q0 < n;
     const int64_t q = valid ? q0 : 0;
+    const int E1 = 4 * KT, E = valid ? nsplit * E1 : 0, NST = 4 * nsplit;
+    const uint32_t lowmask = (1u << obits) - 1u;
+    // ---- round trip 1
+    const uint32_t* kq = keys + q * (int64_t)nsplit * E1;
+    uint32_t kv[V];
+    const bool has = lane * V < E;
+#pragma unroll
+    for (int i = 0; i < V; i++) kv[i] = has ? kq[lane * V + i] : 0xffffffffu;
+    const float my_pb = (valid && lane < NST) ? pbs[q * NST + lane] : WS_INF;
+    const float xn = xnorm ? xnorm[q] : 0.f;
+    const float* xq = x + q * ldx;
+    if (lane < BDM / 4 && 4 * lane < ((d + 3) & ~3))
+        *(float4*)(&xsh[4 * lane]) = *(const float4*)(xq + 4 * lane);
+    const float M = coef * (xn + *cnmax_p) + 1e-30f;
+    // ---- U
+    float ub[V];
+#pragma unroll
+    for (int i = 0; i < V; i++)
+        ub[i] = kv[i] != 0xffffffffu ? key_decode_hi<L2>(kv[i], lowmask) + M : WS_INF;
+    float U = wave_kth_smallest<V>(ub, k);
+    if (!(U <= WS_INF)) U = WS_INF;
+    const unsigned long long fmask = __ballot(my_pb < WS_INF && my_pb <= U);
+    const int lst = has ? lane * V / KT : 0;  // this lane's stream (V <= KT)
+    const bool lfail = (fmask >> lst) & 1ull;
+    // ---- candidates -> LDS
+    int ns = 0;
+#pragma unroll
+    for (int i = 0; i < V; i++) {
+        bool sv = false;
+        uint32_t j = 0;
+        if (kv[i] != 0xffffffffu && !lfail) {
+            sv = key_decode_lo<L2>(kv[i], lowmask) - M <= U;
+            j = (uint32_t)((lst >> 2) * split_len) + ivf_key_row(kv[i], lowmask, lst & 3);
+        }
+        const unsigned long long m = __ballot(sv);
+        const int pos = ns + __popcll(m & ((1ull << lane) - 1ull));
+        if (sv && pos < CR_CAP) surv[pos] = j;
+        ns += __popcll(m);
+    }
+    {
+        unsigned long long m = fmask;
+        while (m) {
+            const int sidx = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const int sp = sidx >> 2, slot = sidx & 3;
+            const int j0 = sp * split_len, j1 = min(nlist, j0 + split_len);
+            const int ne = (int)cdiv_dev((uint32_t)(j1 - j0), BV) * 16;
+            for (int e0 = 0; e0 < ne; e0 += 64) {
+                const int j = j0 + ivf_stream_row(e0 + lane, slot);
+                const bool in = e0 + lane < ne && j < j1;
+                const unsigned long long bm = __ballot(in);
+                const int pos = ns + __popcll(bm & ((1ull << lane) - 1ull));
+                if (in && pos < CR_CAP) surv[pos] = (uint32_t)j;
+                ns += __popcll(bm);
+            }
+        }
+    }
+    __syncthreads();  // one wave per block: the LDS query and candidate list
     CoarseStream<L2> st;
-    st.E = nsplit * E1;
-    st.part = part + q * st.E;
-    st.xq = x + q * ldx;
+    st.surv = surv;
+    st.keys = kq;
+    st.xs = xsh;
     st.cent = cent;
     st.cnorm = cnorm;
-    st.xn = xnorm ? xnorm[q] : 0.f;
+    st.xn = xn;
+    st.M = M;
+    st.U = U;
     st.ldc = ldc;
     st.d = d;
     st.nlist = nlist;
     st.nsplit = nsplit;
     st.split_len = split_len;
-    st.KT = E1 / 4;
+    st.E = E;
+    st.KT = KT;
     st.lane = lane;
-    st.fmask = 0u;
-    st.U = WS_INF;
-    const int total = valid ? st.E : 0;
-    const float* pu = pub + q * st.E;
-    float ub[V];
-#pragma unroll
-    for (int i = 0; i < V; i++) {
-        const int c = i * 64 + lane;
-        ub[i] = c < total ? pu[c] : WS_INF;
-    }
-    float U = wave_kth_smallest<V>(ub, k);
-    if (!(U <= WS_INF)) U = WS_INF;
-    st.U = U;
-    {
-        bool fl = false;
-        if (valid && lane < 4 * nsplit) {
-            const float pb = pbound[q * 4 * nsplit + lane];
-            fl = pb < WS_INF && pb <= U;
-        }
-        st.fmask = __ballot(fl);
-    }
-    int ns = 0;
-    for (int c0 = 0; c0 < total; c0 += 64) {
-        const int c = c0 + lane;
-        const bool sv = c < total && st.survivor(c);
-        const unsigned long long m = __ballot(sv);
-        const int pos = ns + __popcll(m & ((1ull << lane) - 1ull));
-        if (sv && pos < CR_CAP) surv[w][pos] = (uint32_t)st.part[c];  // centroid id
-        ns += __popcll(m);
-    }
-    st.overflow = ns > CR_CAP;
     st.nsv = ns;
-    st.surv = surv[w];
-    exact_topk_resolve(st, k, L2 ? 1 : 0, lane, valid, D + q * k, I + q * k);
+    st.lowmask = lowmask;
+    st.overflow = ns > CR_CAP;
+    st.fmask = fmask;
+    bool done = false;
+    auto small = [&](auto nbc) {
+        constexpr int NB = decltype(nbc)::value;
+        float k1[NB];
+        long long k2[NB];
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const bool ok = 64 * b + lane < ns;
+            st.emit(ok, ok ? (int)surv[64 * b + lane] : 0, k1[b], k2[b]);
+            if (!(ok && key_admissible(k1[b]))) {
+                k1[b] = WS_INF;
+                k2[b] = WS_NOID;
+            }
+        }
+        return exact_topk_small<NB, OutIdx>(k1, k2, ns, k, L2 ? 1 : 0, lane, valid, D + q * k,
+                                            I + q * k);
+    };
+    if (ns <= 64) done = small(std::integral_constant<int, 1>());
+    else if (ns <= 128) done = small(std::integral_constant<int, 2>());
+    else if (ns <= 256) done = small(std::integral_constant<int, 4>());
+    if (!done) exact_topk_resolve(st, k, L2 ? 1 : 0, lane, valid, D + q * k, I + q * k);
     if (stats && valid && lane == 0) {
         atomicAdd(&stats[0], (uint32_t)min(ns, CR_CAP));
-        atomicAdd(&stats[1], (uint32_t)__popcll(st.fmask));
+        atomicAdd(&stats[1], (uint32_t)__popcll(fmask));
         atomicAdd(&stats[2], st.overflow ? 1u : 0u);
+        atomicAdd(&stats[3], done ? 0u : 1u);
     }
 }
 
@@ -356,11 +414,17 @@ CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k) {
     CoarsePlan p{};
     if (n < 20 || nlist <= 0 || k < 1 || k > kMaxK || bf3_db(d) > BDM)
         return p;
-    int nsplit = nlist >= 2048 ? 4 : nlist >= 1024 ? 2 : 1;
-    const int per = (int)cdiv((size_t)k, (size_t)(4 * nsplit));
-    if (per > 4) return p;
-    int kt = 4;
-    while (kt < 4 * per) kt <<= 1;
+    // splits of >= 512 centroids: enough work items to fill the chip, at most
+    // 16 (the re-rank keeps one thread stream per lane)
+    // Each of the 4 * nsplit thread streams keeps KT keys; it "fails" (is
+    // re-scanned exactly) when more than KT of the top-k + margin fall in it.
+    // With lam = k / (4 nsplit) expected members per stream, KT = 4 / 8 / 16
+    // for lam <= 1/4 / 2 / 4 keeps the Poisson tail below ~1e-3 per query.
+    int nsplit = std::max(1, std::min(16, nlist / 512));
+    while (nsplit > 1 && k > 16 * nsplit) nsplit >>= 1;
+    const double lam = (double)k / (4.0 * nsplit);
+    if (lam > 4.0) return p;
+    const int kt = lam <= 0.25 ? 4 : lam <= 2.0 ? 8 : 16;
     const int split_len = (int)roundup(cdiv((size_t)nlist, (size_t)nsplit), BV);
     nsplit = (int)cdiv((size_t)nlist, (size_t)split_len);
     const int tiles = (int)cdiv((size_t)split_len, BV);
@@ -378,9 +442,8 @@ CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k) {
 
 void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, const float* xnorm,
                     const float* cent, int ldc, const void* cbf, const float* cnorm,
-                    const float* cnmax, int nlist, int d, int k, int metric_l2,
-                    unsigned long long* part, float* pub, float* pbound, float* D, int32_t* I32,
-                    int64_t* I64, hipStream_t s) {
+                    const float* cnmax, int nlist, int d, int k, int metric_l2, uint32_t* keys,
+                    float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(p.ok);
     static uint32_t* stats = nullptr;  // FAISS_AMD_IVF_STATS debug counters
@@ -396,7 +459,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
 #define LAUNCH_NS(L2V, KTV, NSV)                                                              \
     k_coarse_bf3_filter<L2V, KTV, NSV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(            \
             x, ldx, n, d, (const __bf16*)cbf, cnorm, xnorm, nlist, p.nsplit, p.split_len,     \
-            coef, cnmax, p.obits, part, pub, pbound)
+            coef, cnmax, p.obits, keys, pbs)
 #define LAUNCH_A(L2V, KTV)                     \
     do {                                       \
         if (NS == 2) LAUNCH_NS(L2V, KTV, 2);   \
@@ -416,18 +479,17 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
 #undef LAUNCH_A
 #undef LAUNCH_NS
     HIP_LAUNCH_CHECK();
-    const dim3 g2((unsigned)cdiv((size_t)n, 4)), b2(256);
-    const int E1 = 4 * p.kt;
-    const int E = p.nsplit * E1;
-    const int V = E <= 128 ? 2 : E <= 256 ? 4 : E <= 512 ? 8 : 16;
-    FAISS_THROW_IF_NOT(E <= 1024);
+    const int E = p.entries;
+    const int V = E <= 64 ? 1 : E <= 128 ? 2 : E <= 256 ? 4 : E <= 512 ? 8 : 16;
+    FAISS_THROW_IF_NOT(E <= 1024 && V <= p.kt);
 #define LAUNCH_R(L2V, OT, OUT, VV)                                                              \
-    k_coarse_rerank<L2V, OT, VV><<<g2, b2, 0, s>>>(part, pub, pbound, x, ldx, xnorm, cent, ldc, \
-                                                   cnorm, n, d, nlist, p.nsplit, p.split_len,   \
-                                                   E1, k, D, OUT, st_ptr)
+    k_coarse_rerank<L2V, OT, VV><<<dim3((unsigned)n), dim3(64), 0, s>>>(                       \
+            keys, pbs, x, ldx, xnorm, cent, ldc, cnorm, cnmax, coef, n, d, nlist, p.nsplit,     \
+            p.split_len, p.kt, p.obits, k, D, OUT, st_ptr)
 #define LAUNCH_RV(L2V, OT, OUT)                  \
     do {                                         \
-        if (V == 2) LAUNCH_R(L2V, OT, OUT, 2);   \
+        if (V == 1) LAUNCH_R(L2V, OT, OUT, 1);   \
+        else if (V == 2) LAUNCH_R(L2V, OT, OUT, 2); \
         else if (V == 4) LAUNCH_R(L2V, OT, OUT, 4); \
         else if (V == 8) LAUNCH_R(L2V, OT, OUT, 8); \
         else LAUNCH_R(L2V, OT, OUT, 16);         \
@@ -447,7 +509,8 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
         HIP_CHECK(hipMemcpyAsync(h, stats, 16, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
         fprintf(stderr, "[faiss_amd] coarse bf3: nq=%lld k=%d survivors/q=%.2f failing streams/q=%.4f "
-                "overflow=%u\n", (long long)n, k, h[0] / (double)n, h[1] / (double)n, h[2]);
+                "overflow=%u general-resolve=%u\n", (long long)n, k, h[0] / (double)n,
+                h[1] / (double)n, h[2], h[3]);
     }
     HIP_LAUNCH_CHECK();
 }

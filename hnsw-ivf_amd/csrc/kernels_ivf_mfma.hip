@@ -300,16 +300,6 @@ constexpr int RR_W = 1;  // waves (queries) per block: one, for fine-grained pac
 // (the re-rank's barriers sit in wave-uniform branches: one wave per block)
 static_assert(RR_W == 1, "k_ivf_rerank assumes one wave per block");
 
-__device__ __forceinline__ uint32_t cdiv_dev(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
-
-// list row of a filter key: thread slot (bi, lh) of its (query, list), tile
-// and register index from the ordinal (the 32x32 MFMA block layout)
-__device__ __forceinline__ uint32_t ivf_key_row(uint32_t key, uint32_t lowmask, int slot) {
-    const uint32_t ord = key & lowmask;
-    const uint32_t r = ord & 15u;
-    return (ord >> 4) * BV + 32 * (slot >> 1) + 4 * (slot & 1) + 8 * (r >> 2) + (r & 3);
-}
-
 // exact reference-order distance of the row `grow` each lane names (valid
 // lanes only); 16 rows per pass, 4 lanes per row: lane j' of a row owns the
 // reference's partial sums c[2j'] and c[2j'+1] (dims 8m + 2j' + {0,1}), so a
@@ -388,13 +378,6 @@ __device__ __forceinline__ float eval_rows64(const float* xr /* LDS copy of the 
         __syncthreads();  // the next pass overwrites the staging rows
     }
     return out;
-}
-
-// Rows of thread stream `slot` of a list of length len, enumerated as
-// e = tile * 16 + register (the filter's visiting order within the stream)
-__device__ __forceinline__ int ivf_stream_row(int e, int slot) {
-    const int r = e & 15;
-    return (e >> 4) * BV + 32 * (slot >> 1) + 4 * (slot & 1) + 8 * (r >> 2) + (r & 3);
 }
 
 template <bool L2>
