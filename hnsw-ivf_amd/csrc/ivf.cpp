@@ -485,8 +485,14 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
         b.mark_keys = s_part_.as<uint32_t>();
         b.mark_recs = s_pk2_.as<kern::ProbeRec>();
         b.mark_ke = KQ;
+        const int64_t mi = kern::ivf_max_items(n, np, (int)nlist, QT);
+        s_idesc_.reserve(sizeof(kern::ItemDesc) * mi);
+        s_ient_.reserve(sizeof(uint32_t) * mi * QT);
+        b.item_desc = s_idesc_.as<kern::ItemDesc>();
+        b.item_entries = s_ient_.as<uint32_t>();
     }
-    kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), (int)nlist, QT, b, s);
+    kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), d_list_off_.as<uint32_t>(),
+                     (int)nlist, QT, b, s);
     const int64_t max_items = kern::ivf_max_items(n, np, (int)nlist, QT);
     const bool l2 = metric_type == METRIC_L2;
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(n, 4));

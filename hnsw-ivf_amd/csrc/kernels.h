@@ -85,12 +85,24 @@ struct alignas(16) ProbeRec {
     uint32_t pad;
 };
 
+// work item of the list-centric IVF scans: list, queries in the item, list
+// length and arena offset
+struct alignas(16) ItemDesc {
+    uint32_t l, nq, len, off;
+};
+
 struct IVFBuckets {
     uint32_t* counts;      // [nlist]
     uint32_t* bucket_off;  // [nlist + 1]
     uint32_t* item_off;    // [nlist + 1]
     uint32_t* cursor;      // [n * nprobe]: slot of each entry in its bucket
     uint32_t* entries;     // [n * nprobe], entry = q * nprobe + rank
+    uint32_t* item_list = nullptr;  // [max_items]: list of each work item
+    // optional (MFMA filter path): per work item its descriptor and its
+    // entries at a fixed stride of QT (so a work item's first loads do not
+    // depend on each other)
+    ItemDesc* item_desc = nullptr;         // [max_items]
+    uint32_t* item_entries = nullptr;      // [max_items * QT]
     // optional (MFMA filter path): entries whose list is invalid or empty get
     // empty partials (part ~0, pub / pbound +inf), so the re-rank reads every
     // entry without consulting the assignment
@@ -99,7 +111,7 @@ struct IVFBuckets {
     int mark_ke = 0;
 };
 void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
-                int nlist, int QT, IVFBuckets b, hipStream_t s);
+                const uint32_t* list_off, int nlist, int QT, IVFBuckets b, hipStream_t s);
 // IndexIVFStats counters of a batch (faiss/IndexIVF.cpp:1184-1198):
 // stats[0] += non-empty lists visited, stats[1] += codes scanned (device)
 void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_len, int nlist,

@@ -37,12 +37,54 @@ __global__ void k_bucket_count(const int32_t* __restrict__ assign, int64_t total
     if (l >= 0 && l < nlist && list_len[l] > 0) pos[e] = atomicAdd(&counts[l], 1u);
 }
 
+// Same with a block-local LDS histogram (nlist <= BC_MAXL): BC_PER entries
+// per thread take their slot from an LDS atomic, then one global atomic per
+// non-empty bin reserves the block's range of each bucket.
+constexpr int BC_PER = 16;
+constexpr int BC_MAXL = 16384;
+__global__ __launch_bounds__(1024) void k_bucket_count_lds(const int32_t* __restrict__ assign,
+                                                           int64_t total,
+                                                           const uint32_t* __restrict__ list_len,
+                                                           int nlist, uint32_t* __restrict__ counts,
+                                                           uint32_t* __restrict__ pos) {
+    extern __shared__ uint32_t hist[];  // [nlist]
+    const int t = threadIdx.x;
+    for (int i = t; i < nlist; i += 1024) hist[i] = 0u;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * 1024 * BC_PER;
+    int ll[BC_PER];
+    uint32_t lp[BC_PER];
+#pragma unroll
+    for (int j = 0; j < BC_PER; j++) {
+        const int64_t e = base + (int64_t)j * 1024 + t;
+        int l = -1;
+        if (e < total) {
+            l = assign[e];
+            if (!(l >= 0 && l < nlist && list_len[l] > 0)) l = -1;
+        }
+        ll[j] = l;
+        lp[j] = l >= 0 ? atomicAdd(&hist[l], 1u) : 0u;
+    }
+    __syncthreads();
+    for (int i = t; i < nlist; i += 1024) {
+        const uint32_t c = hist[i];
+        if (c) hist[i] = atomicAdd(&counts[i], c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < BC_PER; j++) {
+        const int64_t e = base + (int64_t)j * 1024 + t;
+        if (ll[j] >= 0) pos[e] = hist[ll[j]] + lp[j];
+    }
+}
+
 // single-workgroup exclusive scan of counts -> bucket_off, ceil(counts/QT)
-// -> item_off
+// -> item_off; per work item its list when asked
 __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict__ counts,
                                                       int nlist, int QT,
                                                       uint32_t* __restrict__ bucket_off,
-                                                      uint32_t* __restrict__ item_off) {
+                                                      uint32_t* __restrict__ item_off,
+                                                      uint32_t* __restrict__ item_list) {
     __shared__ uint32_t sb[1024], si[1024];
     const int t = threadIdx.x;
     const int per = (nlist + 1023) / 1024;
@@ -70,8 +112,11 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
         bucket_off[l] = rb;
         item_off[l] = ri;
         uint32_t c = counts[l];
+        const uint32_t ni = (c + QT - 1) / QT;
+        if (item_list)
+            for (uint32_t i = 0; i < ni; i++) item_list[ri + i] = (uint32_t)l;  // item -> list
         rb += c;
-        ri += (c + QT - 1) / QT;
+        ri += ni;
     }
     if (t == 1023) {
         bucket_off[nlist] = sb[1023];
@@ -80,16 +125,34 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
 }
 
 __global__ void k_bucket_fill(const int32_t* __restrict__ assign, int64_t total,
-                              const uint32_t* __restrict__ list_len, int nlist,
+                              const uint32_t* __restrict__ list_len, int nlist, int QT,
                               const uint32_t* __restrict__ bucket_off,
+                              const uint32_t* __restrict__ item_off,
                               const uint32_t* __restrict__ pos, uint32_t* __restrict__ entries,
+                              uint32_t* __restrict__ item_entries, ItemDesc* __restrict__ item_desc,
+                              const uint32_t* __restrict__ counts,
+                              const uint32_t* __restrict__ list_off,
                               uint32_t* __restrict__ mkeys, ProbeRec* __restrict__ mrecs,
                               int ke) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
     int l = assign[e];
     if (l >= 0 && l < nlist && list_len[l] > 0) {
-        entries[bucket_off[l] + pos[e]] = (uint32_t)e;
+        const uint32_t p = pos[e];
+        if (item_entries) {
+            const uint32_t item = item_off[l] + p / QT;
+            item_entries[item * QT + p % QT] = (uint32_t)e;
+            if (p % QT == 0) {  // the item's first entry writes its descriptor
+                ItemDesc dsc;
+                dsc.l = (uint32_t)l;
+                dsc.nq = min((uint32_t)QT, counts[l] - p);
+                dsc.len = list_len[l];
+                dsc.off = list_off[l];
+                item_desc[item] = dsc;
+            }
+        } else {
+            entries[bucket_off[l] + p] = (uint32_t)e;
+        }
     } else if (mkeys) {
         for (int i = 0; i < ke; i++) mkeys[e * ke + i] = 0xffffffffu;
         ProbeRec pr;
@@ -130,21 +193,28 @@ void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_
 }
 
 void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
-                int nlist, int QT, IVFBuckets b, hipStream_t s) {
+                const uint32_t* list_off, int nlist, int QT, IVFBuckets b, hipStream_t s) {
     int64_t total = n * nprobe;
     FAISS_THROW_IF_NOT_MSG(total < (1ll << 32), "n * nprobe must fit in 32 bits");
     HIP_CHECK(hipMemsetAsync(b.counts, 0, sizeof(uint32_t) * nlist, s));
     if (total > 0) {
-        k_bucket_count<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
-                assign, total, list_len, nlist, b.counts, b.cursor);
+        if (nlist <= BC_MAXL)
+            k_bucket_count_lds<<<dim3((unsigned)cdiv(total, 1024 * BC_PER)), dim3(1024),
+                                 sizeof(uint32_t) * nlist, s>>>(assign, total, list_len, nlist,
+                                                                b.counts, b.cursor);
+        else
+            k_bucket_count<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
+                    assign, total, list_len, nlist, b.counts, b.cursor);
         HIP_LAUNCH_CHECK();
     }
-    k_bucket_scan<<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off, b.item_off);
+    k_bucket_scan<<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off, b.item_off,
+                                                 b.item_list);
     HIP_LAUNCH_CHECK();
     if (total > 0) {
         k_bucket_fill<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
-                assign, total, list_len, nlist, b.bucket_off, b.cursor, b.entries, b.mark_keys,
-                b.mark_recs, b.mark_ke);
+                assign, total, list_len, nlist, QT, b.bucket_off, b.item_off, b.cursor, b.entries,
+                b.item_entries, b.item_desc, b.counts, list_off, b.mark_keys, b.mark_recs,
+                b.mark_ke);
         HIP_LAUNCH_CHECK();
     }
 }

@@ -103,8 +103,11 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         const float* __restrict__ rres, const float* __restrict__ rmax,
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
         int nprobe, float coef, int obits, const uint32_t* __restrict__ bucket_off,
-        const uint32_t* __restrict__ item_off, const uint32_t* __restrict__ entries,
-        uint32_t* __restrict__ keys, ProbeRec* __restrict__ recs) {
+        const uint32_t* __restrict__ item_off, const ItemDesc* __restrict__ item_desc,
+        const uint32_t* __restrict__ item_entries, uint32_t max_items,
+        uint32_t* __restrict__ keys, ProbeRec* __restrict__ recs,
+        unsigned long long* __restrict__ ftrace) {
+    const unsigned long long ft0 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     // two code tiles (double buffer), row stride CSB bytes = (Y3 ? 4 : 2) * DB + 16
     __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * ((Y3 ? 4 : 2) * 16 * NS + 16)];
     __shared__ __attribute__((aligned(16))) float ynt[2][BV];  // row norm (L2) / bias (IP)
@@ -115,22 +118,22 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t xcd = blockIdx.x & 7u, rest = blockIdx.x >> 3;
     const uint32_t item = 4u * ((rest >> 2) * 8u + xcd) + (rest & 3u);
-    if (item >= item_off[nlist]) return;
-    int lo = 0, hi = nlist;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (item_off[mid] <= item) lo = mid; else hi = mid;
-    }
-    const int l = lo;
-    const uint32_t qb = bucket_off[l] + (item - item_off[l]) * BQ;
-    const int nQ = (int)min((uint32_t)BQ, bucket_off[l + 1] - qb);
+    // one round trip: the item count, the item's descriptor and its entries
+    // (fixed stride BQ) are independent loads
+    const uint32_t nitems = item_off[nlist];
+    const uint32_t it = item < max_items ? item : 0u;
+    const ItemDesc dsc = item_desc[it];
+    const uint32_t e_raw = t < BQ ? item_entries[(size_t)it * BQ + t] : 0u;
+    if (item >= nitems) return;
+    const int l = (int)dsc.l;
+    const int nQ = (int)dsc.nq;
     if (t < BQ) {
-        const uint32_t e = t < nQ ? entries[qb + t] : 0u;
+        const uint32_t e = t < nQ ? e_raw : 0u;
         ent_s[t] = e;
         qrow_s[t] = t < nQ ? (int32_t)(e / (uint32_t)nprobe) : -1;
     }
-    const int len = (int)list_len[l];
-    const int64_t row0 = list_off[l];
+    const int len = (int)dsc.len;
+    const int64_t row0 = dsc.off;
     constexpr int DB = 16 * NS;
     constexpr int CSB = (Y3 ? 4 : 2) * DB + 16;  // LDS row stride (bytes)
     constexpr int RU = (Y3 ? DB / 4 : DB / 8);   // uint4 staged per code row
@@ -141,12 +144,6 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     const int qloc = 32 * bj + li;   // this thread's query (0..63)
     const bool active = 32 * bj < nQ;  // wave-uniform
     const float* ynl = ynorm + row0;
-    __syncthreads();
-
-    // ---- query fragments (B operand): registers for the whole work item
-    bf16x8 bh[NS], bl[NS];
-    float xn = 0.f;
-    if (active) load_query_frags<NS>(x, ldx, d, qrow_s[qloc], lh, bh, bl, xn);
 
     // ---- code tiles: global -> registers -> LDS (+ the tile's row norms)
     uint4 pf[PF];
@@ -182,10 +179,21 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         }
         if (t < BV / 4) *(float4*)(&ynt[buf][4 * t]) = pn;
     };
+    // the first tile's loads go out before the query fragments' (which wait
+    // on the entries -> query rows chain)
     fetch(0);
+    __syncthreads();
+
+    const unsigned long long fta = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    // ---- query fragments (B operand): registers for the whole work item
+    bf16x8 bh[NS], bl[NS];
+    float xn = 0.f;
+    if (active) load_query_frags<NS>(x, ldx, d, qrow_s[qloc], lh, bh, bl, xn);
+    const unsigned long long ftb = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     stash(0);
     if (BV < len) fetch(BV);
     __syncthreads();
+    const unsigned long long ft1 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
 
     ThreadQueue32<KT> tq;
     tq.init();
@@ -219,6 +227,7 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     }
 
     // ---- outputs
+    const unsigned long long ft2 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const bool qvalid = qloc < nQ;
     const uint32_t last = tq.q[KT - 1];
     float bnd = WS_INF;  // lower bound of every dropped candidate (none: +inf)
@@ -262,6 +271,15 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             pr.pad = 0u;
             recs[e] = pr;
         }
+    }
+    if (ftrace && t == 0) {
+        ftrace[8 * item + 0] = ft0;
+        ftrace[8 * item + 1] = ft1;
+        ftrace[8 * item + 2] = ft2;
+        ftrace[8 * item + 3] = __builtin_amdgcn_s_memrealtime();
+        ftrace[8 * item + 4] = fta;
+        ftrace[8 * item + 5] = ftb;
+        ftrace[8 * item + 6] = (unsigned long long)len | ((unsigned long long)nQ << 32);
     }
 }
 
@@ -833,6 +851,20 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     // decode (low bits cleared / set).
     const char* prec = getenv("FAISS_AMD_IVF_PREC");
     const bool y3 = prec && !strcmp(prec, "bf16x3");
+    // FAISS_AMD_FILTER_TRACE=<file>: per-work-item timestamps (profiling)
+    static unsigned long long* ftrace_buf = nullptr;
+    static int64_t ftrace_n = 0;
+    const char* ftr = getenv("FAISS_AMD_FILTER_TRACE");
+    unsigned long long* ftrace = nullptr;
+    if (ftr) {
+        if (ftrace_n < grid) {
+            if (ftrace_buf) HIP_CHECK(hipFree(ftrace_buf));
+            HIP_CHECK(hipMalloc(&ftrace_buf, 64 * grid));
+            ftrace_n = grid;
+        }
+        HIP_CHECK(hipMemsetAsync(ftrace_buf, 0, 64 * grid, s));
+        ftrace = ftrace_buf;
+    }
     const float coef = (float)(y3 ? ivf_bf3_coef(d) : ivf_bf2_coef(d));
     {
         ScopedKernelTimer tm(kt, "ivf_flat_scan", 0.0, s);
@@ -842,12 +874,12 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
             k_ivf_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
-                    b.entries, keys, recs);                                                   \
+                    b.item_desc, b.item_entries, (uint32_t)max_items, keys, recs, ftrace);    \
         else                                                                                  \
             k_ivf_bf3_filter<L2V, KTV, NSV, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(\
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
-                    b.entries, keys, recs);                                                   \
+                    b.item_desc, b.item_entries, (uint32_t)max_items, keys, recs, ftrace);    \
     } while (0)
 #define LAUNCH_A(L2V, KTV)                     \
     do {                                       \
@@ -865,6 +897,15 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         if (l2) DISPATCH(LAUNCH_A, true);
         else DISPATCH(LAUNCH_A, false);
         HIP_LAUNCH_CHECK();
+        if (ftrace) {
+            std::vector<unsigned long long> h(8 * grid);
+            HIP_CHECK(hipMemcpyAsync(h.data(), ftrace, 64 * grid, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            if (FILE* f = fopen(ftr, "wb")) {
+                fwrite(h.data(), 64, grid, f);
+                fclose(f);
+            }
+        }
     }
     {
         ScopedKernelTimer tm(kt, "ivf_rerank", 0.0, s);

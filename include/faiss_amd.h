@@ -296,7 +296,7 @@ struct IndexIVF : Index {
     // scratch
     mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_counts_, s_boff_, s_ioff_, s_cur_, s_ent_,
             s_pk1_, s_pk2_, s_q_;
-    mutable DeviceBuffer s_as_, s_ad_, s_stats_;
+    mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_;
 
    private:
     idx_t search_chunk(idx_t n, size_t np, idx_t k) const;
