@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"
@@ -124,6 +125,195 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan(
     }
 }
 
+// ---------------------------------------------------------------- scan v2
+// One workgroup (4 waves) per query, LUT T[m][j] (M x 256 f32) in LDS; the
+// per-code work is M LDS gathers + adds (LDS-gather bound).  M is a template
+// parameter (fully unrolled, codes read as 16-B words).  Selection: each wave
+// keeps a 64-slot sorted queue; a code whose distance is <= the queue's k-th
+// is appended to a per-wave LDS buffer (ballot compaction) and the buffer is
+// folded into the queue 64 at a time, so the sorting network runs only for
+// the few codes that can still enter the top-k.  Ties: (dis, id) order.
+template <int M>
+__global__ __launch_bounds__(256) void k_ivfpq_scan_m(
+        const float* __restrict__ x, int ldx, const float* __restrict__ pq_cent, int dsub,
+        const uint8_t* __restrict__ codes, const float* __restrict__ terms,
+        const int64_t* __restrict__ ids, const uint32_t* __restrict__ list_off,
+        const uint32_t* __restrict__ list_len, int nlist, const int32_t* __restrict__ assign,
+        const float* __restrict__ coarse_dis, int nprobe, int k, int by_residual,
+        float* __restrict__ D, int64_t* __restrict__ I) {
+    constexpr int CS = (M + 3) & ~3;  // code stride (bytes)
+    constexpr int NW = CS / 4;        // 32-bit words per code
+    __shared__ float T[M * 256];
+    // phase-shared scratch (4 KB): the query during the LUT build, then the
+    // per-wave candidate buffers, then the final cross-wave merge
+    __shared__ __attribute__((aligned(16))) uint8_t scratch[4 * 128 * 8];
+    float* xs = reinterpret_cast<float*>(scratch);                          // [512] (d <= 512)
+    float (*bd)[128] = reinterpret_cast<float (*)[128]>(scratch);           // [4][128]
+    uint32_t (*br)[128] = reinterpret_cast<uint32_t (*)[128]>(scratch + 2048);  // [4][128]
+    float (*md)[64] = reinterpret_cast<float (*)[64]>(scratch);             // [4][64]
+    long long (*mi)[64] = reinterpret_cast<long long (*)[64]>(scratch + 1024);  // [4][64]
+    __shared__ uint32_t p_len[64], p_off[64];
+    __shared__ float p_d0[64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t q = blockIdx.x;
+    const int d = M * dsub;
+    for (int j = t; j < d; j += 256) xs[j] = x[q * ldx + j];
+    __syncthreads();
+    // LUT: table 1 (by_residual): -2 <x_m, c_mj>; otherwise ||x_m - c_mj||^2
+    for (int e = t; e < M * 256; e += 256) {
+        const int m = e >> 8;
+        const float* c = pq_cent + (int64_t)e * dsub;
+        const float* xm = xs + m * dsub;
+        float acc = 0.f;
+        if (by_residual) {
+            for (int i = 0; i < dsub; i++) acc = fmaf(xm[i], c[i], acc);
+            T[e] = -2.f * acc;
+        } else {
+            for (int i = 0; i < dsub; i++) {
+                const float df = xm[i] - c[i];
+                acc = fmaf(df, df, acc);
+            }
+            T[e] = acc;
+        }
+    }
+    __syncthreads();
+
+    // per-probe geometry in LDS (one round trip for all probes)
+    if (t < nprobe) {
+        const int lst = assign[q * nprobe + t];
+        const bool ok = lst >= 0 && lst < nlist;
+        p_len[t] = ok ? list_len[lst] : 0u;
+        p_off[t] = ok ? list_off[lst] : 0u;
+        p_d0[t] = by_residual ? coarse_dis[q * nprobe + t] : 0.f;
+    }
+    __syncthreads();
+
+    float qd = WS_INF;
+    long long qi = WS_NOID;
+    float thr = WS_INF;  // the queue's k-th distance
+    int bc = 0;          // buffered candidates (wave-uniform)
+    auto fold = [&](int cnt) {
+        // lanes < cnt take buffered entries 0..cnt-1
+        float cd = WS_INF;
+        long long ci = WS_NOID;
+        if (lane < cnt) {
+            cd = bd[w][lane];
+            ci = (long long)ids[br[w][lane]];
+        }
+        wave_sort64(cd, ci, lane);
+        wave_merge64(qd, qi, cd, ci, lane);
+        thr = __shfl(qd, k - 1);
+    };
+    // flattened (probe, 64-code batch) sequence of this wave: probes w, w+4, ...
+    // The next batch's code words and terms are loaded while this one is
+    // gathered (software pipelining across batches and lists).
+    int r = w, v0 = 0;
+    auto advance = [&](int& rr, int& vv) {
+        vv += 64;
+        while (rr < nprobe && vv >= (int)p_len[rr]) {
+            rr += 4;
+            vv = 0;
+        }
+    };
+    // first batch: skip empty probes
+    while (r < nprobe && p_len[r] == 0u) r += 4;
+    uint32_t wd[NW];
+    float term = 0.f;
+    uint32_t row = 0;
+    bool valid = false;
+    auto load = [&](int rr, int vv, uint32_t (&wo)[NW], float& to, uint32_t& ro, bool& vo) {
+        vo = rr < nprobe && vv + lane < (int)p_len[rr < nprobe ? rr : 0];
+        ro = (rr < nprobe ? p_off[rr] : 0u) + (uint32_t)(vo ? vv + lane : 0);
+        const uint8_t* cp = codes + (size_t)ro * CS;
+        if constexpr (NW % 4 == 0) {
+#pragma unroll
+            for (int i = 0; i < NW; i += 4) {
+                const uint4 u = *(const uint4*)(cp + 4 * i);
+                wo[i] = u.x;
+                wo[i + 1] = u.y;
+                wo[i + 2] = u.z;
+                wo[i + 3] = u.w;
+            }
+        } else if constexpr (NW % 2 == 0) {
+#pragma unroll
+            for (int i = 0; i < NW; i += 2) {
+                const uint2 u = *(const uint2*)(cp + 4 * i);
+                wo[i] = u.x;
+                wo[i + 1] = u.y;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NW; i++) wo[i] = *(const uint32_t*)(cp + 4 * i);
+        }
+        to = by_residual ? terms[ro] : 0.f;
+    };
+    if (r < nprobe) load(r, v0, wd, term, row, valid);
+    while (r < nprobe) {
+        int rn = r, vn = v0;
+        advance(rn, vn);
+        uint32_t wn[NW];
+        float tn = 0.f;
+        uint32_t rown = 0;
+        bool validn = false;
+        if (rn < nprobe) load(rn, vn, wn, tn, rown, validn);
+        float sum = 0.f;
+#pragma unroll
+        for (int m = 0; m < M; m++) sum += T[m * 256 + ((wd[m >> 2] >> (8 * (m & 3))) & 0xffu)];
+        const float dis = by_residual ? p_d0[r] + term + sum : sum;
+        const bool pass = valid && key_admissible(dis) && dis <= thr;
+        const unsigned long long pm = __ballot(pass);
+        if (pm) {
+            const int pos = bc + __popcll(pm & ((1ull << lane) - 1ull));
+            if (pass) {
+                bd[w][pos] = dis;
+                br[w][pos] = row;
+            }
+            bc += __popcll(pm);
+            if (bc >= 64) {
+                fold(64);
+                // keep the overflow (< 64 entries) at the front
+                const bool mv = lane < bc - 64;
+                const float od = mv ? bd[w][64 + lane] : 0.f;
+                const uint32_t orw = mv ? br[w][64 + lane] : 0u;
+                if (mv) {
+                    bd[w][lane] = od;
+                    br[w][lane] = orw;
+                }
+                bc -= 64;
+            }
+        }
+        r = rn;
+        v0 = vn;
+#pragma unroll
+        for (int i = 0; i < NW; i++) wd[i] = wn[i];
+        term = tn;
+        row = rown;
+        valid = validn;
+    }
+    if (bc > 0) fold(bc);
+    __syncthreads();  // the candidate buffers are reused for the merge
+    // merge the 4 wave queues
+    md[w][lane] = qd;
+    mi[w][lane] = qi;
+    __syncthreads();
+    if (w == 0) {
+        float fd = WS_INF, td = WS_INF;
+        long long fi = WS_NOID, ti = WS_NOID;
+        for (int ww = 0; ww < 4; ww++) {
+            const float cd = lane < k ? md[ww][lane] : WS_INF;
+            const long long ci = lane < k ? mi[ww][lane] : WS_NOID;
+            wave_offer(fd, fi, cd, ci, td, ti, k, lane);
+        }
+        if (lane < k) {
+            float dis;
+            long long id;
+            from_key(1, fd, fi, dis, id);
+            D[q * k + lane] = dis;
+            I[q * k + lane] = id;
+        }
+    }
+}
+
 void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int ksub, int dsub,
                 const uint8_t* codes, const float* terms, const int64_t* ids,
                 const uint32_t* list_off, const uint32_t* list_len, int nlist,
@@ -131,8 +321,21 @@ void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int k
                 int by_residual, float* D, int64_t* I, hipStream_t s) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
+    FAISS_THROW_IF_NOT_MSG(nprobe >= 1 && nprobe <= 64, "nprobe must be in [1, 64] on this path");
     FAISS_THROW_IF_NOT_MSG(ksub == 256, "only 8-bit PQ codes are supported on this path");
     const int code_stride = (int)roundup((size_t)M, 4);
+    if (M * dsub <= 512 && getenv("FAISS_AMD_PQ_SCAN_V1") == nullptr) {
+#define PQ_M(MV)                                                                               \
+    if (M == MV) {                                                                             \
+        k_ivfpq_scan_m<MV><<<dim3((unsigned)n), dim3(256), 0, s>>>(                            \
+                x, ldx, pq_centroids, dsub, codes, terms, ids, list_off, list_len, nlist, assign, \
+                coarse_dis, nprobe, k, by_residual, D, I);                                     \
+        HIP_LAUNCH_CHECK();                                                                    \
+        return;                                                                                \
+    }
+        PQ_M(8) PQ_M(16) PQ_M(32) PQ_M(48) PQ_M(64)
+#undef PQ_M
+    }
     size_t lds = sizeof(float) * ((size_t)M * ksub + roundup((size_t)M * dsub, 4) + 256) +
                  sizeof(long long) * 256;
     FAISS_THROW_IF_NOT_MSG(lds <= 160 * 1024, "PQ LUT does not fit in LDS");
