@@ -39,6 +39,12 @@ CONFIGS = {
     "c4": dict(workload="IVF16384_HNSW32,Flat", desc="IVF16384_HNSW32,Flat", d=128,
                nb=10_000_000, nq=10_000, nlist=16384, nprobe=64, k=10, ntrain=638_976,
                efSearch=64),
+    # BASELINE.json configs[4]: IndexShardsIVF over 8 GPUs, 100M vectors d=96.
+    # One rank = one of the 8 shards (ids == rank mod 8, faiss GPU shard_type
+    # 1), all 100k queries, so --gpus 1 measures exactly one GPU's share.
+    "c5": dict(workload="IVF65536,PQ48 shard of 100M (1/8)", desc="IVF65536,PQ48", d=96,
+               nb=100_000_000, shards=8, nq=100_000, nlist=65536, nprobe=64, k=10,
+               ntrain=65536 * 39),
 }
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector == fp32 MFMA peak
 PEAK_HBM_GBS = 8000.0
@@ -94,11 +100,26 @@ def main():
 
     d, nb, nq, k, nprobe = cfg["d"], cfg["nb"], cfg["nq"], cfg["k"], cfg["nprobe"]
     t0 = time.time()
-    xb = amd.float_rand(nb * d, 1234).reshape(nb, d)
     index = amd.index_factory(d, cfg["desc"])
-    index.train(xb[:cfg["ntrain"]])
-    ids = np.arange(rank, nb, world, dtype=np.int64)
-    index.add_with_ids(xb[ids], ids)
+    if "shards" in cfg:
+        # rows of the float_rand(nb * d, 1234) set, generated shard-wise
+        assert world <= cfg["shards"]
+        ids = np.arange(rank, nb, cfg["shards"], dtype=np.int64)
+        xb = amd.float_rand_rows(nb, d, 1234, rank, cfg["shards"], len(ids))
+        xt = amd.float_rand_rows(nb, d, 1234, 0, 1, cfg["ntrain"])
+        log(f"[rank {rank}] data: shard {len(ids)} + train {len(xt)} rows in "
+            f"{time.time() - t0:.1f}s")
+        index.verbose = True  # k-means progress (keeps long builds visibly alive)
+        index.train(xt)
+        index.verbose = False
+        del xt
+        log(f"[rank {rank}] trained in {time.time() - t0:.1f}s")
+        index.add_with_ids(xb, ids)
+    else:
+        xb = amd.float_rand(nb * d, 1234).reshape(nb, d)
+        index.train(xb[:cfg["ntrain"]])
+        ids = np.arange(rank, nb, world, dtype=np.int64)
+        index.add_with_ids(xb[ids], ids)
     index.nprobe = nprobe
     if "efSearch" in cfg:
         amd.ParameterSpace().set_index_parameter(index, "quantizer_efSearch", cfg["efSearch"])
@@ -168,7 +189,11 @@ def main():
     kt = index.kernel_times()
     scan_name = "ivfpq_scan" if "PQ" in cfg["desc"] else "ivf_flat_scan"
     scan = [ms for (nm, ms, _) in kt if nm == scan_name]
-    scan_ms = float(np.mean(scan)) if scan else float("nan")
+    # a step may launch the kernel more than once (query chunks): the per-step
+    # kernel time is the sum over the step's launches, priced against the
+    # step's whole algorithmic work
+    launches_per_step = len(scan) / args.steps if scan else 0.0
+    scan_ms = float(np.sum(scan)) / args.steps if scan else float("nan")
     # algorithmic work of one scan launch: sum over (query, probe) of the
     # probed list length x per-candidate cost (Flat: 3*d flops; PQ: M bytes)
     nq_launch = nq * world
@@ -187,8 +212,9 @@ def main():
         achieved = work / (scan_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                     "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                    "kernel": scan_name, "kernel_ms": scan_ms,
-                    "algorithmic_bytes_per_launch": work}
+                    "kernel": scan_name, "kernel_ms_per_step": scan_ms,
+                    "launches_per_step": launches_per_step,
+                    "algorithmic_bytes_per_step": work}
     else:
         # The filter runs on bf16 MFMA: every fp32 operand pair is split
         # (bf16x2: codes hi x queries hi+lo = 2 products; bf16x3: 3), so its
@@ -202,17 +228,20 @@ def main():
         fp32_eq = cands * 3.0 * d / (scan_ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                     "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
-                    "kernel": scan_name, "kernel_ms": scan_ms, "mfma_dtype": "bf16",
-                    "algorithmic_flops_per_launch": work,
+                    "kernel": scan_name, "kernel_ms_per_step": scan_ms,
+                    "launches_per_step": launches_per_step, "mfma_dtype": "bf16",
+                    "algorithmic_flops_per_step": work,
                     "flops_per_candidate": nprod * 2 * dpad,
                     "fp32_equivalent_tflops": fp32_eq,
-                    "streamed_bytes_per_launch": cands * d * 4.0}
+                    "streamed_bytes_per_step": cands * d * 4.0}
     if traffic is not None:
-        # HBM bytes per launch from rocprofv3 PMC (committed summary), and
-        # the bandwidth they imply at the live kernel time
+        # HBM bytes per launch from rocprofv3 PMC (committed summary), scaled
+        # to the step's launches like `achieved`, and the bandwidth they imply
+        # at the live kernel time
+        roofline["traffic"] = traffic * launches_per_step
         roofline["traffic_source"] = traffic_src
-        roofline["traffic_unit"] = "bytes/launch"
-        roofline["traffic_gbs"] = traffic / (scan_ms * 1e-3) / 1e9
+        roofline["traffic_unit"] = "bytes/step"
+        roofline["traffic_gbs"] = traffic * launches_per_step / (scan_ms * 1e-3) / 1e9
 
     # ---- recall@10 of this rank's queries vs exact search (subset)
     recall = None
@@ -220,8 +249,10 @@ def main():
         nr = min(args.recall_queries, nq)
         D_t2, I_t2 = D_t.cpu().numpy(), I_t.cpu().numpy()
         gt = amd.IndexFlatL2(d)
-        gt.add(xb)
+        gt.add(xb)  # the shard's vectors for "shards" configs (shard-local recall)
         _, Igt = gt.search(xq[:nr], k)
+        if "shards" in cfg:
+            Igt = np.where(Igt >= 0, ids[np.maximum(Igt, 0)], -1)
         recall = float(np.mean([len(set(a) & set(b)) / k for a, b in zip(I_t2[:nr], Igt)]))
         del gt
 
@@ -276,7 +307,8 @@ def main():
             "value": qps, "unit": "queries/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": cfg["workload"], "d": d, "nb": nb, "nq_per_gpu": nq,
+            "config": {"workload": cfg["workload"], "d": d, "nb": nb, "vectors_per_gpu": len(ids),
+                       "nq_per_gpu": nq,
                        "nprobe": nprobe, "k": k, "global_batch": nq * world,
                        "parallelism": f"shards{world}" if world > 1 else "single",
                        "recall_at_10": recall, "candidates_per_query": cand_per_q},

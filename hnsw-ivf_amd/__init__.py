@@ -169,6 +169,7 @@ def _declare(L):
         "faiss_amd_Index_type": (C.c_char_p, [_P]),
         "faiss_amd_reset_kernel_times": (C.c_int, [_P]),
         "faiss_amd_float_rand": (C.c_int, [_P, C.c_size_t, C.c_int64]),
+        "faiss_amd_float_rand_rows": (C.c_int, [_P, _I64, C.c_int, C.c_int64, _I64, _I64, _I64]),
         "faiss_amd_last_kernel_times": (C.c_int, [_P, C.POINTER(C.c_int), _P, _P, _P]),
     }
     for name, (res, args) in sig.items():
@@ -651,6 +652,15 @@ def float_rand(n, seed):
     """faiss.float_rand (bit-exact restatement, host)."""
     x = np.empty(n, dtype=np.float32)
     _check(lib().faiss_amd_float_rand(_ptr(x), n, seed))
+    return x
+
+
+def float_rand_rows(n_rows, d, seed, row0=0, step=1, nout=None):
+    """Rows row0, row0+step, ... of float_rand(n_rows * d, seed) as [n_rows][d]."""
+    if nout is None:
+        nout = (n_rows - row0 + step - 1) // step
+    x = np.empty((nout, d), dtype=np.float32)
+    _check(lib().faiss_amd_float_rand_rows(_ptr(x), n_rows, d, seed, row0, step, nout))
     return x
 
 

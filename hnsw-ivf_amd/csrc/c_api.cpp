@@ -593,5 +593,10 @@ int faiss_amd_float_rand(float* x, size_t n, int64_t seed) {
     C_TRY float_rand(x, n, seed);
     C_CATCH
 }
+int faiss_amd_float_rand_rows(float* out, int64_t n_rows, int d, int64_t seed, int64_t row0,
+                              int64_t step, int64_t nout) {
+    C_TRY float_rand_rows(out, n_rows, d, seed, row0, step, nout);
+    C_CATCH
+}
 
 }  // extern "C"

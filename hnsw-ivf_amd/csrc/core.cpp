@@ -447,4 +447,41 @@ void float_rand(float* x, size_t n, int64_t seed) {
     for (auto& t : th) t.join();
 }
 
+// Rows row0, row0 + step, ... (nout of them) of the float_rand(n_rows * d,
+// seed) stream viewed as [n_rows][d], without materialising the whole stream
+// (the 100M-vector synthetic sets): the same 1024 mt19937 blocks as
+// float_rand, each generated once, keeping the selected rows.
+void float_rand_rows(float* out, int64_t n_rows, int d, int64_t seed, int64_t row0, int64_t step,
+                     int64_t nout) {
+    FAISS_THROW_IF_NOT(d > 0 && step > 0 && row0 >= 0);
+    FAISS_THROW_IF_NOT(nout >= 0 && (nout == 0 || row0 + (nout - 1) * step < n_rows));
+    const size_t n = (size_t)n_rows * d;
+    const size_t nblock = n < 1024 ? 1 : 1024;
+    std::mt19937 rng0((unsigned int)seed);
+    int a0 = (int)(rng0() & 0x7fffffff), b0 = (int)(rng0() & 0x7fffffff);
+    auto run = [&](int64_t j0, int64_t j1) {
+        for (int64_t j = j0; j < j1; j++) {
+            std::mt19937 rng((unsigned int)(int64_t)(a0 + j * b0));
+            const size_t istart = j * n / nblock;
+            const size_t iend = (j + 1) * n / nblock;
+            const float mx = (float)std::mt19937::max();
+            for (size_t i = istart; i < iend; i++) {
+                const float v = (float)rng() / mx;
+                const int64_t r = (int64_t)(i / d);
+                if (r < row0 || (r - row0) % step != 0) continue;
+                const int64_t o = (r - row0) / step;
+                if (o < nout) out[(size_t)o * d + (i - (size_t)r * d)] = v;
+            }
+        }
+    };
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < (1 << 20)) nt = 1;
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++) {
+        int64_t j0 = (int64_t)nblock * t / nt, j1 = (int64_t)nblock * (t + 1) / nt;
+        th.emplace_back(run, j0, j1);
+    }
+    for (auto& t : th) t.join();
+}
+
 }  // namespace faiss_amd

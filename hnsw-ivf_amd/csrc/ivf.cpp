@@ -184,9 +184,12 @@ void IndexIVF::quantize_device(idx_t n, const float* x, int ldx, int np, float* 
     quantizer->assign_device(n, x, ldx, np, coarse_dis, assign, qparams, s);
 }
 
-// queries per chunk: bounds the partial-result scratch to ~1 GiB
+// queries per chunk: bounds the partial-result scratch to ~1 GiB (the
+// list-centric Flat scan keeps per-(query, probe) partials; the query-centric
+// PQ scan keeps none)
 idx_t IndexIVF::search_chunk(idx_t n, size_t np, idx_t k) const {
-    const size_t per_q = np * (size_t)std::max<idx_t>(k, 32) * 12 + np * 16;
+    const bool pq = dynamic_cast<const IndexIVFPQ*>(this) != nullptr;
+    const size_t per_q = pq ? np * 16 : np * (size_t)std::max<idx_t>(k, 32) * 12 + np * 16;
     idx_t qchunk = std::max<idx_t>(1, (idx_t)(((size_t)1 << 30) / per_q));
     return std::max<idx_t>(1, std::min<idx_t>(qchunk, n));
 }

@@ -126,6 +126,7 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan(
 }
 
 // ---------------------------------------------------------------- scan v2
+constexpr int PQ_PF = 3;  // code batches in flight per wave
 // One workgroup (4 waves) per query, LUT T[m][j] (M x 256 f32) in LDS; the
 // per-code work is M LDS gathers + adds (LDS-gather bound).  M is a template
 // parameter (fully unrolled, codes read as 16-B words).  Selection: each wave
@@ -205,9 +206,9 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan_m(
         thr = __shfl(qd, k - 1);
     };
     // flattened (probe, 64-code batch) sequence of this wave: probes w, w+4, ...
-    // The next batch's code words and terms are loaded while this one is
-    // gathered (software pipelining across batches and lists).
-    int r = w, v0 = 0;
+    // A ring of PQ_PF batches is in flight: a slot is refilled with the batch
+    // PQ_PF ahead as soon as it has been gathered (HBM latency hidden across
+    // batches and lists).
     auto advance = [&](int& rr, int& vv) {
         vv += 64;
         while (rr < nprobe && vv >= (int)p_len[rr]) {
@@ -215,12 +216,6 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan_m(
             vv = 0;
         }
     };
-    // first batch: skip empty probes
-    while (r < nprobe && p_len[r] == 0u) r += 4;
-    uint32_t wd[NW];
-    float term = 0.f;
-    uint32_t row = 0;
-    bool valid = false;
     auto load = [&](int rr, int vv, uint32_t (&wo)[NW], float& to, uint32_t& ro, bool& vo) {
         vo = rr < nprobe && vv + lane < (int)p_len[rr < nprobe ? rr : 0];
         ro = (rr < nprobe ? p_off[rr] : 0u) + (uint32_t)(vo ? vv + lane : 0);
@@ -247,48 +242,65 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan_m(
         }
         to = by_residual ? terms[ro] : 0.f;
     };
-    if (r < nprobe) load(r, v0, wd, term, row, valid);
-    while (r < nprobe) {
-        int rn = r, vn = v0;
-        advance(rn, vn);
-        uint32_t wn[NW];
-        float tn = 0.f;
-        uint32_t rown = 0;
-        bool validn = false;
-        if (rn < nprobe) load(rn, vn, wn, tn, rown, validn);
-        float sum = 0.f;
+    constexpr int PF = PQ_PF;
+    uint32_t wd[PF][NW];
+    float term[PF];
+    uint32_t row[PF];
+    bool valid[PF];
+    int rs[PF];  // probe of each slot (nprobe: empty)
+    int pr = w, pv = 0;  // next batch to load
+    while (pr < nprobe && p_len[pr] == 0u) pr += 4;
 #pragma unroll
-        for (int m = 0; m < M; m++) sum += T[m * 256 + ((wd[m >> 2] >> (8 * (m & 3))) & 0xffu)];
-        const float dis = by_residual ? p_d0[r] + term + sum : sum;
-        const bool pass = valid && key_admissible(dis) && dis <= thr;
-        const unsigned long long pm = __ballot(pass);
-        if (pm) {
-            const int pos = bc + __popcll(pm & ((1ull << lane) - 1ull));
-            if (pass) {
-                bd[w][pos] = dis;
-                br[w][pos] = row;
+    for (int sl = 0; sl < PF; sl++) {
+        rs[sl] = pr;
+        if (pr < nprobe) {
+            load(pr, pv, wd[sl], term[sl], row[sl], valid[sl]);
+            advance(pr, pv);
+        } else {
+            valid[sl] = false;
+        }
+    }
+    while (rs[0] < nprobe) {
+#pragma unroll
+        for (int sl = 0; sl < PF; sl++) {
+            if (rs[sl] >= nprobe) break;  // wave-uniform: the sequence has ended
+            float sum = 0.f;
+#pragma unroll
+            for (int m = 0; m < M; m++)
+                sum += T[m * 256 + ((wd[sl][m >> 2] >> (8 * (m & 3))) & 0xffu)];
+            const float dis = by_residual ? p_d0[rs[sl]] + term[sl] + sum : sum;
+            const bool pass = valid[sl] && key_admissible(dis) && dis <= thr;
+            const uint32_t prow = row[sl];
+            // refill this slot with the batch PF ahead
+            rs[sl] = pr;
+            if (pr < nprobe) {
+                load(pr, pv, wd[sl], term[sl], row[sl], valid[sl]);
+                advance(pr, pv);
+            } else {
+                valid[sl] = false;
             }
-            bc += __popcll(pm);
-            if (bc >= 64) {
-                fold(64);
-                // keep the overflow (< 64 entries) at the front
-                const bool mv = lane < bc - 64;
-                const float od = mv ? bd[w][64 + lane] : 0.f;
-                const uint32_t orw = mv ? br[w][64 + lane] : 0u;
-                if (mv) {
-                    bd[w][lane] = od;
-                    br[w][lane] = orw;
+            const unsigned long long pm = __ballot(pass);
+            if (pm) {
+                const int pos = bc + __popcll(pm & ((1ull << lane) - 1ull));
+                if (pass) {
+                    bd[w][pos] = dis;
+                    br[w][pos] = prow;
                 }
-                bc -= 64;
+                bc += __popcll(pm);
+                if (bc >= 64) {
+                    fold(64);
+                    // keep the overflow (< 64 entries) at the front
+                    const bool mv = lane < bc - 64;
+                    const float od = mv ? bd[w][64 + lane] : 0.f;
+                    const uint32_t orw = mv ? br[w][64 + lane] : 0u;
+                    if (mv) {
+                        bd[w][lane] = od;
+                        br[w][lane] = orw;
+                    }
+                    bc -= 64;
+                }
             }
         }
-        r = rn;
-        v0 = vn;
-#pragma unroll
-        for (int i = 0; i < NW; i++) wd[i] = wn[i];
-        term = tn;
-        row = rown;
-        valid = validn;
     }
     if (bc > 0) fold(bc);
     __syncthreads();  // the candidate buffers are reused for the merge

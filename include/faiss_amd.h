@@ -401,5 +401,8 @@ Index* index_factory(int d, const char* description, MetricType metric = METRIC_
 
 // float_rand (faiss/utils/random.cpp:95-112), bit-exact restatement
 void float_rand(float* x, size_t n, int64_t seed);
+// selected rows (row0, row0 + step, ...) of float_rand(n_rows * d, seed)
+void float_rand_rows(float* out, int64_t n_rows, int d, int64_t seed, int64_t row0, int64_t step,
+                     int64_t nout);
 
 }  // namespace faiss_amd

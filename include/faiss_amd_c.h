@@ -420,6 +420,11 @@ int faiss_amd_reset_kernel_times(FaissIndex* index);
 /* faiss::float_rand (faiss/utils/random.cpp:95-112), bit-exact restatement:
  * the synthetic inputs of the benchmark are regenerated on the GPU box */
 int faiss_amd_float_rand(float* x, size_t n, int64_t seed);
+/* extension: rows row0, row0 + step, ... (nout of them) of the float_rand
+ * stream of n_rows * d floats viewed as [n_rows][d] (shards of the large
+ * synthetic sets without materialising them) */
+int faiss_amd_float_rand_rows(float* out, int64_t n_rows, int d, int64_t seed, int64_t row0,
+                              int64_t step, int64_t nout);
 
 #ifdef __cplusplus
 }
