@@ -243,6 +243,19 @@ def main():
         roofline["traffic_unit"] = "bytes/step"
         roofline["traffic_gbs"] = traffic * launches_per_step / (scan_ms * 1e-3) / 1e9
 
+    # ---- PCIe-inclusive rate (host buffers through faiss_Index_search: query
+    # upload + result download); reported beside `value`, never as it
+    pcie = None
+    if world == 1 and args.steps > 0:
+        index.search(xq, k)
+        nh = min(args.steps, 5)
+        th = time.perf_counter()
+        for _ in range(nh):
+            index.search(xq, k)
+        th = time.perf_counter() - th
+        pcie = {"value": nq * nh / th, "unit": "queries/s", "ms_per_step": th / nh * 1e3,
+                "what": "faiss_Index_search on host buffers (H2D queries + search + D2H results)"}
+
     # ---- recall@10 of this rank's queries vs exact search (subset)
     recall = None
     if rank == 0 and args.recall_queries > 0:
@@ -267,17 +280,17 @@ def main():
         if fast:
             what = "IVF-Flat scan with 8-way vectorisable partial sums (oracle search_fast)"
 
-            def cpu_search(xs):
-                return ref.search_fast(xs, k, nprobe, nthreads=ncores)
+            def cpu_search(xs, nt=ncores):
+                return ref.search_fast(xs, k, nprobe, nthreads=nt)
         else:
             what = ("IndexIVF::search restated (oracle search: coarse "
                     + ("HNSW" if "HNSW" in cfg["desc"] else "flat") + " quantizer, "
                     + ("IVF-PQ table %d scan" % ref.use_precomputed_table if is_pq
                        else "IVF-Flat scan") + f", {ncores} query slices)")
 
-            def cpu_search(xs):
-                D_, I_, _, _ = ref.search(xs, k, nprobe, efSearch=ef, nslices=ncores,
-                                          nthreads=ncores)
+            def cpu_search(xs, nt=ncores):
+                D_, I_, _, _ = ref.search(xs, k, nprobe, efSearch=ef, nslices=nt,
+                                          nthreads=nt)
                 return D_, I_
         probe = min(200, nq)
         tc = time.perf_counter()
@@ -294,11 +307,18 @@ def main():
             if tcpu >= args.cpu_seconds or passes >= 50:
                 break
         agree = float(np.mean(Ic == I_t.cpu().numpy()[:ns]))
+        # one-thread rate (report 1 thread too), ~1/5 of the budget
+        n1 = int(max(1, min(ns, ns * passes * (args.cpu_seconds / 5) / max(tcpu, 1e-3)
+                            / max(ncores, 1))))
+        tc = time.perf_counter()
+        cpu_search(xq[:n1], 1)
+        t1c = time.perf_counter() - tc
         cpu = {"value": ns * passes / tcpu, "unit": "queries/s", "cores": ncores,
                "kind": "port",
                "sample": f"{passes} pass(es) over {ns} of the {nq} queries, same index, "
                          f"{what}, {tcpu:.1f}s wall on {ncores} threads",
-               "id_agreement_vs_gpu": agree}
+               "id_agreement_vs_gpu": agree,
+               "one_thread": {"value": n1 / t1c, "unit": "queries/s", "queries": n1}}
 
     if rank == 0:
         out = {
@@ -314,6 +334,7 @@ def main():
                        "recall_at_10": recall, "candidates_per_query": cand_per_q},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

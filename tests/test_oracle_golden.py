@@ -39,6 +39,17 @@ def test_float_rand_matches_reference(orc, amd, fx):
                           fx["float_rand_1M_1234_head_tail"])
 
 
+def test_float_rand_rows_is_strided_slice(orc, amd):
+    # bench.py draws a shard's rows (rank, rank + nshards, ...) of the global
+    # float_rand matrix without materialising it; both block-size regimes
+    for n_rows, d in ((300, 3), (20000, 96)):
+        full = orc.float_rand(n_rows * d, 77).reshape(n_rows, d)
+        for row0, step in ((0, 1), (3, 8), (n_rows - 1, 5)):
+            nout = (n_rows - 1 - row0) // step + 1
+            got = amd.float_rand_rows(n_rows, d, 77, row0=row0, step=step, nout=nout)
+            assert np.array_equal(got, full[row0::step]), (n_rows, row0, step)
+
+
 def test_fvec_evaluation_order_matches_reference(orc, fx):
     # faiss/utils/distances_simd.cpp:220-300 as compiled with the reference's
     # AVX2 flags; the oracle restates that order (oracle.c ref_dist_)
