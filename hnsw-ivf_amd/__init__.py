@@ -118,6 +118,12 @@ def _declare(L):
         "faiss_IndexIVF_nlist": (C.c_size_t, [_P]),
         "faiss_IndexIVF_nprobe": (C.c_size_t, [_P]),
         "faiss_IndexIVF_set_nprobe": (None, [_P, C.c_size_t]),
+        "faiss_SearchParametersIVF_max_codes": (C.c_size_t, [_P]),
+        "faiss_SearchParametersIVF_set_max_codes": (None, [_P, C.c_size_t]),
+        "faiss_amd_IndexIVF_max_codes": (C.c_size_t, [_P]),
+        "faiss_amd_IndexIVF_set_max_codes": (None, [_P, C.c_size_t]),
+        "faiss_amd_IndexIVF_parallel_mode": (C.c_int, [_P]),
+        "faiss_amd_IndexIVF_set_parallel_mode": (None, [_P, C.c_int]),
         "faiss_IndexIVF_quantizer": (_P, [_P]),
         "faiss_IndexIVF_own_fields": (C.c_int, [_P]),
         "faiss_IndexIVF_set_own_fields": (None, [_P, C.c_int]),
@@ -411,6 +417,22 @@ class IndexIVF(Index):
     @nprobe.setter
     def nprobe(self, v):
         lib().faiss_IndexIVF_set_nprobe(self.h, int(v))
+
+    @property
+    def max_codes(self):
+        return lib().faiss_amd_IndexIVF_max_codes(self.h)
+
+    @max_codes.setter
+    def max_codes(self, v):
+        lib().faiss_amd_IndexIVF_set_max_codes(self.h, int(v))
+
+    @property
+    def parallel_mode(self):
+        return lib().faiss_amd_IndexIVF_parallel_mode(self.h)
+
+    @parallel_mode.setter
+    def parallel_mode(self, v):
+        lib().faiss_amd_IndexIVF_set_parallel_mode(self.h, int(v))
 
     @property
     def code_size(self):

@@ -4,6 +4,7 @@
 // 0 / -2 (FaissException) / -4 (std::exception) / -1 (other), and stores the
 // message in a thread-local slot read by faiss_get_last_error()
 // (reference c_api/macros_impl.h:22-56, c_api/error_impl.cpp:15-26).
+#include <cmath>
 #include <cstring>
 #include <string>
 
@@ -131,6 +132,22 @@ size_t faiss_SearchParametersIVF_nprobe(const FaissSearchParametersIVF* p) {
 }
 void faiss_SearchParametersIVF_set_nprobe(FaissSearchParametersIVF* p, size_t v) {
     reinterpret_cast<SearchParamsC*>(p)->ivf.nprobe = v;
+}
+size_t faiss_SearchParametersIVF_max_codes(const FaissSearchParametersIVF* p) {
+    return reinterpret_cast<const SearchParamsC*>(p)->ivf.max_codes;
+}
+void faiss_SearchParametersIVF_set_max_codes(FaissSearchParametersIVF* p, size_t v) {
+    reinterpret_cast<SearchParamsC*>(p)->ivf.max_codes = v;
+}
+size_t faiss_amd_IndexIVF_max_codes(const FaissIndexIVF* index) { return IVF(index)->max_codes; }
+void faiss_amd_IndexIVF_set_max_codes(FaissIndexIVF* index, size_t v) {
+    IVF(index)->max_codes = v;
+}
+int faiss_amd_IndexIVF_parallel_mode(const FaissIndexIVF* index) {
+    return IVF(index)->parallel_mode;
+}
+void faiss_amd_IndexIVF_set_parallel_mode(FaissIndexIVF* index, int v) {
+    IVF(index)->parallel_mode = v;
 }
 void faiss_amd_SearchParametersIVF_set_quantizer_efSearch(FaissSearchParametersIVF* p, int ef) {
     auto sp = reinterpret_cast<SearchParamsC*>(p);
@@ -463,6 +480,14 @@ int faiss_ParameterSpace_set_index_parameter(const FaissParameterSpace*, FaissIn
         auto h = dynamic_cast<IndexHNSW*>(q);
         FAISS_THROW_IF_NOT_MSG(h, "quantizer is not an IndexHNSW");
         h->hnsw.efSearch = (int)val;
+    } else if (n == "max_codes") {
+        // faiss/AutoTune.cpp:530-535
+        const size_t mc = std::isfinite(val) ? (size_t)val : 0;
+        if (auto s = dynamic_cast<IndexShardsIVF*>(ix)) {
+            for (auto* sh : s->shards) sh->max_codes = mc;
+        } else {
+            IVF(index)->max_codes = mc;
+        }
     } else {
         FAISS_THROW_MSG("ParameterSpace::set_index_parameter: unknown parameter " + n);
     }

@@ -194,6 +194,33 @@ idx_t IndexIVF::search_chunk(idx_t n, size_t np, idx_t k) const {
     return std::max<idx_t>(1, std::min<idx_t>(qchunk, n));
 }
 
+namespace {
+// faiss/IndexIVF.cpp:445-460, 595-631: parallel_mode 0 and 3 are both
+// query-parallel with the same per-query scan (3 only changes the OpenMP
+// split), which is what the GPU path computes; 1 and 2 split a query's probes
+// across threads and the PARALLEL_MODE_NO_HEAP_INIT flag accumulates into the
+// caller's arrays — neither is offered here.
+void check_parallel_mode(int pm) {
+    FAISS_THROW_IF_NOT_FMT(pm == 0 || pm == 3,
+                           "parallel_mode %d not supported on the GPU path (0 and 3 are)", pm);
+}
+}  // namespace
+
+const int32_t* IndexIVF::apply_max_codes(idx_t n, int np, const int32_t* assign,
+                                         size_t max_codes, const uint32_t** lim,
+                                         hipStream_t s) const {
+    *lim = nullptr;
+    if (max_codes == 0 || n <= 0) return assign;  // 0 = unlimited (IndexIVF.cpp:452-454)
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    s_lim_.reserve(sizeof(uint32_t) * n * np);
+    s_alim_.reserve(sizeof(int32_t) * n * np);
+    kern::probe_limits(assign, n, np, d_list_len_.as<uint32_t>(), (int)nlist,
+                       (int64_t)std::min<size_t>(max_codes, (size_t)INT64_MAX),
+                       s_alim_.as<int32_t>(), s_lim_.as<uint32_t>(), s);
+    *lim = s_lim_.as<uint32_t>();
+    return s_alim_.as<int32_t>();
+}
+
 void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
                              idx_t* labels, const SearchParameters* params_in,
                              hipStream_t s) const {
@@ -206,8 +233,7 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     }
     const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
-    FAISS_THROW_IF_NOT_MSG((params ? params->max_codes : max_codes) == 0,
-                           "max_codes is not supported on the GPU path");
+    const size_t mc = params ? params->max_codes : max_codes;
     FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
     DevGuard dg(device);
     sync_device();
@@ -221,8 +247,10 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
         const idx_t nq = std::min(qchunk, n - q0);
         quantize_device(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(), s_ci_.as<int32_t>(),
                         params ? params->quantizer_params : nullptr, s);
-        search_preassigned_device(nq, x + q0 * ldx, ldx, k, (int)np, s_ci_.as<int32_t>(),
-                                  s_cd_.as<float>(), distances + q0 * k, labels + q0 * k, s);
+        const uint32_t* lim = nullptr;
+        const int32_t* asg = apply_max_codes(nq, (int)np, s_ci_.as<int32_t>(), mc, &lim, s);
+        search_preassigned_device(nq, x + q0 * ldx, ldx, k, (int)np, asg, s_cd_.as<float>(),
+                                  distances + q0 * k, labels + q0 * k, s, lim);
     }
 }
 
@@ -266,11 +294,10 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
     // faiss/IndexIVF.cpp:399-723 / 870-1200 (parallel_mode 0 semantics)
     FAISS_THROW_IF_NOT(k > 0);
     FAISS_THROW_IF_NOT_MSG(!store_pairs, "store_pairs is not supported on the GPU path");
-    FAISS_THROW_IF_NOT_MSG(parallel_mode == 0, "only parallel_mode 0 runs on the GPU path");
+    check_parallel_mode(parallel_mode);
     const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
-    FAISS_THROW_IF_NOT_MSG((params ? params->max_codes : max_codes) == 0,
-                           "max_codes is not supported on the GPU path");
+    const size_t mc = params ? params->max_codes : max_codes;
     if (n == 0) return;
     std::vector<int32_t> a32((size_t)n * np);
     for (size_t i = 0; i < (size_t)n * np; i++) {
@@ -301,11 +328,13 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
     HIP_CHECK(hipMemsetAsync(s_stats_.ptr, 0, 2 * sizeof(unsigned long long), s));
     StageEvents ev;
     hipEvent_t e0 = ev.mark(s);
-    search_preassigned_device(n, bx.as<float>(), ldx, k, (int)np, ba.as<int32_t>(),
-                              bc.as<float>(), bd.as<float>(), bi.as<idx_t>(), s);
+    const uint32_t* lim = nullptr;
+    const int32_t* asg = apply_max_codes(n, (int)np, ba.as<int32_t>(), mc, &lim, s);
+    search_preassigned_device(n, bx.as<float>(), ldx, k, (int)np, asg, bc.as<float>(),
+                              bd.as<float>(), bi.as<idx_t>(), s, lim);
     hipEvent_t e1 = ev.mark(s);
-    kern::ivf_visit_stats(ba.as<int32_t>(), n * (int64_t)np, d_list_len_.as<uint32_t>(),
-                          (int)nlist, s_stats_.as<unsigned long long>(), s);
+    kern::ivf_visit_stats(asg, n * (int64_t)np, d_list_len_.as<uint32_t>(), (int)nlist, lim,
+                          s_stats_.as<unsigned long long>(), s);
     unsigned long long st[2];
     HIP_CHECK(hipMemcpyAsync(distances, bd.ptr, sizeof(float) * n * k, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
@@ -347,9 +376,8 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
     }
     const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
-    FAISS_THROW_IF_NOT_MSG(parallel_mode == 0, "only parallel_mode 0 runs on the GPU path");
-    FAISS_THROW_IF_NOT_MSG((params ? params->max_codes : max_codes) == 0,
-                           "max_codes is not supported on the GPU path");
+    check_parallel_mode(parallel_mode);
+    const size_t mc = params ? params->max_codes : max_codes;
     FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
     if (n == 0) return;
     DevGuard dg(device);
@@ -377,13 +405,14 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
         quantize_device(nq, bx.as<float>() + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
                         s_ci_.as<int32_t>(), params ? params->quantizer_params : nullptr, s);
         marks.push_back(ev.mark(s));
-        search_preassigned_device(nq, bx.as<float>() + q0 * ldx, ldx, k, (int)np,
-                                  s_ci_.as<int32_t>(), s_cd_.as<float>(),
-                                  bd.as<float>() + q0 * k, bi.as<idx_t>() + q0 * k, s);
+        const uint32_t* lim = nullptr;
+        const int32_t* asg = apply_max_codes(nq, (int)np, s_ci_.as<int32_t>(), mc, &lim, s);
+        search_preassigned_device(nq, bx.as<float>() + q0 * ldx, ldx, k, (int)np, asg,
+                                  s_cd_.as<float>(), bd.as<float>() + q0 * k,
+                                  bi.as<idx_t>() + q0 * k, s, lim);
         marks.push_back(ev.mark(s));
-        kern::ivf_visit_stats(s_ci_.as<int32_t>(), nq * (int64_t)np,
-                              d_list_len_.as<uint32_t>(), (int)nlist,
-                              s_stats_.as<unsigned long long>(), s);
+        kern::ivf_visit_stats(asg, nq * (int64_t)np, d_list_len_.as<uint32_t>(), (int)nlist,
+                              lim, s_stats_.as<unsigned long long>(), s);
     }
     unsigned long long st[2];
     HIP_CHECK(hipMemcpyAsync(distances, bd.ptr, sizeof(float) * n * k, hipMemcpyDeviceToHost, s));
@@ -462,8 +491,8 @@ void IndexIVFFlat::upload_extra() const {
 
 void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
                                              const int32_t* assign, const float*,
-                                             float* distances, idx_t* labels,
-                                             hipStream_t s) const {
+                                             float* distances, idx_t* labels, hipStream_t s,
+                                             const uint32_t* lim) const {
     if (n <= 0) return;
     sync_device();
     std::lock_guard<std::recursive_mutex> g(mu_);
@@ -476,6 +505,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     s_ent_.reserve(sizeof(uint32_t) * n * np);
     kern::IVFBuckets b{s_counts_.as<uint32_t>(), s_boff_.as<uint32_t>(), s_ioff_.as<uint32_t>(),
                        s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
+    b.lim = lim;
     const char* env = getenv("FAISS_AMD_IVF_SCAN");
     int mode = scan_mode;
     if (env && !strcmp(env, "exact")) mode = 1;
@@ -536,7 +566,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     kern::ivf_exact_fallback(s_flags_.as<uint32_t>(), assign, d_list_off_.as<uint32_t>(),
                              d_list_len_.as<uint32_t>(), (int)nlist, x, ldx,
                              d_codes_.as<float>(), l, d_ids_.as<int64_t>(), d, n, np, (int)k, l2,
-                             distances, labels, s);
+                             lim, distances, labels, s);
 }
 
 // ---------------------------------------------------------------- PQ
@@ -659,8 +689,8 @@ void IndexIVFPQ::upload_extra() const {
 
 void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
                                            const int32_t* assign, const float* centroid_dis,
-                                           float* distances, idx_t* labels,
-                                           hipStream_t s) const {
+                                           float* distances, idx_t* labels, hipStream_t s,
+                                           const uint32_t* lim) const {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_MSG(metric_type == METRIC_L2, "IVFPQ inner product not supported on GPU");
     sync_device();
@@ -668,7 +698,8 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
     kern::ivfpq_scan(x, ldx, d_pq_.as<float>(), (int)pq.M, (int)pq.ksub, (int)pq.dsub,
                      d_codes_.as<uint8_t>(), d_terms_.as<float>(), d_ids_.as<int64_t>(),
                      d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(), (int)nlist, assign,
-                     centroid_dis, n, np, (int)k, by_residual ? 1 : 0, distances, labels, s);
+                     centroid_dis, lim, n, np, (int)k, by_residual ? 1 : 0, distances, labels,
+                     s);
 }
 
 // ---------------------------------------------------------------- shards
@@ -753,9 +784,15 @@ void IndexShardsIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, fl
     for (int no = 0; no < ns; no++) {
         FAISS_THROW_IF_NOT_MSG(shards[no]->nprobe == np || params, "inconsistent nprobe");
         idx_t* li = s_all_i_.as<idx_t>() + (size_t)no * n * k;
-        shards[no]->search_preassigned_device(n, x, ldx, k, (int)np, s_ci_.as<int32_t>(),
-                                              s_cd_.as<float>(),
-                                              s_all_d_.as<float>() + (size_t)no * n * k, li, s);
+        // each shard applies max_codes to its own lists (IndexShardsIVF.cpp:204-213
+        // passes the params to every shard's search_preassigned)
+        const uint32_t* lim = nullptr;
+        const int32_t* asg = shards[no]->apply_max_codes(
+                n, (int)np, s_ci_.as<int32_t>(), params ? params->max_codes : shards[no]->max_codes,
+                &lim, s);
+        shards[no]->search_preassigned_device(n, x, ldx, k, (int)np, asg, s_cd_.as<float>(),
+                                              s_all_d_.as<float>() + (size_t)no * n * k, li, s,
+                                              lim);
         if (successive_ids) kern::translate_labels(li, (int64_t)n * k, translation, s);
         translation += shards[no]->ntotal;
     }

@@ -109,13 +109,23 @@ struct IVFBuckets {
     uint32_t* mark_keys = nullptr;
     ProbeRec* mark_recs = nullptr;
     int mark_ke = 0;
+    // optional (max_codes): rows of each entry's list that are scanned (a
+    // prefix; probe_limits), nullptr = whole lists
+    const uint32_t* lim = nullptr;
 };
+// max_codes (faiss/IndexIVF.cpp:595-631, scan_one_list :546-550): per query,
+// probes in coarse order; the probe that reaches max_codes is cut to the rows
+// still allowed and the later ones are dropped (assign_out -1).  lim[e] = rows
+// of entry e scanned (0 for dropped / empty / invalid probes).
+void probe_limits(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
+                  int nlist, int64_t max_codes, int32_t* assign_out, uint32_t* lim,
+                  hipStream_t s);
 void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
                 const uint32_t* list_off, int nlist, int QT, IVFBuckets b, hipStream_t s);
 // IndexIVFStats counters of a batch (faiss/IndexIVF.cpp:1184-1198):
 // stats[0] += non-empty lists visited, stats[1] += codes scanned (device)
 void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_len, int nlist,
-                     unsigned long long* stats, hipStream_t s);
+                     const uint32_t* lim, unsigned long long* stats, hipStream_t s);
 // upper bound on the number of work items (grid size without a host sync)
 inline int64_t ivf_max_items(int64_t n, int nprobe, int nlist, int QT) {
     return (n * nprobe + QT - 1) / QT + nlist;
@@ -159,7 +169,8 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 void ivf_exact_fallback(const uint32_t* flags, const int32_t* assign, const uint32_t* list_off,
                         const uint32_t* list_len, int nlist, const float* x, int ldx,
                         const float* codes, int ldc, const int64_t* ids, int d, int64_t n,
-                        int nprobe, int k, int metric_l2, float* D, int64_t* I, hipStream_t s);
+                        int nprobe, int k, int metric_l2, const uint32_t* lim, float* D,
+                        int64_t* I, hipStream_t s);
 
 // per-query merge of the nprobe partial top-k, reference
 // faiss/IndexIVF.cpp:595-631 (heap over probes) + Heap.h:421-450 (reorder)
@@ -178,8 +189,8 @@ void ivf_merge(const float* part_k1, const long long* part_k2, const int32_t* as
 void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int ksub, int dsub,
                 const uint8_t* codes, const float* terms, const int64_t* ids,
                 const uint32_t* list_off, const uint32_t* list_len, int nlist,
-                const int32_t* assign, const float* coarse_dis, int64_t n, int nprobe, int k,
-                int by_residual, float* D, int64_t* I, hipStream_t s);
+                const int32_t* assign, const float* coarse_dis, const uint32_t* lim, int64_t n,
+                int nprobe, int k, int by_residual, float* D, int64_t* I, hipStream_t s);
 
 // term[v] = sum_m (||c_{m,code}||^2 + 2 <yC_m, c_{m,code}>) for every arena row
 void ivfpq_terms(const uint8_t* codes, const uint32_t* row_list, int64_t nrows,

@@ -167,12 +167,13 @@ __global__ void k_bucket_fill(const int32_t* __restrict__ assign, int64_t total,
 
 __global__ void k_ivf_visit_stats(const int32_t* __restrict__ assign, int64_t total,
                                   const uint32_t* __restrict__ list_len, int nlist,
+                                  const uint32_t* __restrict__ lim,
                                   unsigned long long* __restrict__ stats) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t len = 0;
     if (e < total) {
         const int l = assign[e];
-        if (l >= 0 && l < nlist) len = list_len[l];
+        if (l >= 0 && l < nlist) len = lim ? lim[e] : list_len[l];
     }
     const unsigned long long nv = __popcll(__ballot(len > 0));
     unsigned long long nd = len;
@@ -185,10 +186,39 @@ __global__ void k_ivf_visit_stats(const int32_t* __restrict__ assign, int64_t to
 }
 
 void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_len, int nlist,
-                     unsigned long long* stats, hipStream_t s) {
+                     const uint32_t* lim, unsigned long long* stats, hipStream_t s) {
     if (total <= 0) return;
-    k_ivf_visit_stats<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(assign, total,
-                                                                            list_len, nlist, stats);
+    k_ivf_visit_stats<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
+            assign, total, list_len, nlist, lim, stats);
+    HIP_LAUNCH_CHECK();
+}
+
+// one thread per query: faiss/IndexIVF.cpp:609-622 (nscan, list_size_max)
+__global__ void k_probe_limits(const int32_t* __restrict__ assign, int64_t n, int nprobe,
+                               const uint32_t* __restrict__ list_len, int nlist,
+                               int64_t max_codes, int32_t* __restrict__ assign_out,
+                               uint32_t* __restrict__ lim) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    int64_t nscan = 0;
+    for (int r = 0; r < nprobe; r++) {
+        const int64_t e = q * nprobe + r;
+        const int l = assign[e];
+        const bool ok = l >= 0 && l < nlist && nscan < max_codes;
+        const uint32_t len = ok ? list_len[l] : 0u;
+        const uint32_t take = (uint32_t)min((int64_t)len, max_codes - nscan);
+        assign_out[e] = ok ? l : -1;
+        lim[e] = take;
+        nscan += take;
+    }
+}
+
+void probe_limits(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
+                  int nlist, int64_t max_codes, int32_t* assign_out, uint32_t* lim,
+                  hipStream_t s) {
+    if (n <= 0) return;
+    k_probe_limits<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s>>>(
+            assign, n, nprobe, list_len, nlist, max_codes, assign_out, lim);
     HIP_LAUNCH_CHECK();
 }
 
@@ -233,8 +263,8 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
         const int64_t* __restrict__ ids, const uint32_t* __restrict__ list_off,
         const uint32_t* __restrict__ list_len, int nlist, int dp, int dp_true, int nprobe,
         int k, const uint32_t* __restrict__ bucket_off, const uint32_t* __restrict__ item_off,
-        const uint32_t* __restrict__ entries, float* __restrict__ part_k1,
-        long long* __restrict__ part_k2) {
+        const uint32_t* __restrict__ entries, const uint32_t* __restrict__ lim,
+        float* __restrict__ part_k1, long long* __restrict__ part_k2) {
     // one array: the end-of-kernel queue merge reuses it (64 KB at KQ=32)
     __shared__ __attribute__((aligned(16))) float smem_xy[(SQT + 64) * SSD];
     float* Xs = smem_xy;
@@ -242,6 +272,7 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
     __shared__ long long ids_s[64];
     __shared__ uint32_t ent_s[SQT];
     __shared__ int32_t qrow_s[SQT];
+    __shared__ int32_t qlim_s[SQT];  // rows of the list scanned for each query
 
     const int t = threadIdx.x;
     const int lane = t & 63;
@@ -264,12 +295,13 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
     const uint32_t chunk = item - item_off[l];
     const uint32_t qb = bucket_off[l] + chunk * SQT;
     const int nQ = (int)min((uint32_t)SQT, bucket_off[l + 1] - qb);
+    const int len = (int)list_len[l];
     if (t < SQT) {
         uint32_t e = t < nQ ? entries[qb + t] : 0u;
         ent_s[t] = e;
         qrow_s[t] = t < nQ ? (int32_t)(e / (uint32_t)nprobe) : -1;
+        qlim_s[t] = lim && t < nQ ? (int32_t)lim[e] : len;
     }
-    const int len = (int)list_len[l];
     const int64_t row0 = list_off[l];
     __syncthreads();
 
@@ -421,8 +453,9 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
             // thread (q = t>>2, s = t&3) owns codes s, s+4, ... of query q
             const int q = t >> 2, s4 = t & 3;
             if (q < nQ) {
+                const int nvq = min(nv, qlim_s[q] - v0);
 #pragma unroll 4
-                for (int j = s4; j < nv; j += 4) {
+                for (int j = s4; j < nvq; j += 4) {
                     float dis = Ds[q * (SVT + 1) + j];
                     float k1 = L2 ? dis : -dis;
                     if (k1 < FLT_MAX) {
@@ -445,7 +478,7 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
                     float k1;
                     long long k2;
                     to_key(L2 ? 1 : 0, dis, my_id, k1, k2);
-                    if (!lane_ok || !key_admissible(k1)) {
+                    if (!lane_ok || v0 + lane >= qlim_s[q] || !key_admissible(k1)) {
                         k1 = WS_INF;
                         k2 = WS_NOID;
                     }
@@ -511,11 +544,11 @@ static void launch_scan(bool l2, int64_t grid, hipStream_t s, const float* x, in
     if (l2)
         k_ivf_flat_scan<true, KQ><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
                 x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, d, nprobe, k, b.bucket_off,
-                b.item_off, b.entries, pk1, pk2);
+                b.item_off, b.entries, b.lim, pk1, pk2);
     else
         k_ivf_flat_scan<false, KQ><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
                 x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, d, nprobe, k, b.bucket_off,
-                b.item_off, b.entries, pk1, pk2);
+                b.item_off, b.entries, b.lim, pk1, pk2);
 }
 
 void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const int64_t* ids,

@@ -105,8 +105,8 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         int nprobe, float coef, int obits, const uint32_t* __restrict__ bucket_off,
         const uint32_t* __restrict__ item_off, const ItemDesc* __restrict__ item_desc,
         const uint32_t* __restrict__ item_entries, uint32_t max_items,
-        uint32_t* __restrict__ keys, ProbeRec* __restrict__ recs,
-        unsigned long long* __restrict__ ftrace) {
+        const uint32_t* __restrict__ lim, uint32_t* __restrict__ keys,
+        ProbeRec* __restrict__ recs, unsigned long long* __restrict__ ftrace) {
     const unsigned long long ft0 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     // two code tiles (double buffer), row stride CSB bytes = (Y3 ? 4 : 2) * DB + 16
     __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * ((Y3 ? 4 : 2) * 16 * NS + 16)];
@@ -243,6 +243,8 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     if (qvalid) {
         // raw 32-bit keys (the re-rank decodes the approx bracket and the row)
         const int64_t e = ent_s[qloc];
+        // max_codes: only a prefix of the list is scanned for this query
+        const uint32_t elen = lim ? min((uint32_t)len, lim[e]) : (uint32_t)len;
         uint32_t* ko = keys + e * (4 * KT) + slot * KT;
 #pragma unroll
         for (int i = 0; i < KT; i++) {
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             const uint32_t ord = key & lowmask;
             const int r = (int)(ord & 15u);
             const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-            ko[i] = (key != 0xffffffffu && row < (uint32_t)len) ? key : 0xffffffffu;
+            ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
         }
         if (slot == 0) {
             // the list's largest margin bounds every kept row's margin:
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             }
             pr.mmax = mmax;
             pr.off = (uint32_t)row0;
-            pr.len = (uint32_t)len;
+            pr.len = elen;
             pr.pad = 0u;
             recs[e] = pr;
         }
@@ -707,12 +709,13 @@ struct FullStream {
     const float* xq;
     const float* codes;
     const int64_t* ids;
+    const uint32_t* lim;  // max_codes: rows scanned per probe (nullptr: all)
     template <class F>
     __device__ __forceinline__ void for_each(F f) const {
         for (int r = 0; r < nprobe; r++) {
             const int lst = asg[r];
             if (lst < 0 || lst >= nlist) continue;
-            const int len = (int)list_len[lst];
+            const int len = (int)(lim ? min(lim[r], list_len[lst]) : list_len[lst]);
             for (int v0 = 0; v0 < len; v0 += 64) {
                 float k1 = WS_INF;
                 long long k2 = WS_NOID, rank = 0;
@@ -736,28 +739,30 @@ __global__ __launch_bounds__(64) void k_ivf_exact_fallback(
         const uint32_t* __restrict__ flags, const int32_t* __restrict__ assign,
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
         const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
-        const int64_t* __restrict__ ids, int d, int nprobe, int k, float* __restrict__ D,
-        int64_t* __restrict__ I) {
+        const int64_t* __restrict__ ids, int d, int nprobe, int k,
+        const uint32_t* __restrict__ lim, float* __restrict__ D, int64_t* __restrict__ I) {
     const int64_t q = blockIdx.x;
     if (flags[q] == 0u) return;
     FullStream<L2> st{assign + q * nprobe, list_off, list_len, nlist, nprobe, d, ldc,
-                      (int)threadIdx.x, x + q * ldx, codes, ids};
+                      (int)threadIdx.x, x + q * ldx, codes, ids,
+                      lim ? lim + q * nprobe : nullptr};
     exact_topk_resolve(st, k, L2 ? 1 : 0, (int)threadIdx.x, true, D + q * k, I + q * k);
 }
 
 void ivf_exact_fallback(const uint32_t* flags, const int32_t* assign, const uint32_t* list_off,
                         const uint32_t* list_len, int nlist, const float* x, int ldx,
                         const float* codes, int ldc, const int64_t* ids, int d, int64_t n,
-                        int nprobe, int k, int metric_l2, float* D, int64_t* I, hipStream_t s) {
+                        int nprobe, int k, int metric_l2, const uint32_t* lim, float* D,
+                        int64_t* I, hipStream_t s) {
     if (n <= 0) return;
     if (metric_l2)
         k_ivf_exact_fallback<true><<<dim3((unsigned)n), dim3(64), 0, s>>>(
                 flags, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, nprobe, k,
-                D, I);
+                lim, D, I);
     else
         k_ivf_exact_fallback<false><<<dim3((unsigned)n), dim3(64), 0, s>>>(
                 flags, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, nprobe, k,
-                D, I);
+                lim, D, I);
     HIP_LAUNCH_CHECK();
 }
 
@@ -874,12 +879,12 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
             k_ivf_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
-                    b.item_desc, b.item_entries, (uint32_t)max_items, keys, recs, ftrace);    \
+                    b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, keys, recs, ftrace);    \
         else                                                                                  \
             k_ivf_bf3_filter<L2V, KTV, NSV, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(\
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
-                    b.item_desc, b.item_entries, (uint32_t)max_items, keys, recs, ftrace);    \
+                    b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, keys, recs, ftrace);    \
     } while (0)
 #define LAUNCH_A(L2V, KTV)                     \
     do {                                       \

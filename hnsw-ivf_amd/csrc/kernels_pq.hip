@@ -32,8 +32,9 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan(
         int dsub, const uint8_t* __restrict__ codes, int code_stride,
         const float* __restrict__ terms, const int64_t* __restrict__ ids,
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
-        const int32_t* __restrict__ assign, const float* __restrict__ coarse_dis, int nprobe,
-        int k, int by_residual, float* __restrict__ D, int64_t* __restrict__ I) {
+        const int32_t* __restrict__ assign, const float* __restrict__ coarse_dis,
+        const uint32_t* __restrict__ lim, int nprobe, int k, int by_residual,
+        float* __restrict__ D, int64_t* __restrict__ I) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* T = smem;                    // [M * ksub]
     float* xq = T + M * ksub;           // [M * dsub]
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan(
     for (int r = w; r < nprobe; r += 4) {
         const int lst = assign[q * nprobe + r];
         if (lst < 0 || lst >= nlist) continue;
-        const int len = (int)list_len[lst];
+        const int len = (int)(lim ? min(lim[q * nprobe + r], list_len[lst]) : list_len[lst]);
         if (len == 0) continue;
         const float dis0 = by_residual ? coarse_dis[q * nprobe + r] : 0.f;
         const int64_t row0 = list_off[lst];
@@ -140,8 +141,8 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan_m(
         const uint8_t* __restrict__ codes, const float* __restrict__ terms,
         const int64_t* __restrict__ ids, const uint32_t* __restrict__ list_off,
         const uint32_t* __restrict__ list_len, int nlist, const int32_t* __restrict__ assign,
-        const float* __restrict__ coarse_dis, int nprobe, int k, int by_residual,
-        float* __restrict__ D, int64_t* __restrict__ I) {
+        const float* __restrict__ coarse_dis, const uint32_t* __restrict__ lim, int nprobe,
+        int k, int by_residual, float* __restrict__ D, int64_t* __restrict__ I) {
     constexpr int CS = (M + 3) & ~3;  // code stride (bytes)
     constexpr int NW = CS / 4;        // 32-bit words per code
     __shared__ float T[M * 256];
@@ -183,7 +184,8 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan_m(
     if (t < nprobe) {
         const int lst = assign[q * nprobe + t];
         const bool ok = lst >= 0 && lst < nlist;
-        p_len[t] = ok ? list_len[lst] : 0u;
+        // max_codes: a prefix of the list (lim), faiss/IndexIVF.cpp:546-550
+        p_len[t] = ok ? (lim ? min(lim[q * nprobe + t], list_len[lst]) : list_len[lst]) : 0u;
         p_off[t] = ok ? list_off[lst] : 0u;
         p_d0[t] = by_residual ? coarse_dis[q * nprobe + t] : 0.f;
     }
@@ -329,8 +331,8 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan_m(
 void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int ksub, int dsub,
                 const uint8_t* codes, const float* terms, const int64_t* ids,
                 const uint32_t* list_off, const uint32_t* list_len, int nlist,
-                const int32_t* assign, const float* coarse_dis, int64_t n, int nprobe, int k,
-                int by_residual, float* D, int64_t* I, hipStream_t s) {
+                const int32_t* assign, const float* coarse_dis, const uint32_t* lim, int64_t n,
+                int nprobe, int k, int by_residual, float* D, int64_t* I, hipStream_t s) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
     FAISS_THROW_IF_NOT_MSG(nprobe >= 1 && nprobe <= 64, "nprobe must be in [1, 64] on this path");
@@ -341,7 +343,7 @@ void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int k
     if (M == MV) {                                                                             \
         k_ivfpq_scan_m<MV><<<dim3((unsigned)n), dim3(256), 0, s>>>(                            \
                 x, ldx, pq_centroids, dsub, codes, terms, ids, list_off, list_len, nlist, assign, \
-                coarse_dis, nprobe, k, by_residual, D, I);                                     \
+                coarse_dis, lim, nprobe, k, by_residual, D, I);                                \
         HIP_LAUNCH_CHECK();                                                                    \
         return;                                                                                \
     }
@@ -353,7 +355,7 @@ void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int k
     FAISS_THROW_IF_NOT_MSG(lds <= 160 * 1024, "PQ LUT does not fit in LDS");
     k_ivfpq_scan<<<dim3((unsigned)n), dim3(256), lds, s>>>(
             x, ldx, pq_centroids, M, ksub, dsub, codes, code_stride, terms, ids, list_off,
-            list_len, nlist, assign, coarse_dis, nprobe, k, by_residual, D, I);
+            list_len, nlist, assign, coarse_dis, lim, nprobe, k, by_residual, D, I);
     HIP_LAUNCH_CHECK();
 }
 

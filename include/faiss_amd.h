@@ -268,11 +268,19 @@ struct IndexIVF : Index {
                                   bool store_pairs, const SearchParametersIVF* params,
                                   IndexIVFStats* ivf_stats,
                                   QueryLatencyStats* per_query_stats) const;
-    // device form (int32 assignments)
+    // device form (int32 assignments).  lim (optional, max_codes): rows of
+    // each (query, probe) list scanned, from apply_max_codes
     virtual void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k,
                                            int nprobe, const int32_t* assign,
                                            const float* centroid_dis, float* distances,
-                                           idx_t* labels, hipStream_t stream) const = 0;
+                                           idx_t* labels, hipStream_t stream,
+                                           const uint32_t* lim = nullptr) const = 0;
+    // max_codes (faiss/IndexIVF.cpp:595-631): per query, the probe prefix
+    // scanned before nscan reaches max_codes; returns the assignment with the
+    // dropped probes set to -1 and sets *lim (both in index scratch)
+    const int32_t* apply_max_codes(idx_t n, int nprobe, const int32_t* assign,
+                                   size_t max_codes, const uint32_t** lim,
+                                   hipStream_t stream) const;
     void quantize_device(idx_t n, const float* x, int ldx, int nprobe, float* coarse_dis,
                          int32_t* assign, const SearchParameters* qparams,
                          hipStream_t stream) const;
@@ -296,7 +304,7 @@ struct IndexIVF : Index {
     // scratch
     mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_counts_, s_boff_, s_ioff_, s_cur_, s_ent_,
             s_pk1_, s_pk2_, s_q_;
-    mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_;
+    mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_;
 
    private:
     idx_t search_chunk(idx_t n, size_t np, idx_t k) const;
@@ -314,8 +322,8 @@ struct IndexIVFFlat : IndexIVF {
                         uint8_t* codes) const override;
     void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
                                    const int32_t* assign, const float* centroid_dis,
-                                   float* distances, idx_t* labels,
-                                   hipStream_t stream) const override;
+                                   float* distances, idx_t* labels, hipStream_t stream,
+                                   const uint32_t* lim = nullptr) const override;
     void reconstruct(idx_t key, float* recons) const override;
 
    protected:
@@ -344,8 +352,8 @@ struct IndexIVFPQ : IndexIVF {
                         uint8_t* codes) const override;
     void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
                                    const int32_t* assign, const float* centroid_dis,
-                                   float* distances, idx_t* labels,
-                                   hipStream_t stream) const override;
+                                   float* distances, idx_t* labels, hipStream_t stream,
+                                   const uint32_t* lim = nullptr) const override;
     // faiss/IndexIVFPQ.cpp:364-459: choose 0/1 like the reference (the GPU
     // path uses per-code terms either way)
     void precompute_table();

@@ -115,6 +115,16 @@ int faiss_SearchParametersIVF_new_with(
 void faiss_SearchParametersIVF_free(FaissSearchParametersIVF* obj);
 size_t faiss_SearchParametersIVF_nprobe(const FaissSearchParametersIVF*);
 void faiss_SearchParametersIVF_set_nprobe(FaissSearchParametersIVF*, size_t);
+/* c_api/IndexIVF_c.h:35 (FAISS_DECLARE_GETTER_SETTER max_codes); 0 = unlimited */
+size_t faiss_SearchParametersIVF_max_codes(const FaissSearchParametersIVF*);
+void faiss_SearchParametersIVF_set_max_codes(FaissSearchParametersIVF*, size_t);
+/* extension: IndexIVF::max_codes / parallel_mode (faiss/IndexIVF.h:200-214;
+ * the reference C API has no binding; ParameterSpace "max_codes" sets the
+ * former, faiss/AutoTune.cpp:530-535).  parallel_mode 0 and 3 run here. */
+size_t faiss_amd_IndexIVF_max_codes(const FaissIndexIVF*);
+void faiss_amd_IndexIVF_set_max_codes(FaissIndexIVF*, size_t);
+int faiss_amd_IndexIVF_parallel_mode(const FaissIndexIVF*);
+void faiss_amd_IndexIVF_set_parallel_mode(FaissIndexIVF*, int);
 /* extension: efSearch of an HNSW coarse quantizer for this call, 0 = keep
  * (reference SearchParametersIVF::quantizer_params -> SearchParametersHNSW,
  * faiss/IndexIVF.h:77-85, faiss/impl/HNSW.h:46-52) */

@@ -505,9 +505,21 @@ void oracle_ivfpq_prepare(oracle_ivf_t* ivf) {
 }
 
 /* ------------------------------------------------------------ preassigned */
+/* faiss/IndexIVF.cpp:595-631 (parallel_mode 0): probes in coarse order; with
+ * max_codes > 0 a list is cut to max_codes - nscan rows (scan_one_list's
+ * list_size_max, :546-550) and the scan stops once nscan >= max_codes. */
 void oracle_ivf_search_preassigned(const oracle_ivf_t* ivf, size_t n, const float* x, size_t k,
                                    size_t nprobe, const int64_t* keys, const float* coarse_dis,
                                    float* D, int64_t* I, int nthreads) {
+    oracle_ivf_search_preassigned_mc(ivf, n, x, k, nprobe, keys, coarse_dis, 0, D, I, NULL,
+                                     nthreads);
+}
+
+void oracle_ivf_search_preassigned_mc(const oracle_ivf_t* ivf, size_t n, const float* x,
+                                      size_t k, size_t nprobe, const int64_t* keys,
+                                      const float* coarse_dis, int64_t max_codes, float* D,
+                                      int64_t* I, int64_t* ndis, int nthreads) {
+    int64_t ndis_tot = 0;
     const int cmax = ivf->metric == 1;
     const int d = ivf->d;
     const int M = ivf->pq_M;
@@ -518,9 +530,10 @@ void oracle_ivf_search_preassigned(const oracle_ivf_t* ivf, size_t n, const floa
         float* sim2 = M ? (float*)malloc(sizeof(float) * M * ksub) : NULL;
         float* sim = M ? (float*)malloc(sizeof(float) * M * ksub) : NULL;
         float* resid = (float*)malloc(sizeof(float) * d);
-#pragma omp for schedule(dynamic, 8)
+#pragma omp for schedule(dynamic, 8) reduction(+ : ndis_tot)
         for (int64_t i = 0; i < (int64_t)n; i++) {
             const float* xi = x + i * d;
+            int64_t nscan = 0;
             float* hv = D + i * k;
             int64_t* hi = I + i * k;
             oracle_heap_heapify(cmax, k, hv, hi);
@@ -544,6 +557,8 @@ void oracle_ivf_search_preassigned(const oracle_ivf_t* ivf, size_t n, const floa
                 if (key < 0 || key >= ivf->nlist) continue;
                 int64_t l0 = ivf->list_off[key], l1 = ivf->list_off[key + 1];
                 if (l1 == l0) continue;
+                if (max_codes > 0 && l1 - l0 > max_codes - nscan) l1 = l0 + (max_codes - nscan);
+                nscan += l1 - l0;
                 if (!M) {
                     /* IVFFlatScanner::scan_codes */
                     for (int64_t j = l0; j < l1; j++) {
@@ -580,13 +595,16 @@ void oracle_ivf_search_preassigned(const oracle_ivf_t* ivf, size_t n, const floa
                             oracle_heap_replace_top(cmax, k, hv, hi, dis, ivf->ids[j]);
                     }
                 }
+                if (max_codes > 0 && nscan >= max_codes) break;
             }
+            ndis_tot += nscan;
             oracle_heap_reorder(cmax, k, hv, hi);
         }
         free(sim2);
         free(sim);
         free(resid);
     }
+    if (ndis) *ndis = ndis_tot;
 }
 
 void oracle_ivf_search(const oracle_ivf_t* ivf, size_t n, const float* x, size_t k,

@@ -105,6 +105,12 @@ void oracle_ivfpq_prepare(oracle_ivf_t* ivf);
 void oracle_ivf_search_preassigned(const oracle_ivf_t* ivf, size_t n, const float* x, size_t k,
                                    size_t nprobe, const int64_t* keys, const float* coarse_dis,
                                    float* D, int64_t* I, int nthreads);
+/* the same with max_codes (0 = unlimited, IndexIVF.cpp:452-454, :609-622)
+ * and the ndis total (indexIVF_stats.ndis) */
+void oracle_ivf_search_preassigned_mc(const oracle_ivf_t* ivf, size_t n, const float* x,
+                                      size_t k, size_t nprobe, const int64_t* keys,
+                                      const float* coarse_dis, int64_t max_codes, float* D,
+                                      int64_t* I, int64_t* ndis, int nthreads);
 
 /* IndexIVF::search: nslices query slices (the reference uses
  * min(omp_max_threads, n)), coarse per slice, then search_preassigned. */

@@ -56,6 +56,9 @@ def lib():
         L.oracle_ivf_search_preassigned.argtypes = [C.POINTER(IVFStruct), C.c_size_t, _P,
                                                     C.c_size_t, C.c_size_t, _P, _P, _P, _P,
                                                     C.c_int]
+        L.oracle_ivf_search_preassigned_mc.argtypes = [C.POINTER(IVFStruct), C.c_size_t, _P,
+                                                       C.c_size_t, C.c_size_t, _P, _P,
+                                                       C.c_int64, _P, _P, _P, C.c_int]
         L.oracle_ivf_search.argtypes = [C.POINTER(IVFStruct), C.c_size_t, _P, C.c_size_t,
                                         C.c_size_t, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
         L.oracle_ivf_search_fast.argtypes = [C.POINTER(IVFStruct), C.c_size_t, _P, C.c_size_t,
@@ -217,17 +220,19 @@ class IVFOracle:
                                 _p(I), _p(CI), _p(CD), nthreads or nthreads_default())
         return D, I, CD, CI
 
-    def search_preassigned(self, x, k, keys, coarse_dis, nthreads=None):
+    def search_preassigned(self, x, k, keys, coarse_dis, nthreads=None, max_codes=0,
+                           return_ndis=False):
         x = np.ascontiguousarray(x, np.float32)
         keys = np.ascontiguousarray(keys, np.int64)
         coarse_dis = np.ascontiguousarray(coarse_dis, np.float32)
         n, nprobe = keys.shape
         D = np.empty((n, k), np.float32)
         I = np.empty((n, k), np.int64)
-        lib().oracle_ivf_search_preassigned(C.byref(self.s), n, _p(x), k, nprobe, _p(keys),
-                                            _p(coarse_dis), _p(D), _p(I),
-                                            nthreads or nthreads_default())
-        return D, I
+        nd = np.zeros(1, np.int64)
+        lib().oracle_ivf_search_preassigned_mc(C.byref(self.s), n, _p(x), k, nprobe, _p(keys),
+                                               _p(coarse_dis), max_codes, _p(D), _p(I), _p(nd),
+                                               nthreads or nthreads_default())
+        return (D, I, int(nd[0])) if return_ndis else (D, I)
 
     def search_fast(self, x, k, nprobe, nthreads=None):
         x = np.ascontiguousarray(x, np.float32)
