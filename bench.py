@@ -50,7 +50,7 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector == fp32 MFMA peak
 PEAK_HBM_GBS = 8000.0
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 # dominant kernel per workload (device symbol substring) for the PMC traffic
-DOMINANT = {"flat": "k_ivf_bf3_filter", "pq": "k_ivfpq_scan"}
+DOMINANT = {"flat": "k_ivf_bf3_filter", "pq": "k_ivfpq_scan", "pqm": "k_ivfpq_filter"}
 
 
 def pmc_traffic(config, kernel_sub):
@@ -188,6 +188,9 @@ def main():
     # ---- dominant kernel: HIP events over the timed region (lib-side)
     kt = index.kernel_times()
     scan_name = "ivfpq_scan" if "PQ" in cfg["desc"] else "ivf_flat_scan"
+    pq_mfma = any(nm == "ivfpq_filter" for (nm, _, _) in kt)
+    if pq_mfma:
+        scan_name = "ivfpq_filter"  # list-centric bf16 MFMA filter over decoded codes
     scan = [ms for (nm, ms, _) in kt if nm == scan_name]
     # a step may launch the kernel more than once (query chunks): the per-step
     # kernel time is the sum over the step's launches, priced against the
@@ -205,8 +208,9 @@ def main():
     cand_per_q = float(sizes[ci_h.cpu().numpy().astype(np.int64)].sum()) / nq
     cands = cand_per_q * nq_launch
     is_pq = "PQ" in cfg["desc"]
-    traffic, traffic_src = pmc_traffic(args.config, DOMINANT["pq" if is_pq else "flat"])
-    if is_pq:
+    traffic, traffic_src = pmc_traffic(
+        args.config, DOMINANT["pqm" if pq_mfma else "pq" if is_pq else "flat"])
+    if is_pq and not pq_mfma:
         M = index.pq_info()["M"]
         work = cands * M  # code bytes streamed (LUT-gather bound)
         achieved = work / (scan_ms * 1e-3) / 1e9
@@ -215,6 +219,22 @@ def main():
                     "kernel": scan_name, "kernel_ms_per_step": scan_ms,
                     "launches_per_step": launches_per_step,
                     "algorithmic_bytes_per_step": work}
+    elif is_pq:
+        # IVF-PQ on the list-centric filter: codes are decoded to bf16 and
+        # multiplied against the queries' bf16 hi + lo split (2 MFMA passes),
+        # 2 * 2d bf16 flops per candidate, priced against the dense bf16 peak;
+        # the streamed-code model (M bytes per candidate) is reported beside it
+        M = index.pq_info()["M"]
+        dpad = -(-d // 16) * 16
+        work = cands * 2 * 2.0 * dpad
+        achieved = work / (scan_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
+                    "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
+                    "kernel": scan_name, "kernel_ms_per_step": scan_ms,
+                    "launches_per_step": launches_per_step, "mfma_dtype": "bf16",
+                    "algorithmic_flops_per_step": work, "flops_per_candidate": 4 * dpad,
+                    "streamed_code_bytes_per_step": cands * M,
+                    "streamed_code_gbs": cands * M / (scan_ms * 1e-3) / 1e9}
     else:
         # The filter runs on bf16 MFMA: every fp32 operand pair is split
         # (bf16x2: codes hi x queries hi+lo = 2 products; bf16x3: 3), so its

@@ -120,6 +120,7 @@ def _declare(L):
         "faiss_IndexIVF_set_nprobe": (None, [_P, C.c_size_t]),
         "faiss_SearchParametersIVF_max_codes": (C.c_size_t, [_P]),
         "faiss_SearchParametersIVF_set_max_codes": (None, [_P, C.c_size_t]),
+        "faiss_amd_IndexIVFPQ_set_use_precomputed_table": (C.c_int, [_P, C.c_int]),
         "faiss_amd_IndexIVF_max_codes": (C.c_size_t, [_P]),
         "faiss_amd_IndexIVF_set_max_codes": (None, [_P, C.c_size_t]),
         "faiss_amd_IndexIVF_parallel_mode": (C.c_int, [_P]),
@@ -556,6 +557,14 @@ class IndexIVFPQ(IndexIVF):
                                                C.byref(up)))
         return dict(M=M.value, nbits=nb.value, by_residual=bool(br.value),
                     use_precomputed_table=up.value)
+
+    @property
+    def use_precomputed_table(self):
+        return self.pq_info()["use_precomputed_table"]
+
+    @use_precomputed_table.setter
+    def use_precomputed_table(self, v):
+        _check(lib().faiss_amd_IndexIVFPQ_set_use_precomputed_table(self.h, int(v)))
 
     @property
     def pq_centroids(self):

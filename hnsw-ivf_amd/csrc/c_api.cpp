@@ -331,6 +331,14 @@ int faiss_amd_IndexIVFPQ_info(const FaissIndexIVFPQ* index, size_t* M, size_t* n
     *use_precomputed_table = pq->use_precomputed_table;
     C_CATCH
 }
+int faiss_amd_IndexIVFPQ_set_use_precomputed_table(FaissIndexIVFPQ* index, int v) {
+    C_TRY auto pq = dynamic_cast<IndexIVFPQ*>(IX(index));
+    FAISS_THROW_IF_NOT_MSG(pq, "not an IndexIVFPQ");
+    FAISS_THROW_IF_NOT_MSG(v == 0 || (v == 1 && pq->by_residual && pq->metric_type == faiss_amd::METRIC_L2),
+                           "use_precomputed_table: 0, or 1 for by-residual L2");
+    pq->use_precomputed_table = v;
+    C_CATCH
+}
 
 // ---------------- IndexHNSW
 int faiss_amd_IndexHNSWFlat_new_with(FaissIndexHNSW** p_index, int d, int M,

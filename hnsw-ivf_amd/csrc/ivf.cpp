@@ -189,8 +189,11 @@ void IndexIVF::quantize_device(idx_t n, const float* x, int ldx, int np, float* 
 // PQ scan keeps none)
 idx_t IndexIVF::search_chunk(idx_t n, size_t np, idx_t k) const {
     const bool pq = dynamic_cast<const IndexIVFPQ*>(this) != nullptr;
-    const size_t per_q = pq ? np * 16 : np * (size_t)std::max<idx_t>(k, 32) * 12 + np * 16;
-    idx_t qchunk = std::max<idx_t>(1, (idx_t)(((size_t)1 << 30) / per_q));
+    // Flat: direct-scan partials (k keys + ids per probe) or filter keys;
+    // PQ: filter keys (<= 32 per probe) + probe records + buckets
+    const size_t per_q = pq ? np * (32 * 4 + 32 + 16) + 16
+                            : np * (size_t)std::max<idx_t>(k, 32) * 12 + np * 16;
+    idx_t qchunk = std::max<idx_t>(1, (idx_t)(((size_t)4 << 30) / per_q));
     return std::max<idx_t>(1, std::min<idx_t>(qchunk, n));
 }
 
@@ -685,6 +688,38 @@ void IndexIVFPQ::upload_extra() const {
         kern::ivfpq_terms(d_codes_.as<uint8_t>(), d_row_list_.as<uint32_t>(), arena_rows_,
                           d_cent_.as<float>(), ldc, d_pq_.as<float>(), (int)pq.M, (int)pq.ksub,
                           (int)pq.dsub, d_terms_.as<float>(), s);
+    // list-centric MFMA scan: decode table, row / list norms (any k, nprobe)
+    pq_mfma_ready_ = false;
+    if (by_residual && metric_type == METRIC_L2 && pq.ksub == 256 &&
+        kern::ivfpq_mfma_eligible(d, (int)pq.M, 1, 1) && arena_rows_ > 0) {
+        const size_t rows = arena_rows_;
+        d_dec_.reserve(sizeof(uint16_t) * pq.centroids.size());
+        d_prn_.reserve(sizeof(float) * rows);
+        d_prr_.reserve(sizeof(float) * rows);
+        d_lRmax_.reserve(sizeof(float) * nlist);
+        d_lrmax_.reserve(sizeof(float) * nlist);
+        d_cnorm_.reserve(sizeof(float) * nlist);
+        kern::pq_decode_prep(d_pq_.as<float>(), (int)pq.M, (int)pq.dsub, d_codes_.as<uint8_t>(),
+                             device_code_stride(), (int64_t)rows, d_dec_.ptr, d_prn_.as<float>(),
+                             d_prr_.as<float>(), s);
+        kern::ivf_list_ynmax(d_prn_.as<float>(), d_list_off_.as<uint32_t>(),
+                             d_list_len_.as<uint32_t>(), (int)nlist, d_lRmax_.as<float>(), s);
+        kern::ivf_list_ynmax(d_prr_.as<float>(), d_list_off_.as<uint32_t>(),
+                             d_list_len_.as<uint32_t>(), (int)nlist, d_lrmax_.as<float>(), s);
+        std::vector<float> cn(nlist);
+        for (size_t l = 0; l < nlist; l++) {
+            double a = 0.0;
+            for (int j = 0; j < d; j++) a += (double)cent[l * ldc + j] * cent[l * ldc + j];
+            cn[l] = (float)(std::sqrt(a) * (1.0 + 1e-6));
+        }
+        HIP_CHECK(hipMemcpyAsync(d_cnorm_.ptr, cn.data(), sizeof(float) * nlist,
+                                 hipMemcpyHostToDevice, s));
+        size_t mx = 0;
+        for (size_t li = 0; li < nlist; li++) mx = std::max(mx, invlists->list_size(li));
+        pq_obits_ = kern::ivf_bf3_obits((uint32_t)std::min<size_t>(mx, 0xffffffffu));
+        pq_mfma_ready_ = pq_obits_ <= 14;
+        HIP_CHECK(hipStreamSynchronize(s));  // cn is a host temporary
+    }
 }
 
 void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
@@ -694,6 +729,74 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_MSG(metric_type == METRIC_L2, "IVFPQ inner product not supported on GPU");
     sync_device();
+    // list-centric bf16 MFMA filter + exact re-rank in the reference's table
+    // arithmetic (default where eligible; FAISS_AMD_PQ_SCAN=lut forces the
+    // query-centric LUT scan below)
+    const char* penv = getenv("FAISS_AMD_PQ_SCAN");
+    const bool lut = penv && !strcmp(penv, "lut");
+    if (!lut && pq_mfma_ready_ && kern::ivfpq_mfma_eligible(d, (int)pq.M, (int)k, np)) {
+        std::lock_guard<std::recursive_mutex> g(mu_);
+        const int QT = 64;
+        s_counts_.reserve(sizeof(uint32_t) * nlist);
+        s_cur_.reserve(sizeof(uint32_t) * std::max<idx_t>(n * np, 1));
+        s_boff_.reserve(sizeof(uint32_t) * (nlist + 1));
+        s_ioff_.reserve(sizeof(uint32_t) * (nlist + 1));
+        s_ent_.reserve(sizeof(uint32_t) * n * np);
+        kern::IVFBuckets b{s_counts_.as<uint32_t>(), s_boff_.as<uint32_t>(),
+                           s_ioff_.as<uint32_t>(), s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
+        b.lim = lim;
+        const int KE = kern::ivf_mfma_kq((int)k, d);
+        s_pkeys_.reserve(sizeof(uint32_t) * n * np * KE);
+        s_precs_.reserve(sizeof(kern::ProbeRec) * n * np);
+        b.mark_keys = s_pkeys_.as<uint32_t>();
+        b.mark_recs = s_precs_.as<kern::ProbeRec>();
+        b.mark_ke = KE;
+        const int64_t mi = kern::ivf_max_items(n, np, (int)nlist, QT);
+        s_idesc_.reserve(sizeof(kern::ItemDesc) * mi);
+        s_ient_.reserve(sizeof(uint32_t) * mi * QT);
+        b.item_desc = s_idesc_.as<kern::ItemDesc>();
+        b.item_entries = s_ient_.as<uint32_t>();
+        kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), d_list_off_.as<uint32_t>(),
+                         (int)nlist, QT, b, s);
+        const bool dbg = getenv("FAISS_AMD_IVF_STATS") != nullptr;
+        s_pflags_.reserve(4 * sizeof(uint32_t));
+        if (dbg) HIP_CHECK(hipMemsetAsync(s_pflags_.ptr, 0, 4 * sizeof(uint32_t), s));
+        int KT = 0;
+        {
+            ScopedKernelTimer tm(&ktimes, "ivfpq_filter", 0.0, s);
+            kern::ivfpq_filter(x, ldx, d, (int)pq.M, d_dec_.ptr, d_codes_.as<uint8_t>(),
+                               d_terms_.as<float>(), centroid_dis, d_cnorm_.as<float>(),
+                               d_lrmax_.as<float>(), d_lRmax_.as<float>(), (int)nlist, n, np,
+                               (int)k, pq_obits_, b, mi, s_pkeys_.as<uint32_t>(),
+                               s_precs_.as<kern::ProbeRec>(), &KT, s);
+        }
+        {
+            ScopedKernelTimer tm(&ktimes, "ivfpq_rerank", 0.0, s);
+            kern::PQArgs pa;
+            pa.pq_cent = d_pq_.as<float>();
+            pa.cent = d_cent_.as<float>();
+            pa.ldcent = ld();
+            pa.cdis = centroid_dis;
+            pa.codes = d_codes_.as<uint8_t>();
+            pa.cs = device_code_stride();
+            pa.M = (int)pq.M;
+            pa.table1 = use_precomputed_table == 1 ? 1 : 0;
+            kern::ivfpq_rerank(s_pkeys_.as<uint32_t>(), s_precs_.as<kern::ProbeRec>(), x, ldx, d,
+                               d_ids_.as<int64_t>(), pa, (int)pq.dsub, n, np, KT, pq_obits_,
+                               (int)k, distances, labels,
+                               dbg ? s_pflags_.as<uint32_t>() : nullptr, s);
+        }
+        if (dbg) {
+            uint32_t st[4];
+            HIP_CHECK(hipMemcpyAsync(st, s_pflags_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            fprintf(stderr,
+                    "[faiss_amd] ivfpq mfma scan: nq=%lld survivors/q=%.2f failing streams/q=%.4f "
+                    "overflow queries=%u general-resolve queries=%u\n",
+                    (long long)n, st[0] / (double)n, st[1] / (double)n, st[2], st[3]);
+        }
+        return;
+    }
     ScopedKernelTimer tm(&ktimes, "ivfpq_scan", 0.0, s);
     kern::ivfpq_scan(x, ldx, d_pq_.as<float>(), (int)pq.M, (int)pq.ksub, (int)pq.dsub,
                      d_codes_.as<uint8_t>(), d_terms_.as<float>(), d_ids_.as<int64_t>(),

@@ -122,6 +122,31 @@ void probe_limits(const int32_t* assign, int64_t n, int nprobe, const uint32_t* 
                   hipStream_t s);
 void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
                 const uint32_t* list_off, int nlist, int QT, IVFBuckets b, hipStream_t s);
+// IVF-PQ list-centric MFMA filter + exact re-rank (kernels_pq_mfma.hip)
+struct PQArgs {
+    const float* pq_cent = nullptr;  // [M][256][dsub] fp32
+    const float* cent = nullptr;     // coarse centroids [nlist][ldcent]
+    int ldcent = 0;
+    const float* cdis = nullptr;     // coarse distances [n][nprobe] (table 1 dis0)
+    const uint8_t* codes = nullptr;  // arena codes, cs bytes per row
+    int cs = 0;
+    int M = 0;
+    int table1 = 0;  // use_precomputed_table == 1 (else table 0, by residual)
+};
+bool ivfpq_mfma_eligible(int d, int M, int k, int nprobe);
+double ivfpq_mfma_coef(int d, int M);
+// bf16 decode table ([M][256][dsub] bf16) and per-row |y_R|, |y_R - bf16(y_R)|
+void pq_decode_prep(const float* pq_cent, int M, int dsub, const uint8_t* codes, int cs,
+                    int64_t rows, void* dec, float* rnorm, float* rres, hipStream_t s);
+void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const uint8_t* codes,
+                  const float* terms, const float* cdis, const float* cnorm, const float* lrmax,
+                  const float* lRmax, int nlist, int64_t n, int nprobe, int k, int obits,
+                  const IVFBuckets& b, int64_t max_items, uint32_t* keys, ProbeRec* recs,
+                  int* kt_out, hipStream_t s);
+void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx, int d,
+                  const int64_t* ids, const PQArgs& pa, int dsub, int64_t n, int nprobe, int KT,
+                  int obits, int k, float* D, int64_t* I, uint32_t* stats, hipStream_t s);
+
 // IndexIVFStats counters of a batch (faiss/IndexIVF.cpp:1184-1198):
 // stats[0] += non-empty lists visited, stats[1] += codes scanned (device)
 void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_len, int nlist,

@@ -15,6 +15,8 @@
 // second kernel merges the nprobe partial lists of each query.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cfloat>
 
 #include "common.h"
@@ -165,31 +167,50 @@ __global__ void k_bucket_fill(const int32_t* __restrict__ assign, int64_t total,
     }
 }
 
-__global__ void k_ivf_visit_stats(const int32_t* __restrict__ assign, int64_t total,
-                                  const uint32_t* __restrict__ list_len, int nlist,
-                                  const uint32_t* __restrict__ lim,
-                                  unsigned long long* __restrict__ stats) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t len = 0;
-    if (e < total) {
+// grid-stride partial counts per thread, one atomic pair per work-group
+__global__ __launch_bounds__(256) void k_ivf_visit_stats(const int32_t* __restrict__ assign,
+                                                         int64_t total,
+                                                         const uint32_t* __restrict__ list_len,
+                                                         int nlist,
+                                                         const uint32_t* __restrict__ lim,
+                                                         unsigned long long* __restrict__ stats) {
+    unsigned long long nv = 0, nd = 0;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
         const int l = assign[e];
+        uint32_t len = 0;
         if (l >= 0 && l < nlist) len = lim ? lim[e] : list_len[l];
+        nv += len > 0 ? 1 : 0;
+        nd += len;
     }
-    const unsigned long long nv = __popcll(__ballot(len > 0));
-    unsigned long long nd = len;
 #pragma unroll
-    for (int m = 32; m > 0; m >>= 1) nd += __shfl_xor(nd, m);
-    if ((threadIdx.x & 63) == 0 && nv) {
-        atomicAdd(&stats[0], nv);
-        atomicAdd(&stats[1], nd);
+    for (int m = 32; m > 0; m >>= 1) {
+        nv += __shfl_xor(nv, m);
+        nd += __shfl_xor(nd, m);
+    }
+    __shared__ unsigned long long red[2][4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][w] = nv;
+        red[1][w] = nd;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long a = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        const unsigned long long b = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        if (a) {
+            atomicAdd(&stats[0], a);
+            atomicAdd(&stats[1], b);
+        }
     }
 }
 
 void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_len, int nlist,
                      const uint32_t* lim, unsigned long long* stats, hipStream_t s) {
     if (total <= 0) return;
-    k_ivf_visit_stats<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
-            assign, total, list_len, nlist, lim, stats);
+    const int64_t grid = std::min<int64_t>(cdiv(total, 256), 1024);
+    k_ivf_visit_stats<<<dim3((unsigned)grid), dim3(256), 0, s>>>(assign, total, list_len, nlist,
+                                                                 lim, stats);
     HIP_LAUNCH_CHECK();
 }
 

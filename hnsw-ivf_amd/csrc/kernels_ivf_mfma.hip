@@ -400,7 +400,40 @@ __device__ __forceinline__ float eval_rows64(const float* xr /* LDS copy of the 
     return out;
 }
 
-template <bool L2>
+// IVF-PQ exact distance of the code at arena row `grow`, probe list l, with
+// the reference's own table arithmetic (oracle_ivf_search_preassigned, i.e.
+// faiss/IndexIVFPQ.cpp:560-566 / 634-700, precomputed table :413-430,
+// distance_single_code code_distance-generic.h:16-79):
+//   table 1: dis0 = coarse_dis, sim = fmaf(-2, <x_m, c>, fmaf(2, <y_C,m, c>, |c|^2))
+//   table 0: dis0 = 0, sim = |(x - y_C)_m - c|^2
+// dis = dis0 + (((0 + sim_0) + sim_1) + ...), every small product in the
+// fvec order of ref_arith.h.  xs: the query (LDS).
+template <int PQD>
+__device__ __forceinline__ float pq_exact(const PQArgs& pa, const float* xs, uint32_t grow,
+                                          uint32_t l, float d0) {
+    const uint8_t* cp = pa.codes + (size_t)grow * pa.cs;
+    const float* yc = pa.cent + (size_t)l * pa.ldcent;
+    float acc = 0.f;
+    for (int m = 0; m < pa.M; m++) {
+        const int j = cp[m];
+        const float* c = pa.pq_cent + ((size_t)m * 256 + j) * PQD;
+        float sim;
+        if (pa.table1) {
+            const float s2 = ref_ip(xs + m * PQD, c, PQD);
+            const float P = fmaf(2.f, ref_ip(yc + m * PQD, c, PQD), ref_norm(c, PQD));
+            sim = fmaf(-2.f, s2, P);
+        } else {
+            __attribute__((aligned(16))) float rr[PQD];
+#pragma unroll
+            for (int i = 0; i < PQD; i++) rr[i] = xs[m * PQD + i] - yc[m * PQD + i];
+            sim = ref_l2(rr, c, PQD);
+        }
+        acc += sim;
+    }
+    return (pa.table1 ? d0 : 0.f) + acc;
+}
+
+template <bool L2, int PQD = 0>
 struct RerankStream {
     const uint32_t* surv;    // arena rows of the candidates (LDS)
     const uint16_t* sprobe;  // their probe rank
@@ -417,11 +450,22 @@ struct RerankStream {
     uint32_t my_fail;         // lane r: failing streams of probe r (4 bits)
     float my_m;               // lane r: probe r's margin
     uint32_t my_off, my_len;  // lane r: probe r's arena geometry
+    uint32_t my_l;            // PQ: lane r: probe r's list
+    float my_d0;              // PQ: lane r: probe r's coarse distance
+    PQArgs pa;
 
-    __device__ __forceinline__ void emit(bool ok, uint32_t grow, float& k1, long long& k2) const {
+    __device__ __forceinline__ void emit(bool ok, uint32_t grow, int r, float& k1,
+                                         long long& k2) const {
         // the id load is issued before the rows', so both share one round trip
         const long long idv = ok ? (long long)ids[grow] : 0ll;
-        const float dis = eval_rows64<L2>(xs, stage, xq, codes, ldc, d, grow, ok, lane);
+        float dis;
+        if constexpr (PQD > 0) {
+            const uint32_t l = __shfl(my_l, r);
+            const float d0 = __shfl(my_d0, r);
+            dis = ok ? pq_exact<PQD>(pa, xs, grow, l, d0) : 0.f;
+        } else {
+            dis = eval_rows64<L2>(xs, stage, xq, codes, ldc, d, grow, ok, lane);
+        }
         k1 = WS_INF;
         k2 = WS_NOID;
         if (ok) to_key(L2 ? 1 : 0, dis, idv, k1, k2);
@@ -432,10 +476,11 @@ struct RerankStream {
             for (int s0 = 0; s0 < nsv; s0 += 64) {
                 bool ok = s0 + lane < nsv;
                 const uint32_t grow = ok ? surv[s0 + lane] : 0u;
-                const long long rank = ok ? (((long long)sprobe[s0 + lane] << 32) | grow) : 0;
+                const int rp = ok ? (int)sprobe[s0 + lane] : 0;
+                const long long rank = ok ? (((long long)rp << 32) | grow) : 0;
                 float k1;
                 long long k2;
-                emit(ok, grow, k1, k2);
+                emit(ok, grow, rp, k1, k2);
                 f(ok && key_admissible(k1), k1, k2, rank);
             }
             return;
@@ -459,7 +504,7 @@ struct RerankStream {
             const long long rank = ((long long)r << 32) | grow;
             float k1;
             long long k2;
-            emit(ok, grow, k1, k2);
+            emit(ok, grow, r, k1, k2);
             f(ok && key_admissible(k1), k1, k2, rank);
         }
         // every row of the failing streams
@@ -479,7 +524,7 @@ struct RerankStream {
                     const long long rank = ((long long)r << 32) | grow;
                     float k1;
                     long long k2;
-                    emit(ok, grow, k1, k2);
+                    emit(ok, grow, r, k1, k2);
                     f(ok && key_admissible(k1), k1, k2, rank);
                 }
             }
@@ -487,13 +532,13 @@ struct RerankStream {
     }
 };
 
-template <bool L2, int V>
+template <bool L2, int V, int PQD = 0>
 __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
         const uint32_t* __restrict__ keys, const ProbeRec* __restrict__ recs,
         const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
         const int64_t* __restrict__ ids, int d, int64_t n, int nprobe, int KT, int obits, int k,
         float* __restrict__ D, int64_t* __restrict__ I, uint32_t* __restrict__ stats,
-        unsigned long long* __restrict__ trace) {
+        unsigned long long* __restrict__ trace, PQArgs pa) {
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ uint32_t surv[RR_W][RR_CAP];
     __shared__ uint16_t sprobe[RR_W][RR_CAP];
@@ -533,7 +578,11 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
     pr.off = 0u;
     pr.len = 0u;
     pr.pad = 0u;
-    if (valid && lane < nprobe) pr = recs[q * nprobe + lane];
+    float my_d0 = 0.f;
+    if (valid && lane < nprobe) {
+        pr = recs[q * nprobe + lane];
+        if constexpr (PQD > 0) my_d0 = pa.table1 ? pa.cdis[q * nprobe + lane] : 0.f;
+    }
     const float* xq = x + q * ldx;
     if (lane < BDM / 4 && 4 * lane < (d & ~3))
         *(float4*)(&xsh[w][4 * lane]) = *(const float4*)(xq + 4 * lane);
@@ -633,7 +682,7 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
     }
     __syncthreads();  // the LDS query copy and candidate list (every wave gets here)
     const unsigned long long t_c = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    RerankStream<L2> st;
+    RerankStream<L2, PQD> st;
     st.surv = surv[w];
     st.sprobe = sprobe[w];
     st.ids = ids;
@@ -656,6 +705,9 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
     st.my_m = pr.mmax;
     st.my_off = pr.off;
     st.my_len = pr.len;
+    st.my_l = pr.pad;
+    st.my_d0 = my_d0;
+    st.pa = pa;
     // ---- round trip 2: candidate rows and ids; up to 4 batches are ranked
     // directly, anything else goes through the general resolve
     bool done = false;
@@ -667,7 +719,8 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
 #pragma unroll
         for (int b = 0; b < NB; b++) {
             const bool ok = 64 * b + lane < ns;
-            st.emit(ok, ok ? surv[w][64 * b + lane] : 0u, k1[b], k2[b]);
+            st.emit(ok, ok ? surv[w][64 * b + lane] : 0u, ok ? (int)sprobe[w][64 * b + lane] : 0,
+                    k1[b], k2[b]);
             if (!(ok && key_admissible(k1[b]))) {
                 k1[b] = WS_INF;
                 k2[b] = WS_NOID;
@@ -932,7 +985,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 #define LAUNCH_B(L2V, VV)                                                                      \
     k_ivf_rerank<L2V, VV><<<dim3((unsigned)cdiv(n, RR_W)), dim3(64 * RR_W), 0, s>>>(           \
             keys, recs, x, ldx, codes, ldc, ids, d, n, nprobe, KE / 4, obits, k, D, I, stats,   \
-            trace)
+            trace, PQArgs{})
 #define DISPATCH_V(L2V)                      \
     do {                                     \
         if (V == 2) LAUNCH_B(L2V, 2);        \
@@ -959,6 +1012,37 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 #undef LAUNCH_B
 #undef DISPATCH
     }
+}
+
+// IVF-PQ re-rank: the Flat re-rank's certified candidate selection with the
+// reference LUT arithmetic as the exact evaluator (pq_exact)
+void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx, int d,
+                  const int64_t* ids, const PQArgs& pa, int dsub, int64_t n, int nprobe, int KT,
+                  int obits, int k, float* D, int64_t* I, uint32_t* stats, hipStream_t s) {
+    if (n <= 0) return;
+    FAISS_THROW_IF_NOT(d <= BDM && d % 4 == 0);
+    const int KE = 4 * KT;
+    const int E = nprobe * KE;
+    const int V = E <= 128 ? 2 : E <= 256 ? 4 : E <= 512 ? 8 : E <= 1024 ? 16 : 32;
+#define LAUNCH_P(VV, DS)                                                                        \
+    k_ivf_rerank<true, VV, DS><<<dim3((unsigned)cdiv(n, RR_W)), dim3(64 * RR_W), 0, s>>>(       \
+            keys, recs, x, ldx, nullptr, 0, ids, d, n, nprobe, KT, obits, k, D, I, stats,         \
+            nullptr, pa)
+#define DISPATCH_P(DS)                       \
+    do {                                     \
+        if (V == 2) LAUNCH_P(2, DS);         \
+        else if (V == 4) LAUNCH_P(4, DS);    \
+        else if (V == 8) LAUNCH_P(8, DS);    \
+        else if (V == 16) LAUNCH_P(16, DS);  \
+        else LAUNCH_P(32, DS);               \
+    } while (0)
+    if (dsub == 2) DISPATCH_P(2);
+    else if (dsub == 4) DISPATCH_P(4);
+    else if (dsub == 8) DISPATCH_P(8);
+    else FAISS_THROW_MSG("ivfpq_rerank: dsub must be 2, 4 or 8");
+    HIP_LAUNCH_CHECK();
+#undef DISPATCH_P
+#undef LAUNCH_P
 }
 
 }  // namespace kern

@@ -1,0 +1,358 @@
+// kernels_pq_mfma.hip — IVF-PQ list scan as a certified bf16 MFMA filter over
+// decoded codes (reference: IVFPQScanner, faiss/IndexIVFPQ.cpp:483-933, and
+// the scan loop faiss/IndexIVF.cpp:595-631).
+//
+// The query-centric LUT scan (kernels_pq.hip) pays one LDS gather per code
+// byte per query and is bound by LDS bank conflicts.  Here the work is
+// list-centric like the IVF-Flat filter: a work item is (list, <= 64 queries
+// probing it), each 64-row tile of the list is decoded ONCE into bf16 MFMA
+// A-fragments (one gather of dsub centroid values per code byte, from a bf16
+// copy of the PQ centroids held in LDS for the whole kernel) and multiplied
+// against the 64 queries' bf16 hi+lo fragments.  For the by-residual L2
+// distance
+//     ||x - y_C - y_R||^2 = coarse_dis + term(row) - 2 <x, y_R>,
+//     term(row) = ||y_R||^2 + 2 <y_C, y_R>             (per arena row)
+// so the filter key is  coarse_dis(q, probe) + term - 2 acc.
+//
+// Certification (the same scheme as the Flat filter, kernels_ivf_mfma.hip):
+// with R = ||y_R||, r = ||y_R - bf16(y_R)|| (per row, list maxima rmax/Rmax),
+// |approx - reference| <= 2 ||x|| r + coef (||x|| + ||y_C|| + R)^2, where coef
+// covers the bf16 split of the query (2^-16), the f32 accumulation of the
+// MFMA, the rounding of term, of the reference's LUT construction and
+// summation (tables 0 and 1) and of coarse_dis (ivfpq_mfma_coef).  The kernel
+// keeps, per (query, list), 4 thread streams x KT best 32-bit keys plus a
+// lower bound of every dropped key; the re-rank (k_ivf_rerank with PQD > 0)
+// evaluates every candidate that can reach the top-k with the reference's
+// own table arithmetic (oracle_ivf_search_preassigned, IndexIVFPQ.cpp:
+// 634-700 + code_distance-generic.h:16-79), so results equal the reference's.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+#include "bf3.h"
+#include "common.h"
+#include "kernels.h"
+#include "wave_select.h"
+
+namespace faiss_amd {
+namespace kern {
+
+// bf16 copy of the PQ centroids, [M][256][dsub] (the decode table)
+__global__ void k_pq_dec_table(const float* __restrict__ pq_cent, int n, __bf16* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (__bf16)pq_cent[i];
+}
+
+// per arena row: R = ||y_R|| and r = ||y_R - bf16(y_R)|| (rounded up)
+__global__ void k_pq_row_res(const uint8_t* __restrict__ codes, int cs, int64_t rows, int M,
+                             int dsub, const float* __restrict__ pq_cent,
+                             float* __restrict__ rnorm, float* __restrict__ rres) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= rows) return;
+    double s = 0.0, e = 0.0;
+    for (int m = 0; m < M; m++) {
+        const int j = codes[v * cs + m];
+        const float* c = pq_cent + ((int64_t)m * 256 + j) * dsub;
+        for (int i = 0; i < dsub; i++) {
+            const double y = c[i];
+            const double yh = (double)(float)(__bf16)c[i];
+            s += y * y;
+            e += (y - yh) * (y - yh);
+        }
+    }
+    rnorm[v] = (float)(sqrt(s) * (1.0 + 1e-6));
+    rres[v] = (float)(sqrt(e) * (1.0 + 1e-6));
+}
+
+void pq_decode_prep(const float* pq_cent, int M, int dsub, const uint8_t* codes, int cs,
+                    int64_t rows, void* dec, float* rnorm, float* rres, hipStream_t s) {
+    const int n = M * 256 * dsub;
+    k_pq_dec_table<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s>>>(pq_cent, n, (__bf16*)dec);
+    HIP_LAUNCH_CHECK();
+    if (rows > 0) {
+        k_pq_row_res<<<dim3((unsigned)cdiv(rows, 256)), dim3(256), 0, s>>>(
+                codes, cs, rows, M, dsub, pq_cent, rnorm, rres);
+        HIP_LAUNCH_CHECK();
+    }
+}
+
+double ivfpq_mfma_coef(int d, int M) {
+    const double u = 1.0 / 16777216.0;
+    // query split + MFMA accumulation + term + reference LUT build / sum +
+    // coarse distance, each bounded by a multiple of (|x| + |y_C| + R)^2
+    return 1.02 / 65536.0 + (4.0 * d + 2.0 * M + 64.0) * u;
+}
+
+// A fragment of one lane: row `cw` (its code words), dims [16 s + 8 lh, +8)
+// decoded from the LDS table (8 / DSUB entries of DSUB bf16 each).
+template <int DSUB, int NS, int NWC>
+__device__ __forceinline__ void pq_decode_frags(const uint32_t (&cw)[NWC], int lh,
+                                                const uint8_t* __restrict__ dec,
+                                                bf16x8 (&ah)[NS]) {
+    constexpr int E = 8 / DSUB;  // subquantizers per fragment
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        // subquantizers m0 .. m0 + E - 1, m0 = (16 s + 8 lh) / DSUB
+        uint32_t w32[4];
+#pragma unroll
+        for (int u = 0; u < E; u++) {
+            // byte m of the code, m = (16 s) / DSUB + lh * E + u
+            const int mb = (16 * s) / DSUB + u;  // compile-time part
+            const int m_lo = mb, m_hi = mb + E;  // lh = 0 / 1
+            const uint32_t wl = cw[m_lo >> 2], wh = cw[m_hi >> 2];
+            const uint32_t blo = (wl >> (8 * (m_lo & 3))) & 0xffu;
+            const uint32_t bhi = (wh >> (8 * (m_hi & 3))) & 0xffu;
+            const uint32_t j = lh ? bhi : blo;
+            const int m = lh ? m_hi : m_lo;
+            const uint8_t* src = dec + ((size_t)m * 256 + j) * (2 * DSUB);
+            if constexpr (DSUB == 2) {
+                w32[u] = *(const uint32_t*)src;
+            } else if constexpr (DSUB == 4) {
+                const uint2 v = *(const uint2*)src;
+                w32[2 * u] = v.x;
+                w32[2 * u + 1] = v.y;
+            } else {
+                const uint4 v = *(const uint4*)src;
+                w32[0] = v.x;
+                w32[1] = v.y;
+                w32[2] = v.z;
+                w32[3] = v.w;
+            }
+        }
+        union {
+            uint32_t w[4];
+            bf16x8 v;
+        } cv;
+#pragma unroll
+        for (int i = 0; i < 4; i++) cv.w[i] = w32[i];
+        ah[s] = cv.v;
+    }
+}
+
+// One work item = (list, <= 64 queries); persistent work-groups walk the
+// items with stride gridDim.x, so the LDS decode table is loaded once per
+// work-group.  Wave layout, keys, streams and outputs as k_ivf_bf3_filter.
+template <int DSUB, int NS, int KT>
+__global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
+        const float* __restrict__ x, int ldx, const __bf16* __restrict__ dec_g,
+        const uint8_t* __restrict__ codes, const float* __restrict__ terms,
+        const float* __restrict__ cdis, const float* __restrict__ cnorm,
+        const float* __restrict__ lrmax, const float* __restrict__ lRmax, int nlist, int nprobe,
+        float coef, int obits, const uint32_t* __restrict__ item_off,
+        const ItemDesc* __restrict__ item_desc, const uint32_t* __restrict__ item_entries,
+        const uint32_t* __restrict__ lim, uint32_t* __restrict__ keys,
+        ProbeRec* __restrict__ recs) {
+    constexpr int D = 16 * NS;
+    constexpr int M = D / DSUB;
+    constexpr int CS = (M + 3) & ~3;  // code stride (bytes)
+    constexpr int NWC = CS / 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dec[];  // [M][256][DSUB] bf16
+    __shared__ __attribute__((aligned(16))) float ynt[2][BV];      // term per row (+inf pad)
+    __shared__ uint32_t ent_s[BQ];
+    __shared__ int32_t qrow_s[BQ];
+    __shared__ float bnd_s[BQ][4];
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    {
+        constexpr int NW16 = M * 256 * DSUB * 2 / 16;
+        const uint4* src = (const uint4*)dec_g;
+        for (int i = t; i < NW16; i += 256) ((uint4*)dec)[i] = src[i];
+    }
+    const int bi = w >> 1, bj = w & 1;
+    const int li = lane & 31, lh = lane >> 5;
+    const int slot = 2 * bi + lh;
+    const int qloc = 32 * bj + li;
+    const uint32_t lowmask = (1u << obits) - 1u;
+    const uint32_t nitems = item_off[nlist];
+
+    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+        const ItemDesc dsc = item_desc[it];
+        const uint32_t e_raw = t < BQ ? item_entries[(size_t)it * BQ + t] : 0u;
+        const int l = (int)dsc.l;
+        const int nQ = (int)dsc.nq;
+        const int len = (int)dsc.len;
+        const int64_t row0 = dsc.off;
+        if (t < BQ) {
+            const uint32_t e = t < nQ ? e_raw : 0u;
+            ent_s[t] = e;
+            qrow_s[t] = t < nQ ? (int32_t)(e / (uint32_t)nprobe) : -1;
+        }
+        // first tile: this lane's code row and the tile's terms
+        uint32_t cw[NWC];
+        auto load_codes = [&](int v0n) {
+            const int r = v0n + 32 * bi + li;
+            const uint8_t* cp = codes + (row0 + (r < len ? r : 0)) * CS;
+            if constexpr (CS % 16 == 0) {
+#pragma unroll
+                for (int i = 0; i < NWC; i += 4) {
+                    const uint4 v = *(const uint4*)(cp + 4 * i);
+                    cw[i] = v.x;
+                    cw[i + 1] = v.y;
+                    cw[i + 2] = v.z;
+                    cw[i + 3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < NWC; i++) cw[i] = *(const uint32_t*)(cp + 4 * i);
+            }
+        };
+        float4 tn = make_float4(0.f, 0.f, 0.f, 0.f);
+        auto load_terms = [&](int v0n) {
+            if (t < BV / 4) {
+                const int r = 4 * t;
+                const int nvn = min(BV, len - v0n);
+                // rows < roundup(len, 16) are inside the list's arena slot
+                const float4 v = r < nvn ? *(const float4*)(terms + row0 + v0n + r)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+                tn.x = r + 0 < nvn ? v.x : WS_INF;
+                tn.y = r + 1 < nvn ? v.y : WS_INF;
+                tn.z = r + 2 < nvn ? v.z : WS_INF;
+                tn.w = r + 3 < nvn ? v.w : WS_INF;
+            }
+        };
+        load_codes(0);
+        load_terms(0);
+        __syncthreads();  // ent_s / qrow_s (and, first time, the decode table)
+
+        const bool active = 32 * bj < nQ;
+        bf16x8 bh[NS], bl[NS];
+        float xn = 0.f, base = 0.f;
+        if (active) {
+            load_query_frags<NS>(x, ldx, D, qrow_s[qloc], lh, bh, bl, xn);
+            base = cdis[ent_s[qloc]];
+        }
+        ThreadQueue32<KT> tq;
+        tq.init();
+        for (int v0 = 0, tile = 0; v0 < len; v0 += BV, tile++) {
+            const int buf = tile & 1;
+            if (t < BV / 4) *(float4*)(&ynt[buf][4 * t]) = tn;
+            bf16x8 ah[NS];
+            if (active) pq_decode_frags<DSUB, NS, NWC>(cw, lh, dec, ah);
+            if (v0 + BV < len) {
+                load_codes(v0 + BV);
+                load_terms(v0 + BV);
+            }
+            __syncthreads();
+            if (active) {
+                float4 yq[4];
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+                    yq[g] = *(const float4*)(&ynt[buf][32 * bi + 4 * lh + 8 * g]);
+                floatx16 acc;
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[r] = 0.f;
+#pragma unroll
+                for (int s = 0; s < NS; s++) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
+                }
+                const uint32_t ordbase = (uint32_t)tile << 4;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int g = r >> 2, c = r & 3;
+                    const float yv = c == 0 ? yq[g].x : c == 1 ? yq[g].y : c == 2 ? yq[g].z : yq[g].w;
+                    const float a = fmaf(-2.f, acc[r], base + yv);
+                    tq.push(key_encode<true>(a, lowmask, ordbase | (uint32_t)r));
+                }
+            }
+        }
+
+        // ---- outputs (as k_ivf_bf3_filter)
+        const bool qvalid = qloc < nQ;
+        const uint32_t last = tq.q[KT - 1];
+        float bnd = WS_INF;
+        if (last != 0xffffffffu) {
+            const int row = (int)ivf_key_row(last, lowmask, slot);
+            if (row < len) bnd = key_decode_lo<true>(last, lowmask);
+        }
+        bnd_s[qloc][slot] = bnd;
+        __syncthreads();
+        if (qvalid) {
+            const int64_t e = ent_s[qloc];
+            const uint32_t elen = lim ? min((uint32_t)len, lim[e]) : (uint32_t)len;
+            uint32_t* ko = keys + e * (4 * KT) + slot * KT;
+#pragma unroll
+            for (int i = 0; i < KT; i++) {
+                const uint32_t key = tq.q[i];
+                const uint32_t row = ivf_key_row(key, lowmask, slot);
+                ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
+            }
+            if (slot == 0) {
+                const float xl = sqrtf(xn);
+                const float sr = xl + cnorm[l] + lRmax[l];
+                const float mmax = 2.f * (2.f * xl * lrmax[l] + coef * sr * sr) + 1e-30f;
+                ProbeRec pr;
+#pragma unroll
+                for (int sl = 0; sl < 4; sl++) {
+                    const float b = bnd_s[qloc][sl];
+                    pr.pb[sl] = b < WS_INF ? b - mmax : WS_INF;
+                }
+                pr.mmax = mmax;
+                pr.off = (uint32_t)row0;
+                pr.len = elen;
+                pr.pad = (uint32_t)l;
+                recs[e] = pr;
+            }
+        }
+        __syncthreads();  // ent_s / bnd_s / ynt are reused by the next item
+    }
+}
+
+bool ivfpq_mfma_eligible(int d, int M, int k, int nprobe) {
+    if (d % 16 != 0 || M <= 0 || d % M != 0 || k > 32 || nprobe > 64) return false;
+    const int dsub = d / M, NS = d / 16;
+    if (dsub != 2 && dsub != 4 && dsub != 8) return false;
+    return NS == 4 || NS == 6 || NS == 8;
+}
+
+void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const uint8_t* codes,
+                  const float* terms, const float* cdis, const float* cnorm, const float* lrmax,
+                  const float* lRmax, int nlist, int64_t n, int nprobe, int k, int obits,
+                  const IVFBuckets& b, int64_t max_items, uint32_t* keys, ProbeRec* recs,
+                  int* kt_out, hipStream_t s) {
+    FAISS_THROW_IF_NOT(ivfpq_mfma_eligible(d, M, k, nprobe));
+    FAISS_THROW_IF_NOT(b.item_desc && b.item_entries);
+    FAISS_THROW_IF_NOT(obits >= 4 && obits <= 14);
+    const int KE = ivf_mfma_kq(k, d);
+    FAISS_THROW_IF_NOT(KE > 0);
+    *kt_out = KE / 4;
+    const int dsub = d / M, NS = d / 16;
+    const size_t lds = (size_t)M * 256 * dsub * 2;
+    // persistent grid: enough work-groups to fill every CU at the occupancy
+    // the LDS table allows, never more than the items
+    int dev = 0, ncu = 256;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / (lds + 4096))));
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(max_items, (int64_t)ncu * per_cu));
+    const float coef = (float)ivfpq_mfma_coef(d, M);
+#define PQF(DS, NSV, KTV)                                                                      \
+    if (dsub == DS && NS == NSV && KE / 4 == KTV) {                                            \
+        auto kfn = k_ivfpq_filter<DS, NSV, KTV>;                                               \
+        static bool attr = false;                                                              \
+        if (!attr) {                                                                           \
+            HIP_CHECK(hipFuncSetAttribute((const void*)kfn,                                    \
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,          \
+                                          (int)lds));                                          \
+            attr = true;                                                                       \
+        }                                                                                      \
+        kfn<<<dim3((unsigned)grid), dim3(256), lds, s>>>(                                      \
+                x, ldx, (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, nlist,    \
+                nprobe, coef, obits, b.item_off, b.item_desc, b.item_entries, b.lim, keys,     \
+                recs);                                                                         \
+        HIP_LAUNCH_CHECK();                                                                    \
+        return;                                                                                \
+    }
+#define PQF_KT(DS, NSV) PQF(DS, NSV, 2) PQF(DS, NSV, 4) PQF(DS, NSV, 8)
+#define PQF_NS(DS) PQF_KT(DS, 4) PQF_KT(DS, 6) PQF_KT(DS, 8)
+    PQF_NS(2) PQF_NS(4) PQF_NS(8)
+#undef PQF_NS
+#undef PQF_KT
+#undef PQF
+    FAISS_THROW_MSG("ivfpq_filter: no kernel instance for this geometry");
+}
+
+}  // namespace kern
+}  // namespace faiss_amd

@@ -361,6 +361,12 @@ struct IndexIVFPQ : IndexIVF {
    protected:
     void upload_extra() const override;
     mutable DeviceBuffer d_pq_, d_terms_, d_cent_;
+    // list-centric MFMA scan (kernels_pq_mfma.hip): bf16 decode table, per
+    // row |y_R| and bf16 residual norm, per list maxima, |y_C| per list
+    mutable DeviceBuffer d_dec_, d_prn_, d_prr_, d_lRmax_, d_lrmax_, d_cnorm_;
+    mutable DeviceBuffer s_pkeys_, s_precs_, s_pflags_;
+    mutable int pq_obits_ = 0;
+    mutable bool pq_mfma_ready_ = false;
 };
 
 // ---------------------------------------------------------------- shards

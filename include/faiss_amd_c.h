@@ -263,6 +263,10 @@ int faiss_amd_IndexIVFPQ_info(
         size_t* nbits,
         int* by_residual,
         int* use_precomputed_table);
+/* faiss IndexIVFPQ::use_precomputed_table (faiss/IndexIVFPQ.h:41-47): the
+ * table the reference's scanner would use (0 or 1); selects the exact
+ * arithmetic of the GPU re-rank.  0 is always valid, 1 needs by_residual L2 */
+int faiss_amd_IndexIVFPQ_set_use_precomputed_table(FaissIndexIVFPQ* index, int v);
 
 /* ---------------- IndexHNSWFlat (C++ faiss/IndexHNSW.h:IndexHNSWFlat) ---- */
 int faiss_amd_IndexHNSWFlat_new_with(

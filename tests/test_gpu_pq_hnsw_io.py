@@ -155,3 +155,48 @@ def test_merge_knn_results_device_and_host(amd, orc, gpu):
     Dr, Ir = orc.merge_knn_results(Dall, Iall)
     D, I = amd.merge_knn_results(Dall, Iall)
     assert np.array_equal(I, Ir) and np.array_equal(D, Dr)
+
+
+@pytest.mark.parametrize("table", [1, 0])
+@pytest.mark.parametrize("k,nprobe", [(1, 1), (10, 8), (5, 17), (32, 8)])
+def test_ivfpq_mfma_bit_exact_vs_oracle(amd, orc, pq_index, monkeypatch, table, k, nprobe):
+    # list-centric MFMA filter + re-rank in the reference's table arithmetic
+    # (oracle_ivf_search_preassigned: IndexIVFPQ.cpp:560-700) -> the same ids
+    # and the same fp32 distances as the restated reference, for both tables
+    idx, _ = pq_index
+    xq = rand(orc, 400, 64, 34)
+    Dq, Iq = idx.quantizer.search(xq, nprobe)
+    idx.nprobe = nprobe
+    idx.use_precomputed_table = table
+    try:
+        D, I = idx.search_preassigned(xq, k, Iq, Dq)
+        monkeypatch.setenv("FAISS_AMD_PQ_SCAN", "lut")
+        Dl, Il = idx.search_preassigned(xq, k, Iq, Dq)
+    finally:
+        idx.use_precomputed_table = 1
+    ref = orc.IVFOracle.from_index(idx)
+    ref.s.use_precomputed_table = table
+    Dr, Ir = ref.search_preassigned(xq, k, Iq, Dq)
+    assert_same_results(D, I, Dr, Ir)
+    # the query-centric LUT scan (its own summation order) agrees to 1e-4
+    assert (Il == Ir).mean() > 0.97
+    ok = Il == Ir
+    np.testing.assert_allclose(Dl[ok], Dr[ok], rtol=1e-4, atol=1e-5)
+
+
+def test_ivfpq_mfma_duplicate_codes_ties(amd, orc, gpu):
+    # many identical codes: exact distance ties at the k boundary resolve by
+    # the reference's arrival-order rule (the Flat tie machinery)
+    d, nlist = 64, 16  # d in {64, 96, 128}: the MFMA path's geometries
+    base = rand(orc, 2000, d, 35)
+    xb = np.repeat(base[:400], 8, axis=0) + 0.0
+    idx = amd.index_factory(d, f"IVF{nlist},PQ16")
+    idx.train(base)
+    idx.add(xb)
+    xq = rand(orc, 200, d, 36)
+    idx.nprobe = 4
+    Dq, Iq = idx.quantizer.search(xq, 4)
+    D, I = idx.search_preassigned(xq, 10, Iq, Dq)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir = ref.search_preassigned(xq, 10, Iq, Dq)
+    assert_same_results(D, I, Dr, Ir)
