@@ -156,9 +156,13 @@ void IndexFlat::sync_device() const {
         if (kern::bf3_db_host(d) <= 128) {
             const int DB = kern::bf3_db_host(d);
             d_cbf_.reserve((size_t)ntotal * 2 * DB * 2);
-            d_cnmax_.reserve(sizeof(float));
+            // {max |c|^2, max |c - bf16(c)|}: the coarse filter's margins
+            d_cnmax_.reserve(2 * sizeof(float));
             kern::split_bf16(d_xb_.as<float>(), ntotal, d, l, DB, d_cbf_.ptr, s);
             kern::array_max(d_norms_.as<float>(), ntotal, d_cnmax_.as<float>(), s);
+            s_tile_.reserve(sizeof(float) * ntotal);
+            kern::row_resnorm_bf16(d_xb_.as<float>(), ntotal, d, l, s_tile_.as<float>(), s);
+            kern::array_max(s_tile_.as<float>(), ntotal, d_cnmax_.as<float>() + 1, s);
         }
     }
     HIP_CHECK(hipStreamSynchronize(s));

@@ -25,6 +25,7 @@
 #include <cfloat>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "bf3.h"
@@ -69,6 +70,16 @@ __device__ __forceinline__ float ip_seq(const float* __restrict__ a, const float
     return acc;
 }
 
+// the query's margin: bf16x3, coef (|x|^2 + max|c|^2); bf16x2 (centroids
+// rounded to bf16, queries split), Cauchy-Schwarz on the centroid rounding
+// residual: 2 (2 |x| max|c - bf16(c)| + coef (|x|^2 + max|c|^2)).
+// cm = {max |c|^2, max |c - bf16(c)|}
+__device__ __forceinline__ float coarse_margin(float xn, const float* __restrict__ cm, float coef,
+                                               bool y3) {
+    return y3 ? coef * (xn + cm[0]) + 1e-30f
+              : 2.f * (2.f * sqrtf(xn) * cm[1] + coef * (xn + cm[0])) + 1e-30f;
+}
+
 // Pipeline as in the IVF-Flat filter (kernels_ivf_mfma.hip): one barrier per
 // 64-centroid tile, tile t+1 stashed from registers while t is computed, the
 // centroid norms (L2) / a +inf bias for rows past the split (IP) travel with
@@ -80,13 +91,14 @@ __device__ __forceinline__ float ip_seq(const float* __restrict__ a, const float
 // empty) and a lower bound of every candidate the stream dropped (+inf when
 // none), after subtracting the query's largest margin M = coef (|x|^2 +
 // max|c|^2) (the re-rank uses the same M for every entry of the query).
-template <bool L2, int KT, int NS>
+template <bool L2, int KT, int NS, bool Y3>
 __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
         const float* __restrict__ x, int ldx, int64_t n, int d, const __bf16* __restrict__ cbf,
         const float* __restrict__ cnorm, const float* __restrict__ xnorm, int nlist,
         int nsplit, int split_len, float coef, const float* __restrict__ cnmax_p, int obits,
         uint32_t* __restrict__ keys, float* __restrict__ pbs) {
-    __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * (4 * 16 * NS + 16)];
+    // Y3: centroid rows hi | lo (bf16x3); else hi only (bf16x2, half the bytes)
+    __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * ((Y3 ? 4 : 2) * 16 * NS + 16)];
     __shared__ __attribute__((aligned(16))) float ynt[2][BV];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     // blocks b and b+8 share an XCD: consecutive splits of one query block
@@ -95,7 +107,8 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
     const int sp = (int)(blockIdx.x % nsplit);
     const int c0 = sp * split_len;
     const int len = min(split_len, nlist - c0);
-    constexpr int DB = 16 * NS, CSB = 4 * DB + 16, RU = DB / 4;
+    constexpr int DB = 16 * NS, CSB = (Y3 ? 4 : 2) * DB + 16, RU = Y3 ? DB / 4 : DB / 8;
+    constexpr int PF = (BV * RU + 255) / 256;  // uint4 per thread per tile
     const int bi = w >> 1, bj = w & 1, li = lane & 31, lh = lane >> 5;
     const int slot = 2 * bi + lh, qloc = 32 * bj + li;
     const int64_t q = qb * BQ + qloc;
@@ -103,15 +116,14 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
     float xn_approx;
     load_query_frags<NS>(x, ldx, d, q < n ? (int)q : -1, lh, bh, bl, xn_approx);
     const float xn = q < n ? xnorm[q] : 0.f;  // the reference-order norm (exact side)
-    const float cnmax = *cnmax_p;
     const float* cn = cnorm + c0;
 
-    uint4 pf[8];
+    uint4 pf[PF];
     float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
     auto fetch = [&](int v0n) {
         const int nvn = min(BV, len - v0n);
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
+        for (int s = 0; s < PF; s++) {
             const int e = t + 256 * s;
             const int r = e / RU, c = e - r * RU;
             pf[s] = make_uint4(0u, 0u, 0u, 0u);
@@ -130,7 +142,7 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
     auto stash = [&](int buf) {
         uint8_t* T = tiles + buf * BV * CSB;
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
+        for (int s = 0; s < PF; s++) {
             const int e = t + 256 * s;
             const int r = e / RU, c = e - r * RU;
             if (e < BV * RU) *(uint4*)(T + r * CSB + 16 * c) = pf[s];
@@ -154,8 +166,8 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
         float4 yq[4];
 #pragma unroll
         for (int g = 0; g < 4; g++) yq[g] = *(const float4*)(&ynt[buf][32 * bi + 4 * lh + 8 * g]);
-        const floatx16 acc =
-                bf3_block<NS>(tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh, bh, bl);
+        const uint8_t* arow = tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh;
+        const floatx16 acc = Y3 ? bf3_block<NS>(arow, bh, bl) : bf2_block<NS>(arow, bh, bl);
         const uint32_t ordbase = (uint32_t)tile << 4;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
@@ -168,7 +180,7 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
         __syncthreads();
     }
     if (q < n) {
-        const float M = coef * (xn + cnmax) + 1e-30f;
+        const float M = coarse_margin(xn, cnmax_p, coef, Y3);
         const int E1 = 4 * KT;
         uint32_t* ko = keys + (q * nsplit + sp) * E1 + slot * KT;
 #pragma unroll
@@ -277,9 +289,9 @@ __global__ __launch_bounds__(64, 4) void k_coarse_rerank(
         const uint32_t* __restrict__ keys, const float* __restrict__ pbs,
         const float* __restrict__ x, int ldx, const float* __restrict__ xnorm,
         const float* __restrict__ cent, int ldc, const float* __restrict__ cnorm,
-        const float* __restrict__ cnmax_p, float coef, int64_t n, int d, int nlist, int nsplit,
-        int split_len, int KT, int obits, int k, float* __restrict__ D, OutIdx* __restrict__ I,
-        uint32_t* __restrict__ stats) {
+        const float* __restrict__ cnmax_p, float coef, int y3, int64_t n, int d, int nlist,
+        int nsplit, int split_len, int KT, int obits, int k, float* __restrict__ D,
+        OutIdx* __restrict__ I, uint32_t* __restrict__ stats) {
     __shared__ uint32_t surv[CR_CAP];
     __shared__ __attribute__((aligned(16))) float xsh[BDM];
     const int lane = threadIdx.x;
@@ -299,7 +311,7 @@ __global__ __launch_bounds__(64, 4) void k_coarse_rerank(
     const float* xq = x + q * ldx;
     if (lane < BDM / 4 && 4 * lane < ((d + 3) & ~3))
         *(float4*)(&xsh[4 * lane]) = *(const float4*)(xq + 4 * lane);
-    const float M = coef * (xn + *cnmax_p) + 1e-30f;
+    const float M = coarse_margin(xn, cnmax_p, coef, y3 != 0);
     // ---- U
     float ub[V];
 #pragma unroll
@@ -452,14 +464,28 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     if (dbg) HIP_CHECK(hipMemsetAsync(stats, 0, 16, s));
     FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldc % 4 == 0);
     const int NS = bf3_db(d) / 16;
-    const float coef = (float)ivf_bf3_coef(d);
+    // bf16x3 by default.  FAISS_AMD_COARSE_PREC=bf16x2 (two MFMA passes, half
+    // the centroid bytes) is exact too, but its Cauchy-Schwarz margin on the
+    // centroids' bf16 rounding (cnmax[1]) is ~20x wider than the bf16x3 one:
+    // centroids near a query are dense, so on uniform data (c2: 0.4 -> 1.9 ms
+    // per step) the streams overflow and fail; kept for clustered data
+    const char* prec = getenv("FAISS_AMD_COARSE_PREC");
+    const bool y3 = !(prec && !strcmp(prec, "bf16x2"));
+    const float coef = (float)(y3 ? ivf_bf3_coef(d) : ivf_bf2_coef(d));
     const int64_t nqb = (int64_t)cdiv((size_t)n, BQ);
     const int64_t grid = nqb * p.nsplit;
     FAISS_THROW_IF_NOT(grid < (1ll << 31));
 #define LAUNCH_NS(L2V, KTV, NSV)                                                              \
-    k_coarse_bf3_filter<L2V, KTV, NSV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(            \
-            x, ldx, n, d, (const __bf16*)cbf, cnorm, xnorm, nlist, p.nsplit, p.split_len,     \
-            coef, cnmax, p.obits, keys, pbs)
+    do {                                                                                      \
+        if (y3)                                                                               \
+            k_coarse_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+                    x, ldx, n, d, (const __bf16*)cbf, cnorm, xnorm, nlist, p.nsplit,          \
+                    p.split_len, coef, cnmax, p.obits, keys, pbs);                            \
+        else                                                                                  \
+            k_coarse_bf3_filter<L2V, KTV, NSV, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+                    x, ldx, n, d, (const __bf16*)cbf, cnorm, xnorm, nlist, p.nsplit,          \
+                    p.split_len, coef, cnmax, p.obits, keys, pbs);                            \
+    } while (0)
 #define LAUNCH_A(L2V, KTV)                     \
     do {                                       \
         if (NS == 2) LAUNCH_NS(L2V, KTV, 2);   \
@@ -484,7 +510,8 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     FAISS_THROW_IF_NOT(E <= 1024 && V <= p.kt);
 #define LAUNCH_R(L2V, OT, OUT, VV)                                                              \
     k_coarse_rerank<L2V, OT, VV><<<dim3((unsigned)n), dim3(64), 0, s>>>(                       \
-            keys, pbs, x, ldx, xnorm, cent, ldc, cnorm, cnmax, coef, n, d, nlist, p.nsplit,     \
+            keys, pbs, x, ldx, xnorm, cent, ldc, cnorm, cnmax, coef, y3 ? 1 : 0, n, d, nlist,  \
+            p.nsplit,                                                                           \
             p.split_len, p.kt, p.obits, k, D, OUT, st_ptr)
 #define LAUNCH_RV(L2V, OT, OUT)                  \
     do {                                         \

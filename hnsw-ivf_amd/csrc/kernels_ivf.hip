@@ -49,9 +49,13 @@ __global__ __launch_bounds__(1024) void k_bucket_count_lds(const int32_t* __rest
                                                            const uint32_t* __restrict__ list_len,
                                                            int nlist, uint32_t* __restrict__ counts,
                                                            uint32_t* __restrict__ pos) {
-    extern __shared__ uint32_t hist[];  // [nlist]
+    extern __shared__ uint32_t hist[];  // [min(nlist, BC_MAXL)]
     const int t = threadIdx.x;
-    for (int i = t; i < nlist; i += 1024) hist[i] = 0u;
+    // lists [lbase, lbase + nl) of this block row (nlist > BC_MAXL: one row
+    // of blocks per range, each reading every entry)
+    const int lbase = (int)blockIdx.y * BC_MAXL;
+    const int nl = min(BC_MAXL, nlist - lbase);
+    for (int i = t; i < nl; i += 1024) hist[i] = 0u;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * 1024 * BC_PER;
     int ll[BC_PER];
@@ -64,13 +68,14 @@ __global__ __launch_bounds__(1024) void k_bucket_count_lds(const int32_t* __rest
             l = assign[e];
             if (!(l >= 0 && l < nlist && list_len[l] > 0)) l = -1;
         }
+        l = (l >= lbase && l < lbase + nl) ? l - lbase : -1;
         ll[j] = l;
         lp[j] = l >= 0 ? atomicAdd(&hist[l], 1u) : 0u;
     }
     __syncthreads();
-    for (int i = t; i < nlist; i += 1024) {
+    for (int i = t; i < nl; i += 1024) {
         const uint32_t c = hist[i];
-        if (c) hist[i] = atomicAdd(&counts[i], c);
+        if (c) hist[i] = atomicAdd(&counts[lbase + i], c);
     }
     __syncthreads();
 #pragma unroll
@@ -81,48 +86,70 @@ __global__ __launch_bounds__(1024) void k_bucket_count_lds(const int32_t* __rest
 }
 
 // single-workgroup exclusive scan of counts -> bucket_off, ceil(counts/QT)
-// -> item_off; per work item its list when asked
+// -> item_off; per work item its list when asked.  Chunks of 4096 lists:
+// 4 consecutive counts per thread, shuffle scan per wave, 16 wave totals
+// through LDS; a running carry between chunks.
 __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict__ counts,
                                                       int nlist, int QT,
                                                       uint32_t* __restrict__ bucket_off,
                                                       uint32_t* __restrict__ item_off,
                                                       uint32_t* __restrict__ item_list) {
-    __shared__ uint32_t sb[1024], si[1024];
-    const int t = threadIdx.x;
-    const int per = (nlist + 1023) / 1024;
-    const int l0 = t * per, l1 = min(nlist, l0 + per);
-    uint32_t sbk = 0, sit = 0;
-    for (int l = l0; l < l1; l++) {
-        uint32_t c = counts[l];
-        sbk += c;
-        sit += (c + QT - 1) / QT;
-    }
-    sb[t] = sbk;
-    si[t] = sit;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over 1024 partials
-    for (int off = 1; off < 1024; off <<= 1) {
-        uint32_t vb = t >= off ? sb[t - off] : 0u;
-        uint32_t vi = t >= off ? si[t - off] : 0u;
+    __shared__ uint32_t wb[16], wi[16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t carry_b = 0, carry_i = 0;
+    for (int c0 = 0; c0 < nlist; c0 += 4096) {
+        const int l0 = c0 + 4 * t;
+        uint32_t c[4], n[4];
+        uint32_t sb = 0, si = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            c[j] = l0 + j < nlist ? counts[l0 + j] : 0u;
+            n[j] = (c[j] + QT - 1) / QT;
+            sb += c[j];
+            si += n[j];
+        }
+        // inclusive wave scan of the thread sums
+        uint32_t ib = sb, ii = si;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t vb = __shfl_up(ib, off), vi = __shfl_up(ii, off);
+            if (lane >= off) {
+                ib += vb;
+                ii += vi;
+            }
+        }
+        if (lane == 63) {
+            wb[w] = ib;
+            wi[w] = ii;
+        }
         __syncthreads();
-        sb[t] += vb;
-        si[t] += vi;
-        __syncthreads();
+        uint32_t pb = carry_b, pi = carry_i, tb = 0, ti = 0;
+#pragma unroll
+        for (int v = 0; v < 16; v++) {
+            pb += v < w ? wb[v] : 0u;
+            pi += v < w ? wi[v] : 0u;
+            tb += wb[v];
+            ti += wi[v];
+        }
+        __syncthreads();  // wb / wi are rewritten by the next chunk
+        uint32_t rb = pb + ib - sb, ri = pi + ii - si;  // exclusive prefix of this thread
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (l0 + j < nlist) {
+                bucket_off[l0 + j] = rb;
+                item_off[l0 + j] = ri;
+                if (item_list)
+                    for (uint32_t i = 0; i < n[j]; i++) item_list[ri + i] = (uint32_t)(l0 + j);
+            }
+            rb += c[j];
+            ri += n[j];
+        }
+        carry_b += tb;
+        carry_i += ti;
     }
-    uint32_t rb = sb[t] - sbk, ri = si[t] - sit;  // exclusive prefix
-    for (int l = l0; l < l1; l++) {
-        bucket_off[l] = rb;
-        item_off[l] = ri;
-        uint32_t c = counts[l];
-        const uint32_t ni = (c + QT - 1) / QT;
-        if (item_list)
-            for (uint32_t i = 0; i < ni; i++) item_list[ri + i] = (uint32_t)l;  // item -> list
-        rb += c;
-        ri += ni;
-    }
-    if (t == 1023) {
-        bucket_off[nlist] = sb[1023];
-        item_off[nlist] = si[1023];
+    if (t == 0) {
+        bucket_off[nlist] = carry_b;
+        item_off[nlist] = carry_i;
     }
 }
 
@@ -249,13 +276,10 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
     FAISS_THROW_IF_NOT_MSG(total < (1ll << 32), "n * nprobe must fit in 32 bits");
     HIP_CHECK(hipMemsetAsync(b.counts, 0, sizeof(uint32_t) * nlist, s));
     if (total > 0) {
-        if (nlist <= BC_MAXL)
-            k_bucket_count_lds<<<dim3((unsigned)cdiv(total, 1024 * BC_PER)), dim3(1024),
-                                 sizeof(uint32_t) * nlist, s>>>(assign, total, list_len, nlist,
-                                                                b.counts, b.cursor);
-        else
-            k_bucket_count<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
-                    assign, total, list_len, nlist, b.counts, b.cursor);
+        const int nr = (int)cdiv(nlist, BC_MAXL);  // list ranges (LDS histogram each)
+        k_bucket_count_lds<<<dim3((unsigned)cdiv(total, 1024 * BC_PER), (unsigned)nr), dim3(1024),
+                             sizeof(uint32_t) * std::min(nlist, BC_MAXL), s>>>(
+                assign, total, list_len, nlist, b.counts, b.cursor);
         HIP_LAUNCH_CHECK();
     }
     k_bucket_scan<<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off, b.item_off,

@@ -409,26 +409,56 @@ __device__ __forceinline__ float eval_rows64(const float* xr /* LDS copy of the 
 // dis = dis0 + (((0 + sim_0) + sim_1) + ...), every small product in the
 // fvec order of ref_arith.h.  xs: the query (LDS).
 template <int PQD>
+__device__ __forceinline__ float pq_sim(const PQArgs& pa, const float* xm, const float* ym,
+                                        const float* c) {
+    if (pa.table1) {
+        const float s2 = ref_ip(xm, c, PQD);
+        const float P = fmaf(2.f, ref_ip(ym, c, PQD), ref_norm(c, PQD));
+        return fmaf(-2.f, s2, P);
+    }
+    __attribute__((aligned(16))) float rr[PQD];
+#pragma unroll
+    for (int i = 0; i < PQD; i++) rr[i] = xm[i] - ym[i];
+    return ref_l2(rr, c, PQD);
+}
+
+template <int PQD>
 __device__ __forceinline__ float pq_exact(const PQArgs& pa, const float* xs, uint32_t grow,
                                           uint32_t l, float d0) {
     const uint8_t* cp = pa.codes + (size_t)grow * pa.cs;
     const float* yc = pa.cent + (size_t)l * pa.ldcent;
     float acc = 0.f;
-    for (int m = 0; m < pa.M; m++) {
-        const int j = cp[m];
-        const float* c = pa.pq_cent + ((size_t)m * 256 + j) * PQD;
-        float sim;
-        if (pa.table1) {
-            const float s2 = ref_ip(xs + m * PQD, c, PQD);
-            const float P = fmaf(2.f, ref_ip(yc + m * PQD, c, PQD), ref_norm(c, PQD));
-            sim = fmaf(-2.f, s2, P);
-        } else {
-            __attribute__((aligned(16))) float rr[PQD];
+    // UB subquantizers per step (32 centroid + coarse floats in flight):
+    // their code bytes and rows are loaded together, then summed in m order
+    constexpr int UB = PQD == 2 ? 8 : PQD == 4 ? 4 : 2;
+    int m0 = 0;
+    for (; m0 + UB <= pa.M; m0 += UB) {
+        // code rows are 4-B aligned (cs is a multiple of 4, m0 of UB)
+        uint32_t cb[(UB + 3) / 4];
+        if constexpr (UB >= 4) {
 #pragma unroll
-            for (int i = 0; i < PQD; i++) rr[i] = xs[m * PQD + i] - yc[m * PQD + i];
-            sim = ref_l2(rr, c, PQD);
+            for (int i = 0; i < UB / 4; i++) cb[i] = *(const uint32_t*)(cp + m0 + 4 * i);
+        } else {
+            cb[0] = (uint32_t)cp[m0] | ((uint32_t)cp[m0 + 1] << 8);
         }
-        acc += sim;
+        __attribute__((aligned(16))) float cv[UB][PQD];
+        __attribute__((aligned(16))) float yv[UB][PQD];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const uint32_t j = (cb[u >> 2] >> (8 * (u & 3))) & 0xffu;
+            const float* c = pa.pq_cent + ((size_t)(m0 + u) * 256 + j) * PQD;
+#pragma unroll
+            for (int i = 0; i < PQD; i++) {
+                cv[u][i] = c[i];
+                yv[u][i] = yc[(m0 + u) * PQD + i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) acc += pq_sim<PQD>(pa, xs + (m0 + u) * PQD, yv[u], cv[u]);
+    }
+    for (int m = m0; m < pa.M; m++) {
+        const int j = cp[m];
+        acc += pq_sim<PQD>(pa, xs + m * PQD, yc + m * PQD, pa.pq_cent + ((size_t)m * 256 + j) * PQD);
     }
     return (pa.table1 ? d0 : 0.f) + acc;
 }

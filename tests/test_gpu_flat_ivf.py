@@ -269,3 +269,21 @@ def test_filter_precisions_identical(amd, orc, cfg1, monkeypatch, k):
     ref = out[("exact", "bf16x2")]
     for key, (D, I) in out.items():
         assert_same_results(D, I, *ref)
+
+
+@pytest.mark.gpu
+def test_ivf_many_lists_bucketing(amd, orc, gpu):
+    # nlist > 16384: the bucket count runs one LDS histogram per list range
+    # (c5's IVF65536 geometry), the scan walks the counts in 4096-list chunks
+    d, nlist = 16, 20000
+    xb = rand(orc, 2 * nlist, d, 71)
+    idx = amd.index_factory(d, f"IVF{nlist},Flat")
+    idx.train(xb)
+    idx.add(xb)
+    xq = rand(orc, 3000, d, 72)
+    idx.nprobe = 16
+    Dq, Iq = idx.quantizer.search(xq, 16)
+    D, I = idx.search_preassigned(xq, 10, Iq, Dq)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir = ref.search_preassigned(xq, 10, Iq, Dq)
+    assert_same_results(D, I, Dr, Ir)
