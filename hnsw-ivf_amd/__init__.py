@@ -119,6 +119,18 @@ def _declare(L):
         "faiss_IndexIVF_nprobe": (C.c_size_t, [_P]),
         "faiss_IndexIVF_set_nprobe": (None, [_P, C.c_size_t]),
         "faiss_SearchParametersIVF_max_codes": (C.c_size_t, [_P]),
+        "faiss_IDSelector_is_member": (C.c_int, [_P, _I64]),
+        "faiss_IDSelector_free": (None, [_P]),
+        "faiss_IDSelectorRange_new": (C.c_int, [C.POINTER(_P), _I64, _I64]),
+        "faiss_IDSelectorBatch_new": (C.c_int, [C.POINTER(_P), C.c_size_t, _P]),
+        "faiss_amd_IDSelectorArray_new": (C.c_int, [C.POINTER(_P), C.c_size_t, _P]),
+        "faiss_IDSelectorBitmap_new": (C.c_int, [C.POINTER(_P), C.c_size_t, _P]),
+        "faiss_IDSelectorNot_new": (C.c_int, [C.POINTER(_P), _P]),
+        "faiss_IDSelectorAnd_new": (C.c_int, [C.POINTER(_P), _P, _P]),
+        "faiss_IDSelectorOr_new": (C.c_int, [C.POINTER(_P), _P, _P]),
+        "faiss_IDSelectorXOr_new": (C.c_int, [C.POINTER(_P), _P, _P]),
+        "faiss_SearchParameters_new": (C.c_int, [C.POINTER(_P), _P]),
+        "faiss_SearchParameters_free": (None, [_P]),
         "faiss_SearchParametersIVF_set_max_codes": (None, [_P, C.c_size_t]),
         "faiss_amd_IndexIVFPQ_set_use_precomputed_table": (C.c_int, [_P, C.c_int]),
         "faiss_amd_IndexIVF_max_codes": (C.c_size_t, [_P]),
@@ -596,11 +608,82 @@ class IndexShardsIVF(IndexIVF):
         return lib().faiss_amd_IndexShardsIVF_count(self.h)
 
 
+class IDSelector:
+    """faiss/impl/IDSelector.h selectors (membership evaluated on the GPU for
+    every inverted-list row; non-members are skipped by the IVF scans)."""
+
+    def __init__(self, h, keep=()):
+        self.h = h
+        self._keep = keep  # borrowed arrays / child selectors stay alive
+
+    def is_member(self, i):
+        return bool(lib().faiss_IDSelector_is_member(self.h, int(i)))
+
+    def __del__(self):
+        try:
+            lib().faiss_IDSelector_free(self.h)
+        except Exception:
+            pass
+
+
+def IDSelectorRange(imin, imax):
+    p = C.c_void_p()
+    _check(lib().faiss_IDSelectorRange_new(C.byref(p), int(imin), int(imax)))
+    return IDSelector(p)
+
+
+def IDSelectorBatch(ids):
+    ids = np.ascontiguousarray(ids, dtype=np.int64)
+    p = C.c_void_p()
+    _check(lib().faiss_IDSelectorBatch_new(C.byref(p), len(ids), _ptr(ids)))
+    return IDSelector(p)
+
+
+def IDSelectorArray(ids):
+    ids = np.ascontiguousarray(ids, dtype=np.int64)
+    p = C.c_void_p()
+    _check(lib().faiss_amd_IDSelectorArray_new(C.byref(p), len(ids), _ptr(ids)))
+    return IDSelector(p, (ids,))
+
+
+def IDSelectorBitmap(bitmap):
+    bm = np.ascontiguousarray(bitmap, dtype=np.uint8)
+    p = C.c_void_p()
+    _check(lib().faiss_IDSelectorBitmap_new(C.byref(p), len(bm), _ptr(bm)))
+    return IDSelector(p, (bm,))
+
+
+def IDSelectorNot(sel):
+    p = C.c_void_p()
+    _check(lib().faiss_IDSelectorNot_new(C.byref(p), sel.h))
+    return IDSelector(p, (sel,))
+
+
+def _sel_binary(fn, a, b):
+    p = C.c_void_p()
+    _check(fn(C.byref(p), a.h, b.h))
+    return IDSelector(p, (a, b))
+
+
+def IDSelectorAnd(a, b):
+    return _sel_binary(lib().faiss_IDSelectorAnd_new, a, b)
+
+
+def IDSelectorOr(a, b):
+    return _sel_binary(lib().faiss_IDSelectorOr_new, a, b)
+
+
+def IDSelectorXOr(a, b):
+    return _sel_binary(lib().faiss_IDSelectorXOr_new, a, b)
+
+
 class SearchParametersIVF:
-    def __init__(self, nprobe=1, max_codes=0, quantizer_efSearch=0):
+    def __init__(self, nprobe=1, max_codes=0, quantizer_efSearch=0, sel=None):
         p = C.c_void_p()
-        _check(lib().faiss_SearchParametersIVF_new_with(C.byref(p), None, nprobe, max_codes))
+        _check(lib().faiss_SearchParametersIVF_new_with(C.byref(p), sel.h if sel else None,
+                                                        nprobe, max_codes))
         self.h = p
+        self._sel = sel
         if quantizer_efSearch:
             lib().faiss_amd_SearchParametersIVF_set_quantizer_efSearch(self.h,
                                                                        int(quantizer_efSearch))

@@ -117,13 +117,70 @@ int faiss_SearchParametersIVF_new(FaissSearchParametersIVF** p_sp) {
 }
 int faiss_SearchParametersIVF_new_with(FaissSearchParametersIVF** p_sp, void* sel, size_t nprobe,
                                        size_t max_codes) {
-    C_TRY FAISS_THROW_IF_NOT_MSG(sel == nullptr, "IDSelector is not supported on this path");
-    auto sp = new SearchParamsC();
+    C_TRY auto sp = new SearchParamsC();
+    sp->ivf.sel = reinterpret_cast<IDSelector*>(sel);
     sp->ivf.nprobe = nprobe;
     sp->ivf.max_codes = max_codes;
     *p_sp = reinterpret_cast<FaissSearchParametersIVF*>(sp);
     C_CATCH
 }
+// ---------------- IDSelector (c_api/impl/AuxIndexStructures_c.h:50-110)
+int faiss_SearchParameters_new(FaissSearchParameters** p_sp, FaissIDSelector* sel) {
+    C_TRY auto sp = new SearchParamsC();
+    sp->ivf.sel = reinterpret_cast<IDSelector*>(sel);
+    sp->ivf.nprobe = 0;  // 0 = the index's own nprobe (plain SearchParameters)
+    *p_sp = reinterpret_cast<FaissSearchParameters*>(sp);
+    C_CATCH
+}
+void faiss_SearchParameters_free(FaissSearchParameters* obj) {
+    delete reinterpret_cast<SearchParamsC*>(obj);
+}
+static IDSelector* SEL(FaissIDSelector* p) { return reinterpret_cast<IDSelector*>(p); }
+static const IDSelector* SEL(const FaissIDSelector* p) {
+    return reinterpret_cast<const IDSelector*>(p);
+}
+int faiss_IDSelector_is_member(const FaissIDSelector* sel, idx_t id) {
+    return SEL(sel)->is_member(id) ? 1 : 0;
+}
+void faiss_IDSelector_free(FaissIDSelector* sel) { delete SEL(sel); }
+int faiss_IDSelectorRange_new(FaissIDSelectorRange** p_sel, idx_t imin, idx_t imax) {
+    C_TRY* p_sel = reinterpret_cast<FaissIDSelectorRange*>(new IDSelectorRange(imin, imax));
+    C_CATCH
+}
+int faiss_IDSelectorBatch_new(FaissIDSelectorBatch** p_sel, size_t n, const idx_t* indices) {
+    C_TRY* p_sel = reinterpret_cast<FaissIDSelectorBatch*>(new IDSelectorBatch(n, indices));
+    C_CATCH
+}
+int faiss_amd_IDSelectorArray_new(FaissIDSelector** p_sel, size_t n, const idx_t* ids) {
+    C_TRY* p_sel = reinterpret_cast<FaissIDSelector*>(new IDSelectorArray(n, ids));
+    C_CATCH
+}
+int faiss_IDSelectorBitmap_new(FaissIDSelectorBitmap** p_sel, size_t n, const uint8_t* bitmap) {
+    C_TRY* p_sel = reinterpret_cast<FaissIDSelectorBitmap*>(new IDSelectorBitmap(n, bitmap));
+    C_CATCH
+}
+int faiss_IDSelectorNot_new(FaissIDSelectorNot** p_sel, const FaissIDSelector* sel) {
+    C_TRY* p_sel = reinterpret_cast<FaissIDSelectorNot*>(new IDSelectorNot(SEL(sel)));
+    C_CATCH
+}
+static int sel_binary(FaissIDSelector** p, const FaissIDSelector* a, const FaissIDSelector* b,
+                      int op) {
+    C_TRY* p = reinterpret_cast<FaissIDSelector*>(new IDSelectorBinary(SEL(a), SEL(b), op));
+    C_CATCH
+}
+int faiss_IDSelectorAnd_new(FaissIDSelectorAnd** p_sel, const FaissIDSelector* lhs,
+                            const FaissIDSelector* rhs) {
+    return sel_binary(reinterpret_cast<FaissIDSelector**>(p_sel), lhs, rhs, 0);
+}
+int faiss_IDSelectorOr_new(FaissIDSelectorOr** p_sel, const FaissIDSelector* lhs,
+                           const FaissIDSelector* rhs) {
+    return sel_binary(reinterpret_cast<FaissIDSelector**>(p_sel), lhs, rhs, 1);
+}
+int faiss_IDSelectorXOr_new(FaissIDSelectorXOr** p_sel, const FaissIDSelector* lhs,
+                            const FaissIDSelector* rhs) {
+    return sel_binary(reinterpret_cast<FaissIDSelector**>(p_sel), lhs, rhs, 2);
+}
+
 void faiss_SearchParametersIVF_free(FaissSearchParametersIVF* obj) {
     delete reinterpret_cast<SearchParamsC*>(obj);
 }

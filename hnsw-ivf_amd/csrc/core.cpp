@@ -273,7 +273,10 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
 }
 
 void IndexFlat::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
-                              idx_t* labels, const SearchParameters*, hipStream_t s) const {
+                              idx_t* labels, const SearchParameters* params,
+                              hipStream_t s) const {
+    FAISS_THROW_IF_NOT_MSG(!params || !params->sel,
+                           "IDSelector is supported by the IVF indexes only on this path");
     DeviceGuard g(device);
     knn_device<idx_t>(n, x, ldx, (int)k, distances, labels, s);
 }

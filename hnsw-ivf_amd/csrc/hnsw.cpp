@@ -460,6 +460,8 @@ void IndexHNSW::search_stats(idx_t n, const float* x, idx_t k, float* distances,
 void IndexHNSW::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
                               idx_t* labels, const SearchParameters* params,
                               hipStream_t s) const {
+    FAISS_THROW_IF_NOT_MSG(!params || !params->sel,
+                           "IDSelector is supported by the IVF indexes only on this path");
     DevGuard2 dg(device);
     hnsw_device<idx_t>(n, x, ldx, (int)k, distances, labels, params, s);
 }

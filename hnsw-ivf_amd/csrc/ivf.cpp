@@ -224,6 +224,17 @@ const int32_t* IndexIVF::apply_max_codes(idx_t n, int np, const int32_t* assign,
     return s_alim_.as<int32_t>();
 }
 
+const uint8_t* IndexIVF::apply_selector(const SearchParameters* params, hipStream_t s) const {
+    if (!params || !params->sel) return nullptr;
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    const int64_t rows = std::max<int64_t>((int64_t)arena_rows_, 1);
+    s_selmask_.reserve((size_t)rows + 16);
+    HIP_CHECK(hipMemsetAsync(s_selmask_.ptr, 0, (size_t)rows + 16, s));
+    params->sel->mark_device(d_ids_.as<int64_t>(), (int64_t)arena_rows_, s_selmask_.as<uint8_t>(),
+                             s);
+    return s_selmask_.as<uint8_t>();
+}
+
 void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
                              idx_t* labels, const SearchParameters* params_in,
                              hipStream_t s) const {
@@ -234,12 +245,13 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
         params = dynamic_cast<const SearchParametersIVF*>(params_in);
         FAISS_THROW_IF_NOT_MSG(params, "IndexIVF params have incorrect type");
     }
-    const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
+    const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
     const size_t mc = params ? params->max_codes : max_codes;
     FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
     DevGuard dg(device);
     sync_device();
+    const uint8_t* selm = apply_selector(params, s);
     // device API: asynchronous, so indexIVF_stats is maintained by the host
     // entry points (search / search_stats / search_preassigned) only
     const idx_t qchunk = search_chunk(n, np, k);
@@ -253,7 +265,7 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
         const uint32_t* lim = nullptr;
         const int32_t* asg = apply_max_codes(nq, (int)np, s_ci_.as<int32_t>(), mc, &lim, s);
         search_preassigned_device(nq, x + q0 * ldx, ldx, k, (int)np, asg, s_cd_.as<float>(),
-                                  distances + q0 * k, labels + q0 * k, s, lim);
+                                  distances + q0 * k, labels + q0 * k, s, lim, selm);
     }
 }
 
@@ -298,7 +310,7 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
     FAISS_THROW_IF_NOT(k > 0);
     FAISS_THROW_IF_NOT_MSG(!store_pairs, "store_pairs is not supported on the GPU path");
     check_parallel_mode(parallel_mode);
-    const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
+    const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
     const size_t mc = params ? params->max_codes : max_codes;
     if (n == 0) return;
@@ -333,8 +345,9 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
     hipEvent_t e0 = ev.mark(s);
     const uint32_t* lim = nullptr;
     const int32_t* asg = apply_max_codes(n, (int)np, ba.as<int32_t>(), mc, &lim, s);
+    const uint8_t* selm = apply_selector(params, s);
     search_preassigned_device(n, bx.as<float>(), ldx, k, (int)np, asg, bc.as<float>(),
-                              bd.as<float>(), bi.as<idx_t>(), s, lim);
+                              bd.as<float>(), bi.as<idx_t>(), s, lim, selm);
     hipEvent_t e1 = ev.mark(s);
     kern::ivf_visit_stats(asg, n * (int64_t)np, d_list_len_.as<uint32_t>(), (int)nlist, lim,
                           s_stats_.as<unsigned long long>(), s);
@@ -377,7 +390,7 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
         params = dynamic_cast<const SearchParametersIVF*>(params_in);
         FAISS_THROW_IF_NOT_MSG(params, "IndexIVF params have incorrect type");
     }
-    const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
+    const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
     check_parallel_mode(parallel_mode);
     const size_t mc = params ? params->max_codes : max_codes;
@@ -402,6 +415,7 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
     HIP_CHECK(hipMemsetAsync(s_stats_.ptr, 0, 2 * sizeof(unsigned long long), s));
     StageEvents ev;
     std::vector<hipEvent_t> marks;
+    const uint8_t* selm = apply_selector(params, s);
     for (idx_t q0 = 0; q0 < n; q0 += qchunk) {
         const idx_t nq = std::min(qchunk, n - q0);
         marks.push_back(ev.mark(s));
@@ -412,7 +426,7 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
         const int32_t* asg = apply_max_codes(nq, (int)np, s_ci_.as<int32_t>(), mc, &lim, s);
         search_preassigned_device(nq, bx.as<float>() + q0 * ldx, ldx, k, (int)np, asg,
                                   s_cd_.as<float>(), bd.as<float>() + q0 * k,
-                                  bi.as<idx_t>() + q0 * k, s, lim);
+                                  bi.as<idx_t>() + q0 * k, s, lim, selm);
         marks.push_back(ev.mark(s));
         kern::ivf_visit_stats(asg, nq * (int64_t)np, d_list_len_.as<uint32_t>(), (int)nlist,
                               lim, s_stats_.as<unsigned long long>(), s);
@@ -495,7 +509,7 @@ void IndexIVFFlat::upload_extra() const {
 void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
                                              const int32_t* assign, const float*,
                                              float* distances, idx_t* labels, hipStream_t s,
-                                             const uint32_t* lim) const {
+                                             const uint32_t* lim, const uint8_t* sel) const {
     if (n <= 0) return;
     sync_device();
     std::lock_guard<std::recursive_mutex> g(mu_);
@@ -509,6 +523,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     kern::IVFBuckets b{s_counts_.as<uint32_t>(), s_boff_.as<uint32_t>(), s_ioff_.as<uint32_t>(),
                        s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
     b.lim = lim;
+    b.sel = sel;
     const char* env = getenv("FAISS_AMD_IVF_SCAN");
     int mode = scan_mode;
     if (env && !strcmp(env, "exact")) mode = 1;
@@ -569,7 +584,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     kern::ivf_exact_fallback(s_flags_.as<uint32_t>(), assign, d_list_off_.as<uint32_t>(),
                              d_list_len_.as<uint32_t>(), (int)nlist, x, ldx,
                              d_codes_.as<float>(), l, d_ids_.as<int64_t>(), d, n, np, (int)k, l2,
-                             lim, distances, labels, s);
+                             lim, sel, distances, labels, s);
 }
 
 // ---------------------------------------------------------------- PQ
@@ -725,7 +740,7 @@ void IndexIVFPQ::upload_extra() const {
 void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
                                            const int32_t* assign, const float* centroid_dis,
                                            float* distances, idx_t* labels, hipStream_t s,
-                                           const uint32_t* lim) const {
+                                           const uint32_t* lim, const uint8_t* sel) const {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_MSG(metric_type == METRIC_L2, "IVFPQ inner product not supported on GPU");
     sync_device();
@@ -745,6 +760,7 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         kern::IVFBuckets b{s_counts_.as<uint32_t>(), s_boff_.as<uint32_t>(),
                            s_ioff_.as<uint32_t>(), s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
         b.lim = lim;
+        b.sel = sel;
         const int KE = kern::ivf_mfma_kq((int)k, d);
         s_pkeys_.reserve(sizeof(uint32_t) * n * np * KE);
         s_precs_.reserve(sizeof(kern::ProbeRec) * n * np);
@@ -783,7 +799,7 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
             pa.table1 = use_precomputed_table == 1 ? 1 : 0;
             kern::ivfpq_rerank(s_pkeys_.as<uint32_t>(), s_precs_.as<kern::ProbeRec>(), x, ldx, d,
                                d_ids_.as<int64_t>(), pa, (int)pq.dsub, n, np, KT, pq_obits_,
-                               (int)k, distances, labels,
+                               (int)k, sel, distances, labels,
                                dbg ? s_pflags_.as<uint32_t>() : nullptr, s);
         }
         if (dbg) {
@@ -801,8 +817,8 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
     kern::ivfpq_scan(x, ldx, d_pq_.as<float>(), (int)pq.M, (int)pq.ksub, (int)pq.dsub,
                      d_codes_.as<uint8_t>(), d_terms_.as<float>(), d_ids_.as<int64_t>(),
                      d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(), (int)nlist, assign,
-                     centroid_dis, lim, n, np, (int)k, by_residual ? 1 : 0, distances, labels,
-                     s);
+                     centroid_dis, lim, sel, n, np, (int)k, by_residual ? 1 : 0, distances,
+                     labels, s);
 }
 
 // ---------------------------------------------------------------- shards
@@ -871,7 +887,7 @@ void IndexShardsIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, fl
                                    hipStream_t s) const {
     // faiss/IndexShardsIVF.cpp:158-245
     const SearchParametersIVF* params = dynamic_cast<const SearchParametersIVF*>(params_in);
-    const size_t np = std::min(nlist, params ? params->nprobe : nprobe);
+    const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0 && k > 0);
     const int ns = (int)shards.size();
     FAISS_THROW_IF_NOT(ns > 0);
@@ -893,9 +909,10 @@ void IndexShardsIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, fl
         const int32_t* asg = shards[no]->apply_max_codes(
                 n, (int)np, s_ci_.as<int32_t>(), params ? params->max_codes : shards[no]->max_codes,
                 &lim, s);
+        const uint8_t* selm = shards[no]->apply_selector(params, s);
         shards[no]->search_preassigned_device(n, x, ldx, k, (int)np, asg, s_cd_.as<float>(),
                                               s_all_d_.as<float>() + (size_t)no * n * k, li, s,
-                                              lim);
+                                              lim, selm);
         if (successive_ids) kern::translate_labels(li, (int64_t)n * k, translation, s);
         translation += shards[no]->ntotal;
     }

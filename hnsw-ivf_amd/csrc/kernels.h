@@ -112,6 +112,8 @@ struct IVFBuckets {
     // optional (max_codes): rows of each entry's list that are scanned (a
     // prefix; probe_limits), nullptr = whole lists
     const uint32_t* lim = nullptr;
+    // optional (IDSelector): arena-row membership mask, nullptr = every row
+    const uint8_t* sel = nullptr;
 };
 // max_codes (faiss/IndexIVF.cpp:595-631, scan_one_list :546-550): per query,
 // probes in coarse order; the probe that reaches max_codes is cut to the rows
@@ -133,6 +135,9 @@ struct PQArgs {
     int M = 0;
     int table1 = 0;  // use_precomputed_table == 1 (else table 0, by residual)
 };
+struct RerankSel {  // IDSelector mask of the arena rows (nullptr = all)
+    const uint8_t* sel = nullptr;
+};
 bool ivfpq_mfma_eligible(int d, int M, int k, int nprobe);
 double ivfpq_mfma_coef(int d, int M);
 // bf16 decode table ([M][256][dsub] bf16) and per-row |y_R|, |y_R - bf16(y_R)|
@@ -145,7 +150,8 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
                   int* kt_out, hipStream_t s);
 void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx, int d,
                   const int64_t* ids, const PQArgs& pa, int dsub, int64_t n, int nprobe, int KT,
-                  int obits, int k, float* D, int64_t* I, uint32_t* stats, hipStream_t s);
+                  int obits, int k, const uint8_t* sel, float* D, int64_t* I, uint32_t* stats,
+                  hipStream_t s);
 
 // IndexIVFStats counters of a batch (faiss/IndexIVF.cpp:1184-1198):
 // stats[0] += non-empty lists visited, stats[1] += codes scanned (device)
@@ -194,8 +200,8 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 void ivf_exact_fallback(const uint32_t* flags, const int32_t* assign, const uint32_t* list_off,
                         const uint32_t* list_len, int nlist, const float* x, int ldx,
                         const float* codes, int ldc, const int64_t* ids, int d, int64_t n,
-                        int nprobe, int k, int metric_l2, const uint32_t* lim, float* D,
-                        int64_t* I, hipStream_t s);
+                        int nprobe, int k, int metric_l2, const uint32_t* lim,
+                        const uint8_t* sel, float* D, int64_t* I, hipStream_t s);
 
 // per-query merge of the nprobe partial top-k, reference
 // faiss/IndexIVF.cpp:595-631 (heap over probes) + Heap.h:421-450 (reorder)
@@ -214,7 +220,8 @@ void ivf_merge(const float* part_k1, const long long* part_k2, const int32_t* as
 void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int ksub, int dsub,
                 const uint8_t* codes, const float* terms, const int64_t* ids,
                 const uint32_t* list_off, const uint32_t* list_len, int nlist,
-                const int32_t* assign, const float* coarse_dis, const uint32_t* lim, int64_t n,
+                const int32_t* assign, const float* coarse_dis, const uint32_t* lim,
+                const uint8_t* sel, int64_t n,
                 int nprobe, int k, int by_residual, float* D, int64_t* I, hipStream_t s);
 
 // term[v] = sum_m (||c_{m,code}||^2 + 2 <yC_m, c_{m,code}>) for every arena row

@@ -309,7 +309,8 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
         const uint32_t* __restrict__ list_len, int nlist, int dp, int dp_true, int nprobe,
         int k, const uint32_t* __restrict__ bucket_off, const uint32_t* __restrict__ item_off,
         const uint32_t* __restrict__ entries, const uint32_t* __restrict__ lim,
-        float* __restrict__ part_k1, long long* __restrict__ part_k2) {
+        const uint8_t* __restrict__ sel, float* __restrict__ part_k1,
+        long long* __restrict__ part_k2) {
     // one array: the end-of-kernel queue merge reuses it (64 KB at KQ=32)
     __shared__ __attribute__((aligned(16))) float smem_xy[(SQT + 64) * SSD];
     float* Xs = smem_xy;
@@ -501,6 +502,7 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
                 const int nvq = min(nv, qlim_s[q] - v0);
 #pragma unroll 4
                 for (int j = s4; j < nvq; j += 4) {
+                    if (sel && !sel[row0 + v0 + j]) continue;  // IDSelector (use_sel)
                     float dis = Ds[q * (SVT + 1) + j];
                     float k1 = L2 ? dis : -dis;
                     if (k1 < FLT_MAX) {
@@ -513,7 +515,7 @@ __global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
             }
         } else {
             // wave w owns queries w*16 .. w*16+15
-            const bool lane_ok = lane < nv;
+            const bool lane_ok = lane < nv && (!sel || sel[row0 + v0 + lane]);
             const long long my_id = ids_s[lane];
 #pragma unroll
             for (int qq = 0; qq < NQW; qq++) {
@@ -589,11 +591,11 @@ static void launch_scan(bool l2, int64_t grid, hipStream_t s, const float* x, in
     if (l2)
         k_ivf_flat_scan<true, KQ><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
                 x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, d, nprobe, k, b.bucket_off,
-                b.item_off, b.entries, b.lim, pk1, pk2);
+                b.item_off, b.entries, b.lim, b.sel, pk1, pk2);
     else
         k_ivf_flat_scan<false, KQ><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
                 x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, d, nprobe, k, b.bucket_off,
-                b.item_off, b.entries, b.lim, pk1, pk2);
+                b.item_off, b.entries, b.lim, b.sel, pk1, pk2);
 }
 
 void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const int64_t* ids,

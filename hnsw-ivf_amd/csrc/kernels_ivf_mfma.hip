@@ -105,8 +105,9 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         int nprobe, float coef, int obits, const uint32_t* __restrict__ bucket_off,
         const uint32_t* __restrict__ item_off, const ItemDesc* __restrict__ item_desc,
         const uint32_t* __restrict__ item_entries, uint32_t max_items,
-        const uint32_t* __restrict__ lim, uint32_t* __restrict__ keys,
-        ProbeRec* __restrict__ recs, unsigned long long* __restrict__ ftrace) {
+        const uint32_t* __restrict__ lim, const uint8_t* __restrict__ sel,
+        uint32_t* __restrict__ keys, ProbeRec* __restrict__ recs,
+        unsigned long long* __restrict__ ftrace) {
     const unsigned long long ft0 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     // two code tiles (double buffer), row stride CSB bytes = (Y3 ? 4 : 2) * DB + 16
     __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * ((Y3 ? 4 : 2) * 16 * NS + 16)];
@@ -163,10 +164,13 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             // rows < roundup(len, 16) are inside the list's arena slot
             float4 v = r < nvn ? *(const float4*)(ynl + v0n + r) : make_float4(0.f, 0.f, 0.f, 0.f);
             if (!L2) v = make_float4(0.f, 0.f, 0.f, 0.f);
-            pn.x = r + 0 < nvn ? v.x : WS_INF;
-            pn.y = r + 1 < nvn ? v.y : WS_INF;
-            pn.z = r + 2 < nvn ? v.z : WS_INF;
-            pn.w = r + 3 < nvn ? v.w : WS_INF;
+            // non-members of an IDSelector are treated as padding rows
+            uchar4 ms = make_uchar4(1, 1, 1, 1);
+            if (sel && r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
+            pn.x = r + 0 < nvn && ms.x ? v.x : WS_INF;
+            pn.y = r + 1 < nvn && ms.y ? v.y : WS_INF;
+            pn.z = r + 2 < nvn && ms.z ? v.z : WS_INF;
+            pn.w = r + 3 < nvn && ms.w ? v.w : WS_INF;
         }
     };
     auto stash = [&](int buf) {
@@ -252,7 +256,8 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             const uint32_t ord = key & lowmask;
             const int r = (int)(ord & 15u);
             const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-            ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
+            ko[i] = (key != 0xffffffffu && row < elen && (!sel || sel[row0 + row])) ? key
+                                                                                  : 0xffffffffu;
         }
         if (slot == 0) {
             // the list's largest margin bounds every kept row's margin:
@@ -483,6 +488,7 @@ struct RerankStream {
     uint32_t my_l;            // PQ: lane r: probe r's list
     float my_d0;              // PQ: lane r: probe r's coarse distance
     PQArgs pa;
+    const uint8_t* sel;       // IDSelector mask of the arena rows (nullptr: all)
 
     __device__ __forceinline__ void emit(bool ok, uint32_t grow, int r, float& k1,
                                          long long& k2) const {
@@ -549,7 +555,7 @@ struct RerankStream {
                 if (!((fl >> sl) & 1u)) continue;
                 for (int e0 = 0; e0 < ne; e0 += 64) {
                     const int row = ivf_stream_row(e0 + lane, sl);
-                    const bool ok = e0 + lane < ne && row < (int)len;
+                    const bool ok = e0 + lane < ne && row < (int)len && (!sel || sel[o + row]);
                     const uint32_t grow = o + (uint32_t)(ok ? row : 0);
                     const long long rank = ((long long)r << 32) | grow;
                     float k1;
@@ -568,7 +574,7 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
         const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
         const int64_t* __restrict__ ids, int d, int64_t n, int nprobe, int KT, int obits, int k,
         float* __restrict__ D, int64_t* __restrict__ I, uint32_t* __restrict__ stats,
-        unsigned long long* __restrict__ trace, PQArgs pa) {
+        unsigned long long* __restrict__ trace, PQArgs pa, const uint8_t* __restrict__ sel) {
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ uint32_t surv[RR_W][RR_CAP];
     __shared__ uint16_t sprobe[RR_W][RR_CAP];
@@ -698,7 +704,7 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
                 if (!((fl >> sl) & 1u)) continue;
                 for (int e0 = 0; e0 < ne; e0 += 64) {
                     const int row = ivf_stream_row(e0 + lane, sl);
-                    const bool in = e0 + lane < ne && row < (int)len;
+                    const bool in = e0 + lane < ne && row < (int)len && (!sel || sel[o + row]);
                     const unsigned long long bm = __ballot(in);
                     const int pos = ns + __popcll(bm & ((1ull << lane) - 1ull));
                     if (in && pos < RR_CAP) {
@@ -738,6 +744,7 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
     st.my_l = pr.pad;
     st.my_d0 = my_d0;
     st.pa = pa;
+    st.sel = sel;
     // ---- round trip 2: candidate rows and ids; up to 4 batches are ranked
     // directly, anything else goes through the general resolve
     bool done = false;
@@ -793,6 +800,7 @@ struct FullStream {
     const float* codes;
     const int64_t* ids;
     const uint32_t* lim;  // max_codes: rows scanned per probe (nullptr: all)
+    const uint8_t* sel;   // IDSelector mask of the arena rows (nullptr: all)
     template <class F>
     __device__ __forceinline__ void for_each(F f) const {
         for (int r = 0; r < nprobe; r++) {
@@ -802,7 +810,8 @@ struct FullStream {
             for (int v0 = 0; v0 < len; v0 += 64) {
                 float k1 = WS_INF;
                 long long k2 = WS_NOID, rank = 0;
-                bool ok = v0 + lane < len;
+                bool ok = v0 + lane < len &&
+                          (!sel || sel[(int64_t)list_off[lst] + v0 + lane]);
                 if (ok) {
                     const int64_t grow = (int64_t)list_off[lst] + v0 + lane;
                     const float* yr = codes + grow * ldc;
@@ -823,29 +832,30 @@ __global__ __launch_bounds__(64) void k_ivf_exact_fallback(
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
         const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
         const int64_t* __restrict__ ids, int d, int nprobe, int k,
-        const uint32_t* __restrict__ lim, float* __restrict__ D, int64_t* __restrict__ I) {
+        const uint32_t* __restrict__ lim, const uint8_t* __restrict__ sel,
+        float* __restrict__ D, int64_t* __restrict__ I) {
     const int64_t q = blockIdx.x;
     if (flags[q] == 0u) return;
     FullStream<L2> st{assign + q * nprobe, list_off, list_len, nlist, nprobe, d, ldc,
                       (int)threadIdx.x, x + q * ldx, codes, ids,
-                      lim ? lim + q * nprobe : nullptr};
+                      lim ? lim + q * nprobe : nullptr, sel};
     exact_topk_resolve(st, k, L2 ? 1 : 0, (int)threadIdx.x, true, D + q * k, I + q * k);
 }
 
 void ivf_exact_fallback(const uint32_t* flags, const int32_t* assign, const uint32_t* list_off,
                         const uint32_t* list_len, int nlist, const float* x, int ldx,
                         const float* codes, int ldc, const int64_t* ids, int d, int64_t n,
-                        int nprobe, int k, int metric_l2, const uint32_t* lim, float* D,
-                        int64_t* I, hipStream_t s) {
+                        int nprobe, int k, int metric_l2, const uint32_t* lim,
+                        const uint8_t* sel, float* D, int64_t* I, hipStream_t s) {
     if (n <= 0) return;
     if (metric_l2)
         k_ivf_exact_fallback<true><<<dim3((unsigned)n), dim3(64), 0, s>>>(
                 flags, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, nprobe, k,
-                lim, D, I);
+                lim, sel, D, I);
     else
         k_ivf_exact_fallback<false><<<dim3((unsigned)n), dim3(64), 0, s>>>(
                 flags, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, nprobe, k,
-                lim, D, I);
+                lim, sel, D, I);
     HIP_LAUNCH_CHECK();
 }
 
@@ -962,12 +972,12 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
             k_ivf_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
-                    b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, keys, recs, ftrace);    \
+                    b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, b.sel, keys, recs, ftrace);    \
         else                                                                                  \
             k_ivf_bf3_filter<L2V, KTV, NSV, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(\
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
-                    b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, keys, recs, ftrace);    \
+                    b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, b.sel, keys, recs, ftrace);    \
     } while (0)
 #define LAUNCH_A(L2V, KTV)                     \
     do {                                       \
@@ -1015,7 +1025,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 #define LAUNCH_B(L2V, VV)                                                                      \
     k_ivf_rerank<L2V, VV><<<dim3((unsigned)cdiv(n, RR_W)), dim3(64 * RR_W), 0, s>>>(           \
             keys, recs, x, ldx, codes, ldc, ids, d, n, nprobe, KE / 4, obits, k, D, I, stats,   \
-            trace, PQArgs{})
+            trace, PQArgs{}, b.sel)
 #define DISPATCH_V(L2V)                      \
     do {                                     \
         if (V == 2) LAUNCH_B(L2V, 2);        \
@@ -1048,7 +1058,8 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 // reference LUT arithmetic as the exact evaluator (pq_exact)
 void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx, int d,
                   const int64_t* ids, const PQArgs& pa, int dsub, int64_t n, int nprobe, int KT,
-                  int obits, int k, float* D, int64_t* I, uint32_t* stats, hipStream_t s) {
+                  int obits, int k, const uint8_t* sel, float* D, int64_t* I, uint32_t* stats,
+                  hipStream_t s) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(d <= BDM && d % 4 == 0);
     const int KE = 4 * KT;
@@ -1057,7 +1068,7 @@ void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, in
 #define LAUNCH_P(VV, DS)                                                                        \
     k_ivf_rerank<true, VV, DS><<<dim3((unsigned)cdiv(n, RR_W)), dim3(64 * RR_W), 0, s>>>(       \
             keys, recs, x, ldx, nullptr, 0, ids, d, n, nprobe, KT, obits, k, D, I, stats,         \
-            nullptr, pa)
+            nullptr, pa, sel)
 #define DISPATCH_P(DS)                       \
     do {                                     \
         if (V == 2) LAUNCH_P(2, DS);         \

@@ -33,8 +33,8 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan(
         const float* __restrict__ terms, const int64_t* __restrict__ ids,
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
         const int32_t* __restrict__ assign, const float* __restrict__ coarse_dis,
-        const uint32_t* __restrict__ lim, int nprobe, int k, int by_residual,
-        float* __restrict__ D, int64_t* __restrict__ I) {
+        const uint32_t* __restrict__ lim, const uint8_t* __restrict__ sel, int nprobe, int k,
+        int by_residual, float* __restrict__ D, int64_t* __restrict__ I) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* T = smem;                    // [M * ksub]
     float* xq = T + M * ksub;           // [M * dsub]
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan(
             const int v = v0 + lane;
             float k1 = WS_INF;
             long long k2 = WS_NOID;
-            if (v < len) {
+            if (v < len && (!sel || sel[row0 + v])) {
                 const int64_t row = row0 + v;
                 const uint32_t* cw = (const uint32_t*)(codes + row * code_stride);
                 float s = 0.f;
@@ -141,8 +141,9 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan_m(
         const uint8_t* __restrict__ codes, const float* __restrict__ terms,
         const int64_t* __restrict__ ids, const uint32_t* __restrict__ list_off,
         const uint32_t* __restrict__ list_len, int nlist, const int32_t* __restrict__ assign,
-        const float* __restrict__ coarse_dis, const uint32_t* __restrict__ lim, int nprobe,
-        int k, int by_residual, float* __restrict__ D, int64_t* __restrict__ I) {
+        const float* __restrict__ coarse_dis, const uint32_t* __restrict__ lim,
+        const uint8_t* __restrict__ sel, int nprobe, int k, int by_residual,
+        float* __restrict__ D, int64_t* __restrict__ I) {
     constexpr int CS = (M + 3) & ~3;  // code stride (bytes)
     constexpr int NW = CS / 4;        // 32-bit words per code
     __shared__ float T[M * 256];
@@ -221,6 +222,7 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan_m(
     auto load = [&](int rr, int vv, uint32_t (&wo)[NW], float& to, uint32_t& ro, bool& vo) {
         vo = rr < nprobe && vv + lane < (int)p_len[rr < nprobe ? rr : 0];
         ro = (rr < nprobe ? p_off[rr] : 0u) + (uint32_t)(vo ? vv + lane : 0);
+        vo = vo && (!sel || sel[ro]);  // IDSelector (use_sel)
         const uint8_t* cp = codes + (size_t)ro * CS;
         if constexpr (NW % 4 == 0) {
 #pragma unroll
@@ -331,8 +333,9 @@ __global__ __launch_bounds__(256) void k_ivfpq_scan_m(
 void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int ksub, int dsub,
                 const uint8_t* codes, const float* terms, const int64_t* ids,
                 const uint32_t* list_off, const uint32_t* list_len, int nlist,
-                const int32_t* assign, const float* coarse_dis, const uint32_t* lim, int64_t n,
-                int nprobe, int k, int by_residual, float* D, int64_t* I, hipStream_t s) {
+                const int32_t* assign, const float* coarse_dis, const uint32_t* lim,
+                const uint8_t* sel, int64_t n, int nprobe, int k, int by_residual, float* D,
+                int64_t* I, hipStream_t s) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
     FAISS_THROW_IF_NOT_MSG(nprobe >= 1 && nprobe <= 64, "nprobe must be in [1, 64] on this path");
@@ -343,7 +346,7 @@ void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int k
     if (M == MV) {                                                                             \
         k_ivfpq_scan_m<MV><<<dim3((unsigned)n), dim3(256), 0, s>>>(                            \
                 x, ldx, pq_centroids, dsub, codes, terms, ids, list_off, list_len, nlist, assign, \
-                coarse_dis, lim, nprobe, k, by_residual, D, I);                                \
+                coarse_dis, lim, sel, nprobe, k, by_residual, D, I);                           \
         HIP_LAUNCH_CHECK();                                                                    \
         return;                                                                                \
     }
@@ -355,7 +358,7 @@ void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int k
     FAISS_THROW_IF_NOT_MSG(lds <= 160 * 1024, "PQ LUT does not fit in LDS");
     k_ivfpq_scan<<<dim3((unsigned)n), dim3(256), lds, s>>>(
             x, ldx, pq_centroids, M, ksub, dsub, codes, code_stride, terms, ids, list_off,
-            list_len, nlist, assign, coarse_dis, lim, nprobe, k, by_residual, D, I);
+            list_len, nlist, assign, coarse_dis, lim, sel, nprobe, k, by_residual, D, I);
     HIP_LAUNCH_CHECK();
 }
 

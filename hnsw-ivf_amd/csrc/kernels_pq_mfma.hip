@@ -142,8 +142,8 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
         const float* __restrict__ lrmax, const float* __restrict__ lRmax, int nlist, int nprobe,
         float coef, int obits, const uint32_t* __restrict__ item_off,
         const ItemDesc* __restrict__ item_desc, const uint32_t* __restrict__ item_entries,
-        const uint32_t* __restrict__ lim, uint32_t* __restrict__ keys,
-        ProbeRec* __restrict__ recs) {
+        const uint32_t* __restrict__ lim, const uint8_t* __restrict__ sel,
+        uint32_t* __restrict__ keys, ProbeRec* __restrict__ recs) {
     constexpr int D = 16 * NS;
     constexpr int M = D / DSUB;
     constexpr int CS = (M + 3) & ~3;  // code stride (bytes)
@@ -206,10 +206,13 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
                 // rows < roundup(len, 16) are inside the list's arena slot
                 const float4 v = r < nvn ? *(const float4*)(terms + row0 + v0n + r)
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
-                tn.x = r + 0 < nvn ? v.x : WS_INF;
-                tn.y = r + 1 < nvn ? v.y : WS_INF;
-                tn.z = r + 2 < nvn ? v.z : WS_INF;
-                tn.w = r + 3 < nvn ? v.w : WS_INF;
+                // non-members of an IDSelector are treated as padding rows
+                uchar4 ms = make_uchar4(1, 1, 1, 1);
+                if (sel && r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
+                tn.x = r + 0 < nvn && ms.x ? v.x : WS_INF;
+                tn.y = r + 1 < nvn && ms.y ? v.y : WS_INF;
+                tn.z = r + 2 < nvn && ms.z ? v.z : WS_INF;
+                tn.w = r + 3 < nvn && ms.w ? v.w : WS_INF;
             }
         };
         load_codes(0);
@@ -277,7 +280,9 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
             for (int i = 0; i < KT; i++) {
                 const uint32_t key = tq.q[i];
                 const uint32_t row = ivf_key_row(key, lowmask, slot);
-                ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
+                ko[i] = (key != 0xffffffffu && row < elen && (!sel || sel[row0 + row]))
+                                ? key
+                                : 0xffffffffu;
             }
             if (slot == 0) {
                 const float xl = sqrtf(xn);
@@ -340,8 +345,8 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
         }                                                                                      \
         kfn<<<dim3((unsigned)grid), dim3(256), lds, s>>>(                                      \
                 x, ldx, (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, nlist,    \
-                nprobe, coef, obits, b.item_off, b.item_desc, b.item_entries, b.lim, keys,     \
-                recs);                                                                         \
+                nprobe, coef, obits, b.item_off, b.item_desc, b.item_entries, b.lim, b.sel,    \
+                keys, recs);                                                                   \
         HIP_LAUNCH_CHECK();                                                                    \
         return;                                                                                \
     }

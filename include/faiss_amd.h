@@ -23,8 +23,67 @@
 
 namespace faiss_amd {
 
+// ---------------------------------------------------------------- selectors
+// faiss/impl/IDSelector.h:20-180.  is_member() is the reference predicate;
+// mark_device() evaluates it for every arena row on the GPU (mask[r] = 1 when
+// ids[r] is a member; ids < 0 are padding rows and never members).
+struct IDSelector {
+    virtual ~IDSelector() = default;
+    virtual bool is_member(idx_t id) const = 0;
+    virtual void mark_device(const idx_t* ids, int64_t n, uint8_t* mask,
+                             hipStream_t stream) const = 0;
+};
+struct IDSelectorRange : IDSelector {  // [imin, imax)
+    idx_t imin, imax;
+    bool assume_sorted;  // reference fast path; same members here
+    IDSelectorRange(idx_t imin, idx_t imax, bool assume_sorted = false)
+            : imin(imin), imax(imax), assume_sorted(assume_sorted) {}
+    bool is_member(idx_t id) const override { return id >= imin && id < imax; }
+    void mark_device(const idx_t* ids, int64_t n, uint8_t* mask, hipStream_t s) const override;
+};
+struct IDSelectorArray : IDSelector {  // the n ids (not owned)
+    size_t n;
+    const idx_t* ids;
+    IDSelectorArray(size_t n, const idx_t* ids) : n(n), ids(ids) {}
+    bool is_member(idx_t id) const override;
+    void mark_device(const idx_t* ids, int64_t n, uint8_t* mask, hipStream_t s) const override;
+};
+struct IDSelectorBatch : IDSelector {  // a set of ids (copied)
+    std::vector<idx_t> sorted;
+    IDSelectorBatch(size_t n, const idx_t* indices);
+    bool is_member(idx_t id) const override;
+    void mark_device(const idx_t* ids, int64_t n, uint8_t* mask, hipStream_t s) const override;
+};
+struct IDSelectorBitmap : IDSelector {  // n bytes, bit i of the map (not owned)
+    size_t n;
+    const uint8_t* bitmap;
+    IDSelectorBitmap(size_t n, const uint8_t* bitmap) : n(n), bitmap(bitmap) {}
+    bool is_member(idx_t id) const override {
+        const uint64_t i = (uint64_t)id;
+        return (i >> 3) < n && ((bitmap[i >> 3] >> (i & 7)) & 1);
+    }
+    void mark_device(const idx_t* ids, int64_t n, uint8_t* mask, hipStream_t s) const override;
+};
+struct IDSelectorNot : IDSelector {
+    const IDSelector* sel;
+    explicit IDSelectorNot(const IDSelector* sel) : sel(sel) {}
+    bool is_member(idx_t id) const override { return !sel->is_member(id); }
+    void mark_device(const idx_t* ids, int64_t n, uint8_t* mask, hipStream_t s) const override;
+};
+struct IDSelectorBinary : IDSelector {  // And / Or / XOr
+    const IDSelector *lhs, *rhs;
+    int op;  // 0 and, 1 or, 2 xor
+    IDSelectorBinary(const IDSelector* l, const IDSelector* r, int op) : lhs(l), rhs(r), op(op) {}
+    bool is_member(idx_t id) const override {
+        const bool a = lhs->is_member(id), b = rhs->is_member(id);
+        return op == 0 ? (a && b) : op == 1 ? (a || b) : (a != b);
+    }
+    void mark_device(const idx_t* ids, int64_t n, uint8_t* mask, hipStream_t s) const override;
+};
+
 // ---------------------------------------------------------------- params
 struct SearchParameters {  // faiss/Index.h:63-70
+    IDSelector* sel = nullptr;  // only the vectors whose id is a member
     virtual ~SearchParameters() = default;
 };
 struct SearchParametersHNSW : SearchParameters {  // faiss/impl/HNSW.h:46-52
@@ -274,7 +333,11 @@ struct IndexIVF : Index {
                                            int nprobe, const int32_t* assign,
                                            const float* centroid_dis, float* distances,
                                            idx_t* labels, hipStream_t stream,
-                                           const uint32_t* lim = nullptr) const = 0;
+                                           const uint32_t* lim = nullptr,
+                                           const uint8_t* sel = nullptr) const = 0;
+    // IDSelector of the call -> arena-row membership mask (index scratch),
+    // nullptr when there is none (faiss/IndexIVF.cpp:418-430)
+    const uint8_t* apply_selector(const SearchParameters* params, hipStream_t stream) const;
     // max_codes (faiss/IndexIVF.cpp:595-631): per query, the probe prefix
     // scanned before nscan reaches max_codes; returns the assignment with the
     // dropped probes set to -1 and sets *lim (both in index scratch)
@@ -304,7 +367,8 @@ struct IndexIVF : Index {
     // scratch
     mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_counts_, s_boff_, s_ioff_, s_cur_, s_ent_,
             s_pk1_, s_pk2_, s_q_;
-    mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_;
+    mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_,
+            s_selmask_;
 
    private:
     idx_t search_chunk(idx_t n, size_t np, idx_t k) const;
@@ -323,7 +387,8 @@ struct IndexIVFFlat : IndexIVF {
     void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
                                    const int32_t* assign, const float* centroid_dis,
                                    float* distances, idx_t* labels, hipStream_t stream,
-                                   const uint32_t* lim = nullptr) const override;
+                                   const uint32_t* lim = nullptr,
+                                   const uint8_t* sel = nullptr) const override;
     void reconstruct(idx_t key, float* recons) const override;
 
    protected:
@@ -353,7 +418,8 @@ struct IndexIVFPQ : IndexIVF {
     void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
                                    const int32_t* assign, const float* centroid_dis,
                                    float* distances, idx_t* labels, hipStream_t stream,
-                                   const uint32_t* lim = nullptr) const override;
+                                   const uint32_t* lim = nullptr,
+                                   const uint8_t* sel = nullptr) const override;
     // faiss/IndexIVFPQ.cpp:364-459: choose 0/1 like the reference (the GPU
     // path uses per-code terms either way)
     void precompute_table();

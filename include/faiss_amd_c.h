@@ -109,10 +109,40 @@ int faiss_Index_reset(FaissIndex* index);
 int faiss_SearchParametersIVF_new(FaissSearchParametersIVF** p_sp);
 int faiss_SearchParametersIVF_new_with(
         FaissSearchParametersIVF** p_sp,
-        void* sel, /* FaissIDSelector*: must be NULL (selectors not supported) */
+        void* sel, /* FaissIDSelector* or NULL (borrowed) */
         size_t nprobe,
         size_t max_codes);
 void faiss_SearchParametersIVF_free(FaissSearchParametersIVF* obj);
+
+/* ---------------- IDSelector (c_api/impl/AuxIndexStructures_c.h:50-110,
+ * c_api/Index_c.h:44-46).  Membership as faiss/impl/IDSelector.cpp; the IVF
+ * searches evaluate it on the GPU for every arena row and skip non-members
+ * (faiss/IndexIVFFlat.cpp:165-167).  Selectors passed to another selector or
+ * to search parameters are borrowed, not owned. */
+typedef struct FaissIDSelector_H FaissIDSelector;
+typedef struct FaissIDSelector_H FaissIDSelectorRange;
+typedef struct FaissIDSelector_H FaissIDSelectorBatch;
+typedef struct FaissIDSelector_H FaissIDSelectorBitmap;
+typedef struct FaissIDSelector_H FaissIDSelectorNot;
+typedef struct FaissIDSelector_H FaissIDSelectorAnd;
+typedef struct FaissIDSelector_H FaissIDSelectorOr;
+typedef struct FaissIDSelector_H FaissIDSelectorXOr;
+int faiss_SearchParameters_new(FaissSearchParameters** p_sp, FaissIDSelector* sel);
+void faiss_SearchParameters_free(FaissSearchParameters* obj);
+int faiss_IDSelector_is_member(const FaissIDSelector* sel, idx_t id);
+void faiss_IDSelector_free(FaissIDSelector* sel);
+int faiss_IDSelectorRange_new(FaissIDSelectorRange** p_sel, idx_t imin, idx_t imax);
+int faiss_IDSelectorBatch_new(FaissIDSelectorBatch** p_sel, size_t n, const idx_t* indices);
+/* extension: faiss::IDSelectorArray (faiss/impl/IDSelector.h:54-66), ids borrowed */
+int faiss_amd_IDSelectorArray_new(FaissIDSelector** p_sel, size_t n, const idx_t* ids);
+int faiss_IDSelectorBitmap_new(FaissIDSelectorBitmap** p_sel, size_t n, const uint8_t* bitmap);
+int faiss_IDSelectorNot_new(FaissIDSelectorNot** p_sel, const FaissIDSelector* sel);
+int faiss_IDSelectorAnd_new(FaissIDSelectorAnd** p_sel, const FaissIDSelector* lhs_sel,
+                            const FaissIDSelector* rhs_sel);
+int faiss_IDSelectorOr_new(FaissIDSelectorOr** p_sel, const FaissIDSelector* lhs_sel,
+                           const FaissIDSelector* rhs_sel);
+int faiss_IDSelectorXOr_new(FaissIDSelectorXOr** p_sel, const FaissIDSelector* lhs_sel,
+                            const FaissIDSelector* rhs_sel);
 size_t faiss_SearchParametersIVF_nprobe(const FaissSearchParametersIVF*);
 void faiss_SearchParametersIVF_set_nprobe(FaissSearchParametersIVF*, size_t);
 /* c_api/IndexIVF_c.h:35 (FAISS_DECLARE_GETTER_SETTER max_codes); 0 = unlimited */
