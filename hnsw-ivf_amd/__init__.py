@@ -23,7 +23,9 @@ LIB_PATH = os.path.join(_HERE, "lib", "libfaiss_amd.so")
 
 METRIC_INNER_PRODUCT = 0
 METRIC_L2 = 1
-IO_FLAG_MMAP = 8 | 0x646F0000  # reference faiss/index_io.h (accepted, lists are loaded to HBM)
+IO_FLAG_ONDISK_SAME_DIR = 4  # reference faiss/index_io.h:51
+IO_FLAG_SKIP_IVF_DATA = 8  # :53
+IO_FLAG_MMAP = 8 | 0x646F0000  # :64 — lists mapped from the file, streamed to HBM
 
 _lib = None
 
@@ -170,6 +172,7 @@ def _declare(L):
         "faiss_amd_IndexShardsIVF_count": (C.c_int, [_P]),
         "faiss_write_index": (C.c_int, [_P, _P]),
         "faiss_write_index_fname": (C.c_int, [_P, C.c_char_p]),
+        "faiss_amd_write_index_ondisk": (C.c_int, [_P, C.c_char_p, C.c_char_p]),
         "faiss_read_index": (C.c_int, [_P, C.c_int, C.POINTER(_P)]),
         "faiss_read_index_fname": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_P)]),
         "faiss_index_factory": (C.c_int, [C.POINTER(_P), C.c_int, C.c_char_p, C.c_int]),
@@ -740,6 +743,13 @@ def read_index(fname, io_flags=0):
 
 def write_index(index, fname):
     _check(lib().faiss_write_index_fname(index.h, str(fname).encode()))
+
+
+def write_index_ondisk(index, fname, lists_fname):
+    """IVF index file whose lists live in `lists_fname` (OnDiskInvertedLists
+    layout, faiss/invlists/OnDiskInvertedLists.cpp:683-704)."""
+    _check(lib().faiss_amd_write_index_ondisk(index.h, str(fname).encode(),
+                                               str(lists_fname).encode()))
 
 
 def merge_knn_results(Dall, Iall, keep_max=False):

@@ -297,15 +297,15 @@ size_t faiss_IndexIVF_get_list_size(const FaissIndexIVF* index, size_t list_no) 
 void faiss_IndexIVF_invlists_get_ids(const FaissIndexIVF* index, size_t list_no, idx_t* out) {
     auto v = IVFc(index);
     if (!v || list_no >= v->nlist) return;
-    const auto& ids = v->invlists->ids[list_no];
-    memcpy(out, ids.data(), sizeof(idx_t) * ids.size());
+    const size_t n = v->invlists->list_size(list_no);
+    if (n) memcpy(out, v->invlists->get_ids(list_no), sizeof(idx_t) * n);
 }
 void faiss_amd_IndexIVF_invlists_get_codes(const FaissIndexIVF* index, size_t list_no,
                                            uint8_t* codes) {
     auto v = IVFc(index);
     if (!v || list_no >= v->nlist) return;
-    const auto& c = v->invlists->codes[list_no];
-    memcpy(codes, c.data(), c.size());
+    const size_t n = v->invlists->list_size(list_no) * v->invlists->code_size;
+    if (n) memcpy(codes, v->invlists->get_codes(list_no), n);
 }
 size_t faiss_amd_IndexIVF_code_size(const FaissIndexIVF* index) {
     auto v = IVFc(index);
@@ -497,6 +497,11 @@ int faiss_write_index(const FaissIndex* idx, FILE* f) {
 }
 int faiss_write_index_fname(const FaissIndex* idx, const char* fname) {
     C_TRY write_index(IX(idx), fname);
+    C_CATCH
+}
+int faiss_amd_write_index_ondisk(const FaissIndex* idx, const char* fname,
+                                 const char* lists_fname) {
+    C_TRY write_index_ondisk(IX(idx), fname, lists_fname);
     C_CATCH
 }
 int faiss_read_index(FILE* f, int io_flags, FaissIndex** p_out) {

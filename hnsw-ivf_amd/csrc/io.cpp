@@ -19,12 +19,31 @@
 //             efSearch:int, dummy int), storage index         (:300-316,760-778)
 //   vectors carry a size_t element-count prefix (faiss/impl/io_macros.h:62-67)
 //   fourcc = little-endian chars (faiss/impl/io.cpp:237-241)
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
 #include <cstring>
 #include <string>
 
 #include "../../include/faiss_amd.h"
 
 namespace faiss_amd {
+
+MappedFile::MappedFile(int fd, const std::string& nm) : name(nm) {
+    struct stat st;
+    FAISS_THROW_IF_NOT_MSG(fstat(fd, &st) == 0, std::string("fstat failed: ") + strerror(errno));
+    size = (size_t)st.st_size;
+    if (size == 0) return;
+    void* p = mmap(nullptr, size, PROT_READ, MAP_SHARED, fd, 0);
+    FAISS_THROW_IF_NOT_MSG(p != MAP_FAILED, std::string("could not mmap: ") + strerror(errno));
+    ptr = (const uint8_t*)p;
+}
+MappedFile::~MappedFile() {
+    if (ptr) munmap((void*)ptr, size);
+}
 
 namespace {
 uint32_t fourcc(const char* s) {
@@ -42,6 +61,7 @@ std::string fourcc_str(uint32_t h) {
 
 struct Writer {
     FILE* f;
+    const char* ondisk_fname = nullptr;  // write_index_ondisk: lists go to this file
     void bytes(const void* p, size_t n) {
         if (n && fwrite(p, 1, n, f) != n) FAISS_THROW_MSG("write error");
     }
@@ -56,6 +76,7 @@ struct Writer {
 };
 struct Reader {
     FILE* f;
+    std::string name;  // file name when reading from a named file (IO_FLAG_ONDISK_SAME_DIR)
     void bytes(void* p, size_t n) {
         if (n && fread(p, 1, n, f) != n) FAISS_THROW_MSG("read error: truncated index file");
     }
@@ -112,41 +133,97 @@ void apply_header(Index* idx, const Header& h) {
     idx->metric_arg = h.metric_arg;
 }
 
+// `ilod` metadata (faiss/invlists/OnDiskInvertedLists.cpp:683-704): lists as
+// (size, capacity, offset) triples, an empty free-slot table, the data file
+// name and its size.
+void write_ilod(const ArrayInvertedLists* il, Writer& w, const std::string& fname,
+                const std::vector<size_t>& lists, size_t totsize) {
+    w.one(fourcc("ilod"));
+    w.one<size_t>(il->nlist);
+    w.one<size_t>(il->code_size);
+    w.one<size_t>(il->nlist);
+    w.bytes(lists.data(), sizeof(size_t) * lists.size());
+    w.one<size_t>(0);
+    std::vector<char> fn(fname.begin(), fname.end());
+    w.vec(fn);
+    w.one<size_t>(totsize);
+}
+
 void write_invlists(const ArrayInvertedLists* il, Writer& w) {
+    if (w.ondisk_fname) {
+        // data file: per non-empty list codes[size*code_size] then ids[size]
+        FILE* df = fopen(w.ondisk_fname, "wb");
+        FAISS_THROW_IF_NOT_MSG(df, std::string("could not open ") + w.ondisk_fname);
+        Writer dw{df};
+        std::vector<size_t> lists(3 * il->nlist, 0);
+        size_t o = 0;
+        try {
+            for (size_t l = 0; l < il->nlist; l++) {
+                const size_t n = il->list_size(l);
+                lists[3 * l] = lists[3 * l + 1] = n;
+                lists[3 * l + 2] = o;
+                if (!n) continue;
+                dw.bytes(il->get_codes(l), n * il->code_size);
+                dw.bytes(il->get_ids(l), n * sizeof(idx_t));
+                o += n * (il->code_size + sizeof(idx_t));
+            }
+        } catch (...) {
+            fclose(df);
+            throw;
+        }
+        fclose(df);
+        write_ilod(il, w, w.ondisk_fname, lists, o);
+        return;
+    }
+    if (il->map && il->map_ondisk) {
+        // lists still live in an `ilod` data file: write its metadata again
+        std::vector<size_t> lists(3 * il->nlist, 0);
+        for (size_t l = 0; l < il->nlist; l++) {
+            const size_t n = il->map_sizes[l];
+            if (!n) continue;
+            const size_t o = (size_t)(il->map_codes[l] - il->map->ptr);
+            const size_t cap = il->code_size
+                                   ? (size_t)((const uint8_t*)il->map_ids[l] - il->map_codes[l]) /
+                                         il->code_size
+                                   : n;
+            lists[3 * l] = n;
+            lists[3 * l + 1] = cap;
+            lists[3 * l + 2] = o;
+        }
+        write_ilod(il, w, il->map->name, lists, il->map->size);
+        return;
+    }
     w.one(fourcc("ilar"));
     w.one<size_t>(il->nlist);
     w.one<size_t>(il->code_size);
     size_t n_non0 = 0;
     for (size_t i = 0; i < il->nlist; i++)
-        if (!il->ids[i].empty()) n_non0++;
+        if (il->list_size(i)) n_non0++;
     std::vector<size_t> sizes;
     if (n_non0 > il->nlist / 2) {
         w.one(fourcc("full"));
-        for (size_t i = 0; i < il->nlist; i++) sizes.push_back(il->ids[i].size());
+        for (size_t i = 0; i < il->nlist; i++) sizes.push_back(il->list_size(i));
     } else {
         w.one(fourcc("sprs"));
         for (size_t i = 0; i < il->nlist; i++) {
-            if (!il->ids[i].empty()) {
+            if (il->list_size(i)) {
                 sizes.push_back(i);
-                sizes.push_back(il->ids[i].size());
+                sizes.push_back(il->list_size(i));
             }
         }
     }
     w.vec(sizes);
     for (size_t i = 0; i < il->nlist; i++) {
-        size_t n = il->ids[i].size();
+        size_t n = il->list_size(i);
         if (n) {
-            w.bytes(il->codes[i].data(), n * il->code_size);
-            w.bytes(il->ids[i].data(), n * sizeof(idx_t));
+            w.bytes(il->get_codes(i), n * il->code_size);
+            w.bytes(il->get_ids(i), n * sizeof(idx_t));
         }
     }
 }
-void read_invlists(ArrayInvertedLists* il, Reader& r, size_t nlist, size_t code_size) {
-    uint32_t h = r.one<uint32_t>();
-    FAISS_THROW_IF_NOT_MSG(h == fourcc("ilar"),
-                           "unsupported inverted-list type " + fourcc_str(h));
-    size_t nl = r.one<size_t>(), cs = r.one<size_t>();
-    FAISS_THROW_IF_NOT(nl == nlist && cs == code_size);
+
+// The `ilar` list sizes block (faiss/impl/index_read.cpp:243-297).
+std::vector<size_t> read_ilar_sizes(Reader& r, size_t nl) {
     std::vector<size_t> sizes(nl, 0);
     uint32_t lt = r.one<uint32_t>();
     if (lt == fourcc("full")) {
@@ -161,6 +238,111 @@ void read_invlists(ArrayInvertedLists* il, Reader& r, size_t nlist, size_t code_
         }
     } else {
         FAISS_THROW_MSG("list_type not recognized: " + fourcc_str(lt));
+    }
+    return sizes;
+}
+
+std::string dir_of(const std::string& path) {
+    size_t slash = path.find_last_of('/');
+    return slash == std::string::npos ? std::string("./") : path.substr(0, slash + 1);
+}
+
+void read_invlists(ArrayInvertedLists* il, Reader& r, size_t nlist, size_t code_size,
+                   int io_flags) {
+    uint32_t h = r.one<uint32_t>();
+    if (h == fourcc("ilod")) {
+        // OnDiskInvertedLists (faiss/invlists/OnDiskInvertedLists.cpp:706-757):
+        // nlist, code_size, vector<List{size,capacity,offset}>, vector<Slot>,
+        // vector<char> filename, totsize.  List l = codes[capacity*code_size]
+        // then ids[capacity] at `offset` in the data file.
+        size_t nl = r.one<size_t>(), cs = r.one<size_t>();
+        FAISS_THROW_IF_NOT(nl == nlist && cs == code_size);
+        std::vector<size_t> lists;  // 3 size_t per list (POD OnDiskOneList)
+        {
+            size_t n = r.one<size_t>();
+            FAISS_THROW_IF_NOT_MSG(n == nl, "ilod: list table size != nlist");
+            lists.resize(3 * n);
+            r.bytes(lists.data(), sizeof(size_t) * 3 * n);
+        }
+        std::vector<size_t> slots;  // 2 size_t per slot (free space, unused here)
+        {
+            size_t n = r.one<size_t>();
+            FAISS_THROW_IF_NOT(n < ((size_t)1 << 40));
+            slots.resize(2 * n);
+            r.bytes(slots.data(), sizeof(size_t) * 2 * n);
+        }
+        std::vector<char> fn;
+        r.vec(fn);
+        std::string filename(fn.begin(), fn.end());
+        size_t totsize = r.one<size_t>();
+        if (io_flags & IO_FLAG_ONDISK_SAME_DIR) {
+            FAISS_THROW_IF_NOT_MSG(!r.name.empty(),
+                                   "IO_FLAG_ONDISK_SAME_DIR only supported when reading from file");
+            size_t slash = filename.find_last_of('/');
+            filename = dir_of(r.name) + (slash == std::string::npos ? filename
+                                                                    : filename.substr(slash + 1));
+        }
+        il->reset();
+        // The reference skips do_mmap() under IO_FLAG_SKIP_IVF_DATA (:752) and
+        // a later search would dereference a null mapping; here the data file
+        // is mapped in every case.
+        int fd = open(filename.c_str(), O_RDONLY);
+        FAISS_THROW_IF_NOT_MSG(fd >= 0, "could not open on-disk inverted lists " + filename);
+        auto m = std::make_shared<MappedFile>(fd, filename);
+        close(fd);
+        FAISS_THROW_IF_NOT_MSG(m->size >= totsize || totsize == 0,
+                               "on-disk inverted lists file shorter than totsize");
+        il->map_codes.assign(nl, nullptr);
+        il->map_ids.assign(nl, nullptr);
+        il->map_sizes.assign(nl, 0);
+        for (size_t l = 0; l < nl; l++) {
+            const size_t size = lists[3 * l], cap = lists[3 * l + 1], o = lists[3 * l + 2];
+            FAISS_THROW_IF_NOT_MSG(size <= cap, "ilod: list size > capacity");
+            if (!size) continue;
+            FAISS_THROW_IF_NOT_MSG(o + cap * (cs + sizeof(idx_t)) <= m->size,
+                                   "ilod: list extends past the end of the data file");
+            il->map_sizes[l] = size;
+            il->map_codes[l] = m->ptr + o;
+            il->map_ids[l] = (const idx_t*)(m->ptr + o + cap * cs);
+        }
+        il->map = m;
+        il->map_ondisk = true;
+        return;
+    }
+    FAISS_THROW_IF_NOT_MSG(h == fourcc("ilar"),
+                           "unsupported inverted-list type " + fourcc_str(h));
+    size_t nl = r.one<size_t>(), cs = r.one<size_t>();
+    FAISS_THROW_IF_NOT(nl == nlist && cs == code_size);
+    std::vector<size_t> sizes = read_ilar_sizes(r, nl);
+    if (io_flags & IO_FLAG_SKIP_IVF_DATA) {
+        // faiss/impl/index_read.cpp:214-225: the hook is chosen by the flag's
+        // high 16 bits; only the mmap hook ("ilod", IO_FLAG_MMAP) exists.
+        const uint32_t h2 = ((uint32_t)io_flags & 0xffff0000u) | (fourcc("il__") & 0xffffu);
+        FAISS_THROW_IF_NOT_MSG(h2 == fourcc("ilod"),
+                               "read_InvertedLists: could not load ArrayInvertedLists as " +
+                                   fourcc_str(h2));
+        // OnDiskInvertedListsIOHook::read_ArrayInvertedLists
+        // (faiss/invlists/OnDiskInvertedLists.cpp:759-800): map the whole
+        // index file, lists point at their codes/ids, reading resumes after.
+        FAISS_THROW_IF_NOT_MSG(r.f, "mmap only supported for File objects");
+        long o0 = ftell(r.f);
+        FAISS_THROW_IF_NOT_MSG(o0 >= 0, "ftell failed");
+        auto m = std::make_shared<MappedFile>(fileno(r.f), r.name);
+        size_t o = (size_t)o0;
+        il->reset();
+        il->map_codes.assign(nl, nullptr);
+        il->map_ids.assign(nl, nullptr);
+        il->map_sizes = sizes;
+        for (size_t i = 0; i < nl; i++) {
+            const size_t bytes = sizes[i] * (cs + sizeof(idx_t));
+            FAISS_THROW_IF_NOT_MSG(o + bytes <= m->size, "read error: truncated index file");
+            il->map_codes[i] = m->ptr + o;
+            il->map_ids[i] = (const idx_t*)(m->ptr + o + sizes[i] * cs);
+            o += bytes;
+        }
+        il->map = m;
+        FAISS_THROW_IF_NOT(fseek(r.f, (long)o, SEEK_SET) == 0);
+        return;
     }
     for (size_t i = 0; i < nl; i++) {
         il->ids[i].resize(sizes[i]);
@@ -294,7 +476,7 @@ Index* read_index_impl(Reader& r, int io_flags) {
         ivf->own_fields = true;
         apply_header(ivf, hd);
         ivf->nprobe = nprobe;
-        read_invlists(ivf->invlists.get(), r, nlist, ivf->code_size);
+        read_invlists(ivf->invlists.get(), r, nlist, ivf->code_size, io_flags);
         if (auto pqi = dynamic_cast<IndexIVFPQ*>(ivf)) {
             // faiss/impl/index_read.cpp:510-516
             if (pqi->is_trained && pqi->by_residual) pqi->precompute_table();
@@ -309,6 +491,20 @@ void write_index(const Index* idx, FILE* f) {
     Writer w{f};
     write_index_impl(idx, w);
 }
+void write_index_ondisk(const Index* idx, const char* fname, const char* lists_fname) {
+    FAISS_THROW_IF_NOT_MSG(dynamic_cast<const IndexIVF*>(idx),
+                           "write_index_ondisk: only IVF indexes have inverted lists");
+    FILE* f = fopen(fname, "wb");
+    FAISS_THROW_IF_NOT_MSG(f, std::string("could not open ") + fname + " for writing");
+    try {
+        Writer w{f, lists_fname};
+        write_index_impl(idx, w);
+    } catch (...) {
+        fclose(f);
+        throw;
+    }
+    fclose(f);
+}
 void write_index(const Index* idx, const char* fname) {
     FILE* f = fopen(fname, "wb");
     FAISS_THROW_IF_NOT_MSG(f, std::string("could not open ") + fname + " for writing");
@@ -321,7 +517,7 @@ void write_index(const Index* idx, const char* fname) {
     fclose(f);
 }
 Index* read_index(FILE* f, int io_flags) {
-    Reader r{f};
+    Reader r{f, ""};
     return read_index_impl(r, io_flags);
 }
 Index* read_index(const char* fname, int io_flags) {
@@ -329,7 +525,8 @@ Index* read_index(const char* fname, int io_flags) {
     FAISS_THROW_IF_NOT_MSG(f, std::string("could not open ") + fname + " for reading");
     Index* idx = nullptr;
     try {
-        idx = read_index(f, io_flags);
+        Reader r{f, fname};
+        idx = read_index_impl(r, io_flags);
     } catch (...) {
         fclose(f);
         throw;

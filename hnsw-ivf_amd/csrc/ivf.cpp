@@ -35,13 +35,32 @@ ArrayInvertedLists::ArrayInvertedLists(size_t nl, size_t cs) : nlist(nl), code_s
     codes.resize(nl);
     ids.resize(nl);
 }
+void ArrayInvertedLists::materialize() {
+    if (!map) return;
+    for (size_t l = 0; l < nlist; l++) {
+        const size_t n = map_sizes[l];
+        codes[l].assign(map_codes[l], map_codes[l] + n * code_size);
+        ids[l].assign(map_ids[l], map_ids[l] + n);
+    }
+    map.reset();
+    map_ondisk = false;
+    map_codes.clear();
+    map_ids.clear();
+    map_sizes.clear();
+}
 void ArrayInvertedLists::add_entries(size_t l, size_t n, const idx_t* ids_in,
                                      const uint8_t* codes_in) {
     FAISS_THROW_IF_NOT(l < nlist);
+    materialize();
     ids[l].insert(ids[l].end(), ids_in, ids_in + n);
     codes[l].insert(codes[l].end(), codes_in, codes_in + n * code_size);
 }
 void ArrayInvertedLists::reset() {
+    map.reset();
+    map_ondisk = false;
+    map_codes.clear();
+    map_ids.clear();
+    map_sizes.clear();
     for (size_t l = 0; l < nlist; l++) {
         codes[l].clear();
         ids[l].clear();
@@ -146,25 +165,76 @@ void IndexIVF::sync_device() const {
     }
     off[nlist] = (uint32_t)rows;
     arena_rows_ = rows;
-    std::vector<uint8_t> hc(std::max<size_t>(rows, 1) * dstride, 0);
+    const size_t code_bytes = std::max<size_t>(rows, 1) * dstride;
     std::vector<idx_t> hi(std::max<size_t>(rows, 1), -1);
     std::vector<uint32_t> hl(std::max<size_t>(rows, 1), 0xffffffffu);
     for (size_t l = 0; l < nlist; l++) {
         const size_t n = len[l];
-        for (size_t i = 0; i < n; i++) {
-            memcpy(hc.data() + (off[l] + i) * dstride, invlists->codes[l].data() + i * code_size,
-                   code_size);
-            hl[off[l] + i] = (uint32_t)l;
-        }
-        if (n) memcpy(hi.data() + off[l], invlists->ids[l].data(), sizeof(idx_t) * n);
+        for (size_t i = 0; i < n; i++) hl[off[l] + i] = (uint32_t)l;
+        if (n) memcpy(hi.data() + off[l], invlists->get_ids(l), sizeof(idx_t) * n);
     }
     // + tail padding: the re-rank reads BDM floats from any row start
-    d_codes_.reserve(hc.size() + sizeof(float) * kern::BDM_HOST);
+    d_codes_.reserve(code_bytes + sizeof(float) * kern::BDM_HOST);
     d_ids_.reserve(sizeof(idx_t) * hi.size());
     d_row_list_.reserve(sizeof(uint32_t) * hl.size());
     d_list_off_.reserve(sizeof(uint32_t) * (nlist + 1));
     d_list_len_.reserve(sizeof(uint32_t) * std::max<size_t>(nlist, 1));
-    HIP_CHECK(hipMemcpyAsync(d_codes_.ptr, hc.data(), hc.size(), hipMemcpyHostToDevice, s));
+    // Codes: packed arena order into two pinned staging buffers, each copied
+    // to HBM while the other fills (no whole-arena host image; mapped lists
+    // are read from the page cache exactly once).
+    {
+        const size_t cap = std::max<size_t>(dstride, std::min<size_t>(code_bytes, 64u << 20) /
+                                                         dstride * dstride);
+        uint8_t* buf[2] = {nullptr, nullptr};
+        hipEvent_t ev[2];
+        for (int b = 0; b < 2; b++) {
+            HIP_CHECK(hipHostMalloc((void**)&buf[b], cap, hipHostMallocDefault));
+            HIP_CHECK(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming));
+        }
+        int cur = 0;
+        size_t fill = 0, dev_pos = 0, pending[2] = {0, 0};
+        auto flush = [&]() {
+            if (!fill) return;
+            HIP_CHECK(hipMemcpyAsync((uint8_t*)d_codes_.ptr + dev_pos, buf[cur], fill,
+                                     hipMemcpyHostToDevice, s));
+            HIP_CHECK(hipEventRecord(ev[cur], s));
+            pending[cur] = 1;
+            dev_pos += fill;
+            fill = 0;
+            cur ^= 1;
+            if (pending[cur]) HIP_CHECK(hipEventSynchronize(ev[cur]));
+            pending[cur] = 0;
+        };
+        auto put_rows = [&](const uint8_t* src, size_t nrows) {  // src == nullptr: zero rows
+            while (nrows) {
+                const size_t take = std::min(nrows, (cap - fill) / dstride);
+                uint8_t* dst = buf[cur] + fill;
+                if (src && dstride == code_size) {
+                    memcpy(dst, src, take * code_size);
+                } else {
+                    memset(dst, 0, take * dstride);
+                    if (src)
+                        for (size_t i = 0; i < take; i++)
+                            memcpy(dst + i * dstride, src + i * code_size, code_size);
+                }
+                if (src) src += take * code_size;
+                fill += take * dstride;
+                nrows -= take;
+                if (fill + dstride > cap) flush();
+            }
+        };
+        for (size_t l = 0; l < nlist; l++) {
+            put_rows(invlists->get_codes(l), len[l]);
+            put_rows(nullptr, roundup(len[l], 16) - len[l]);
+        }
+        if (rows == 0) put_rows(nullptr, 1);
+        flush();
+        HIP_CHECK(hipStreamSynchronize(s));
+        for (int b = 0; b < 2; b++) {
+            HIP_CHECK(hipEventDestroy(ev[b]));
+            HIP_CHECK(hipHostFree(buf[b]));
+        }
+    }
     HIP_CHECK(hipMemcpyAsync(d_ids_.ptr, hi.data(), sizeof(idx_t) * hi.size(),
                              hipMemcpyHostToDevice, s));
     HIP_CHECK(hipMemcpyAsync(d_row_list_.ptr, hl.data(), sizeof(uint32_t) * hl.size(),
@@ -471,10 +541,10 @@ void IndexIVFFlat::encode_vectors(idx_t n, const float* x, const idx_t*, uint8_t
 
 void IndexIVFFlat::reconstruct(idx_t key, float* recons) const {
     for (size_t l = 0; l < nlist; l++) {
-        const auto& ids = invlists->ids[l];
-        for (size_t i = 0; i < ids.size(); i++)
+        const idx_t* ids = invlists->get_ids(l);
+        for (size_t i = 0; i < invlists->list_size(l); i++)
             if (ids[i] == key) {
-                memcpy(recons, invlists->codes[l].data() + i * code_size, code_size);
+                memcpy(recons, invlists->get_codes(l) + i * code_size, code_size);
                 return;
             }
     }

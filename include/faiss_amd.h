@@ -277,12 +277,40 @@ struct IndexHNSWFlat : IndexHNSW {
 // ---------------------------------------------------------------- IVF
 // faiss/invlists/InvertedLists.h:243-275 (ArrayInvertedLists) on the host,
 // one contiguous arena in HBM.
+// A read-only file mapping (mmap, PROT_READ, MAP_SHARED) that inverted lists
+// can point into: `read_index(..., IO_FLAG_MMAP)` on an `ilar` file
+// (faiss/invlists/OnDiskInvertedLists.cpp:759-800) and the `ilod` on-disk
+// list file (:706-757).  Unmapped when the last list set using it goes.
+struct MappedFile {
+    const uint8_t* ptr = nullptr;
+    size_t size = 0;
+    std::string name;
+    explicit MappedFile(int fd, const std::string& name);
+    ~MappedFile();
+};
+
+// faiss/invlists/InvertedLists.h:37-275 (ArrayInvertedLists) with the
+// OnDiskInvertedLists read-only case folded in: a list lives either in host
+// vectors (codes[l], ids[l]) or, when `map` is set, in the mapped file
+// (map_codes[l], map_ids[l], map_sizes[l]).  Mapped lists are streamed
+// straight from the mapping through pinned staging buffers into HBM
+// (IndexIVF::sync_device); an add on a mapped set first copies it into host
+// memory (the reference's mmapped lists are read-only and throw instead).
 struct ArrayInvertedLists {
     size_t nlist = 0, code_size = 0;
     std::vector<std::vector<uint8_t>> codes;
     std::vector<std::vector<idx_t>> ids;
+    std::shared_ptr<MappedFile> map;
+    std::vector<const uint8_t*> map_codes;
+    std::vector<const idx_t*> map_ids;
+    std::vector<size_t> map_sizes;
+    bool map_ondisk = false;  // mapping is an `ilod` data file (written back as `ilod`)
     ArrayInvertedLists(size_t nlist, size_t code_size);
-    size_t list_size(size_t l) const { return ids[l].size(); }
+    bool is_mapped() const { return (bool)map; }
+    size_t list_size(size_t l) const { return map ? map_sizes[l] : ids[l].size(); }
+    const uint8_t* get_codes(size_t l) const { return map ? map_codes[l] : codes[l].data(); }
+    const idx_t* get_ids(size_t l) const { return map ? map_ids[l] : ids[l].data(); }
+    void materialize();  // copy mapped lists into host vectors and drop the mapping
     void add_entries(size_t l, size_t n, const idx_t* ids, const uint8_t* codes);
     void reset();
 };
@@ -471,9 +499,22 @@ void merge_knn_results(size_t n, size_t k, int nshard, const float* all_distance
                        MetricType metric);
 
 // faiss/index_io.h
+// faiss/index_io.h:37-64
+constexpr int IO_FLAG_SKIP_STORAGE = 1;
+constexpr int IO_FLAG_READ_ONLY = 2;
+constexpr int IO_FLAG_ONDISK_SAME_DIR = 4;
+constexpr int IO_FLAG_SKIP_IVF_DATA = 8;
+constexpr int IO_FLAG_SKIP_PRECOMPUTE_TABLE = 16;
+constexpr int IO_FLAG_PQ_SKIP_SDC_TABLE = 32;
+constexpr int IO_FLAG_MMAP = IO_FLAG_SKIP_IVF_DATA | 0x646f0000;
 void write_index(const Index* idx, const char* fname);
 void write_index(const Index* idx, FILE* f);
 Index* read_index(const char* fname, int io_flags = 0);
+// IVF index whose inverted lists go to a separate `ilod` data file
+// (OnDiskInvertedLists layout, faiss/invlists/OnDiskInvertedLists.cpp:683-704),
+// as the reference produces with OnDiskInvertedLists + replace_invlists +
+// write_index.
+void write_index_ondisk(const Index* idx, const char* fname, const char* lists_fname);
 Index* read_index(FILE* f, int io_flags = 0);
 
 // faiss/index_factory.h (subset: Flat, IVFn[_HNSWm],Flat|PQm[xb][np], HNSWm)

@@ -364,6 +364,15 @@ int faiss_write_index(const FaissIndex* idx, FILE* f);                   /* :28 
 int faiss_write_index_fname(const FaissIndex* idx, const char* fname);   /* :33 */
 int faiss_read_index(FILE* f, int io_flags, FaissIndex** p_out);         /* :41 */
 int faiss_read_index_fname(const char* fname, int io_flags, FaissIndex** p_out); /* :46 */
+/* faiss/index_io.h:37-64 flags: IO_FLAG_MMAP (8 | 0x646f0000) maps the index
+ * file's `ilar` lists (faiss/invlists/OnDiskInvertedLists.cpp:759-800);
+ * `ilod` lists are always mapped from their data file (:706-757),
+ * IO_FLAG_ONDISK_SAME_DIR (4) looks for it next to the index file. */
+/* IVF index with its lists in a separate OnDiskInvertedLists data file: the
+ * reference's OnDiskInvertedLists + replace_invlists + write_index
+ * (faiss/invlists/OnDiskInvertedLists.cpp:683-704). */
+int faiss_amd_write_index_ondisk(const FaissIndex* idx, const char* fname,
+                                 const char* lists_fname);
 
 /* ---------------- factory / tuning ---------------- */
 /* c_api/index_factory_c.h:24-28; supports "Flat", "IVF<n>,Flat",
