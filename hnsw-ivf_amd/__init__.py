@@ -106,6 +106,17 @@ def _declare(L):
         "faiss_Index_add_with_ids": (C.c_int, [_P, _I64, _P, _P]),
         "faiss_Index_search": (C.c_int, [_P, _I64, _P, _I64, _P, _P]),
         "faiss_Index_search_with_params": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P]),
+        "faiss_RangeSearchResult_new": (C.c_int, [C.POINTER(_P), _I64]),
+        "faiss_RangeSearchResult_free": (None, [_P]),
+        "faiss_RangeSearchResult_nq": (C.c_size_t, [_P]),
+        "faiss_RangeSearchResult_buffer_size": (C.c_size_t, [_P]),
+        "faiss_RangeSearchResult_lims": (None, [_P, C.POINTER(C.POINTER(C.c_size_t))]),
+        "faiss_RangeSearchResult_labels": (None, [_P, C.POINTER(C.POINTER(C.c_int64)),
+                                                  C.POINTER(C.POINTER(C.c_float))]),
+        "faiss_Index_range_search": (C.c_int, [_P, _I64, _P, C.c_float, _P]),
+        "faiss_amd_Index_range_search_with_params": (C.c_int, [_P, _I64, _P, C.c_float, _P, _P]),
+        "faiss_IndexIVF_range_search_preassigned": (C.c_int, [_P, _I64, _P, C.c_float, _P, _P,
+                                                              _P]),
         "faiss_Index_reset": (C.c_int, [_P]),
         "faiss_SearchParametersIVF_new": (C.c_int, [C.POINTER(_P)]),
         "faiss_SearchParametersIVF_new_with": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t]),
@@ -298,6 +309,16 @@ class Index:
                                                         _ptr(D), _ptr(I)))
         return D, I
 
+    def range_search(self, x, radius, params=None):
+        """faiss Index.range_search: (lims [n+1], D, I) in the reference's scan order."""
+        x = _f32(x)
+        n = x.shape[0]
+        return _range_call(n, lambda r: (
+            lib().faiss_Index_range_search(self.h, n, _ptr(x), float(radius), r)
+            if params is None else
+            lib().faiss_amd_Index_range_search_with_params(self.h, n, _ptr(x), float(radius),
+                                                           params.h, r)))
+
     def reset(self):
         _check(lib().faiss_Index_reset(self.h))
 
@@ -487,6 +508,17 @@ class IndexIVF(Index):
                                                        _ptr(centroid_dis), _ptr(D), _ptr(I),
                                                        int(store_pairs)))
         return D, I
+
+    def range_search_preassigned(self, x, radius, assign, centroid_dis=None):
+        x = _f32(x)
+        n = x.shape[0]
+        assign = np.ascontiguousarray(assign, dtype=np.int64)
+        if assign.shape != (n, min(self.nprobe, self.nlist)):
+            raise ValueError("assign must be [n, nprobe] (the index's nprobe)")
+        cd = (np.zeros(assign.shape, np.float32) if centroid_dis is None
+              else np.ascontiguousarray(centroid_dis, dtype=np.float32))
+        return _range_call(n, lambda r: lib().faiss_IndexIVF_range_search_preassigned(
+            self.h, n, _ptr(x), float(radius), _ptr(assign), _ptr(cd), r))
 
     def search_stats(self, x, k, params=None):
         """IndexIVF::search_stats: (D, I, per-query QueryLatencyStats records)."""
@@ -716,6 +748,28 @@ class ParameterSpace:
 
 
 # ---------------------------------------------------------------- helpers
+def _range_call(n, fn):
+    """Run a range-search C call on a fresh RangeSearchResult and copy it out."""
+    r = C.c_void_p()
+    _check(lib().faiss_RangeSearchResult_new(C.byref(r), n))
+    try:
+        _check(fn(r))
+        lp = C.POINTER(C.c_size_t)()
+        lib().faiss_RangeSearchResult_lims(r, C.byref(lp))
+        lims = np.ctypeslib.as_array(lp, shape=(n + 1,)).copy()
+        tot = int(lims[-1])
+        I = np.empty(tot, np.int64)
+        D = np.empty(tot, np.float32)
+        if tot:
+            ip, dp = C.POINTER(C.c_int64)(), C.POINTER(C.c_float)()
+            lib().faiss_RangeSearchResult_labels(r, C.byref(ip), C.byref(dp))
+            I[:] = np.ctypeslib.as_array(ip, shape=(tot,))
+            D[:] = np.ctypeslib.as_array(dp, shape=(tot,))
+        return lims, D, I
+    finally:
+        lib().faiss_RangeSearchResult_free(r)
+
+
 def _wrap(h, owner=None):
     """Wrap a raw FaissIndex* in the Python class of its dynamic type."""
     h = C.c_void_p(h) if not isinstance(h, C.c_void_p) else h

@@ -490,6 +490,51 @@ int faiss_amd_IndexShardsIVF_count(const FaissIndexShardsIVF* index) {
     return s ? (int)s->shards.size() : 0;
 }
 
+// ---------------- range search
+static RangeSearchResult* RSR(FaissRangeSearchResult* p) {
+    return reinterpret_cast<RangeSearchResult*>(p);
+}
+int faiss_RangeSearchResult_new(FaissRangeSearchResult** p_rsr, idx_t nq) {
+    C_TRY FAISS_THROW_IF_NOT(nq >= 0);
+    *p_rsr = reinterpret_cast<FaissRangeSearchResult*>(new RangeSearchResult((size_t)nq));
+    C_CATCH
+}
+void faiss_RangeSearchResult_free(FaissRangeSearchResult* obj) { delete RSR(obj); }
+size_t faiss_RangeSearchResult_nq(const FaissRangeSearchResult* rsr) {
+    return reinterpret_cast<const RangeSearchResult*>(rsr)->nq;
+}
+size_t faiss_RangeSearchResult_buffer_size(const FaissRangeSearchResult* rsr) {
+    return reinterpret_cast<const RangeSearchResult*>(rsr)->buffer_size();
+}
+void faiss_RangeSearchResult_lims(FaissRangeSearchResult* rsr, size_t** lims) {
+    *lims = RSR(rsr)->lims.data();
+}
+void faiss_RangeSearchResult_labels(FaissRangeSearchResult* rsr, idx_t** labels,
+                                    float** distances) {
+    *labels = RSR(rsr)->labels.data();
+    *distances = RSR(rsr)->distances.data();
+}
+int faiss_Index_range_search(const FaissIndex* index, idx_t n, const float* x, float radius,
+                             FaissRangeSearchResult* result) {
+    C_TRY IX(index)->range_search(n, x, radius, RSR(result), nullptr);
+    C_CATCH
+}
+int faiss_amd_Index_range_search_with_params(const FaissIndex* index, idx_t n, const float* x,
+                                             float radius, const FaissSearchParameters* params,
+                                             FaissRangeSearchResult* result) {
+    C_TRY IX(index)->range_search(n, x, radius, RSR(result), resolve_params(params));
+    C_CATCH
+}
+int faiss_IndexIVF_range_search_preassigned(const FaissIndexIVF* index, idx_t n,
+                                            const float* x, float radius, const idx_t* assign,
+                                            const float* centroid_dis,
+                                            FaissRangeSearchResult* result) {
+    C_TRY auto v = IVFc(index);
+    FAISS_THROW_IF_NOT_MSG(v, "index is not an IndexIVF");
+    v->range_search_preassigned(n, x, radius, assign, centroid_dis, RSR(result));
+    C_CATCH
+}
+
 // ---------------- I/O
 int faiss_write_index(const FaissIndex* idx, FILE* f) {
     C_TRY write_index(IX(idx), f);

@@ -91,6 +91,11 @@ void Index::reconstruct(idx_t, float*) const {
     FAISS_THROW_MSG("reconstruct not implemented for this type of index");
 }
 
+void Index::range_search(idx_t, const float*, float, RangeSearchResult*,
+                         const SearchParameters*) const {
+    FAISS_THROW_MSG("range search not implemented for this type of index");  // faiss/Index.cpp:39
+}
+
 hipStream_t Index::stream() const { return device_context(device).stream; }
 
 // Host entry: upload (zero-padded rows), search_device, download.

@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <cinttypes>
 #include <cstring>
 
 #include "../../include/faiss_amd.h"
@@ -989,6 +990,172 @@ void IndexShardsIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, fl
     kern::merge_rows(s_all_d_.as<float>(), s_all_i_.as<idx_t>(), n, (ns << 16) | (int)k, (int)k,
                      metric_type == METRIC_L2, distances, labels, s);
     HIP_CHECK(hipStreamSynchronize(s));
+}
+
+}  // namespace faiss_amd
+
+// ---------------------------------------------------------------- range search
+namespace faiss_amd {
+
+void IndexIVF::range_search(idx_t n, const float* x, float radius, RangeSearchResult* result,
+                            const SearchParameters* params_in) const {
+    // faiss/IndexIVF.cpp:1203-1241
+    const SearchParametersIVF* params = nullptr;
+    if (params_in) {
+        params = dynamic_cast<const SearchParametersIVF*>(params_in);
+        FAISS_THROW_IF_NOT_MSG(params, "IndexIVF params have incorrect type");
+    }
+    FAISS_THROW_IF_NOT(result && result->nq == (size_t)n);
+    const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
+    FAISS_THROW_IF_NOT(np > 0);
+    FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
+    FAISS_THROW_IF_NOT_MSG(dynamic_cast<const IndexIVFFlat*>(this),
+                           "range search is implemented for IndexIVFFlat only on this path");
+    check_parallel_mode(parallel_mode);
+    result->lims.assign((size_t)n + 1, 0);
+    result->labels.clear();
+    result->distances.clear();
+    if (n == 0) return;
+    DevGuard dg(device);
+    sync_device();
+    hipStream_t s = stream();
+    const int ldx = ld();
+    DeviceBuffer bx, bcd, bci;
+    bx.reserve(sizeof(float) * n * ldx);
+    bcd.reserve(sizeof(float) * n * np);
+    bci.reserve(sizeof(int32_t) * n * np);
+    if (ldx != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * n * ldx, s));
+    HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ldx, x, sizeof(float) * d,
+                               sizeof(float) * d, n, hipMemcpyHostToDevice, s));
+    const auto t0 = std::chrono::steady_clock::now();
+    quantize_device(n, bx.as<float>(), ldx, (int)np, bcd.as<float>(), bci.as<int32_t>(),
+                    params ? params->quantizer_params : nullptr, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+    const auto t1 = std::chrono::steady_clock::now();
+    indexIVF_stats.quantization_time +=
+            std::chrono::duration<double, std::milli>(t1 - t0).count();
+    quantizer->fold_device_stats();
+    const uint8_t* selm = apply_selector(params, s);
+    range_device(n, bx.as<float>(), ldx, (int)np, bci.as<int32_t>(), radius, selm, result,
+                 &indexIVF_stats, s);
+    indexIVF_stats.search_time += std::chrono::duration<double, std::milli>(
+                                          std::chrono::steady_clock::now() - t1)
+                                          .count();
+}
+
+void IndexIVF::range_search_preassigned(idx_t n, const float* x, float radius,
+                                        const idx_t* assign, const float* /*centroid_dis*/,
+                                        RangeSearchResult* result, bool store_pairs,
+                                        const SearchParametersIVF* params,
+                                        IndexIVFStats* stats) const {
+    // faiss/IndexIVF.cpp:1243-1400 (parallel_mode 0)
+    FAISS_THROW_IF_NOT(result && result->nq == (size_t)n);
+    FAISS_THROW_IF_NOT_MSG(!store_pairs, "store_pairs is not supported on the GPU path");
+    const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
+    FAISS_THROW_IF_NOT(np > 0);
+    FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
+    FAISS_THROW_IF_NOT_MSG(dynamic_cast<const IndexIVFFlat*>(this),
+                           "range search is implemented for IndexIVFFlat only on this path");
+    check_parallel_mode(parallel_mode);
+    result->lims.assign((size_t)n + 1, 0);
+    result->labels.clear();
+    result->distances.clear();
+    if (n == 0) return;
+    std::vector<int32_t> a32((size_t)n * np);
+    for (size_t i = 0; i < a32.size(); i++) {
+        const idx_t key = assign[i];
+        FAISS_THROW_IF_NOT_FMT(key < (idx_t)nlist, "Invalid key=%" PRId64 " at ik=%zd nlist=%zd\n",
+                               (int64_t)key, i % np, nlist);
+        a32[i] = key < 0 ? -1 : (int32_t)key;
+    }
+    DevGuard dg(device);
+    sync_device();
+    hipStream_t s = stream();
+    const int ldx = ld();
+    DeviceBuffer bx, bci;
+    bx.reserve(sizeof(float) * n * ldx);
+    bci.reserve(sizeof(int32_t) * n * np);
+    if (ldx != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * n * ldx, s));
+    HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ldx, x, sizeof(float) * d,
+                               sizeof(float) * d, n, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(bci.ptr, a32.data(), sizeof(int32_t) * a32.size(),
+                             hipMemcpyHostToDevice, s));
+    const uint8_t* selm = apply_selector(params, s);
+    range_device(n, bx.as<float>(), ldx, (int)np, bci.as<int32_t>(), radius, selm, result,
+                 stats ? stats : &indexIVF_stats, s);
+}
+
+void IndexIVF::range_device(idx_t n, const float* x, int ldx, int np, const int32_t* assign,
+                            float radius, const uint8_t* selm, RangeSearchResult* result,
+                            IndexIVFStats* stats, hipStream_t s) const {
+    // queries per pass: grid n*np < 2^31 and bounded count scratch
+    const idx_t qc = std::max<idx_t>(1, std::min<idx_t>(n, ((idx_t)1 << 26) / np));
+    const int ldc = (int)roundup((size_t)d, 4);
+    std::vector<uint32_t> cnt;
+    std::vector<int32_t> hassign;
+    std::vector<uint64_t> offs;
+    DeviceBuffer bc, bo, bd, bi;
+    size_t nlistv = 0, ndis = 0;
+    result->lims.assign((size_t)n + 1, 0);
+    for (idx_t q0 = 0; q0 < n; q0 += qc) {
+        const idx_t nc = std::min(qc, n - q0);
+        const size_t m = (size_t)nc * np;
+        const int32_t* a = assign + (size_t)q0 * np;
+        bc.reserve(sizeof(uint32_t) * m);
+        kern::ivf_range_flat(x + (size_t)q0 * ldx, nc, ldx, a, np, d_codes_.as<float>(), ldc,
+                             d_ids_.as<int64_t>(), d_list_off_.as<uint32_t>(),
+                             d_list_len_.as<uint32_t>(), (int)nlist, d,
+                             metric_type == METRIC_L2, radius, selm, bc.as<uint32_t>(), nullptr,
+                             nullptr, nullptr, s);
+        cnt.resize(m);
+        hassign.resize(m);
+        HIP_CHECK(hipMemcpyAsync(cnt.data(), bc.ptr, sizeof(uint32_t) * m, hipMemcpyDeviceToHost,
+                                 s));
+        HIP_CHECK(hipMemcpyAsync(hassign.data(), a, sizeof(int32_t) * m, hipMemcpyDeviceToHost,
+                                 s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        // (query, probe) offsets in the reference's order: query-major, probe
+        // order within a query (RangeQueryResult per query, :1334-1345)
+        offs.resize(m);
+        const size_t base = result->labels.size();
+        uint64_t tot = 0;
+        for (idx_t i = 0; i < nc; i++) {
+            result->lims[(size_t)(q0 + i)] = base + tot;
+            for (int p = 0; p < np; p++) {
+                const size_t j = (size_t)i * np + p;
+                offs[j] = tot;
+                tot += cnt[j];
+                const int32_t key = hassign[j];
+                if (key >= 0 && invlists->list_size((size_t)key) > 0) {
+                    nlistv++;
+                    ndis += invlists->list_size((size_t)key);
+                }
+            }
+        }
+        if (tot) {
+            bo.reserve(sizeof(uint64_t) * m);
+            bd.reserve(sizeof(float) * tot);
+            bi.reserve(sizeof(idx_t) * tot);
+            HIP_CHECK(hipMemcpyAsync(bo.ptr, offs.data(), sizeof(uint64_t) * m,
+                                     hipMemcpyHostToDevice, s));
+            kern::ivf_range_flat(x + (size_t)q0 * ldx, nc, ldx, a, np, d_codes_.as<float>(), ldc,
+                                 d_ids_.as<int64_t>(), d_list_off_.as<uint32_t>(),
+                                 d_list_len_.as<uint32_t>(), (int)nlist, d,
+                                 metric_type == METRIC_L2, radius, selm, nullptr,
+                                 bo.as<uint64_t>(), bd.as<float>(), bi.as<int64_t>(), s);
+            result->labels.resize(base + tot);
+            result->distances.resize(base + tot);
+            HIP_CHECK(hipMemcpyAsync(result->distances.data() + base, bd.ptr, sizeof(float) * tot,
+                                     hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipMemcpyAsync(result->labels.data() + base, bi.ptr, sizeof(idx_t) * tot,
+                                     hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+        }
+    }
+    result->lims[(size_t)n] = result->labels.size();
+    stats->nq += (size_t)n;
+    stats->nlist += nlistv;
+    stats->ndis += ndis;
 }
 
 }  // namespace faiss_amd

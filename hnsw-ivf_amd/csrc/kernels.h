@@ -256,5 +256,15 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, hipStream_t s);
 
+// IVF-Flat range search (kernels_range.hip): one wave per (query, probe).
+// offsets == nullptr: counts[q*np+p] = hits (dis < radius for L2, > for IP,
+// selector rows only); else the hits are written at offsets[q*np+p] in row
+// order.  Grid = n*np workgroups (n*np < 2^31).
+void ivf_range_flat(const float* x, int64_t n, int ldx, const int32_t* assign, int np,
+                    const float* codes, int ldc, const int64_t* ids, const uint32_t* list_off,
+                    const uint32_t* list_len, int nlist, int d, int metric_l2, float radius,
+                    const uint8_t* selm, uint32_t* counts, const uint64_t* offsets, float* outD,
+                    int64_t* outI, hipStream_t s);
+
 }  // namespace kern
 }  // namespace faiss_amd

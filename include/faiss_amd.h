@@ -141,6 +141,17 @@ struct HNSWStats {
 };
 extern HNSWStats hnsw_stats;
 
+// faiss/impl/AuxIndexStructures.h:30-60: results of query i are
+// labels/distances[lims[i], lims[i+1]), in the order the scan found them.
+struct RangeSearchResult {
+    size_t nq = 0;
+    std::vector<size_t> lims;
+    std::vector<idx_t> labels;
+    std::vector<float> distances;
+    explicit RangeSearchResult(size_t nq = 0) : nq(nq), lims(nq + 1, 0) {}
+    size_t buffer_size() const { return labels.size(); }
+};
+
 // ---------------------------------------------------------------- Index
 struct Index {
     int d = 0;
@@ -172,6 +183,10 @@ struct Index {
                                hipStream_t stream) const;
     virtual void reset() = 0;
     virtual void reconstruct(idx_t key, float* recons) const;
+    // faiss/Index.h:183-196: all vectors with distance < radius (L2) or
+    // > radius (IP); only IndexIVFFlat implements it on this path
+    virtual void range_search(idx_t n, const float* x, float radius, RangeSearchResult* result,
+                              const SearchParameters* params = nullptr) const;
     virtual void sync_device() const {}
     // fold device-side search counters (HNSWStats) into the host globals
     virtual void fold_device_stats() const {}
@@ -349,6 +364,16 @@ struct IndexIVF : Index {
                             const float* centroid_dis, float* distances, idx_t* labels,
                             bool store_pairs, const SearchParametersIVF* params = nullptr,
                             IndexIVFStats* stats = nullptr) const;
+    // faiss/IndexIVF.cpp:1203-1241 (coarse nprobe, then the preassigned scan)
+    void range_search(idx_t n, const float* x, float radius, RangeSearchResult* result,
+                      const SearchParameters* params = nullptr) const override;
+    // faiss/IndexIVF.cpp:1243-1400; assign = [n][nprobe] host list numbers
+    // (centroid_dis unused by the Flat scanner); parallel_mode 0 order
+    void range_search_preassigned(idx_t n, const float* x, float radius, const idx_t* assign,
+                                  const float* centroid_dis, RangeSearchResult* result,
+                                  bool store_pairs = false,
+                                  const SearchParametersIVF* params = nullptr,
+                                  IndexIVFStats* stats = nullptr) const;
     // faiss/IndexIVF.cpp:870-1200 (per-query list_scan_us)
     void search_preassigned_stats(idx_t n, const float* x, idx_t k, const idx_t* assign,
                                   const float* centroid_dis, float* distances, idx_t* labels,
@@ -363,6 +388,10 @@ struct IndexIVF : Index {
                                            idx_t* labels, hipStream_t stream,
                                            const uint32_t* lim = nullptr,
                                            const uint8_t* sel = nullptr) const = 0;
+    // range scan of device-resident queries / assignments into host results
+    void range_device(idx_t n, const float* x, int ldx, int np, const int32_t* assign,
+                      float radius, const uint8_t* sel, RangeSearchResult* result,
+                      IndexIVFStats* stats, hipStream_t s) const;
     // IDSelector of the call -> arena-row membership mask (index scratch),
     // nullptr when there is none (faiss/IndexIVF.cpp:418-430)
     const uint8_t* apply_selector(const SearchParameters* params, hipStream_t stream) const;

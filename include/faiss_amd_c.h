@@ -359,6 +359,28 @@ int faiss_amd_IndexShardsIVF_new(
 int faiss_amd_IndexShardsIVF_add_shard(FaissIndexShardsIVF* index, FaissIndex* shard);
 int faiss_amd_IndexShardsIVF_count(const FaissIndexShardsIVF* index);
 
+/* ---------------- range search (c_api/impl/AuxIndexStructures_c.h:20-50,
+ * c_api/Index_c.h:148-153, c_api/IndexIVF_c.h range_search_preassigned) ----
+ * Results of query i: labels/distances[lims[i], lims[i+1]) in the reference's
+ * scan order (probe order, then list order).  IndexIVFFlat only. */
+typedef struct FaissRangeSearchResult_H FaissRangeSearchResult;
+int faiss_RangeSearchResult_new(FaissRangeSearchResult** p_rsr, idx_t nq);
+void faiss_RangeSearchResult_free(FaissRangeSearchResult* obj);
+size_t faiss_RangeSearchResult_nq(const FaissRangeSearchResult* rsr);
+size_t faiss_RangeSearchResult_buffer_size(const FaissRangeSearchResult* rsr);
+void faiss_RangeSearchResult_lims(FaissRangeSearchResult* rsr, size_t** lims);
+void faiss_RangeSearchResult_labels(FaissRangeSearchResult* rsr, idx_t** labels,
+                                    float** distances);
+int faiss_Index_range_search(const FaissIndex* index, idx_t n, const float* x, float radius,
+                             FaissRangeSearchResult* result);
+int faiss_amd_Index_range_search_with_params(const FaissIndex* index, idx_t n, const float* x,
+                                             float radius, const FaissSearchParameters* params,
+                                             FaissRangeSearchResult* result);
+int faiss_IndexIVF_range_search_preassigned(const FaissIndexIVF* index, idx_t n,
+                                            const float* x, float radius, const idx_t* assign,
+                                            const float* centroid_dis,
+                                            FaissRangeSearchResult* result);
+
 /* ---------------- I/O (c_api/index_io_c.h) ---------------- */
 int faiss_write_index(const FaissIndex* idx, FILE* f);                   /* :28 */
 int faiss_write_index_fname(const FaissIndex* idx, const char* fname);   /* :33 */

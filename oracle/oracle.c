@@ -704,3 +704,40 @@ void oracle_merge_knn_results(size_t n, size_t k, int nshard, const float* all_d
     free(shard_ids);
     free(heap_vals);
 }
+
+/* IVF-Flat range search, parallel_mode 0 (faiss/IndexIVF.cpp:1243-1400 with
+ * IVFFlatScanner::scan_codes_range, faiss/IndexIVFFlat.cpp:181-201): per
+ * query, probes in order, rows in list order; a row is kept when
+ * C::cmp(radius, dis) (L2: dis < radius, IP: dis > radius) and, with a
+ * selector mask (per concatenated row, may be NULL), when it is a member.
+ * Writes lims[n+1]; D/I are written up to `cap` entries; returns the total. */
+int64_t oracle_ivf_range_preassigned(const oracle_ivf_t* ivf, size_t n, const float* x,
+                                     size_t nprobe, const int64_t* keys, float radius,
+                                     const uint8_t* selmask, size_t* lims, float* D, int64_t* I,
+                                     int64_t cap) {
+    const int l2 = ivf->metric == 1;
+    const int d = ivf->d;
+    int64_t tot = 0;
+    for (size_t i = 0; i < n; i++) {
+        lims[i] = (size_t)tot;
+        const float* xi = x + i * d;
+        for (size_t ik = 0; ik < nprobe; ik++) {
+            const int64_t key = keys[i * nprobe + ik];
+            if (key < 0 || key >= ivf->nlist) continue;
+            for (int64_t r = ivf->list_off[key]; r < ivf->list_off[key + 1]; r++) {
+                if (selmask && !selmask[r]) continue;
+                const float* y = (const float*)(ivf->codes + (size_t)r * ivf->code_size);
+                const float dis = ref_dist_(xi, y, d, l2);
+                if (l2 ? (dis < radius) : (radius < dis)) {
+                    if (tot < cap) {
+                        D[tot] = dis;
+                        I[tot] = ivf->ids[r];
+                    }
+                    tot++;
+                }
+            }
+        }
+    }
+    lims[n] = (size_t)tot;
+    return tot;
+}

@@ -65,6 +65,10 @@ def lib():
                                              C.c_size_t, _P, _P, C.c_int]
         L.oracle_merge_knn_results.argtypes = [C.c_size_t, C.c_size_t, C.c_int, _P, _P, _P, _P,
                                                C.c_int]
+        L.oracle_ivf_range_preassigned.argtypes = [C.POINTER(IVFStruct), C.c_size_t, _P,
+                                                   C.c_size_t, _P, C.c_float, _P, _P, _P, _P,
+                                                   C.c_int64]
+        L.oracle_ivf_range_preassigned.restype = C.c_int64
         L.oracle_max_threads.restype = C.c_int
         _lib = L
     return _lib
@@ -233,6 +237,22 @@ class IVFOracle:
                                                _p(coarse_dis), max_codes, _p(D), _p(I), _p(nd),
                                                nthreads or nthreads_default())
         return (D, I, int(nd[0])) if return_ndis else (D, I)
+
+    def range_search_preassigned(self, x, radius, keys, selmask=None):
+        """IVF-Flat range search (faiss/IndexIVF.cpp:1243-1400): (lims, D, I).
+        selmask: per concatenated row uint8 membership (IDSelector), or None."""
+        x = np.ascontiguousarray(x, np.float32)
+        keys = np.ascontiguousarray(keys, np.int64)
+        n, nprobe = keys.shape
+        lims = np.zeros(n + 1, np.uint64)
+        sm = None if selmask is None else np.ascontiguousarray(selmask, np.uint8)
+        args = (C.byref(self.s), n, _p(x), nprobe, _p(keys), float(radius),
+                _p(sm) if sm is not None else None, _p(lims))
+        tot = lib().oracle_ivf_range_preassigned(*args, None, None, 0)
+        D = np.empty(tot, np.float32)
+        I = np.empty(tot, np.int64)
+        lib().oracle_ivf_range_preassigned(*args, _p(D), _p(I), tot)
+        return lims.astype(np.int64), D, I
 
     def search_fast(self, x, k, nprobe, nthreads=None):
         x = np.ascontiguousarray(x, np.float32)

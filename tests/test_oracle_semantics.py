@@ -87,3 +87,41 @@ def test_oracle_ivf_exhaustive_equals_knn(orc):
     Dk, Ik = orc.knn(xq, xb, 10, blas_form=False)
     np.testing.assert_array_equal(I, Ik)
     np.testing.assert_array_equal(D, Dk)
+
+
+def test_oracle_range_search_restatement(orc):
+    """oracle_ivf_range_preassigned against a direct loop over the reference
+    semantics (faiss/IndexIVF.cpp:1283-1345, IndexIVFFlat.cpp:181-201):
+    probes in order, rows in list order, strict C::cmp(radius, dis)."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    d, nlist = 12, 7
+    sizes = rng.integers(0, 30, nlist)
+    off = np.zeros(nlist + 1, np.int64)
+    off[1:] = np.cumsum(sizes)
+    vecs = rng.random((int(off[-1]), d), dtype=np.float32)
+    ids = rng.permutation(int(off[-1])).astype(np.int64) * 3
+    xq = rng.random((9, d), dtype=np.float32)
+    keys = rng.integers(-1, nlist, (9, 4))
+    for metric, radius in ((1, 1.2), (0, 3.0)):
+        ref = orc.IVFOracle(d, nlist, metric, off, vecs.view(np.uint8).reshape(len(vecs), -1), ids)
+        sel = (ids % 2 == 0).astype(np.uint8)
+        for selmask in (None, sel):
+            lims, D, I = ref.range_search_preassigned(xq, radius, keys, selmask)
+            eD, eI, elims = [], [], [0]
+            for i in range(9):
+                for key in keys[i]:
+                    if key < 0:
+                        continue
+                    for r in range(off[key], off[key + 1]):
+                        if selmask is not None and not selmask[r]:
+                            continue
+                        dis = (orc.fvec_L2sqr(xq[i], vecs[r]) if metric == 1
+                               else orc.fvec_inner_product(xq[i], vecs[r]))
+                        if (dis < radius) if metric == 1 else (dis > radius):
+                            eD.append(dis)
+                            eI.append(ids[r])
+                elims.append(len(eI))
+            assert lims.tolist() == elims
+            assert I.tolist() == eI
+            assert np.array_equal(D, np.array(eD, np.float32))
