@@ -1009,8 +1009,6 @@ void IndexIVF::range_search(idx_t n, const float* x, float radius, RangeSearchRe
     const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
     FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
-    FAISS_THROW_IF_NOT_MSG(dynamic_cast<const IndexIVFFlat*>(this),
-                           "range search is implemented for IndexIVFFlat only on this path");
     check_parallel_mode(parallel_mode);
     result->lims.assign((size_t)n + 1, 0);
     result->labels.clear();
@@ -1036,15 +1034,15 @@ void IndexIVF::range_search(idx_t n, const float* x, float radius, RangeSearchRe
             std::chrono::duration<double, std::milli>(t1 - t0).count();
     quantizer->fold_device_stats();
     const uint8_t* selm = apply_selector(params, s);
-    range_device(n, bx.as<float>(), ldx, (int)np, bci.as<int32_t>(), radius, selm, result,
-                 &indexIVF_stats, s);
+    range_device(n, bx.as<float>(), ldx, (int)np, bci.as<int32_t>(), bcd.as<float>(), radius,
+                 selm, result, &indexIVF_stats, s);
     indexIVF_stats.search_time += std::chrono::duration<double, std::milli>(
                                           std::chrono::steady_clock::now() - t1)
                                           .count();
 }
 
 void IndexIVF::range_search_preassigned(idx_t n, const float* x, float radius,
-                                        const idx_t* assign, const float* /*centroid_dis*/,
+                                        const idx_t* assign, const float* centroid_dis,
                                         RangeSearchResult* result, bool store_pairs,
                                         const SearchParametersIVF* params,
                                         IndexIVFStats* stats) const {
@@ -1054,8 +1052,6 @@ void IndexIVF::range_search_preassigned(idx_t n, const float* x, float radius,
     const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
     FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
-    FAISS_THROW_IF_NOT_MSG(dynamic_cast<const IndexIVFFlat*>(this),
-                           "range search is implemented for IndexIVFFlat only on this path");
     check_parallel_mode(parallel_mode);
     result->lims.assign((size_t)n + 1, 0);
     result->labels.clear();
@@ -1072,25 +1068,71 @@ void IndexIVF::range_search_preassigned(idx_t n, const float* x, float radius,
     sync_device();
     hipStream_t s = stream();
     const int ldx = ld();
-    DeviceBuffer bx, bci;
+    DeviceBuffer bx, bci, bcd;
     bx.reserve(sizeof(float) * n * ldx);
     bci.reserve(sizeof(int32_t) * n * np);
+    if (centroid_dis) {
+        bcd.reserve(sizeof(float) * n * np);
+        HIP_CHECK(hipMemcpyAsync(bcd.ptr, centroid_dis, sizeof(float) * n * np,
+                                 hipMemcpyHostToDevice, s));
+    }
     if (ldx != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * n * ldx, s));
     HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ldx, x, sizeof(float) * d,
                                sizeof(float) * d, n, hipMemcpyHostToDevice, s));
     HIP_CHECK(hipMemcpyAsync(bci.ptr, a32.data(), sizeof(int32_t) * a32.size(),
                              hipMemcpyHostToDevice, s));
     const uint8_t* selm = apply_selector(params, s);
-    range_device(n, bx.as<float>(), ldx, (int)np, bci.as<int32_t>(), radius, selm, result,
+    range_device(n, bx.as<float>(), ldx, (int)np, bci.as<int32_t>(),
+                 centroid_dis ? bcd.as<float>() : nullptr, radius, selm, result,
                  stats ? stats : &indexIVF_stats, s);
 }
 
+void IndexIVF::range_launch(const float*, idx_t, int, const int32_t*, const float*, int, float,
+                            const uint8_t*, uint32_t*, const uint64_t*, float*, idx_t*,
+                            hipStream_t) const {
+    FAISS_THROW_MSG("range search not implemented for this type of index");
+}
+
+void IndexIVFFlat::range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
+                                const float*, int np, float radius, const uint8_t* selm,
+                                uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
+                                hipStream_t s) const {
+    kern::ivf_range_flat(x, n, ldx, assign, np, d_codes_.as<float>(), ld(),
+                         d_ids_.as<int64_t>(), d_list_off_.as<uint32_t>(),
+                         d_list_len_.as<uint32_t>(), (int)nlist, d, metric_type == METRIC_L2,
+                         radius, selm, counts, offs, D, I, s);
+}
+
+void IndexIVFPQ::range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
+                              const float* cdis, int np, float radius, const uint8_t* selm,
+                              uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
+                              hipStream_t s) const {
+    FAISS_THROW_IF_NOT_MSG(metric_type == METRIC_L2 && by_residual,
+                           "IVF-PQ range search: L2 by-residual indexes only on this path");
+    FAISS_THROW_IF_NOT_MSG(pq.nbits == 8 && (pq.dsub == 2 || pq.dsub == 4 || pq.dsub == 8),
+                           "IVF-PQ range search: PQ8 with dsub 2, 4 or 8 on this path");
+    FAISS_THROW_IF_NOT_MSG(cdis || use_precomputed_table != 1,
+                           "IVF-PQ range search with precomputed tables needs centroid_dis");
+    kern::PQArgs pa;
+    pa.pq_cent = d_pq_.as<float>();
+    pa.cent = d_cent_.as<float>();
+    pa.ldcent = ld();
+    pa.cdis = cdis;
+    pa.codes = d_codes_.as<uint8_t>();
+    pa.cs = device_code_stride();
+    pa.M = (int)pq.M;
+    pa.table1 = use_precomputed_table == 1 ? 1 : 0;
+    kern::ivfpq_range(x, n, ldx, assign, np, pa, (int)pq.dsub, d_ids_.as<int64_t>(),
+                      d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(), (int)nlist, radius,
+                      selm, counts, offs, D, I, s);
+}
+
 void IndexIVF::range_device(idx_t n, const float* x, int ldx, int np, const int32_t* assign,
-                            float radius, const uint8_t* selm, RangeSearchResult* result,
+                            const float* cdis, float radius, const uint8_t* selm,
+                            RangeSearchResult* result,
                             IndexIVFStats* stats, hipStream_t s) const {
     // queries per pass: grid n*np < 2^31 and bounded count scratch
     const idx_t qc = std::max<idx_t>(1, std::min<idx_t>(n, ((idx_t)1 << 26) / np));
-    const int ldc = (int)roundup((size_t)d, 4);
     std::vector<uint32_t> cnt;
     std::vector<int32_t> hassign;
     std::vector<uint64_t> offs;
@@ -1102,11 +1144,9 @@ void IndexIVF::range_device(idx_t n, const float* x, int ldx, int np, const int3
         const size_t m = (size_t)nc * np;
         const int32_t* a = assign + (size_t)q0 * np;
         bc.reserve(sizeof(uint32_t) * m);
-        kern::ivf_range_flat(x + (size_t)q0 * ldx, nc, ldx, a, np, d_codes_.as<float>(), ldc,
-                             d_ids_.as<int64_t>(), d_list_off_.as<uint32_t>(),
-                             d_list_len_.as<uint32_t>(), (int)nlist, d,
-                             metric_type == METRIC_L2, radius, selm, bc.as<uint32_t>(), nullptr,
-                             nullptr, nullptr, s);
+        const float* cd = cdis ? cdis + (size_t)q0 * np : nullptr;
+        range_launch(x + (size_t)q0 * ldx, nc, ldx, a, cd, np, radius, selm, bc.as<uint32_t>(),
+                     nullptr, nullptr, nullptr, s);
         cnt.resize(m);
         hassign.resize(m);
         HIP_CHECK(hipMemcpyAsync(cnt.data(), bc.ptr, sizeof(uint32_t) * m, hipMemcpyDeviceToHost,
@@ -1138,11 +1178,8 @@ void IndexIVF::range_device(idx_t n, const float* x, int ldx, int np, const int3
             bi.reserve(sizeof(idx_t) * tot);
             HIP_CHECK(hipMemcpyAsync(bo.ptr, offs.data(), sizeof(uint64_t) * m,
                                      hipMemcpyHostToDevice, s));
-            kern::ivf_range_flat(x + (size_t)q0 * ldx, nc, ldx, a, np, d_codes_.as<float>(), ldc,
-                                 d_ids_.as<int64_t>(), d_list_off_.as<uint32_t>(),
-                                 d_list_len_.as<uint32_t>(), (int)nlist, d,
-                                 metric_type == METRIC_L2, radius, selm, nullptr,
-                                 bo.as<uint64_t>(), bd.as<float>(), bi.as<int64_t>(), s);
+            range_launch(x + (size_t)q0 * ldx, nc, ldx, a, cd, np, radius, selm, nullptr,
+                         bo.as<uint64_t>(), bd.as<float>(), bi.as<int64_t>(), s);
             result->labels.resize(base + tot);
             result->distances.resize(base + tot);
             HIP_CHECK(hipMemcpyAsync(result->distances.data() + base, bd.ptr, sizeof(float) * tot,

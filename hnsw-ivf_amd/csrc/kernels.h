@@ -266,5 +266,14 @@ void ivf_range_flat(const float* x, int64_t n, int ldx, const int32_t* assign, i
                     const uint8_t* selm, uint32_t* counts, const uint64_t* offsets, float* outD,
                     int64_t* outI, hipStream_t s);
 
+// IVF-PQ range search (kernels_ivf_mfma.hip): same contract as
+// ivf_range_flat, distances by the reference table arithmetic (pq_exact);
+// pa.cdis = coarse distances [n][np] (table 1 dis0).  L2, by residual.
+void ivfpq_range(const float* x, int64_t n, int ldx, const int32_t* assign, int np,
+                 const PQArgs& pa, int dsub, const int64_t* ids, const uint32_t* list_off,
+                 const uint32_t* list_len, int nlist, float radius, const uint8_t* selm,
+                 uint32_t* counts, const uint64_t* offsets, float* outD, int64_t* outI,
+                 hipStream_t s);
+
 }  // namespace kern
 }  // namespace faiss_amd

@@ -1054,6 +1054,77 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     }
 }
 
+namespace {
+// IVF-PQ range scan (faiss/IndexIVFPQ.cpp:1254-1279 scan_codes_range with
+// RangeSearchResults :780-799): one wave per (query, probe), 64 rows per
+// step, every code evaluated by pq_exact (the reference table arithmetic,
+// bit-exact with the k-NN path) and kept when dis < radius.  Pass 1 counts,
+// pass 2 writes in row order (see kernels_range.hip for the Flat twin).
+template <int PQD, bool FILL>
+__global__ __launch_bounds__(64) void k_ivfpq_range(
+        const float* __restrict__ x, int ldx, const int32_t* __restrict__ assign, int np,
+        PQArgs pa, const int64_t* __restrict__ ids, const uint32_t* __restrict__ list_off,
+        const uint32_t* __restrict__ list_len, int nlist, float radius,
+        const uint8_t* __restrict__ selm, uint32_t* __restrict__ counts,
+        const uint64_t* __restrict__ offsets, float* __restrict__ outD,
+        int64_t* __restrict__ outI) {
+    const int64_t qp = blockIdx.x;
+    const int64_t q = qp / np;
+    const int lane = threadIdx.x;
+    const int32_t key = assign[qp];
+    uint32_t cnt = 0;
+    if (key >= 0 && key < nlist) {
+        const uint32_t off = list_off[key], len = list_len[key];
+        const float* xq = x + q * (int64_t)ldx;
+        const float d0 = pa.table1 ? pa.cdis[qp] : 0.f;
+        const uint64_t base = FILL ? offsets[qp] : 0;
+        const uint64_t below = (1ull << lane) - 1ull;
+        for (uint32_t r0 = 0; r0 < len; r0 += 64) {
+            const uint32_t r = r0 + lane;
+            bool hit = false;
+            float dis = 0.f;
+            if (r < len && (!selm || selm[(uint64_t)off + r])) {
+                dis = pq_exact<PQD>(pa, xq, off + r, (uint32_t)key, d0);
+                hit = dis < radius;
+            }
+            const uint64_t m = __ballot(hit);
+            if (FILL && hit) {
+                const uint64_t o = base + cnt + (uint32_t)__popcll(m & below);
+                outD[o] = dis;
+                outI[o] = ids[(uint64_t)off + r];
+            }
+            cnt += (uint32_t)__popcll(m);
+        }
+    }
+    if (!FILL && lane == 0) counts[qp] = cnt;
+}
+}  // namespace
+
+void ivfpq_range(const float* x, int64_t n, int ldx, const int32_t* assign, int np,
+                 const PQArgs& pa, int dsub, const int64_t* ids, const uint32_t* list_off,
+                 const uint32_t* list_len, int nlist, float radius, const uint8_t* selm,
+                 uint32_t* counts, const uint64_t* offsets, float* outD, int64_t* outI,
+                 hipStream_t s) {
+    if (n <= 0 || np <= 0) return;
+    const dim3 grid((unsigned)(n * np)), block(64);
+#define PQR_LAUNCH(DS, F)                                                                     \
+    k_ivfpq_range<DS, F><<<grid, block, 0, s>>>(x, ldx, assign, np, pa, ids, list_off,        \
+                                                list_len, nlist, radius, selm, counts,        \
+                                                offsets, outD, outI)
+#define PQR_DISPATCH(DS)                                  \
+    do {                                                  \
+        if (offsets) PQR_LAUNCH(DS, true);                \
+        else PQR_LAUNCH(DS, false);                       \
+    } while (0)
+    if (dsub == 2) PQR_DISPATCH(2);
+    else if (dsub == 4) PQR_DISPATCH(4);
+    else if (dsub == 8) PQR_DISPATCH(8);
+    else FAISS_THROW_MSG("ivfpq_range: dsub must be 2, 4 or 8");
+    HIP_LAUNCH_CHECK();
+#undef PQR_DISPATCH
+#undef PQR_LAUNCH
+}
+
 // IVF-PQ re-rank: the Flat re-rank's certified candidate selection with the
 // reference LUT arithmetic as the exact evaluator (pq_exact)
 void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx, int d,

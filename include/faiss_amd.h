@@ -390,7 +390,8 @@ struct IndexIVF : Index {
                                            const uint8_t* sel = nullptr) const = 0;
     // range scan of device-resident queries / assignments into host results
     void range_device(idx_t n, const float* x, int ldx, int np, const int32_t* assign,
-                      float radius, const uint8_t* sel, RangeSearchResult* result,
+                      const float* cdis, float radius, const uint8_t* sel,
+                      RangeSearchResult* result,
                       IndexIVFStats* stats, hipStream_t s) const;
     // IDSelector of the call -> arena-row membership mask (index scratch),
     // nullptr when there is none (faiss/IndexIVF.cpp:418-430)
@@ -426,6 +427,12 @@ struct IndexIVF : Index {
             s_pk1_, s_pk2_, s_q_;
     mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_,
             s_selmask_;
+    // one pass of the range scan (counts when offs == nullptr, else fill);
+    // cdis = coarse distances [n][np] on the device (PQ table 1 dis0)
+    virtual void range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
+                              const float* cdis, int np, float radius, const uint8_t* sel,
+                              uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
+                              hipStream_t s) const;
 
    private:
     idx_t search_chunk(idx_t n, size_t np, idx_t k) const;
@@ -450,6 +457,12 @@ struct IndexIVFFlat : IndexIVF {
 
    protected:
     void upload_extra() const override;
+    // one pass of the range scan (counts when offs == nullptr, else fill);
+    // cdis = coarse distances [n][np] on the device (PQ table 1 dis0)
+    virtual void range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
+                              const float* cdis, int np, float radius, const uint8_t* sel,
+                              uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
+                              hipStream_t s) const override;
     mutable DeviceBuffer d_ynorm_, d_ynmax_, d_cbf_, d_rres_, d_rmax_, s_part_, s_flags_;
     mutable int obits_ = 4;
 };
@@ -483,6 +496,12 @@ struct IndexIVFPQ : IndexIVF {
 
    protected:
     void upload_extra() const override;
+    // one pass of the range scan (counts when offs == nullptr, else fill);
+    // cdis = coarse distances [n][np] on the device (PQ table 1 dis0)
+    virtual void range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
+                              const float* cdis, int np, float radius, const uint8_t* sel,
+                              uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
+                              hipStream_t s) const override;
     mutable DeviceBuffer d_pq_, d_terms_, d_cent_;
     // list-centric MFMA scan (kernels_pq_mfma.hip): bf16 decode table, per
     // row |y_R| and bf16 residual norm, per list maxima, |y_C| per list

@@ -705,29 +705,74 @@ void oracle_merge_knn_results(size_t n, size_t k, int nshard, const float* all_d
     free(heap_vals);
 }
 
-/* IVF-Flat range search, parallel_mode 0 (faiss/IndexIVF.cpp:1243-1400 with
- * IVFFlatScanner::scan_codes_range, faiss/IndexIVFFlat.cpp:181-201): per
+/* IVF range search, parallel_mode 0 (faiss/IndexIVF.cpp:1243-1400 with
+ * IVFFlatScanner::scan_codes_range, faiss/IndexIVFFlat.cpp:181-201, and
+ * IVFPQScanner::scan_codes_range, faiss/IndexIVFPQ.cpp:1254-1279 with
+ * RangeSearchResults :780-799 — the same tables as the k-NN scan above): per
  * query, probes in order, rows in list order; a row is kept when
  * C::cmp(radius, dis) (L2: dis < radius, IP: dis > radius) and, with a
  * selector mask (per concatenated row, may be NULL), when it is a member.
- * Writes lims[n+1]; D/I are written up to `cap` entries; returns the total. */
+ * Writes lims[n+1]; D/I are written up to `cap` entries; returns the total.
+ * PQ: L2 only. */
 int64_t oracle_ivf_range_preassigned(const oracle_ivf_t* ivf, size_t n, const float* x,
-                                     size_t nprobe, const int64_t* keys, float radius,
+                                     size_t nprobe, const int64_t* keys,
+                                     const float* coarse_dis, float radius,
                                      const uint8_t* selmask, size_t* lims, float* D, int64_t* I,
                                      int64_t cap) {
     const int l2 = ivf->metric == 1;
     const int d = ivf->d;
+    const int M = ivf->pq_M;
+    const int ksub = M ? 1 << ivf->pq_nbits : 0;
+    const int dsub = M ? d / M : 0;
+    float* sim = M ? (float*)malloc(sizeof(float) * M * ksub) : NULL;
+    float* sim2 = M ? (float*)malloc(sizeof(float) * M * ksub) : NULL;
+    float* resid = (float*)malloc(sizeof(float) * d);
     int64_t tot = 0;
     for (size_t i = 0; i < n; i++) {
         lims[i] = (size_t)tot;
         const float* xi = x + i * d;
+        if (M) { /* init_query_L2 (IndexIVFPQ.cpp:560-566) */
+            for (int m = 0; m < M; m++)
+                for (int j = 0; j < ksub; j++) {
+                    const float* c = ivf->pq_centroids + ((size_t)m * ksub + j) * dsub;
+                    if (!ivf->by_residual)
+                        sim[m * ksub + j] = oracle_fvec_L2sqr(xi + m * dsub, c, dsub);
+                    else if (ivf->use_precomputed_table == 1)
+                        sim2[m * ksub + j] = oracle_fvec_inner_product(xi + m * dsub, c, dsub);
+                }
+        }
         for (size_t ik = 0; ik < nprobe; ik++) {
             const int64_t key = keys[i * nprobe + ik];
             if (key < 0 || key >= ivf->nlist) continue;
+            float dis0 = 0.f;
+            if (M && ivf->by_residual) { /* set_list: precompute_list_tables_L2 */
+                if (ivf->use_precomputed_table == 1) {
+                    dis0 = coarse_dis[i * nprobe + ik];
+                    const float* P = ivf->precomputed_table + (size_t)key * M * ksub;
+                    for (int e = 0; e < M * ksub; e++) sim[e] = fmaf(-2.f, sim2[e], P[e]);
+                } else {
+                    const float* c = ivf->hnsw ? ivf->hnsw->storage + key * d
+                                               : ivf->centroids + key * d;
+                    for (int j = 0; j < d; j++) resid[j] = xi[j] - c[j];
+                    for (int m = 0; m < M; m++)
+                        for (int j = 0; j < ksub; j++)
+                            sim[m * ksub + j] = oracle_fvec_L2sqr(
+                                    resid + m * dsub,
+                                    ivf->pq_centroids + ((size_t)m * ksub + j) * dsub, dsub);
+                }
+            }
             for (int64_t r = ivf->list_off[key]; r < ivf->list_off[key + 1]; r++) {
                 if (selmask && !selmask[r]) continue;
-                const float* y = (const float*)(ivf->codes + (size_t)r * ivf->code_size);
-                const float dis = ref_dist_(xi, y, d, l2);
+                float dis;
+                if (M) {
+                    const uint8_t* code = ivf->codes + (size_t)r * ivf->code_size;
+                    float acc = 0.f;
+                    for (int m = 0; m < M; m++) acc += sim[m * ksub + code[m]];
+                    dis = dis0 + acc;
+                } else {
+                    const float* y = (const float*)(ivf->codes + (size_t)r * ivf->code_size);
+                    dis = ref_dist_(xi, y, d, l2);
+                }
                 if (l2 ? (dis < radius) : (radius < dis)) {
                     if (tot < cap) {
                         D[tot] = dis;
@@ -739,5 +784,8 @@ int64_t oracle_ivf_range_preassigned(const oracle_ivf_t* ivf, size_t n, const fl
         }
     }
     lims[n] = (size_t)tot;
+    free(sim);
+    free(sim2);
+    free(resid);
     return tot;
 }

@@ -128,10 +128,12 @@ void oracle_merge_knn_results(size_t n, size_t k, int nshard, const float* all_d
 
 int oracle_max_threads(void);
 
-/* IVF-Flat range search restated (faiss/IndexIVF.cpp:1243-1400,
- * faiss/IndexIVFFlat.cpp:181-201); returns the number of results */
+/* IVF range search restated (faiss/IndexIVF.cpp:1243-1400,
+ * faiss/IndexIVFFlat.cpp:181-201, faiss/IndexIVFPQ.cpp:1254-1279); returns
+ * the number of results; coarse_dis used by PQ table 1 only */
 int64_t oracle_ivf_range_preassigned(const oracle_ivf_t* ivf, size_t n, const float* x,
-                                     size_t nprobe, const int64_t* keys, float radius,
+                                     size_t nprobe, const int64_t* keys,
+                                     const float* coarse_dis, float radius,
                                      const uint8_t* selmask, size_t* lims, float* D, int64_t* I,
                                      int64_t cap);
 

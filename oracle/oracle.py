@@ -66,8 +66,8 @@ def lib():
         L.oracle_merge_knn_results.argtypes = [C.c_size_t, C.c_size_t, C.c_int, _P, _P, _P, _P,
                                                C.c_int]
         L.oracle_ivf_range_preassigned.argtypes = [C.POINTER(IVFStruct), C.c_size_t, _P,
-                                                   C.c_size_t, _P, C.c_float, _P, _P, _P, _P,
-                                                   C.c_int64]
+                                                   C.c_size_t, _P, _P, C.c_float, _P, _P, _P,
+                                                   _P, C.c_int64]
         L.oracle_ivf_range_preassigned.restype = C.c_int64
         L.oracle_max_threads.restype = C.c_int
         _lib = L
@@ -238,15 +238,18 @@ class IVFOracle:
                                                nthreads or nthreads_default())
         return (D, I, int(nd[0])) if return_ndis else (D, I)
 
-    def range_search_preassigned(self, x, radius, keys, selmask=None):
-        """IVF-Flat range search (faiss/IndexIVF.cpp:1243-1400): (lims, D, I).
-        selmask: per concatenated row uint8 membership (IDSelector), or None."""
+    def range_search_preassigned(self, x, radius, keys, selmask=None, coarse_dis=None):
+        """IVF range search (faiss/IndexIVF.cpp:1243-1400): (lims, D, I).
+        selmask: per concatenated row uint8 membership (IDSelector), or None;
+        coarse_dis: [n, nprobe] (IVF-PQ with precomputed tables)."""
         x = np.ascontiguousarray(x, np.float32)
         keys = np.ascontiguousarray(keys, np.int64)
         n, nprobe = keys.shape
+        cd = (np.zeros((n, nprobe), np.float32) if coarse_dis is None
+              else np.ascontiguousarray(coarse_dis, np.float32))
         lims = np.zeros(n + 1, np.uint64)
         sm = None if selmask is None else np.ascontiguousarray(selmask, np.uint8)
-        args = (C.byref(self.s), n, _p(x), nprobe, _p(keys), float(radius),
+        args = (C.byref(self.s), n, _p(x), nprobe, _p(keys), _p(cd), float(radius),
                 _p(sm) if sm is not None else None, _p(lims))
         tot = lib().oracle_ivf_range_preassigned(*args, None, None, 0)
         D = np.empty(tot, np.float32)

@@ -139,9 +139,46 @@ def test_range_search_stats(amd, orc, flat_ix):
     assert st.ndis == int(sizes[keys].sum())
 
 
-def test_range_search_pq_not_supported(amd, orc, gpu):
+@pytest.fixture(scope="module")
+def pq_ix(amd, orc, gpu):
+    xb = rand(orc, 8000, 64, 101)
+    idx = amd.index_factory(64, "IVF32,PQ16")
+    idx.train(xb)
+    idx.add(xb)
+    return idx
+
+
+@pytest.mark.parametrize("table", [1, 0])
+def test_range_search_pq_bit_exact(amd, orc, pq_ix, table):
+    # IVFPQScanner::scan_codes_range (IndexIVFPQ.cpp:1254-1279): the k-NN
+    # path's table arithmetic, kept when dis < radius, in scan order
+    idx = pq_ix
+    xq = rand(orc, 200, 64, 102)
+    idx.nprobe = 6
+    idx.use_precomputed_table = table
+    try:
+        D, _ = idx.search(xq, 20)
+        r = float(np.median(D[:, -1]))
+        Dq, Iq = idx.quantizer.search(xq, 6)
+        got_pre = idx.range_search_preassigned(xq, r, Iq, Dq)
+        got = idx.range_search(xq, r)
+        sel = amd.IDSelectorRange(1000, 5000)
+        got_sel = idx.range_search(xq, r, amd.SearchParametersIVF(nprobe=6, sel=sel))
+    finally:
+        idx.use_precomputed_table = 1
+    ref = orc.IVFOracle.from_index(idx)
+    ref.s.use_precomputed_table = table
+    want = ref.range_search_preassigned(xq, r, Iq, coarse_dis=Dq)
+    check_equal(got_pre, want)
+    check_equal(got, want)
+    assert want[0][-1] > 200
+    mask = ((ref.ids >= 1000) & (ref.ids < 5000)).astype(np.uint8)
+    check_equal(got_sel, ref.range_search_preassigned(xq, r, Iq, selmask=mask, coarse_dis=Dq))
+
+
+def test_range_search_pq_ip_not_supported(amd, orc, gpu):
     xb = rand(orc, 3000, D_, 100)
-    idx = amd.index_factory(D_, "IVF16,PQ8")
+    idx = amd.index_factory(D_, "IVF16,PQ8", amd.METRIC_INNER_PRODUCT)
     idx.train(xb)
     idx.add(xb)
     with pytest.raises(amd.FaissError):
