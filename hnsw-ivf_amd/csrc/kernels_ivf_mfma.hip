@@ -96,7 +96,9 @@ __global__ void k_split_bf16(const float* __restrict__ codes, int64_t rows, int 
 // past the list end get norm +inf (L2) / bias +inf (IP): their keys sort
 // after every real candidate and the epilogue drops them by row index.
 // Waves whose 32 query columns are all unused skip the MFMA and selection.
-template <bool L2, int KT, int NS, bool Y3>
+// HS: an IDSelector mask is present (a separate instantiation, so the
+// unfiltered hot path carries no mask loads or registers).
+template <bool L2, int KT, int NS, bool Y3, bool HS>
 __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         const float* __restrict__ x, int ldx, int d, const __bf16* __restrict__ cbf,
         const float* __restrict__ ynorm, const float* __restrict__ ynmax,
@@ -166,7 +168,7 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             if (!L2) v = make_float4(0.f, 0.f, 0.f, 0.f);
             // non-members of an IDSelector are treated as padding rows
             uchar4 ms = make_uchar4(1, 1, 1, 1);
-            if (sel && r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
+            if (HS && r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
             pn.x = r + 0 < nvn && ms.x ? v.x : WS_INF;
             pn.y = r + 1 < nvn && ms.y ? v.y : WS_INF;
             pn.z = r + 2 < nvn && ms.z ? v.z : WS_INF;
@@ -256,8 +258,8 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             const uint32_t ord = key & lowmask;
             const int r = (int)(ord & 15u);
             const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-            ko[i] = (key != 0xffffffffu && row < elen && (!sel || sel[row0 + row])) ? key
-                                                                                  : 0xffffffffu;
+            ko[i] = (key != 0xffffffffu && row < elen && (!HS || sel[row0 + row])) ? key
+                                                                                 : 0xffffffffu;
         }
         if (slot == 0) {
             // the list's largest margin bounds every kept row's margin:
@@ -948,7 +950,9 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     // 32-bit keys' truncation (2^(obits-23) relative) is bracketed by the
     // decode (low bits cleared / set).
     const char* prec = getenv("FAISS_AMD_IVF_PREC");
-    const bool y3 = prec && !strcmp(prec, "bf16x3");
+    // bf16x3 only without a selector (the selector variant is built for the
+    // bf16x2 filter; both give the certified exact result)
+    const bool y3 = prec && !strcmp(prec, "bf16x3") && !b.sel;
     // FAISS_AMD_FILTER_TRACE=<file>: per-work-item timestamps (profiling)
     static unsigned long long* ftrace_buf = nullptr;
     static int64_t ftrace_n = 0;
@@ -968,13 +972,18 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         ScopedKernelTimer tm(kt, "ivf_flat_scan", 0.0, s);
 #define LAUNCH_NS(L2V, KTV, NSV)                                                              \
     do {                                                                                      \
-        if (y3)                                                                               \
-            k_ivf_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+        if (b.sel)                                                                            \
+            k_ivf_bf3_filter<L2V, KTV, NSV, false, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+                    x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
+                    list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
+                    b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, b.sel, keys, recs, ftrace);    \
+        else if (y3)                                                                          \
+            k_ivf_bf3_filter<L2V, KTV, NSV, true, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
                     b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, b.sel, keys, recs, ftrace);    \
         else                                                                                  \
-            k_ivf_bf3_filter<L2V, KTV, NSV, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(\
+            k_ivf_bf3_filter<L2V, KTV, NSV, false, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(\
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
                     b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, b.sel, keys, recs, ftrace);    \

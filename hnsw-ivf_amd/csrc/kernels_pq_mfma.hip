@@ -134,7 +134,8 @@ __device__ __forceinline__ void pq_decode_frags(const uint32_t (&cw)[NWC], int l
 // One work item = (list, <= 64 queries); persistent work-groups walk the
 // items with stride gridDim.x, so the LDS decode table is loaded once per
 // work-group.  Wave layout, keys, streams and outputs as k_ivf_bf3_filter.
-template <int DSUB, int NS, int KT>
+// HS: an IDSelector mask is present (own instantiation; none on the hot path)
+template <int DSUB, int NS, int KT, bool HS>
 __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
         const float* __restrict__ x, int ldx, const __bf16* __restrict__ dec_g,
         const uint8_t* __restrict__ codes, const float* __restrict__ terms,
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
                 // non-members of an IDSelector are treated as padding rows
                 uchar4 ms = make_uchar4(1, 1, 1, 1);
-                if (sel && r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
+                if (HS && r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
                 tn.x = r + 0 < nvn && ms.x ? v.x : WS_INF;
                 tn.y = r + 1 < nvn && ms.y ? v.y : WS_INF;
                 tn.z = r + 2 < nvn && ms.z ? v.z : WS_INF;
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
             for (int i = 0; i < KT; i++) {
                 const uint32_t key = tq.q[i];
                 const uint32_t row = ivf_key_row(key, lowmask, slot);
-                ko[i] = (key != 0xffffffffu && row < elen && (!sel || sel[row0 + row]))
+                ko[i] = (key != 0xffffffffu && row < elen && (!HS || sel[row0 + row]))
                                 ? key
                                 : 0xffffffffu;
             }
@@ -335,13 +336,14 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
     const float coef = (float)ivfpq_mfma_coef(d, M);
 #define PQF(DS, NSV, KTV)                                                                      \
     if (dsub == DS && NS == NSV && KE / 4 == KTV) {                                            \
-        auto kfn = k_ivfpq_filter<DS, NSV, KTV>;                                               \
-        static bool attr = false;                                                              \
-        if (!attr) {                                                                           \
+        auto kfn = b.sel ? k_ivfpq_filter<DS, NSV, KTV, true>                                  \
+                         : k_ivfpq_filter<DS, NSV, KTV, false>;                                 \
+        static bool attr[2] = {false, false};                                                  \
+        if (!attr[b.sel ? 1 : 0]) {                                                            \
             HIP_CHECK(hipFuncSetAttribute((const void*)kfn,                                    \
                                           hipFuncAttributeMaxDynamicSharedMemorySize,          \
                                           (int)lds));                                          \
-            attr = true;                                                                       \
+            attr[b.sel ? 1 : 0] = true;                                                        \
         }                                                                                      \
         kfn<<<dim3((unsigned)grid), dim3(256), lds, s>>>(                                      \
                 x, ldx, (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, nlist,    \
