@@ -166,13 +166,20 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             // rows < roundup(len, 16) are inside the list's arena slot
             float4 v = r < nvn ? *(const float4*)(ynl + v0n + r) : make_float4(0.f, 0.f, 0.f, 0.f);
             if (!L2) v = make_float4(0.f, 0.f, 0.f, 0.f);
-            // non-members of an IDSelector are treated as padding rows
-            uchar4 ms = make_uchar4(1, 1, 1, 1);
-            if (HS && r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
-            pn.x = r + 0 < nvn && ms.x ? v.x : WS_INF;
-            pn.y = r + 1 < nvn && ms.y ? v.y : WS_INF;
-            pn.z = r + 2 < nvn && ms.z ? v.z : WS_INF;
-            pn.w = r + 3 < nvn && ms.w ? v.w : WS_INF;
+            if constexpr (HS) {
+                // non-members of an IDSelector are treated as padding rows
+                uchar4 ms = make_uchar4(1, 1, 1, 1);
+                if (r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
+                pn.x = r + 0 < nvn && ms.x ? v.x : WS_INF;
+                pn.y = r + 1 < nvn && ms.y ? v.y : WS_INF;
+                pn.z = r + 2 < nvn && ms.z ? v.z : WS_INF;
+                pn.w = r + 3 < nvn && ms.w ? v.w : WS_INF;
+            } else {
+                pn.x = r + 0 < nvn ? v.x : WS_INF;
+                pn.y = r + 1 < nvn ? v.y : WS_INF;
+                pn.z = r + 2 < nvn ? v.z : WS_INF;
+                pn.w = r + 3 < nvn ? v.w : WS_INF;
+            }
         }
     };
     auto stash = [&](int buf) {
@@ -258,8 +265,10 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             const uint32_t ord = key & lowmask;
             const int r = (int)(ord & 15u);
             const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-            ko[i] = (key != 0xffffffffu && row < elen && (!HS || sel[row0 + row])) ? key
-                                                                                 : 0xffffffffu;
+            if constexpr (HS)
+                ko[i] = (key != 0xffffffffu && row < elen && sel[row0 + row]) ? key : 0xffffffffu;
+            else
+                ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
         }
         if (slot == 0) {
             // the list's largest margin bounds every kept row's margin:

@@ -207,13 +207,20 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
                 // rows < roundup(len, 16) are inside the list's arena slot
                 const float4 v = r < nvn ? *(const float4*)(terms + row0 + v0n + r)
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
-                // non-members of an IDSelector are treated as padding rows
-                uchar4 ms = make_uchar4(1, 1, 1, 1);
-                if (HS && r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
-                tn.x = r + 0 < nvn && ms.x ? v.x : WS_INF;
-                tn.y = r + 1 < nvn && ms.y ? v.y : WS_INF;
-                tn.z = r + 2 < nvn && ms.z ? v.z : WS_INF;
-                tn.w = r + 3 < nvn && ms.w ? v.w : WS_INF;
+                if constexpr (HS) {
+                    // non-members of an IDSelector are treated as padding rows
+                    uchar4 ms = make_uchar4(1, 1, 1, 1);
+                    if (r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
+                    tn.x = r + 0 < nvn && ms.x ? v.x : WS_INF;
+                    tn.y = r + 1 < nvn && ms.y ? v.y : WS_INF;
+                    tn.z = r + 2 < nvn && ms.z ? v.z : WS_INF;
+                    tn.w = r + 3 < nvn && ms.w ? v.w : WS_INF;
+                } else {
+                    tn.x = r + 0 < nvn ? v.x : WS_INF;
+                    tn.y = r + 1 < nvn ? v.y : WS_INF;
+                    tn.z = r + 2 < nvn ? v.z : WS_INF;
+                    tn.w = r + 3 < nvn ? v.w : WS_INF;
+                }
             }
         };
         load_codes(0);
@@ -281,9 +288,11 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
             for (int i = 0; i < KT; i++) {
                 const uint32_t key = tq.q[i];
                 const uint32_t row = ivf_key_row(key, lowmask, slot);
-                ko[i] = (key != 0xffffffffu && row < elen && (!HS || sel[row0 + row]))
-                                ? key
-                                : 0xffffffffu;
+                if constexpr (HS)
+                    ko[i] = (key != 0xffffffffu && row < elen && sel[row0 + row]) ? key
+                                                                                  : 0xffffffffu;
+                else
+                    ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
             }
             if (slot == 0) {
                 const float xl = sqrtf(xn);
