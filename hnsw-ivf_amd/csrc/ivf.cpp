@@ -249,6 +249,19 @@ void IndexIVF::sync_device() const {
     dirty_ = false;
 }
 
+uint32_t* IndexIVF::bucket_counts(hipStream_t s, uint32_t** next) const {
+    // two halves of nlist counters; a (re)allocation starts both at zero
+    const size_t need = sizeof(uint32_t) * 2 * std::max<size_t>(nlist, 1);
+    if (!s_counts_.ptr || s_counts_.bytes < need) {
+        s_counts_.reserve(need);
+        HIP_CHECK(hipMemsetAsync(s_counts_.ptr, 0, need, s));
+        counts_parity_ = 0;
+    }
+    uint32_t* base = s_counts_.as<uint32_t>();
+    *next = base + (size_t)(1 - counts_parity_) * nlist;
+    return base + (size_t)counts_parity_ * nlist;
+}
+
 void IndexIVF::quantize_device(idx_t n, const float* x, int ldx, int np, float* coarse_dis,
                                int32_t* assign, const SearchParameters* qparams,
                                hipStream_t s) const {
@@ -586,13 +599,15 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     std::lock_guard<std::recursive_mutex> g(mu_);
     const int QT = 64;
     const int l = (int)roundup((size_t)d, 4);
-    s_counts_.reserve(sizeof(uint32_t) * nlist);
+    uint32_t* counts_next = nullptr;
+    uint32_t* counts = bucket_counts(s, &counts_next);
     s_cur_.reserve(sizeof(uint32_t) * std::max<idx_t>(n * np, 1));
     s_boff_.reserve(sizeof(uint32_t) * (nlist + 1));
     s_ioff_.reserve(sizeof(uint32_t) * (nlist + 1));
     s_ent_.reserve(sizeof(uint32_t) * n * np);
-    kern::IVFBuckets b{s_counts_.as<uint32_t>(), s_boff_.as<uint32_t>(), s_ioff_.as<uint32_t>(),
+    kern::IVFBuckets b{counts, s_boff_.as<uint32_t>(), s_ioff_.as<uint32_t>(),
                        s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
+    b.counts_next = counts_next;
     b.lim = lim;
     b.sel = sel;
     const char* env = getenv("FAISS_AMD_IVF_SCAN");
@@ -615,6 +630,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     }
     kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), d_list_off_.as<uint32_t>(),
                      (int)nlist, QT, b, s);
+    flip_counts();
     const int64_t max_items = kern::ivf_max_items(n, np, (int)nlist, QT);
     const bool l2 = metric_type == METRIC_L2;
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(n, 4));
@@ -823,13 +839,15 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
     if (!lut && pq_mfma_ready_ && kern::ivfpq_mfma_eligible(d, (int)pq.M, (int)k, np)) {
         std::lock_guard<std::recursive_mutex> g(mu_);
         const int QT = 64;
-        s_counts_.reserve(sizeof(uint32_t) * nlist);
+        uint32_t* counts_next = nullptr;
+        uint32_t* counts = bucket_counts(s, &counts_next);
         s_cur_.reserve(sizeof(uint32_t) * std::max<idx_t>(n * np, 1));
         s_boff_.reserve(sizeof(uint32_t) * (nlist + 1));
         s_ioff_.reserve(sizeof(uint32_t) * (nlist + 1));
         s_ent_.reserve(sizeof(uint32_t) * n * np);
-        kern::IVFBuckets b{s_counts_.as<uint32_t>(), s_boff_.as<uint32_t>(),
-                           s_ioff_.as<uint32_t>(), s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
+        kern::IVFBuckets b{counts, s_boff_.as<uint32_t>(), s_ioff_.as<uint32_t>(),
+                           s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
+        b.counts_next = counts_next;
         b.lim = lim;
         b.sel = sel;
         const int KE = kern::ivf_mfma_kq((int)k, d);
@@ -845,6 +863,7 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         b.item_entries = s_ient_.as<uint32_t>();
         kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), d_list_off_.as<uint32_t>(),
                          (int)nlist, QT, b, s);
+        flip_counts();
         const bool dbg = getenv("FAISS_AMD_IVF_STATS") != nullptr;
         s_pflags_.reserve(4 * sizeof(uint32_t));
         if (dbg) HIP_CHECK(hipMemsetAsync(s_pflags_.ptr, 0, 4 * sizeof(uint32_t), s));

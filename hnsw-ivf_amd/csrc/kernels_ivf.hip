@@ -93,7 +93,8 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
                                                       int nlist, int QT,
                                                       uint32_t* __restrict__ bucket_off,
                                                       uint32_t* __restrict__ item_off,
-                                                      uint32_t* __restrict__ item_list) {
+                                                      uint32_t* __restrict__ item_list,
+                                                      uint32_t* __restrict__ zero_next) {
     __shared__ uint32_t wb[16], wi[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint32_t carry_b = 0, carry_i = 0;
@@ -104,6 +105,7 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             c[j] = l0 + j < nlist ? counts[l0 + j] : 0u;
+            if (zero_next && l0 + j < nlist) zero_next[l0 + j] = 0u;
             n[j] = (c[j] + QT - 1) / QT;
             sb += c[j];
             si += n[j];
@@ -274,7 +276,7 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
                 const uint32_t* list_off, int nlist, int QT, IVFBuckets b, hipStream_t s) {
     int64_t total = n * nprobe;
     FAISS_THROW_IF_NOT_MSG(total < (1ll << 32), "n * nprobe must fit in 32 bits");
-    HIP_CHECK(hipMemsetAsync(b.counts, 0, sizeof(uint32_t) * nlist, s));
+    if (!b.counts_next) HIP_CHECK(hipMemsetAsync(b.counts, 0, sizeof(uint32_t) * nlist, s));
     if (total > 0) {
         const int nr = (int)cdiv(nlist, BC_MAXL);  // list ranges (LDS histogram each)
         k_bucket_count_lds<<<dim3((unsigned)cdiv(total, 1024 * BC_PER), (unsigned)nr), dim3(1024),
@@ -283,7 +285,7 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
         HIP_LAUNCH_CHECK();
     }
     k_bucket_scan<<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off, b.item_off,
-                                                 b.item_list);
+                                                 b.item_list, b.counts_next);
     HIP_LAUNCH_CHECK();
     if (total > 0) {
         k_bucket_fill<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(

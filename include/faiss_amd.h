@@ -427,6 +427,11 @@ struct IndexIVF : Index {
             s_pk1_, s_pk2_, s_q_;
     mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_,
             s_selmask_;
+    // bucket counts of this call (zero) and the half the call's scan clears
+    // for the next one; flip_counts() after the bucket kernels are queued
+    uint32_t* bucket_counts(hipStream_t s, uint32_t** next) const;
+    void flip_counts() const { counts_parity_ ^= 1; }
+    mutable int counts_parity_ = 0;
     // one pass of the range scan (counts when offs == nullptr, else fill);
     // cdis = coarse distances [n][np] on the device (PQ table 1 dis0)
     virtual void range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
