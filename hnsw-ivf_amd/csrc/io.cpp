@@ -176,21 +176,18 @@ void write_invlists(const ArrayInvertedLists* il, Writer& w) {
         return;
     }
     if (il->map && il->map_ondisk) {
-        // lists still live in an `ilod` data file: write its metadata again
-        std::vector<size_t> lists(3 * il->nlist, 0);
-        for (size_t l = 0; l < il->nlist; l++) {
-            const size_t n = il->map_sizes[l];
-            if (!n) continue;
-            const size_t o = (size_t)(il->map_codes[l] - il->map->ptr);
-            const size_t cap = il->code_size
-                                   ? (size_t)((const uint8_t*)il->map_ids[l] - il->map_codes[l]) /
-                                         il->code_size
-                                   : n;
-            lists[3 * l] = n;
-            lists[3 * l + 1] = cap;
-            lists[3 * l + 2] = o;
-        }
-        write_ilod(il, w, il->map->name, lists, il->map->size);
+        // lists still live in an `ilod` data file: write its metadata back
+        FAISS_THROW_IF_NOT(il->ondisk_lists.size() == 3 * il->nlist);
+        w.one(fourcc("ilod"));
+        w.one<size_t>(il->nlist);
+        w.one<size_t>(il->code_size);
+        w.one<size_t>(il->nlist);
+        w.bytes(il->ondisk_lists.data(), sizeof(size_t) * il->ondisk_lists.size());
+        w.one<size_t>(il->ondisk_slots.size() / 2);
+        w.bytes(il->ondisk_slots.data(), sizeof(size_t) * il->ondisk_slots.size());
+        std::vector<char> fn(il->map->name.begin(), il->map->name.end());
+        w.vec(fn);
+        w.one<size_t>(il->ondisk_totsize);
         return;
     }
     w.one(fourcc("ilar"));
@@ -307,6 +304,9 @@ void read_invlists(ArrayInvertedLists* il, Reader& r, size_t nlist, size_t code_
         }
         il->map = m;
         il->map_ondisk = true;
+        il->ondisk_lists = std::move(lists);
+        il->ondisk_slots = std::move(slots);
+        il->ondisk_totsize = totsize;
         return;
     }
     FAISS_THROW_IF_NOT_MSG(h == fourcc("ilar"),

@@ -45,6 +45,8 @@ void ArrayInvertedLists::materialize() {
     }
     map.reset();
     map_ondisk = false;
+    ondisk_lists.clear();
+    ondisk_slots.clear();
     map_codes.clear();
     map_ids.clear();
     map_sizes.clear();
@@ -59,6 +61,8 @@ void ArrayInvertedLists::add_entries(size_t l, size_t n, const idx_t* ids_in,
 void ArrayInvertedLists::reset() {
     map.reset();
     map_ondisk = false;
+    ondisk_lists.clear();
+    ondisk_slots.clear();
     map_codes.clear();
     map_ids.clear();
     map_sizes.clear();

@@ -320,6 +320,10 @@ struct ArrayInvertedLists {
     std::vector<const idx_t*> map_ids;
     std::vector<size_t> map_sizes;
     bool map_ondisk = false;  // mapping is an `ilod` data file (written back as `ilod`)
+    // `ilod` metadata as read: (size, capacity, offset) per list and the
+    // free-slot table (offset, capacity), written back verbatim
+    std::vector<size_t> ondisk_lists, ondisk_slots;
+    size_t ondisk_totsize = 0;
     ArrayInvertedLists(size_t nlist, size_t code_size);
     bool is_mapped() const { return (bool)map; }
     size_t list_size(size_t l) const { return map ? map_sizes[l] : ids[l].size(); }
