@@ -285,7 +285,13 @@ void read_invlists(ArrayInvertedLists* il, Reader& r, size_t nlist, size_t code_
         // is mapped in every case.
         int fd = open(filename.c_str(), O_RDONLY);
         FAISS_THROW_IF_NOT_MSG(fd >= 0, "could not open on-disk inverted lists " + filename);
-        auto m = std::make_shared<MappedFile>(fd, filename);
+        std::shared_ptr<MappedFile> m;
+        try {
+            m = std::make_shared<MappedFile>(fd, filename);
+        } catch (...) {
+            close(fd);
+            throw;
+        }
         close(fd);
         FAISS_THROW_IF_NOT_MSG(m->size >= totsize || totsize == 0,
                                "on-disk inverted lists file shorter than totsize");
