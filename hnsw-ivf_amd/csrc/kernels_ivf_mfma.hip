@@ -38,6 +38,7 @@
 #include "kernels.h"
 #include "wave_select.h"
 #include "exact_select.h"
+#include "pq_ref.h"
 #include "ref_arith.h"
 #include "bf3.h"
 
@@ -416,26 +417,25 @@ __device__ __forceinline__ float eval_rows64(const float* xr /* LDS copy of the 
     return out;
 }
 
-// IVF-PQ exact distance of the code at arena row `grow`, probe list l, with
-// the reference's own table arithmetic (oracle_ivf_search_preassigned, i.e.
-// faiss/IndexIVFPQ.cpp:560-566 / 634-700, precomputed table :413-430,
-// distance_single_code code_distance-generic.h:16-79):
-//   table 1: dis0 = coarse_dis, sim = fmaf(-2, <x_m, c>, fmaf(2, <y_C,m, c>, |c|^2))
+// IVF-PQ exact distance of the code at arena row `grow`, probe list l, in the
+// reference's own arithmetic (pq_ref.h; faiss/IndexIVFPQ.cpp:604-700 tables,
+// :861-933 scan, code_distance-avx2.h sum order):
+//   table 1: dis0 = coarse_dis, sim = fma(-2, <x_m, c>, fma(2, <y_C,m, c>, |c|^2))
 //   table 0: dis0 = 0, sim = |(x - y_C)_m - c|^2
-// dis = dis0 + (((0 + sim_0) + sim_1) + ...), every small product in the
-// fvec order of ref_arith.h.  xs: the query (LDS).
+// with the table entries in the fvec_*_ny order and the code sum in the
+// distance_four_codes order.  xs: the query (LDS or global).
 template <int PQD>
 __device__ __forceinline__ float pq_sim(const PQArgs& pa, const float* xm, const float* ym,
                                         const float* c) {
     if (pa.table1) {
-        const float s2 = ref_ip(xm, c, PQD);
-        const float P = fmaf(2.f, ref_ip(ym, c, PQD), ref_norm(c, PQD));
+        const float s2 = ny_entry_c<false, PQD>(xm, c);
+        const float P = fmaf(2.f, ny_entry_c<false, PQD>(ym, c), ref_norm(c, PQD));
         return fmaf(-2.f, s2, P);
     }
-    __attribute__((aligned(16))) float rr[PQD];
+    float rr[PQD];
 #pragma unroll
     for (int i = 0; i < PQD; i++) rr[i] = xm[i] - ym[i];
-    return ref_l2(rr, c, PQD);
+    return ny_entry_c<true, PQD>(rr, c);
 }
 
 template <int PQD>
@@ -443,40 +443,36 @@ __device__ __forceinline__ float pq_exact(const PQArgs& pa, const float* xs, uin
                                           uint32_t l, float d0) {
     const uint8_t* cp = pa.codes + (size_t)grow * pa.cs;
     const float* yc = pa.cent + (size_t)l * pa.ldcent;
-    float acc = 0.f;
-    // UB subquantizers per step (32 centroid + coarse floats in flight):
-    // their code bytes and rows are loaded together, then summed in m order
-    constexpr int UB = PQD == 2 ? 8 : PQD == 4 ? 4 : 2;
+    const int M = pa.M;
+    const int m16 = pq_lane_span(M);
+    float p[8], r = 0.f;
     int m0 = 0;
-    for (; m0 + UB <= pa.M; m0 += UB) {
-        // code rows are 4-B aligned (cs is a multiple of 4, m0 of UB)
-        uint32_t cb[(UB + 3) / 4];
-        if constexpr (UB >= 4) {
+    // blocks of 8 sub-quantizers: their code bytes, centroid rows and coarse
+    // rows are loaded together (code rows are 4-B aligned, m0 % 8 == 0)
+    for (; m0 + 8 <= M; m0 += 8) {
+        const uint32_t w0 = *(const uint32_t*)(cp + m0), w1 = *(const uint32_t*)(cp + m0 + 4);
+        float t[8];
 #pragma unroll
-            for (int i = 0; i < UB / 4; i++) cb[i] = *(const uint32_t*)(cp + m0 + 4 * i);
+        for (int u = 0; u < 8; u++) {
+            const uint32_t j = ((u < 4 ? w0 : w1) >> (8 * (u & 3))) & 0xffu;
+            const int m = m0 + u;
+            t[u] = pq_sim<PQD>(pa, xs + m * PQD, yc + m * PQD,
+                               pa.pq_cent + ((size_t)m * 256 + j) * PQD);
+        }
+        if (m0 < m16) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) p[u] = m0 == 0 ? t[u] : p[u] + t[u];
+            if (m0 + 8 == m16) r = reduce8(p);
         } else {
-            cb[0] = (uint32_t)cp[m0] | ((uint32_t)cp[m0 + 1] << 8);
+#pragma unroll
+            for (int u = 0; u < 8; u++) r += t[u];
         }
-        __attribute__((aligned(16))) float cv[UB][PQD];
-        __attribute__((aligned(16))) float yv[UB][PQD];
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const uint32_t j = (cb[u >> 2] >> (8 * (u & 3))) & 0xffu;
-            const float* c = pa.pq_cent + ((size_t)(m0 + u) * 256 + j) * PQD;
-#pragma unroll
-            for (int i = 0; i < PQD; i++) {
-                cv[u][i] = c[i];
-                yv[u][i] = yc[(m0 + u) * PQD + i];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < UB; u++) acc += pq_sim<PQD>(pa, xs + (m0 + u) * PQD, yv[u], cv[u]);
     }
-    for (int m = m0; m < pa.M; m++) {
+    for (int m = m0; m < M; m++) {
         const int j = cp[m];
-        acc += pq_sim<PQD>(pa, xs + m * PQD, yc + m * PQD, pa.pq_cent + ((size_t)m * 256 + j) * PQD);
+        r += pq_sim<PQD>(pa, xs + m * PQD, yc + m * PQD, pa.pq_cent + ((size_t)m * 256 + j) * PQD);
     }
-    return (pa.table1 ? d0 : 0.f) + acc;
+    return (pa.table1 ? d0 : 0.f) + r;
 }
 
 template <bool L2, int PQD = 0>

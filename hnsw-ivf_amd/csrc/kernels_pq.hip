@@ -18,6 +18,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "pq_ref.h"
 #include "wave_select.h"
 
 namespace faiss_amd {
@@ -403,40 +404,72 @@ void ivfpq_terms(const uint8_t* codes, const uint32_t* row_list, int64_t nrows,
 }
 
 // ---------------------------------------------------------------- encode
-// thread per (vector, sub-quantizer); the 256 sub-centroids of m are staged in
-// LDS by the workgroup (blockIdx.y = m).
+// ProductQuantizer::compute_codes for dsub < 16 (faiss/impl/ProductQuantizer.cpp:
+// 398-427 -> compute_code :195-271): per sub-quantizer the nearest of the ksub
+// centroids by fvec_L2sqr_ny_nearest (faiss/utils/distances_simd.cpp:2298-2317).
+//   dsub 2 / 4 / 8: the AVX2 fvec_L2sqr_ny_nearest_D{2,4,8} (:1908-2271):
+//     distances in the ny fma-chain order; 8 lanes (j mod 8) keep their
+//     minimum with `old < new ? old : new` (an equal later distance takes the
+//     lane), then lanes 0..7 are scanned with a strict `>`.
+//   other dsub: fvec_L2sqr_ny (D1 / D12 kernels, else fvec_L2sqr order) and
+//     the first strict minimum.
+// dsub >= 16 takes the reference's BLAS branch (compute_distance_tables via
+// sgemm), whose order is MKL's; the fvec_L2sqr order is used there.
+// Thread per (vector, sub-quantizer); the sub-centroids of m live in LDS.
+template <int DS>
 __global__ __launch_bounds__(256) void k_pq_encode(const float* __restrict__ x, int ldx,
                                                    int64_t n, const int32_t* __restrict__ assign,
                                                    const float* __restrict__ cent, int ldcent,
                                                    const float* __restrict__ pq_cent, int M,
-                                                   int ksub, int dsub,
-                                                   uint8_t* __restrict__ codes, int code_stride) {
-    extern __shared__ float cs[];  // [ksub * dsub]
+                                                   int ksub, uint8_t* __restrict__ codes,
+                                                   int code_stride) {
+    extern __shared__ float cs[];  // [ksub * DS]
     const int m = blockIdx.y;
-    for (int e = threadIdx.x; e < ksub * dsub; e += 256)
-        cs[e] = pq_cent[(int64_t)m * ksub * dsub + e];
+    for (int e = threadIdx.x; e < ksub * DS; e += 256)
+        cs[e] = pq_cent[(int64_t)m * ksub * DS + e];
     __syncthreads();
-    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    float r[32];
-    const int dd = dsub < 32 ? dsub : 32;
-    for (int j = 0; j < dd; j++) {
-        float v = x[i * ldx + m * dsub + j];
-        if (cent) v -= cent[(int64_t)assign[i] * ldcent + m * dsub + j];
+    float r[DS];
+#pragma unroll
+    for (int j = 0; j < DS; j++) {
+        float v = x[i * ldx + m * DS + j];
+        if (cent) v -= cent[(int64_t)assign[i] * ldcent + m * DS + j];
         r[j] = v;
     }
-    float best = WS_INF;
+    constexpr bool lanes = DS == 2 || DS == 4 || DS == 8;
     int bj = 0;
-    for (int j = 0; j < ksub; j++) {
-        const float* c = cs + j * dsub;
-        float s = 0.f;
-        for (int t = 0; t < dd; t++) {
-            float df = r[t] - c[t];
-            s = fmaf(df, df, s);
+    if constexpr (lanes) {
+        float lmin[8];
+        int lidx[8];
+#pragma unroll
+        for (int l = 0; l < 8; l++) {
+            lmin[l] = HUGE_VALF;
+            lidx[l] = 0;
         }
-        if (s < best) {
-            best = s;
-            bj = j;
+        for (int j0 = 0; j0 < ksub; j0 += 8)
+#pragma unroll
+            for (int l = 0; l < 8; l++) {
+                const float s = ny_entry_c<true, DS>(r, cs + (j0 + l) * DS);
+                const bool keep = lmin[l] < s;
+                lidx[l] = keep ? lidx[l] : j0 + l;
+                lmin[l] = keep ? lmin[l] : s;
+            }
+        float cur = HUGE_VALF;
+#pragma unroll
+        for (int l = 0; l < 8; l++)
+            if (cur > lmin[l]) {
+                cur = lmin[l];
+                bj = lidx[l];
+            }
+    } else {
+        float best = HUGE_VALF;
+        for (int j = 0; j < ksub; j++) {
+            const float s = ny_entry<true>(r, cs + j * DS, DS);
+            if (s < best) {
+                best = s;
+                bj = j;
+            }
         }
     }
     codes[i * code_stride + m] = (uint8_t)bj;
@@ -446,13 +479,25 @@ void pq_encode(const float* x, int ldx, int64_t n, const int32_t* assign, const 
                int ldcent, const float* pq_centroids, int M, int ksub, int dsub, uint8_t* codes,
                hipStream_t s) {
     if (n <= 0) return;
-    FAISS_THROW_IF_NOT_MSG(dsub <= 32, "dsub > 32 not supported on this path");
     FAISS_THROW_IF_NOT(ksub <= 256);
+    // the 8-lane argmin assumes whole 8-row groups (ksub = 256 for nbits = 8)
+    FAISS_THROW_IF_NOT(ksub % 8 == 0);
     const int code_stride = (int)roundup((size_t)M, 4);
-    k_pq_encode<<<dim3((unsigned)cdiv(n, 256), (unsigned)M), dim3(256),
-                  sizeof(float) * ksub * dsub, s>>>(x, ldx, n, assign, centroids, ldcent,
-                                                    pq_centroids, M, ksub, dsub, codes,
-                                                    code_stride);
+    const dim3 grid((unsigned)cdiv(n, 256), (unsigned)M);
+    const size_t lds = sizeof(float) * ksub * dsub;
+#define ENC(DS)                                                                             \
+    case DS:                                                                                \
+        k_pq_encode<DS><<<grid, dim3(256), lds, s>>>(x, ldx, n, assign, centroids, ldcent,  \
+                                                     pq_centroids, M, ksub, codes,          \
+                                                     code_stride);                          \
+        break;
+    switch (dsub) {
+        ENC(1) ENC(2) ENC(3) ENC(4) ENC(5) ENC(6) ENC(8) ENC(10) ENC(12) ENC(16) ENC(24)
+        ENC(32)
+        default:
+            FAISS_THROW_FMT("PQ encode: dsub = %d not supported on this path", dsub);
+    }
+#undef ENC
     HIP_LAUNCH_CHECK();
 }
 

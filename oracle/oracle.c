@@ -475,8 +475,163 @@ void oracle_hnsw_search(const oracle_hnsw_t* g, const float* x, size_t n, size_t
 }
 
 /* ------------------------------------------------------------ IVF-PQ */
+/* PQ table entries: fvec_inner_products_ny / fvec_L2sqr_ny
+ * (faiss/utils/distances_simd.cpp:1362-1410) as the AVX2 build compiles them:
+ * dsub 1: one rounded product; dsub 2/4/8: fvec_op_ny_D{2,4,8} AVX2
+ * specialisations (:579-702, :845-975, :1167-1341; ksub = 256 is a multiple of
+ * 8, so the 8-row transposed loop covers every row): acc = t0 (rounded), then
+ * acc = fma(., ., acc) over dims 1..dsub-1; dsub 12: fvec_op_ny_D12 (:1344-1360,
+ * three rounded 4-lane terms added per lane, then horizontal_sum); any other
+ * dsub: the _ref loops (:160-190), i.e. fvec_L2sqr / fvec_inner_product. */
+static float ny_term_(const float* x, const float* y, int dsub, int l2) {
+    switch (dsub) {
+        case 1: {
+            if (l2) {
+                const float t = x[0] - y[0];
+                return t * t;
+            }
+            return x[0] * y[0];
+        }
+        case 2:
+        case 4:
+        case 8: {
+            float acc;
+            if (l2) {
+                const float t = x[0] - y[0];
+                acc = t * t;
+            } else {
+                acc = x[0] * y[0];
+            }
+            for (int j = 1; j < dsub; j++) {
+                if (l2) {
+                    const float t = x[j] - y[j];
+                    acc = fmaf(t, t, acc);
+                } else {
+                    acc = fmaf(x[j], y[j], acc);
+                }
+            }
+            return acc;
+        }
+        case 12: {
+            float a[4];
+            for (int j = 0; j < 4; j++) {
+                float t0, t1, t2;
+                if (l2) {
+                    const float u0 = x[j] - y[j], u1 = x[4 + j] - y[4 + j], u2 = x[8 + j] - y[8 + j];
+                    t0 = u0 * u0, t1 = u1 * u1, t2 = u2 * u2;
+                } else {
+                    t0 = x[j] * y[j], t1 = x[4 + j] * y[4 + j], t2 = x[8 + j] * y[8 + j];
+                }
+                a[j] = (t0 + t1) + t2;
+            }
+            return (a[0] + a[2]) + (a[1] + a[3]);
+        }
+        default:
+            return ref_dist_(x, y, (size_t)dsub, l2);
+    }
+}
+float oracle_pq_ny_ip(const float* x, const float* y, int dsub) { return ny_term_(x, y, dsub, 0); }
+float oracle_pq_ny_l2(const float* x, const float* y, int dsub) { return ny_term_(x, y, dsub, 1); }
+
+/* distance_single_code / distance_four_codes with PQDecoder8 as the AVX2 build
+ * compiles them (faiss/impl/code_distance/code_distance-avx2.h:253-347,
+ * :383-530; both give the same value per code):
+ *   M = 4: horizontal_sum of the 4 gathered entries, (t0+t2)+(t1+t3) (:42-79);
+ *   M = 8: horizontal_sum of 8, ((t0+t4)+(t2+t6))+((t1+t5)+(t3+t7)) (:82-119);
+ *   M >= 16: 8 lanes, lane l accumulates t[16i+l] then t[16i+8+l] for each
+ *   16-block i in order, reduced as the M = 8 case; then the M % 16 leftover
+ *   entries are added one by one (:270-346);
+ *   other M < 16: 0 + t0 + t1 + ... in order. */
+float oracle_pq_code_sum(int M, const float* sim, int ksub, const uint8_t* code) {
+    if (M == 4) {
+        const float t0 = sim[code[0]], t1 = sim[ksub + code[1]];
+        const float t2 = sim[2 * ksub + code[2]], t3 = sim[3 * ksub + code[3]];
+        return (t0 + t2) + (t1 + t3);
+    }
+    float r = 0.f;
+    int m = 0;
+    if (M == 8 || M >= 16) {
+        float p[8];
+        for (int l = 0; l < 8; l++) p[l] = sim[(size_t)l * ksub + code[l]];
+        m = 8;
+        if (M != 8) {
+            const int m16 = M / 16 * 16;
+            for (; m < m16; m += 8)
+                for (int l = 0; l < 8; l++) p[l] += sim[(size_t)(m + l) * ksub + code[m + l]];
+        }
+        r = ((p[0] + p[4]) + (p[2] + p[6])) + ((p[1] + p[5]) + (p[3] + p[7]));
+    }
+    for (; m < M; m++) r += sim[(size_t)m * ksub + code[m]];
+    return r;
+}
+
+/* ProductQuantizer::compute_code for dsub < 16 (faiss/impl/ProductQuantizer.cpp:
+ * 195-271): fvec_L2sqr_ny_nearest per sub-quantizer.  dsub 2/4/8: the AVX2
+ * _D{2,4,8} kernels (faiss/utils/distances_simd.cpp:1908-2271): 8 lanes keep
+ * `old < new ? old : new` (an equal later distance takes the lane), lanes
+ * scanned 0..7 with a strict `>`; other dsub: fvec_L2sqr_ny + first strict
+ * minimum (:2298-2317, :125-140). */
+static int pq_nearest_(const float* x, const float* cent, int dsub, int ksub) {
+    if (dsub == 2 || dsub == 4 || dsub == 8) {
+        float lmin[8];
+        int lidx[8];
+        for (int l = 0; l < 8; l++) lmin[l] = HUGE_VALF, lidx[l] = 0;
+        for (int j = 0; j < ksub; j++) {
+            const float s = ny_term_(x, cent + (size_t)j * dsub, dsub, 1);
+            const int l = j & 7;
+            if (!(lmin[l] < s)) lmin[l] = s, lidx[l] = j;
+        }
+        float cur = HUGE_VALF;
+        int idx = 0;
+        for (int l = 0; l < 8; l++)
+            if (cur > lmin[l]) cur = lmin[l], idx = lidx[l];
+        return idx;
+    }
+    float best = HUGE_VALF;
+    int idx = 0;
+    for (int j = 0; j < ksub; j++) {
+        const float s = ny_term_(x, cent + (size_t)j * dsub, dsub, 1);
+        if (s < best) best = s, idx = j;
+    }
+    return idx;
+}
+
+/* IndexIVFPQ::encode_vectors (faiss/IndexIVFPQ.cpp:142-190): residual x - y_C
+ * (Index::compute_residual; zeros for list_no < 0) when by_residual, then
+ * compute_codes.  codes: [n][M] bytes. */
+void oracle_ivfpq_encode(const oracle_ivf_t* ivf, size_t n, const float* x,
+                         const int64_t* list_nos, uint8_t* codes) {
+    const int M = ivf->pq_M, ksub = 1 << ivf->pq_nbits, d = ivf->d, dsub = d / M;
+#pragma omp parallel
+    {
+        float* r = (float*)malloc(sizeof(float) * d);
+#pragma omp for
+        for (int64_t i = 0; i < (int64_t)n; i++) {
+            const float* xi = x + i * d;
+            if (ivf->by_residual) {
+                const int64_t key = list_nos[i];
+                if (key < 0) {
+                    memset(r, 0, sizeof(float) * d);
+                } else {
+                    const float* c = ivf->hnsw ? ivf->hnsw->storage + key * d
+                                               : ivf->centroids + key * d;
+                    for (int j = 0; j < d; j++) r[j] = xi[j] - c[j];
+                }
+            } else {
+                memcpy(r, xi, sizeof(float) * d);
+            }
+            for (int m = 0; m < M; m++)
+                codes[i * M + m] = (uint8_t)pq_nearest_(
+                        r + m * dsub, ivf->pq_centroids + (size_t)m * ksub * dsub, dsub, ksub);
+        }
+        free(r);
+    }
+}
+
 void oracle_ivfpq_prepare(oracle_ivf_t* ivf) {
-    /* faiss/IndexIVFPQ.cpp:380-406 decision, :408-432 table 1 */
+    /* faiss/IndexIVFPQ.cpp:380-406 decision, :408-432 table 1:
+     * P[key][m][j] = fvec_madd(r_norms, 2.0, <y_C,m, c_mj>) = fma(2, ip, |c_mj|^2)
+     * (fvec_madd AVX2, distances_simd.cpp:3292-3345, is one fma per entry) */
     const int M = ivf->pq_M, ksub = 1 << ivf->pq_nbits, d = ivf->d, dsub = d / M;
     ivf->use_precomputed_table = 0;
     if (!(ivf->metric == 1 && ivf->by_residual)) return;
@@ -495,13 +650,50 @@ void oracle_ivfpq_prepare(oracle_ivf_t* ivf) {
         float* tab = ivf->precomputed_table + (size_t)i * M * ksub;
         for (int m = 0; m < M; m++)
             for (int j = 0; j < ksub; j++) {
-                float ip = oracle_fvec_inner_product(
-                        c + m * dsub, ivf->pq_centroids + ((size_t)m * ksub + j) * dsub, dsub);
-                /* fvec_madd(n, r_norms, 2.0, tab, tab) */
+                const float ip =
+                        ny_term_(c + m * dsub, ivf->pq_centroids + ((size_t)m * ksub + j) * dsub, dsub, 0);
                 tab[m * ksub + j] = fmaf(2.f, ip, rn[m * ksub + j]);
             }
     }
     free(rn);
+}
+
+/* QueryTables (faiss/IndexIVFPQ.cpp:483-751) for one query: init_query
+ * (:545-566) fills sim2 (table 1: <x_m, c>) or sim (not by residual: the
+ * distance / inner-product table of x, also the IP table by residual). */
+static void pq_init_query_(const oracle_ivf_t* ivf, const float* xi, float* sim, float* sim2) {
+    const int M = ivf->pq_M, ksub = 1 << ivf->pq_nbits, dsub = ivf->d / M;
+    const int l2 = ivf->metric == 1;
+    for (int m = 0; m < M; m++)
+        for (int j = 0; j < ksub; j++) {
+            const float* c = ivf->pq_centroids + ((size_t)m * ksub + j) * dsub;
+            if (!l2)
+                sim[m * ksub + j] = ny_term_(xi + m * dsub, c, dsub, 0);
+            else if (!ivf->by_residual)
+                sim[m * ksub + j] = ny_term_(xi + m * dsub, c, dsub, 1);
+            else if (ivf->use_precomputed_table == 1)
+                sim2[m * ksub + j] = ny_term_(xi + m * dsub, c, dsub, 0);
+        }
+}
+/* precompute_list_tables (:604-700): returns dis0 and fills sim for list key */
+static float pq_set_list_(const oracle_ivf_t* ivf, const float* xi, int64_t key, float cdis,
+                          float* sim, const float* sim2, float* resid) {
+    const int M = ivf->pq_M, ksub = 1 << ivf->pq_nbits, d = ivf->d, dsub = d / M;
+    if (!ivf->by_residual) return 0.f;
+    const float* c = ivf->hnsw ? ivf->hnsw->storage + key * d : ivf->centroids + key * d;
+    if (ivf->metric != 1) /* precompute_list_tables_IP (:612-628) */
+        return oracle_fvec_inner_product(xi, c, d);
+    if (ivf->use_precomputed_table == 1) {
+        const float* P = ivf->precomputed_table + (size_t)key * M * ksub;
+        for (int e = 0; e < M * ksub; e++) sim[e] = fmaf(-2.f, sim2[e], P[e]);
+        return cdis;
+    }
+    for (int j = 0; j < d; j++) resid[j] = xi[j] - c[j]; /* Index::compute_residual */
+    for (int m = 0; m < M; m++)
+        for (int j = 0; j < ksub; j++)
+            sim[m * ksub + j] = ny_term_(resid + m * dsub,
+                                         ivf->pq_centroids + ((size_t)m * ksub + j) * dsub, dsub, 1);
+    return 0.f;
 }
 
 /* ------------------------------------------------------------ preassigned */
@@ -524,7 +716,6 @@ void oracle_ivf_search_preassigned_mc(const oracle_ivf_t* ivf, size_t n, const f
     const int d = ivf->d;
     const int M = ivf->pq_M;
     const int ksub = M ? 1 << ivf->pq_nbits : 0;
-    const int dsub = M ? d / M : 0;
 #pragma omp parallel num_threads(nthreads)
     {
         float* sim2 = M ? (float*)malloc(sizeof(float) * M * ksub) : NULL;
@@ -537,21 +728,7 @@ void oracle_ivf_search_preassigned_mc(const oracle_ivf_t* ivf, size_t n, const f
             float* hv = D + i * k;
             int64_t* hi = I + i * k;
             oracle_heap_heapify(cmax, k, hv, hi);
-            if (M) { /* init_query_L2 (IndexIVFPQ.cpp:560-566) */
-                if (!ivf->by_residual) {
-                    for (int m = 0; m < M; m++)
-                        for (int j = 0; j < ksub; j++)
-                            sim[m * ksub + j] = oracle_fvec_L2sqr(
-                                    xi + m * dsub, ivf->pq_centroids + ((size_t)m * ksub + j) * dsub,
-                                    dsub);
-                } else if (ivf->use_precomputed_table) {
-                    for (int m = 0; m < M; m++)
-                        for (int j = 0; j < ksub; j++)
-                            sim2[m * ksub + j] = oracle_fvec_inner_product(
-                                    xi + m * dsub, ivf->pq_centroids + ((size_t)m * ksub + j) * dsub,
-                                    dsub);
-                }
-            }
+            if (M) pq_init_query_(ivf, xi, sim, sim2);
             for (size_t ik = 0; ik < nprobe; ik++) {
                 int64_t key = keys[i * nprobe + ik];
                 if (key < 0 || key >= ivf->nlist) continue;
@@ -569,28 +746,11 @@ void oracle_ivf_search_preassigned_mc(const oracle_ivf_t* ivf, size_t n, const f
                             oracle_heap_replace_top(cmax, k, hv, hi, dis, ivf->ids[j]);
                     }
                 } else {
-                    float dis0 = 0;
-                    if (ivf->by_residual) {
-                        if (ivf->use_precomputed_table == 1) {
-                            dis0 = coarse_dis[i * nprobe + ik];
-                            const float* P = ivf->precomputed_table + (size_t)key * M * ksub;
-                            for (int e = 0; e < M * ksub; e++) sim[e] = fmaf(-2.f, sim2[e], P[e]);
-                        } else {
-                            const float* c = ivf->hnsw ? ivf->hnsw->storage + key * d
-                                                       : ivf->centroids + key * d;
-                            for (int j = 0; j < d; j++) resid[j] = xi[j] - c[j];
-                            for (int m = 0; m < M; m++)
-                                for (int j = 0; j < ksub; j++)
-                                    sim[m * ksub + j] = oracle_fvec_L2sqr(
-                                            resid + m * dsub,
-                                            ivf->pq_centroids + ((size_t)m * ksub + j) * dsub, dsub);
-                        }
-                    }
+                    const float dis0 = pq_set_list_(ivf, xi, key, coarse_dis[i * nprobe + ik],
+                                                    sim, sim2, resid);
                     for (int64_t j = l0; j < l1; j++) {
                         const uint8_t* code = ivf->codes + j * ivf->code_size;
-                        float acc = 0.f;
-                        for (int m = 0; m < M; m++) acc += sim[m * ksub + code[m]];
-                        float dis = dis0 + acc;
+                        const float dis = dis0 + oracle_pq_code_sum(M, sim, ksub, code);
                         if (cmp_(cmax, hv[0], dis))
                             oracle_heap_replace_top(cmax, k, hv, hi, dis, ivf->ids[j]);
                     }
@@ -713,7 +873,7 @@ void oracle_merge_knn_results(size_t n, size_t k, int nshard, const float* all_d
  * C::cmp(radius, dis) (L2: dis < radius, IP: dis > radius) and, with a
  * selector mask (per concatenated row, may be NULL), when it is a member.
  * Writes lims[n+1]; D/I are written up to `cap` entries; returns the total.
- * PQ: L2 only. */
+ * PQ: L2 and inner product. */
 int64_t oracle_ivf_range_preassigned(const oracle_ivf_t* ivf, size_t n, const float* x,
                                      size_t nprobe, const int64_t* keys,
                                      const float* coarse_dis, float radius,
@@ -723,7 +883,6 @@ int64_t oracle_ivf_range_preassigned(const oracle_ivf_t* ivf, size_t n, const fl
     const int d = ivf->d;
     const int M = ivf->pq_M;
     const int ksub = M ? 1 << ivf->pq_nbits : 0;
-    const int dsub = M ? d / M : 0;
     float* sim = M ? (float*)malloc(sizeof(float) * M * ksub) : NULL;
     float* sim2 = M ? (float*)malloc(sizeof(float) * M * ksub) : NULL;
     float* resid = (float*)malloc(sizeof(float) * d);
@@ -731,44 +890,19 @@ int64_t oracle_ivf_range_preassigned(const oracle_ivf_t* ivf, size_t n, const fl
     for (size_t i = 0; i < n; i++) {
         lims[i] = (size_t)tot;
         const float* xi = x + i * d;
-        if (M) { /* init_query_L2 (IndexIVFPQ.cpp:560-566) */
-            for (int m = 0; m < M; m++)
-                for (int j = 0; j < ksub; j++) {
-                    const float* c = ivf->pq_centroids + ((size_t)m * ksub + j) * dsub;
-                    if (!ivf->by_residual)
-                        sim[m * ksub + j] = oracle_fvec_L2sqr(xi + m * dsub, c, dsub);
-                    else if (ivf->use_precomputed_table == 1)
-                        sim2[m * ksub + j] = oracle_fvec_inner_product(xi + m * dsub, c, dsub);
-                }
-        }
+        if (M) pq_init_query_(ivf, xi, sim, sim2);
         for (size_t ik = 0; ik < nprobe; ik++) {
             const int64_t key = keys[i * nprobe + ik];
             if (key < 0 || key >= ivf->nlist) continue;
-            float dis0 = 0.f;
-            if (M && ivf->by_residual) { /* set_list: precompute_list_tables_L2 */
-                if (ivf->use_precomputed_table == 1) {
-                    dis0 = coarse_dis[i * nprobe + ik];
-                    const float* P = ivf->precomputed_table + (size_t)key * M * ksub;
-                    for (int e = 0; e < M * ksub; e++) sim[e] = fmaf(-2.f, sim2[e], P[e]);
-                } else {
-                    const float* c = ivf->hnsw ? ivf->hnsw->storage + key * d
-                                               : ivf->centroids + key * d;
-                    for (int j = 0; j < d; j++) resid[j] = xi[j] - c[j];
-                    for (int m = 0; m < M; m++)
-                        for (int j = 0; j < ksub; j++)
-                            sim[m * ksub + j] = oracle_fvec_L2sqr(
-                                    resid + m * dsub,
-                                    ivf->pq_centroids + ((size_t)m * ksub + j) * dsub, dsub);
-                }
-            }
+            const float dis0 =
+                    M ? pq_set_list_(ivf, xi, key, coarse_dis[i * nprobe + ik], sim, sim2, resid)
+                      : 0.f;
             for (int64_t r = ivf->list_off[key]; r < ivf->list_off[key + 1]; r++) {
                 if (selmask && !selmask[r]) continue;
                 float dis;
                 if (M) {
                     const uint8_t* code = ivf->codes + (size_t)r * ivf->code_size;
-                    float acc = 0.f;
-                    for (int m = 0; m < M; m++) acc += sim[m * ksub + code[m]];
-                    dis = dis0 + acc;
+                    dis = dis0 + oracle_pq_code_sum(M, sim, ksub, code);
                 } else {
                     const float* y = (const float*)(ivf->codes + (size_t)r * ivf->code_size);
                     dis = ref_dist_(xi, y, d, l2);

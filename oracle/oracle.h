@@ -99,6 +99,16 @@ typedef struct {
     float* precomputed_table;   /* [nlist][M][ksub] when table 1 (filled by prepare) */
 } oracle_ivf_t;
 
+/* PQ table entry of one sub-vector in the reference's fvec_*_ny order
+ * (faiss/utils/distances_simd.cpp:1362-1410, AVX2 specialisations) */
+float oracle_pq_ny_ip(const float* x, const float* y, int dsub);
+float oracle_pq_ny_l2(const float* x, const float* y, int dsub);
+/* distance_single_code / distance_four_codes, PQDecoder8, AVX2 order
+ * (faiss/impl/code_distance/code_distance-avx2.h) */
+float oracle_pq_code_sum(int M, const float* sim, int ksub, const uint8_t* code);
+/* IndexIVFPQ::encode_vectors + ProductQuantizer::compute_codes (dsub < 16) */
+void oracle_ivfpq_encode(const oracle_ivf_t* ivf, size_t n, const float* x,
+                         const int64_t* list_nos, uint8_t* codes);
 /* faiss/IndexIVFPQ.cpp:364-459: fills precomputed_table when table 1 */
 void oracle_ivfpq_prepare(oracle_ivf_t* ivf);
 

@@ -70,6 +70,7 @@ def lib():
                                                    _P, C.c_int64]
         L.oracle_ivf_range_preassigned.restype = C.c_int64
         L.oracle_max_threads.restype = C.c_int
+        L.oracle_ivfpq_encode.argtypes = [C.POINTER(IVFStruct), C.c_size_t, _P, _P, _P]
         _lib = L
     return _lib
 
@@ -194,6 +195,13 @@ class IVFOracle:
     def use_precomputed_table(self):
         return self.s.use_precomputed_table
 
+    @use_precomputed_table.setter
+    def use_precomputed_table(self, t):
+        """0 (per-list residual tables) or 1 (needs the table prepare() built)."""
+        if t == 1 and not self.s.precomputed_table:
+            raise ValueError("no precomputed table for this index")
+        self.s.use_precomputed_table = int(t)
+
     @classmethod
     def from_index(cls, idx):
         """Export an hnsw-ivf_amd IndexIVFFlat / IndexIVFPQ (host mirrors)."""
@@ -237,6 +245,14 @@ class IVFOracle:
                                                _p(coarse_dis), max_codes, _p(D), _p(I), _p(nd),
                                                nthreads or nthreads_default())
         return (D, I, int(nd[0])) if return_ndis else (D, I)
+
+    def encode(self, x, list_nos):
+        """IndexIVFPQ::encode_vectors: [n, M] uint8 codes (dsub < 16)."""
+        x = np.ascontiguousarray(x, np.float32)
+        ln = np.ascontiguousarray(list_nos, np.int64)
+        codes = np.empty((x.shape[0], self.s.pq_M), np.uint8)
+        lib().oracle_ivfpq_encode(C.byref(self.s), x.shape[0], _p(x), _p(ln), _p(codes))
+        return codes
 
     def range_search_preassigned(self, x, radius, keys, selmask=None, coarse_dis=None):
         """IVF range search (faiss/IndexIVF.cpp:1243-1400): (lims, D, I).
