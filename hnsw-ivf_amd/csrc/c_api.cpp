@@ -661,7 +661,7 @@ int faiss_amd_IndexIVF_search_preassigned_device(const FaissIndexIVF* index, idx
                                                  idx_t* l_dev, void* stream) {
     C_TRY const IndexIVF* ix = IVF(index);
     FAISS_THROW_IF_NOT_MSG(ix->d % 4 == 0, "device entry points need d % 4 == 0");
-    FAISS_THROW_IF_NOT(nprobe > 0 && nprobe <= kern::kMaxK);
+    FAISS_THROW_IF_NOT(nprobe > 0 && (size_t)nprobe <= ix->nlist);
     ensure_hip();
     ix->sync_device();
     ix->search_preassigned_device(n, x_dev, ldx_of(ix), k, nprobe, assign_dev, cdis_dev, d_dev,
@@ -683,7 +683,8 @@ int faiss_amd_merge_knn_results_device(size_t n, size_t k, int nshard, const flo
                                        const idx_t* all_l, float* d, idx_t* l,
                                        FaissMetricType metric, void* stream) {
     C_TRY ensure_hip();
-    FAISS_THROW_IF_NOT(nshard > 0 && nshard < 32768 && k <= 64);
+    FAISS_THROW_IF_NOT(nshard > 0 && nshard < 32768 && k >= 1 &&
+                       k <= (size_t)kern::kMaxKExact);
     kern::merge_rows(all_d, all_l, (int64_t)n, (nshard << 16) | (int)k, (int)k,
                      metric == ::METRIC_L2, d, l, (hipStream_t)stream);
     C_CATCH

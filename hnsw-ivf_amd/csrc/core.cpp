@@ -186,11 +186,40 @@ const float* IndexFlat::device_norms() const {
 template <class OutIdx>
 void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* distances,
                            OutIdx* labels, hipStream_t s) const {
-    FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kern::kMaxK, "k must be in [1, 64] on this path");
+    FAISS_THROW_IF_NOT_FMT(k >= 1 && k <= kern::kMaxKExact, "k = %d must be in [1, %d]", k,
+                           kern::kMaxKExact);
     sync_device();
     std::lock_guard<std::recursive_mutex> g(mu_);
     const int l = ld();
     const int metric_l2 = metric_type == METRIC_L2;
+    if (k > kern::kMaxK) {
+        // large k (e.g. nprobe > 64): whole distance rows in the reference's
+        // form (direct below 20 queries, else BLAS form on the fp32 tile) and
+        // the exact select with the heap's arrival-order tie rule
+        if (metric_l2) {
+            s_xn_.reserve(sizeof(float) * std::max<idx_t>(n, 1));
+            kern::row_norms(x, n, d, ldx, s_xn_.as<float>(), s);
+        }
+        const idx_t ny = std::max<idx_t>(ntotal, 1);
+        const idx_t qc = std::max<idx_t>(1, std::min<idx_t>(n, ((idx_t)1 << 28) / ny));
+        s_tile_.reserve(sizeof(float) * qc * ny);
+        ScopedKernelTimer tm(&ktimes, "flat_distance+select_exact", 2.0 * n * ntotal * d, s);
+        for (idx_t q0 = 0; q0 < n; q0 += qc) {
+            const idx_t nq = std::min(qc, n - q0);
+            if (ntotal > 0 && n < 20)
+                kern::direct_distances(x + q0 * ldx, nq, ldx, d_xb_.as<float>(), ntotal, l, d,
+                                       metric_l2, s_tile_.as<float>(), ntotal, s);
+            else if (ntotal > 0)
+                kern::pairwise_distances(x + q0 * ldx, nq, ldx,
+                                         metric_l2 ? s_xn_.as<float>() + q0 : nullptr,
+                                         d_xb_.as<float>(), ntotal, l, d_norms_.as<float>(), l,
+                                         metric_l2, s_tile_.as<float>(), ntotal, s);
+            kern::select_rows_exact<OutIdx>(s_tile_.as<float>(), nq, ntotal, ntotal, k,
+                                            metric_l2, 0, distances + q0 * k, labels + q0 * k, k,
+                                            s);
+        }
+        return;
+    }
     constexpr bool i32 = sizeof(OutIdx) == 4;
     int32_t* o32 = i32 ? (int32_t*)labels : nullptr;
     int64_t* o64 = i32 ? nullptr : (int64_t*)labels;

@@ -386,16 +386,30 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
     gd.max_level = hnsw.max_level;
     gd.ntotal = (int)ntotal;
     const int64_t vwords = (int64_t)cdiv(std::max<idx_t>(ntotal, 1), 32);
-    if (vwords * 4 > 64 * 1024) s_visited_.reserve(sizeof(uint32_t) * vwords * n);
     constexpr bool i32 = sizeof(OutIdx) == 4;
     if (!d_stats_.ptr) {
         d_stats_.reserve(4 * sizeof(unsigned long long));
         HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, 4 * sizeof(unsigned long long), s));
     }
+    // queries per launch: the per-query visited bitmaps that do not fit in
+    // LDS live in a scratch kept under 256 MiB (chunks of the batch)
+    const int ef = std::max(efSearch, k);
+    const size_t lds_need = sizeof(float) * ld() + 8 * (size_t)ef + 8 * (size_t)k + 544 +
+                            (size_t)vwords * 4;
+    const bool scratch = lds_need > 64 * 1024;
+    const idx_t qc = scratch ? std::max<idx_t>(1, std::min<idx_t>(
+                                       n, (idx_t)(((size_t)256 << 20) / ((size_t)vwords * 4))))
+                             : n;
+    if (scratch) s_visited_.reserve(sizeof(uint32_t) * vwords * qc);
+    s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(qc, 1));
     ScopedKernelTimer tm(&ktimes, "hnsw_search", 0.0, s);
-    kern::hnsw_search(gd, x, ldx, n, k, efSearch, distances, i32 ? nullptr : (int64_t*)labels,
-                      i32 ? (int32_t*)labels : nullptr, s_visited_.as<uint32_t>(), vwords,
-                      d_stats_.as<unsigned long long>(), s);
+    for (idx_t q0 = 0; q0 < n; q0 += qc) {
+        const idx_t nq = std::min(qc, n - q0);
+        kern::hnsw_search(gd, x + q0 * ldx, ldx, nq, k, efSearch, distances + q0 * k,
+                          i32 ? nullptr : (int64_t*)labels + q0 * k,
+                          i32 ? (int32_t*)labels + q0 * k : nullptr, s_visited_.as<uint32_t>(),
+                          vwords, d_stats_.as<unsigned long long>(), s_flags_.as<uint32_t>(), s);
+    }
 }
 
 // HNSWStats counted by the kernel -> the host global (faiss::hnsw_stats)

@@ -170,6 +170,7 @@ void IndexIVF::sync_device() const {
     }
     off[nlist] = (uint32_t)rows;
     arena_rows_ = rows;
+    max_list_len_ = nlist ? *std::max_element(len.begin(), len.end()) : 0;
     const size_t code_bytes = std::max<size_t>(rows, 1) * dstride;
     std::vector<idx_t> hi(std::max<size_t>(rows, 1), -1);
     std::vector<uint32_t> hl(std::max<size_t>(rows, 1), 0xffffffffu);
@@ -286,14 +287,15 @@ idx_t IndexIVF::search_chunk(idx_t n, size_t np, idx_t k) const {
 }
 
 namespace {
-// faiss/IndexIVF.cpp:445-460, 595-631: parallel_mode 0 and 3 are both
-// query-parallel with the same per-query scan (3 only changes the OpenMP
-// split), which is what the GPU path computes; 1 and 2 split a query's probes
-// across threads and the PARALLEL_MODE_NO_HEAP_INIT flag accumulates into the
-// caller's arrays — neither is offered here.
+// faiss/IndexIVF.cpp:445-460, 595-704: parallel_mode 0 / 3 are query-parallel
+// scans of one heap per query; 1 / 2 split a query's probes across threads
+// and merge the per-thread heaps, which gives the same distances (the
+// reference's own test, tests/test_index_accuracy.py:47-60, asserts equal D).
+// The GPU computes every mode as mode 0.  PARALLEL_MODE_NO_HEAP_INIT (1024)
+// accumulates into the caller's arrays and is not offered.
 void check_parallel_mode(int pm) {
-    FAISS_THROW_IF_NOT_FMT(pm == 0 || pm == 3,
-                           "parallel_mode %d not supported on the GPU path (0 and 3 are)", pm);
+    FAISS_THROW_IF_NOT_FMT(pm >= 0 && pm <= 3,
+                           "parallel_mode %d not supported on the GPU path (0-3 are)", pm);
 }
 }  // namespace
 
@@ -336,7 +338,6 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
     const size_t mc = params ? params->max_codes : max_codes;
-    FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
     DevGuard dg(device);
     sync_device();
     const uint8_t* selm = apply_selector(params, s);
@@ -396,7 +397,6 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
                                         QueryLatencyStats* per_query_stats) const {
     // faiss/IndexIVF.cpp:399-723 / 870-1200 (parallel_mode 0 semantics)
     FAISS_THROW_IF_NOT(k > 0);
-    FAISS_THROW_IF_NOT_MSG(!store_pairs, "store_pairs is not supported on the GPU path");
     check_parallel_mode(parallel_mode);
     const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
@@ -435,7 +435,7 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
     const int32_t* asg = apply_max_codes(n, (int)np, ba.as<int32_t>(), mc, &lim, s);
     const uint8_t* selm = apply_selector(params, s);
     search_preassigned_device(n, bx.as<float>(), ldx, k, (int)np, asg, bc.as<float>(),
-                              bd.as<float>(), bi.as<idx_t>(), s, lim, selm);
+                              bd.as<float>(), bi.as<idx_t>(), s, lim, selm, store_pairs);
     hipEvent_t e1 = ev.mark(s);
     kern::ivf_visit_stats(asg, n * (int64_t)np, d_list_len_.as<uint32_t>(), (int)nlist, lim,
                           s_stats_.as<unsigned long long>(), s);
@@ -482,7 +482,6 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
     FAISS_THROW_IF_NOT(np > 0);
     check_parallel_mode(parallel_mode);
     const size_t mc = params ? params->max_codes : max_codes;
-    FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
     if (n == 0) return;
     DevGuard dg(device);
     sync_device();
@@ -595,11 +594,22 @@ void IndexIVFFlat::upload_extra() const {
 }
 
 void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
-                                             const int32_t* assign, const float*,
+                                             const int32_t* assign, const float* cdis,
                                              float* distances, idx_t* labels, hipStream_t s,
-                                             const uint32_t* lim, const uint8_t* sel) const {
+                                             const uint32_t* lim, const uint8_t* sel,
+                                             bool store_pairs) const {
     if (n <= 0) return;
     sync_device();
+    const char* env = getenv("FAISS_AMD_IVF_SCAN");
+    int mode = scan_mode;
+    if (env && !strcmp(env, "exact")) mode = 1;
+    if (env && !strcmp(env, "mfma")) mode = 0;
+    const int KQ = obits_ <= 14 ? kern::ivf_mfma_kq((int)k, d) : 0;
+    if (mode != 0 || KQ <= 0 || np > kern::kMaxK || store_pairs) {
+        exact_scan_device(n, x, ldx, k, np, assign, cdis, distances, labels, s, lim, sel,
+                          store_pairs);
+        return;
+    }
     std::lock_guard<std::recursive_mutex> g(mu_);
     const int QT = 64;
     const int l = (int)roundup((size_t)d, 4);
@@ -614,68 +624,86 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     b.counts_next = counts_next;
     b.lim = lim;
     b.sel = sel;
-    const char* env = getenv("FAISS_AMD_IVF_SCAN");
-    int mode = scan_mode;
-    if (env && !strcmp(env, "exact")) mode = 1;
-    if (env && !strcmp(env, "mfma")) mode = 0;
-    const int KQ = obits_ <= 14 ? kern::ivf_mfma_kq((int)k, d) : 0;
-    const bool mfma = mode == 0 && KQ > 0;
-    if (mfma) {
-        s_part_.reserve(sizeof(uint32_t) * n * np * KQ);        // raw filter keys
-        s_pk2_.reserve(sizeof(kern::ProbeRec) * n * np);        // per-probe records
-        b.mark_keys = s_part_.as<uint32_t>();
-        b.mark_recs = s_pk2_.as<kern::ProbeRec>();
-        b.mark_ke = KQ;
-        const int64_t mi = kern::ivf_max_items(n, np, (int)nlist, QT);
-        s_idesc_.reserve(sizeof(kern::ItemDesc) * mi);
-        s_ient_.reserve(sizeof(uint32_t) * mi * QT);
-        b.item_desc = s_idesc_.as<kern::ItemDesc>();
-        b.item_entries = s_ient_.as<uint32_t>();
-    }
+    s_part_.reserve(sizeof(uint32_t) * n * np * KQ);  // raw filter keys
+    s_pk2_.reserve(sizeof(kern::ProbeRec) * n * np);  // per-probe records
+    b.mark_keys = s_part_.as<uint32_t>();
+    b.mark_recs = s_pk2_.as<kern::ProbeRec>();
+    b.mark_ke = KQ;
+    const int64_t max_items = kern::ivf_max_items(n, np, (int)nlist, QT);
+    s_idesc_.reserve(sizeof(kern::ItemDesc) * max_items);
+    s_ient_.reserve(sizeof(uint32_t) * max_items * QT);
+    b.item_desc = s_idesc_.as<kern::ItemDesc>();
+    b.item_entries = s_ient_.as<uint32_t>();
     kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), d_list_off_.as<uint32_t>(),
                      (int)nlist, QT, b, s);
     flip_counts();
-    const int64_t max_items = kern::ivf_max_items(n, np, (int)nlist, QT);
     const bool l2 = metric_type == METRIC_L2;
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(n, 4));
-    if (mfma) {
-        const bool dbg = getenv("FAISS_AMD_IVF_STATS") != nullptr;
-        if (dbg) HIP_CHECK(hipMemsetAsync(s_flags_.ptr, 0, 4 * sizeof(uint32_t), s));
-        kern::ivf_flat_scan_mfma(x, ldx, d_codes_.as<float>(), l, d_cbf_.ptr,
-                                 d_ids_.as<int64_t>(), d_ynorm_.as<float>(), d_ynmax_.as<float>(),
-                                 d_rres_.as<float>(), d_rmax_.as<float>(),
-                                 d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(),
-                                 (int)nlist, d, obits_, n, np, (int)k, l2, b, max_items,
-                                 s_part_.as<uint32_t>(), s_pk2_.as<kern::ProbeRec>(),
-                                 dbg ? s_flags_.as<uint32_t>() : nullptr, distances, labels,
-                                 &ktimes, s);
-        if (dbg) {
-            uint32_t st[4];
-            HIP_CHECK(hipMemcpyAsync(st, s_flags_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
-            HIP_CHECK(hipStreamSynchronize(s));
-            fprintf(stderr,
-                    "[faiss_amd] ivf mfma scan: nq=%lld survivors/q=%.2f failing probes/q=%.4f "
-                    "overflow queries=%u general-resolve queries=%u\n",
-                    (long long)n, st[0] / (double)n, st[1] / (double)n, st[2], st[3]);
-        }
-        return;
+    const bool dbg = getenv("FAISS_AMD_IVF_STATS") != nullptr;
+    if (dbg) HIP_CHECK(hipMemsetAsync(s_flags_.ptr, 0, 4 * sizeof(uint32_t), s));
+    kern::ivf_flat_scan_mfma(x, ldx, d_codes_.as<float>(), l, d_cbf_.ptr, d_ids_.as<int64_t>(),
+                             d_ynorm_.as<float>(), d_ynmax_.as<float>(), d_rres_.as<float>(),
+                             d_rmax_.as<float>(), d_list_off_.as<uint32_t>(),
+                             d_list_len_.as<uint32_t>(), (int)nlist, d, obits_, n, np, (int)k, l2,
+                             b, max_items, s_part_.as<uint32_t>(), s_pk2_.as<kern::ProbeRec>(),
+                             dbg ? s_flags_.as<uint32_t>() : nullptr, distances, labels, &ktimes,
+                             s);
+    if (dbg) {
+        uint32_t st[4];
+        HIP_CHECK(hipMemcpyAsync(st, s_flags_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        fprintf(stderr,
+                "[faiss_amd] ivf mfma scan: nq=%lld survivors/q=%.2f failing probes/q=%.4f "
+                "overflow queries=%u general-resolve queries=%u\n",
+                (long long)n, st[0] / (double)n, st[1] / (double)n, st[2], st[3]);
     }
-    s_pk1_.reserve(sizeof(float) * n * np * k);
-    s_pk2_.reserve(sizeof(long long) * n * np * k);
-    {
-        ScopedKernelTimer tm(&ktimes, "ivf_flat_scan", 0.0, s);
-        kern::ivf_flat_scan(x, ldx, d_codes_.as<float>(), l, d_ids_.as<int64_t>(),
-                            d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(), (int)nlist, l,
-                            d, n, np, (int)k, l2, b, max_items, s_pk1_.as<float>(),
-                            s_pk2_.as<long long>(), s);
+}
+
+void IndexIVFFlat::exact_args(void* p) const {
+    auto& a = *(kern::ExactScanArgs*)p;
+    a.codes = d_codes_.as<float>();
+    a.ldc = (int)roundup((size_t)d, 4);
+}
+
+// general exact scan: chunks of queries whose candidate keys fit the scratch
+void IndexIVF::exact_scan_device(idx_t n, const float* x, int ldx, idx_t k, int np,
+                                 const int32_t* assign, const float* cdis, float* distances,
+                                 idx_t* labels, hipStream_t s, const uint32_t* lim,
+                                 const uint8_t* sel, bool store_pairs) const {
+    FAISS_THROW_IF_NOT_FMT(k >= 1 && k <= kern::kMaxKExact, "k = %lld must be in [1, %d]",
+                           (long long)k, kern::kMaxKExact);
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    int64_t cap = 0;
+    const idx_t qc = kern::ivf_exact_chunk(n, np, max_list_len_, (int64_t)arena_rows_, &cap);
+    s_ex_eoff_.reserve(sizeof(uint32_t) * qc * np);
+    s_ex_tot_.reserve(sizeof(uint32_t) * qc);
+    s_ex_keys_.reserve(sizeof(uint32_t) * qc * cap);
+    s_ex_rows_.reserve(sizeof(uint32_t) * qc * cap);
+    kern::ExactScanArgs a;
+    exact_args(&a);
+    a.ldx = ldx;
+    a.d = d;
+    a.np = np;
+    a.k = (int)k;
+    a.l2 = metric_type == METRIC_L2;
+    a.list_off = d_list_off_.as<uint32_t>();
+    a.list_len = d_list_len_.as<uint32_t>();
+    a.nlist = (int)nlist;
+    a.sel = sel;
+    a.ids = d_ids_.as<int64_t>();
+    a.row_list = d_row_list_.as<uint32_t>();
+    a.store_pairs = store_pairs ? 1 : 0;
+    ScopedKernelTimer tm(&ktimes, "ivf_exact_scan", 0.0, s);
+    for (idx_t q0 = 0; q0 < n; q0 += qc) {
+        a.n = std::min(qc, n - q0);
+        a.x = x + q0 * ldx;
+        a.assign = assign + q0 * np;
+        a.cdis = cdis ? cdis + q0 * np : nullptr;
+        a.lim = lim ? lim + q0 * np : nullptr;
+        kern::ivf_exact_search(a, s_ex_eoff_.as<uint32_t>(), s_ex_tot_.as<uint32_t>(),
+                               s_ex_keys_.as<uint32_t>(), s_ex_rows_.as<uint32_t>(), cap,
+                               distances + q0 * k, labels + q0 * k, s);
     }
-    kern::ivf_merge(s_pk1_.as<float>(), s_pk2_.as<long long>(), assign,
-                    d_list_len_.as<uint32_t>(), (int)nlist, n, np, (int)k, l2, distances, labels,
-                    s_flags_.as<uint32_t>(), s);
-    kern::ivf_exact_fallback(s_flags_.as<uint32_t>(), assign, d_list_off_.as<uint32_t>(),
-                             d_list_len_.as<uint32_t>(), (int)nlist, x, ldx,
-                             d_codes_.as<float>(), l, d_ids_.as<int64_t>(), d, n, np, (int)k, l2,
-                             lim, sel, distances, labels, s);
 }
 
 // ---------------------------------------------------------------- PQ
@@ -831,16 +859,20 @@ void IndexIVFPQ::upload_extra() const {
 void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int np,
                                            const int32_t* assign, const float* centroid_dis,
                                            float* distances, idx_t* labels, hipStream_t s,
-                                           const uint32_t* lim, const uint8_t* sel) const {
+                                           const uint32_t* lim, const uint8_t* sel,
+                                           bool store_pairs) const {
     if (n <= 0) return;
-    FAISS_THROW_IF_NOT_MSG(metric_type == METRIC_L2, "IVFPQ inner product not supported on GPU");
     sync_device();
+    FAISS_THROW_IF_NOT_MSG(centroid_dis || !(by_residual && metric_type == METRIC_L2 &&
+                                             use_precomputed_table == 1),
+                           "IVF-PQ with precomputed tables needs centroid_dis");
     // list-centric bf16 MFMA filter + exact re-rank in the reference's table
-    // arithmetic (default where eligible; FAISS_AMD_PQ_SCAN=lut forces the
-    // query-centric LUT scan below)
+    // arithmetic (default where eligible; FAISS_AMD_PQ_SCAN=exact forces the
+    // general exact scan, which serves every other geometry)
     const char* penv = getenv("FAISS_AMD_PQ_SCAN");
-    const bool lut = penv && !strcmp(penv, "lut");
-    if (!lut && pq_mfma_ready_ && kern::ivfpq_mfma_eligible(d, (int)pq.M, (int)k, np)) {
+    const bool force_exact = penv && !strcmp(penv, "exact");
+    if (!force_exact && !store_pairs && pq_mfma_ready_ && metric_type == METRIC_L2 &&
+        by_residual && kern::ivfpq_mfma_eligible(d, (int)pq.M, (int)k, np)) {
         std::lock_guard<std::recursive_mutex> g(mu_);
         const int QT = 64;
         uint32_t* counts_next = nullptr;
@@ -907,12 +939,21 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         }
         return;
     }
-    ScopedKernelTimer tm(&ktimes, "ivfpq_scan", 0.0, s);
-    kern::ivfpq_scan(x, ldx, d_pq_.as<float>(), (int)pq.M, (int)pq.ksub, (int)pq.dsub,
-                     d_codes_.as<uint8_t>(), d_terms_.as<float>(), d_ids_.as<int64_t>(),
-                     d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(), (int)nlist, assign,
-                     centroid_dis, lim, sel, n, np, (int)k, by_residual ? 1 : 0, distances,
-                     labels, s);
+    exact_scan_device(n, x, ldx, k, np, assign, centroid_dis, distances, labels, s, lim, sel,
+                      store_pairs);
+}
+
+void IndexIVFPQ::exact_args(void* p) const {
+    auto& a = *(kern::ExactScanArgs*)p;
+    a.pq.M = (int)pq.M;
+    a.pq.dsub = (int)pq.dsub;
+    a.pq.by_residual = by_residual ? 1 : 0;
+    a.pq.table1 = (metric_type == METRIC_L2 && by_residual && use_precomputed_table == 1) ? 1 : 0;
+    a.pq.pq_cent = d_pq_.as<float>();
+    a.pq.cent = d_cent_.as<float>();
+    a.pq.ldcent = ld();
+    a.pq.codes = d_codes_.as<uint8_t>();
+    a.pq.cs = device_code_stride();
 }
 
 // ---------------------------------------------------------------- shards
@@ -1031,7 +1072,6 @@ void IndexIVF::range_search(idx_t n, const float* x, float radius, RangeSearchRe
     FAISS_THROW_IF_NOT(result && result->nq == (size_t)n);
     const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
-    FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
     check_parallel_mode(parallel_mode);
     result->lims.assign((size_t)n + 1, 0);
     result->labels.clear();
@@ -1071,10 +1111,8 @@ void IndexIVF::range_search_preassigned(idx_t n, const float* x, float radius,
                                         IndexIVFStats* stats) const {
     // faiss/IndexIVF.cpp:1243-1400 (parallel_mode 0)
     FAISS_THROW_IF_NOT(result && result->nq == (size_t)n);
-    FAISS_THROW_IF_NOT_MSG(!store_pairs, "store_pairs is not supported on the GPU path");
     const size_t np = std::min(nlist, params && params->nprobe ? params->nprobe : nprobe);
     FAISS_THROW_IF_NOT(np > 0);
-    FAISS_THROW_IF_NOT_MSG(np <= (size_t)kern::kMaxK, "nprobe must be <= 64 on this path");
     check_parallel_mode(parallel_mode);
     result->lims.assign((size_t)n + 1, 0);
     result->labels.clear();
@@ -1107,11 +1145,11 @@ void IndexIVF::range_search_preassigned(idx_t n, const float* x, float radius,
     const uint8_t* selm = apply_selector(params, s);
     range_device(n, bx.as<float>(), ldx, (int)np, bci.as<int32_t>(),
                  centroid_dis ? bcd.as<float>() : nullptr, radius, selm, result,
-                 stats ? stats : &indexIVF_stats, s);
+                 stats ? stats : &indexIVF_stats, s, store_pairs);
 }
 
 void IndexIVF::range_launch(const float*, idx_t, int, const int32_t*, const float*, int, float,
-                            const uint8_t*, uint32_t*, const uint64_t*, float*, idx_t*,
+                            const uint8_t*, uint32_t*, const uint64_t*, float*, idx_t*, bool,
                             hipStream_t) const {
     FAISS_THROW_MSG("range search not implemented for this type of index");
 }
@@ -1119,9 +1157,9 @@ void IndexIVF::range_launch(const float*, idx_t, int, const int32_t*, const floa
 void IndexIVFFlat::range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
                                 const float*, int np, float radius, const uint8_t* selm,
                                 uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
-                                hipStream_t s) const {
+                                bool store_pairs, hipStream_t s) const {
     kern::ivf_range_flat(x, n, ldx, assign, np, d_codes_.as<float>(), ld(),
-                         d_ids_.as<int64_t>(), d_list_off_.as<uint32_t>(),
+                         store_pairs ? nullptr : d_ids_.as<int64_t>(), d_list_off_.as<uint32_t>(),
                          d_list_len_.as<uint32_t>(), (int)nlist, d, metric_type == METRIC_L2,
                          radius, selm, counts, offs, D, I, s);
 }
@@ -1129,31 +1167,34 @@ void IndexIVFFlat::range_launch(const float* x, idx_t n, int ldx, const int32_t*
 void IndexIVFPQ::range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
                               const float* cdis, int np, float radius, const uint8_t* selm,
                               uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
-                              hipStream_t s) const {
-    FAISS_THROW_IF_NOT_MSG(metric_type == METRIC_L2 && by_residual,
-                           "IVF-PQ range search: L2 by-residual indexes only on this path");
-    FAISS_THROW_IF_NOT_MSG(pq.nbits == 8 && (pq.dsub == 2 || pq.dsub == 4 || pq.dsub == 8),
-                           "IVF-PQ range search: PQ8 with dsub 2, 4 or 8 on this path");
-    FAISS_THROW_IF_NOT_MSG(cdis || use_precomputed_table != 1,
+                              bool store_pairs, hipStream_t s) const {
+    FAISS_THROW_IF_NOT_MSG(cdis || !(metric_type == METRIC_L2 && by_residual &&
+                                     use_precomputed_table == 1),
                            "IVF-PQ range search with precomputed tables needs centroid_dis");
-    kern::PQArgs pa;
-    pa.pq_cent = d_pq_.as<float>();
-    pa.cent = d_cent_.as<float>();
-    pa.ldcent = ld();
-    pa.cdis = cdis;
-    pa.codes = d_codes_.as<uint8_t>();
-    pa.cs = device_code_stride();
-    pa.M = (int)pq.M;
-    pa.table1 = use_precomputed_table == 1 ? 1 : 0;
-    kern::ivfpq_range(x, n, ldx, assign, np, pa, (int)pq.dsub, d_ids_.as<int64_t>(),
-                      d_list_off_.as<uint32_t>(), d_list_len_.as<uint32_t>(), (int)nlist, radius,
-                      selm, counts, offs, D, I, s);
+    kern::ExactScanArgs a;
+    exact_args(&a);
+    a.x = x;
+    a.ldx = ldx;
+    a.d = d;
+    a.n = n;
+    a.np = np;
+    a.l2 = metric_type == METRIC_L2;
+    a.assign = assign;
+    a.cdis = cdis;
+    a.list_off = d_list_off_.as<uint32_t>();
+    a.list_len = d_list_len_.as<uint32_t>();
+    a.nlist = (int)nlist;
+    a.sel = selm;
+    a.ids = d_ids_.as<int64_t>();
+    a.row_list = d_row_list_.as<uint32_t>();
+    a.store_pairs = store_pairs ? 1 : 0;
+    kern::ivfpq_range_exact(a, radius, counts, offs, D, I, s);
 }
 
 void IndexIVF::range_device(idx_t n, const float* x, int ldx, int np, const int32_t* assign,
                             const float* cdis, float radius, const uint8_t* selm,
-                            RangeSearchResult* result,
-                            IndexIVFStats* stats, hipStream_t s) const {
+                            RangeSearchResult* result, IndexIVFStats* stats, hipStream_t s,
+                            bool store_pairs) const {
     // queries per pass: grid n*np < 2^31 and bounded count scratch
     const idx_t qc = std::max<idx_t>(1, std::min<idx_t>(n, ((idx_t)1 << 26) / np));
     std::vector<uint32_t> cnt;
@@ -1169,7 +1210,7 @@ void IndexIVF::range_device(idx_t n, const float* x, int ldx, int np, const int3
         bc.reserve(sizeof(uint32_t) * m);
         const float* cd = cdis ? cdis + (size_t)q0 * np : nullptr;
         range_launch(x + (size_t)q0 * ldx, nc, ldx, a, cd, np, radius, selm, bc.as<uint32_t>(),
-                     nullptr, nullptr, nullptr, s);
+                     nullptr, nullptr, nullptr, store_pairs, s);
         cnt.resize(m);
         hassign.resize(m);
         HIP_CHECK(hipMemcpyAsync(cnt.data(), bc.ptr, sizeof(uint32_t) * m, hipMemcpyDeviceToHost,
@@ -1202,7 +1243,7 @@ void IndexIVF::range_device(idx_t n, const float* x, int ldx, int np, const int3
             HIP_CHECK(hipMemcpyAsync(bo.ptr, offs.data(), sizeof(uint64_t) * m,
                                      hipMemcpyHostToDevice, s));
             range_launch(x + (size_t)q0 * ldx, nc, ldx, a, cd, np, radius, selm, nullptr,
-                         bo.as<uint64_t>(), bd.as<float>(), bi.as<int64_t>(), s);
+                         bo.as<uint64_t>(), bd.as<float>(), bi.as<int64_t>(), store_pairs, s);
             result->labels.resize(base + tot);
             result->distances.resize(base + tot);
             HIP_CHECK(hipMemcpyAsync(result->distances.data() + base, bd.ptr, sizeof(float) * tot,

@@ -19,6 +19,8 @@ namespace faiss_amd {
 namespace kern {
 
 constexpr int kMaxK = 64;  // largest k / nprobe served by the wave queues
+constexpr int kMaxKExact = 2048;  // largest k of the general exact path (faiss GPU's limit,
+                                  // faiss/gpu/utils/DeviceDefs.cuh:28)
 
 // out[i] = sum_j x[i*ld + j]^2, j < d
 void row_norms(const float* x, int64_t n, int d, int ld, float* out, hipStream_t s);
@@ -67,6 +69,11 @@ void select_fix_ip(const float* D, int64_t nx, int64_t ny, int64_t ldD, int k, f
 // (already final (dis,label) form, label -1 = empty) -> [n][k].
 void merge_rows(const float* cand_d, const int64_t* cand_i, int64_t n, int nin_x_kin, int k,
                 int metric_l2, float* out_d, int64_t* out_i, hipStream_t s);
+
+// merge_knn_results for any k (kernels_exact.hip), inputs [nshard][n][kin]
+void merge_rows_general(const float* cand_d, const int64_t* cand_i, int64_t n, int nshard,
+                        int kin, int k, int metric_l2, float* out_d, int64_t* out_i,
+                        hipStream_t s);
 
 // labels >= 0 get += offset (faiss/IndexShardsIVF.cpp translate_labels)
 void translate_labels(int64_t* labels, int64_t n, int64_t offset, hipStream_t s);
@@ -157,6 +164,52 @@ void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, in
                   int obits, int k, const uint8_t* sel, float* D, int64_t* I, uint32_t* stats,
                   hipStream_t s);
 
+// ---------------- general exact path (kernels_exact.hip) ----------------
+// IVF-PQ tables of the exact scan (QueryTables semantics)
+struct ExactPQ {
+    int M = 0, dsub = 0;
+    int by_residual = 1;
+    int table1 = 0;                  // use_precomputed_table == 1 (L2 by residual)
+    const float* pq_cent = nullptr;  // [M][256][dsub]
+    const float* cent = nullptr;     // coarse centroids [nlist][ldcent] fp32
+    int ldcent = 0;
+    const uint8_t* codes = nullptr;  // arena codes
+    int cs = 0;                      // code stride (bytes)
+};
+struct ExactScanArgs {
+    const float* x = nullptr;  // [n][ldx] queries of the chunk
+    int ldx = 0, d = 0;
+    int64_t n = 0;
+    int np = 0, k = 0, l2 = 1;
+    const int32_t* assign = nullptr;  // [n][np]
+    const float* cdis = nullptr;      // [n][np] (PQ table 1: dis0)
+    const uint32_t* list_off = nullptr;
+    const uint32_t* list_len = nullptr;
+    int nlist = 0;
+    const uint32_t* lim = nullptr;  // max_codes prefixes (nullptr: whole lists)
+    const uint8_t* sel = nullptr;   // IDSelector row mask (nullptr: all)
+    const int64_t* ids = nullptr;
+    const uint32_t* row_list = nullptr;  // store_pairs: list of each arena row
+    int store_pairs = 0;
+    const float* codes = nullptr;  // IVF-Flat arena [rows][ldc]
+    int ldc = 0;
+    ExactPQ pq;  // pq.M > 0: IVF-PQ
+};
+// candidates per query (cap) and queries per chunk for a 1 GiB scratch
+int64_t ivf_exact_chunk(int64_t n, int np, uint32_t max_list_len, int64_t arena_rows,
+                        int64_t* cap_out);
+// eoff [n*np], total [n], keys / rows [n*cap] scratch
+void ivf_exact_search(const ExactScanArgs& a, uint32_t* eoff, uint32_t* total, uint32_t* keys,
+                      uint32_t* rows, int64_t cap, float* D, int64_t* I, hipStream_t s);
+// IVF-PQ range scan of any geometry / metric (same contract as ivfpq_range;
+// a.x / a.assign / a.cdis / a.sel / a.ids / a.row_list / a.store_pairs used)
+void ivfpq_range_exact(const ExactScanArgs& a, float radius, uint32_t* counts,
+                       const uint64_t* offsets, float* outD, int64_t* outI, hipStream_t s);
+// exact top-k (reference heap semantics, label = col0 + column) of dense rows
+template <class OutIdx>
+void select_rows_exact(const float* D, int64_t nx, int64_t ny, int64_t ldD, int k, int metric_l2,
+                       int64_t col0, float* out_d, OutIdx* out_i, int64_t ldo, hipStream_t s);
+
 // IndexIVFStats counters of a batch (faiss/IndexIVF.cpp:1184-1198):
 // stats[0] += non-empty lists visited, stats[1] += codes scanned (device)
 void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_len, int nlist,
@@ -166,16 +219,8 @@ inline int64_t ivf_max_items(int64_t n, int nprobe, int nlist, int QT) {
     return (n * nprobe + QT - 1) / QT + nlist;
 }
 
-// IVF-Flat scan, reference faiss/IndexIVFFlat.cpp:155-179 (IVFFlatScanner):
-// exact per-(query, list) top-k of sum (x - y)^2 (or <x,y>) written as
-// internal keys to part_k1/part_k2 [n*nprobe][k].
-void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const int64_t* ids,
-                   const uint32_t* list_off, const uint32_t* list_len, int nlist, int dp, int d,
-                   int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b, int64_t max_items,
-                   float* part_k1, long long* part_k2, hipStream_t s);
-
 // bf16x3-MFMA filter + certified exact re-rank (kernels_ivf_mfma.hip);
-// results are identical to ivf_flat_scan + ivf_merge (+ ivf_exact_fallback).
+// results are identical to the general exact scan (ivf_exact_search).
 // ivf_mfma_kq = entries kept per (query, list); 0 = not eligible
 // (k > 32 or roundup(d, 16) > 128).
 int ivf_mfma_kq(int k, int d);
@@ -200,34 +245,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
                         int64_t max_items, uint32_t* keys, ProbeRec* recs, uint32_t* stats,
                         float* D, int64_t* I, KernelTimes* kt, hipStream_t s);
-// exact re-scan (reference tie rule) of the queries with flags[q] != 0
-void ivf_exact_fallback(const uint32_t* flags, const int32_t* assign, const uint32_t* list_off,
-                        const uint32_t* list_len, int nlist, const float* x, int ldx,
-                        const float* codes, int ldc, const int64_t* ids, int d, int64_t n,
-                        int nprobe, int k, int metric_l2, const uint32_t* lim,
-                        const uint8_t* sel, float* D, int64_t* I, hipStream_t s);
-
-// per-query merge of the nprobe partial top-k, reference
-// faiss/IndexIVF.cpp:595-631 (heap over probes) + Heap.h:421-450 (reorder)
-// flags[q] = 1 when a tie may cross the k boundary (resolve with
-// ivf_exact_fallback, which applies the reference's arrival-order rule)
-void ivf_merge(const float* part_k1, const long long* part_k2, const int32_t* assign,
-               const uint32_t* list_len, int nlist, int64_t n, int nprobe, int k, int metric_l2,
-               float* D, int64_t* I, uint32_t* flags, hipStream_t s);
-
 // ---------------- IVF-PQ ----------------
-// query-centric PQ scan with the LUT in LDS, reference
-// faiss/IndexIVFPQ.cpp:560-566,634-700 (tables), :861-933 (scan).
-// dis = coarse_dis + term[v] + sum_m T[m][code_m]
-//   by_residual: T = -2 <x_m, c_mj>, term[v] = sum_m ||c||^2 + 2<yC_m, c>
-//   otherwise:   T = ||x_m - c_mj||^2, term = 0, coarse_dis = 0
-void ivfpq_scan(const float* x, int ldx, const float* pq_centroids, int M, int ksub, int dsub,
-                const uint8_t* codes, const float* terms, const int64_t* ids,
-                const uint32_t* list_off, const uint32_t* list_len, int nlist,
-                const int32_t* assign, const float* coarse_dis, const uint32_t* lim,
-                const uint8_t* sel, int64_t n,
-                int nprobe, int k, int by_residual, float* D, int64_t* I, hipStream_t s);
-
 // term[v] = sum_m (||c_{m,code}||^2 + 2 <yC_m, c_{m,code}>) for every arena row
 void ivfpq_terms(const uint8_t* codes, const uint32_t* row_list, int64_t nrows,
                  const float* centroids, int ldcent, const float* pq_centroids, int M, int ksub,
@@ -256,9 +274,13 @@ struct HNSWDevice {
 };
 // reference faiss/impl/HNSW.cpp:943-996 (HNSW::search), :852-924 (greedy),
 // :605-741 (search_from_candidates), :1096-1342 (MinimaxHeap)
+// flags: [n] scratch; queries where an exact distance tie makes the batched
+// form unsafe are redone by the sequential kernel (nullptr: no check).
+// max(efSearch, k) > 128 or k > 64: the sequential kernel for every query.
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
-                 int64_t visited_words_per_query, unsigned long long* stats, hipStream_t s);
+                 int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
+                 hipStream_t s);
 
 // IVF-Flat range search (kernels_range.hip): one wave per (query, probe).
 // offsets == nullptr: counts[q*np+p] = hits (dis < radius for L2, > for IP,
@@ -269,15 +291,6 @@ void ivf_range_flat(const float* x, int64_t n, int ldx, const int32_t* assign, i
                     const uint32_t* list_len, int nlist, int d, int metric_l2, float radius,
                     const uint8_t* selm, uint32_t* counts, const uint64_t* offsets, float* outD,
                     int64_t* outI, hipStream_t s);
-
-// IVF-PQ range search (kernels_ivf_mfma.hip): same contract as
-// ivf_range_flat, distances by the reference table arithmetic (pq_exact);
-// pa.cdis = coarse distances [n][np] (table 1 dis0).  L2, by residual.
-void ivfpq_range(const float* x, int64_t n, int ldx, const int32_t* assign, int np,
-                 const PQArgs& pa, int dsub, const int64_t* ids, const uint32_t* list_off,
-                 const uint32_t* list_len, int nlist, float radius, const uint8_t* selm,
-                 uint32_t* counts, const uint64_t* offsets, float* outD, int64_t* outI,
-                 hipStream_t s);
 
 }  // namespace kern
 }  // namespace faiss_amd

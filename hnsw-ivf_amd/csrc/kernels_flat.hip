@@ -401,7 +401,10 @@ void merge_rows(const float* cand_d, const int64_t* cand_i, int64_t n, int nin_x
     // nin_x_kin is encoded by the caller as nshard * 65536 + kin
     int nshard = nin_x_kin >> 16, kin = nin_x_kin & 0xffff;
     if (n <= 0) return;
-    FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
+    if (k > kMaxK) {
+        merge_rows_general(cand_d, cand_i, n, nshard, kin, k, metric_l2, out_d, out_i, s);
+        return;
+    }
     k_merge_shards<<<dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s>>>(
             cand_d, cand_i, n, kin, nshard, k, metric_l2, out_d, out_i);
     HIP_LAUNCH_CHECK();

@@ -299,404 +299,6 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
 // ---------------------------------------------------------------- scan
 constexpr int SQT = 64;   // queries per work item
 constexpr int SVT = 32;   // codes per tile (8 reference-order partial sums per pair)
-constexpr int SDC = 128;  // dims per LDS chunk
-constexpr int SSD = SDC + 4;  // LDS row stride (floats): 528 B, 16-B aligned
-
-// KQ > 0: thread-queue selection (4 threads per query, k <= KQ);
-// KQ == 0: wave64 bitonic queues (16 queries per wave, any k <= 64).
-template <bool L2, int KQ>
-__global__ __launch_bounds__(256, 2) void k_ivf_flat_scan(
-        const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
-        const int64_t* __restrict__ ids, const uint32_t* __restrict__ list_off,
-        const uint32_t* __restrict__ list_len, int nlist, int dp, int dp_true, int nprobe,
-        int k, const uint32_t* __restrict__ bucket_off, const uint32_t* __restrict__ item_off,
-        const uint32_t* __restrict__ entries, const uint32_t* __restrict__ lim,
-        const uint8_t* __restrict__ sel, float* __restrict__ part_k1,
-        long long* __restrict__ part_k2) {
-    // one array: the end-of-kernel queue merge reuses it (64 KB at KQ=32)
-    __shared__ __attribute__((aligned(16))) float smem_xy[(SQT + 64) * SSD];
-    float* Xs = smem_xy;
-    float* Ys = smem_xy + SQT * SSD;
-    __shared__ long long ids_s[64];
-    __shared__ uint32_t ent_s[SQT];
-    __shared__ int32_t qrow_s[SQT];
-    __shared__ int32_t qlim_s[SQT];  // rows of the list scanned for each query
-
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int w = t >> 6;
-    // XCD-aware order: blocks b and b+8 share an XCD (dispatch round-robin),
-    // so groups of 4 consecutive work items (chunks of the same list) are
-    // placed on one XCD and re-read the list from its L2.  Bijective on the
-    // grid (a multiple of 32); affects speed only.
-    const uint32_t xcd = blockIdx.x & 7u, rest = blockIdx.x >> 3;
-    const uint32_t item = 4u * ((rest >> 2) * 8u + xcd) + (rest & 3u);
-    const uint32_t total_items = item_off[nlist];
-    if (item >= total_items) return;
-    // list owning this item: largest l with item_off[l] <= item
-    int lo = 0, hi = nlist;
-    while (hi - lo > 1) {
-        int mid = (lo + hi) >> 1;
-        if (item_off[mid] <= item) lo = mid; else hi = mid;
-    }
-    const int l = lo;
-    const uint32_t chunk = item - item_off[l];
-    const uint32_t qb = bucket_off[l] + chunk * SQT;
-    const int nQ = (int)min((uint32_t)SQT, bucket_off[l + 1] - qb);
-    const int len = (int)list_len[l];
-    if (t < SQT) {
-        uint32_t e = t < nQ ? entries[qb + t] : 0u;
-        ent_s[t] = e;
-        qrow_s[t] = t < nQ ? (int32_t)(e / (uint32_t)nprobe) : -1;
-        qlim_s[t] = lim && t < nQ ? (int32_t)lim[e] : len;
-    }
-    const int64_t row0 = list_off[l];
-    __syncthreads();
-
-    const bool one_chunk = dp <= SDC;
-    auto load_x = [&](int dc) {
-        const int dl = min(SDC, dp - dc);
-        for (int e = t; e < SQT * (SDC / 4); e += 256) {
-            int r = e >> 5, c4 = e & 31;
-            int kc = 4 * c4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            int qr = qrow_s[r];
-            if (qr >= 0 && kc < dl) v = *(const float4*)(x + (int64_t)qr * ldx + dc + kc);
-            *(float4*)(Xs + r * SSD + kc) = v;
-        }
-    };
-    if (one_chunk) load_x(0);
-
-    // selection state
-    constexpr int NQW = KQ > 0 ? 1 : 16;  // wave path: 16 queues per lane
-    float qd[NQW];
-    long long qi[NQW];
-    ThreadQueue<(KQ > 0 ? KQ : 1)> tq;
-    if constexpr (KQ > 0) {
-        tq.init();
-    } else {
-#pragma unroll
-        for (int qq = 0; qq < NQW; qq++) {
-            qd[qq] = WS_INF;
-            qi[qq] = WS_NOID;
-        }
-    }
-    const int qg = t >> 4, vg = t & 15;
-
-    // register prefetch of the next code tile (d <= 128): its HBM latency
-    // overlaps the current tile's compute and selection
-    float4 pf[SVT * (SDC / 4) / 256];
-    auto fetch = [&](int v0n) {
-        const int nvn = min(SVT, len - v0n);
-#pragma unroll
-        for (int s = 0; s < SVT * (SDC / 4) / 256; s++) {
-            const int e = t + 256 * s;
-            const int r = e >> 5, kc = 4 * (e & 31);
-            pf[s] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r < nvn && kc < dp)
-                pf[s] = *(const float4*)(codes + (row0 + v0n + r) * (int64_t)ldc + kc);
-        }
-    };
-    if (one_chunk && len > 0) fetch(0);
-
-    // dims evaluated in the reference order (ref_arith.h): lanes over
-    // i < n8, then the 4-term epilogue and the tail in the last chunk
-    const int d = dp_true;
-    const int n8 = d & ~7;
-    for (int v0 = 0; v0 < len; v0 += SVT) {
-        const int nv = min(SVT, len - v0);
-        RefAcc8 acc[4][2];
-        float res[4][2];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int j = 0; j < 2; j++) acc[i][j].init();
-
-        for (int dc = 0; dc < dp; dc += SDC) {
-            const int dl = min(SDC, dp - dc);
-            if (one_chunk) {
-#pragma unroll
-                for (int s = 0; s < SVT * (SDC / 4) / 256; s++) {
-                    const int e = t + 256 * s;
-                    *(float4*)(Ys + (e >> 5) * SSD + 4 * (e & 31)) = pf[s];
-                }
-                __syncthreads();
-                if (v0 + SVT < len) fetch(v0 + SVT);
-            } else {
-                load_x(dc);
-                for (int e = t; e < SVT * (SDC / 4); e += 256) {
-                    int r = e >> 5, c4 = e & 31;
-                    int kc = 4 * c4;
-                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (r < nv && kc < dl)
-                        v = *(const float4*)(codes + (row0 + v0 + r) * (int64_t)ldc + dc + kc);
-                    *(float4*)(Ys + r * SSD + kc) = v;
-                }
-                __syncthreads();
-            }
-            const int dmain = min(dl, max(0, n8 - dc));
-            for (int dd = 0; dd < dmain; dd += 8) {
-                float4 xa[4][2], yb[2][2];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    xa[i][0] = *(const float4*)(Xs + (qg + 16 * i) * SSD + dd);
-                    xa[i][1] = *(const float4*)(Xs + (qg + 16 * i) * SSD + dd + 4);
-                }
-#pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    yb[j][0] = *(const float4*)(Ys + (vg + 16 * j) * SSD + dd);
-                    yb[j][1] = *(const float4*)(Ys + (vg + 16 * j) * SSD + dd + 4);
-                }
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-#pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        float* c = acc[i][j].c;
-                        c[0] = ref_term_fma<L2>(xa[i][0].x, yb[j][0].x, c[0]);
-                        c[1] = ref_term_fma<L2>(xa[i][0].y, yb[j][0].y, c[1]);
-                        c[2] = ref_term_fma<L2>(xa[i][0].z, yb[j][0].z, c[2]);
-                        c[3] = ref_term_fma<L2>(xa[i][0].w, yb[j][0].w, c[3]);
-                        c[4] = ref_term_fma<L2>(xa[i][1].x, yb[j][1].x, c[4]);
-                        c[5] = ref_term_fma<L2>(xa[i][1].y, yb[j][1].y, c[5]);
-                        c[6] = ref_term_fma<L2>(xa[i][1].z, yb[j][1].z, c[6]);
-                        c[7] = ref_term_fma<L2>(xa[i][1].w, yb[j][1].w, c[7]);
-                    }
-            }
-            if (dc + dl >= dp) {
-                // last chunk: reduce, epilogue, tail (dims n8 .. d-1 are here)
-                const int e0 = n8 - dc;
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-#pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        const float* xr = Xs + (qg + 16 * i) * SSD;
-                        const float* yr = Ys + (vg + 16 * j) * SSD;
-                        float r = acc[i][j].reduce();
-                        int ii = e0;
-                        if (d - n8 >= 4) {
-                            const float t0 = ref_term<L2>(xr[e0], yr[e0]);
-                            const float t1 = ref_term<L2>(xr[e0 + 1], yr[e0 + 1]);
-                            const float t2 = ref_term<L2>(xr[e0 + 2], yr[e0 + 2]);
-                            const float t3 = ref_term<L2>(xr[e0 + 3], yr[e0 + 3]);
-                            r = r + ((t0 + t2) + (t1 + t3));
-                            ii += 4;
-                        }
-                        for (; ii < d - dc; ii++) r = ref_term_fma<L2>(xr[ii], yr[ii], r);
-                        res[i][j] = r;
-                    }
-            }
-            __syncthreads();
-        }
-        // distance tile -> LDS (aliases the Y tile)
-        float* Ds = Ys;
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int j = 0; j < 2; j++) Ds[(qg + 16 * i) * (SVT + 1) + vg + 16 * j] = res[i][j];
-        if constexpr (KQ == 0) {
-            if (t < SVT) ids_s[t] = t < nv ? (long long)ids[row0 + v0 + t] : 0ll;
-        }
-        __syncthreads();
-        if constexpr (KQ > 0) {
-            // thread (q = t>>2, s = t&3) owns codes s, s+4, ... of query q
-            const int q = t >> 2, s4 = t & 3;
-            if (q < nQ) {
-                const int nvq = min(nv, qlim_s[q] - v0);
-#pragma unroll 4
-                for (int j = s4; j < nvq; j += 4) {
-                    if (sel && !sel[row0 + v0 + j]) continue;  // IDSelector (use_sel)
-                    float dis = Ds[q * (SVT + 1) + j];
-                    float k1 = L2 ? dis : -dis;
-                    if (k1 < FLT_MAX) {
-                        const uint32_t r = (uint32_t)(v0 + j);
-                        unsigned long long key =
-                                ((unsigned long long)ordered_f32(k1) << 32) | (L2 ? r : ~r);
-                        tq.push(key, k);
-                    }
-                }
-            }
-        } else {
-            // wave w owns queries w*16 .. w*16+15
-            const bool lane_ok = lane < nv && (!sel || sel[row0 + v0 + lane]);
-            const long long my_id = ids_s[lane];
-#pragma unroll
-            for (int qq = 0; qq < NQW; qq++) {
-                const int q = w * 16 + qq;
-                if (q < nQ) {
-                    float dis = Ds[q * (SVT + 1) + lane];
-                    float k1;
-                    long long k2;
-                    to_key(L2 ? 1 : 0, dis, my_id, k1, k2);
-                    if (!lane_ok || v0 + lane >= qlim_s[q] || !key_admissible(k1)) {
-                        k1 = WS_INF;
-                        k2 = WS_NOID;
-                    }
-                    wave_offer_q(qd[qq], qi[qq], k1, k2, k, lane);
-                }
-            }
-        }
-        __syncthreads();
-    }
-    if constexpr (KQ > 0) {
-        // merge the 4 thread queues of each query through LDS
-        unsigned long long* M = (unsigned long long*)Xs;  // [64][4][KQ] fits Xs+Ys
-        const int q = t >> 2, s4 = t & 3;
-#pragma unroll
-        for (int i = 0; i < KQ; i++) M[(q * 4 + s4) * KQ + i] = tq.q[i];
-        __syncthreads();
-        if (t < nQ) {
-            const unsigned long long* Mq = M + t * 4 * KQ;
-            int p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-            const int64_t e = ent_s[t];
-            for (int j = 0; j < k; j++) {
-                unsigned long long h0 = p0 < KQ ? Mq[p0] : ~0ull;
-                unsigned long long h1 = p1 < KQ ? Mq[KQ + p1] : ~0ull;
-                unsigned long long h2 = p2 < KQ ? Mq[2 * KQ + p2] : ~0ull;
-                unsigned long long h3 = p3 < KQ ? Mq[3 * KQ + p3] : ~0ull;
-                unsigned long long m01 = h0 < h1 ? h0 : h1, m23 = h2 < h3 ? h2 : h3;
-                unsigned long long m = m01 < m23 ? m01 : m23;
-                if (m == h0) p0++;
-                else if (m == h1) p1++;
-                else if (m == h2) p2++;
-                else p3++;
-                float k1 = WS_INF;
-                long long k2 = WS_NOID;
-                if (m != ~0ull) {
-                    k1 = unordered_f32((uint32_t)(m >> 32));
-                    uint32_t r = (uint32_t)m;
-                    if (!L2) r = ~r;
-                    const long long id = ids[row0 + r];
-                    k2 = L2 ? id : -id;
-                }
-                part_k1[e * k + j] = k1;
-                part_k2[e * k + j] = k2;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int qq = 0; qq < NQW; qq++) {
-            const int q = w * 16 + qq;
-            if (q < nQ && lane < k) {
-                const int64_t e = ent_s[q];
-                part_k1[e * k + lane] = qd[qq];
-                part_k2[e * k + lane] = qi[qq];
-            }
-        }
-    }
-}
-
-template <int KQ>
-static void launch_scan(bool l2, int64_t grid, hipStream_t s, const float* x, int ldx,
-                        const float* codes, int ldc, const int64_t* ids, const uint32_t* list_off,
-                        const uint32_t* list_len, int nlist, int dp, int d, int nprobe, int k,
-                        IVFBuckets b, float* pk1, long long* pk2) {
-    if (l2)
-        k_ivf_flat_scan<true, KQ><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
-                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, d, nprobe, k, b.bucket_off,
-                b.item_off, b.entries, b.lim, b.sel, pk1, pk2);
-    else
-        k_ivf_flat_scan<false, KQ><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
-                x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp, d, nprobe, k, b.bucket_off,
-                b.item_off, b.entries, b.lim, b.sel, pk1, pk2);
-}
-
-void ivf_flat_scan(const float* x, int ldx, const float* codes, int ldc, const int64_t* ids,
-                   const uint32_t* list_off, const uint32_t* list_len, int nlist, int dp, int d,
-                   int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b, int64_t max_items,
-                   float* part_k1, long long* part_k2, hipStream_t s) {
-    if (n <= 0) return;
-    FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
-    FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldc % 4 == 0 && dp % 4 == 0);
-    FAISS_THROW_IF_NOT(max_items < (1ll << 31));
-    const bool l2 = metric_l2 != 0;
-    max_items = (int64_t)roundup((size_t)max_items, 32);  // XCD remap needs a multiple of 32
-    if (k <= 10)
-        launch_scan<10>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
-                        d, nprobe, k, b, part_k1, part_k2);
-    else if (k <= 16)
-        launch_scan<16>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
-                        d, nprobe, k, b, part_k1, part_k2);
-    else
-        launch_scan<0>(l2, max_items, s, x, ldx, codes, ldc, ids, list_off, list_len, nlist, dp,
-                       d, nprobe, k, b, part_k1, part_k2);
-    HIP_LAUNCH_CHECK();
-}
-
-// ---------------------------------------------------------------- merge
-// Per query: lexicographic top-k of the nprobe per-list partial top-k.  A
-// boundary tie (the (k+1)-th merged key, or the last key of a full per-list
-// partial, equal to the k-th value) flags the query for the exact re-scan.
-__global__ __launch_bounds__(256) void k_ivf_merge(const float* __restrict__ part_k1,
-                                                   const long long* __restrict__ part_k2,
-                                                   const int32_t* __restrict__ assign,
-                                                   const uint32_t* __restrict__ list_len,
-                                                   int64_t n, int nprobe, int nlist, int k,
-                                                   int metric_l2, float* __restrict__ D,
-                                                   int64_t* __restrict__ I,
-                                                   uint32_t* __restrict__ flags) {
-    const int lane = threadIdx.x & 63;
-    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= n) return;
-    const int K1 = k < 64 ? k + 1 : 64;
-    float qd = WS_INF;
-    long long qi = WS_NOID;
-    float thr_d = WS_INF;
-    long long thr_i = WS_NOID;
-    const int total = nprobe * k;
-    for (int c = 0; c < total; c += 64) {
-        int e = c + lane;
-        float k1 = WS_INF;
-        long long k2 = WS_NOID;
-        if (e < total) {
-            int r = e / k;
-            int lst = assign[q * nprobe + r];
-            if (lst >= 0 && lst < nlist && list_len[lst] > 0) {
-                int64_t p = (q * nprobe) * (int64_t)k + e;
-                k1 = part_k1[p];
-                k2 = part_k2[p];
-            }
-        }
-        wave_offer(qd, qi, k1, k2, thr_d, thr_i, K1, lane);
-    }
-    const float v = __shfl(qd, k - 1);
-    const long long vi = shfl_ll(qi, k - 1);
-    bool amb = false;
-    if (vi != WS_NOID) {
-        int cnt = 0;
-        bool tail = false;
-        for (int c = 0; c < total; c += 64) {
-            int e = c + lane;
-            bool eq = false;
-            if (e < total) {
-                int lst = assign[q * nprobe + e / k];
-                if (lst >= 0 && lst < nlist && list_len[lst] > 0) {
-                    int64_t p = (q * nprobe) * (int64_t)k + e;
-                    eq = part_k2[p] != WS_NOID && part_k1[p] == v;
-                    if (eq && e % k == k - 1) tail = true;
-                }
-            }
-            cnt += __popcll(__ballot(eq));
-        }
-        amb = __ballot(tail) != 0ull || cnt > __popcll(__ballot(lane < k && qd == v));
-    }
-    if (lane < k) {
-        float dis;
-        long long id;
-        from_key(metric_l2, qd, qi, dis, id);
-        D[q * k + lane] = dis;
-        I[q * k + lane] = id;
-    }
-    if (lane == 0) flags[q] = amb ? 1u : 0u;
-}
-
-void ivf_merge(const float* part_k1, const long long* part_k2, const int32_t* assign,
-               const uint32_t* list_len, int nlist, int64_t n, int nprobe, int k, int metric_l2,
-               float* D, int64_t* I, uint32_t* flags, hipStream_t s) {
-    if (n <= 0) return;
-    k_ivf_merge<<<dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s>>>(
-            part_k1, part_k2, assign, list_len, n, nprobe, nlist, k, metric_l2, D, I, flags);
-    HIP_LAUNCH_CHECK();
-}
 
 }  // namespace kern
 }  // namespace faiss_amd

@@ -18,7 +18,6 @@
 //     (dist, id) is emitted.  A list whose KQ-th kept candidate still has
 //     approx - Bmax(list) <= U may have dropped a member: the query is
 //     flagged.
-//  C  k_ivf_exact_fallback: exact scan of the flagged queries only.
 //
 // Error bound (d terms, u = 2^-24, g = d u / (1 - d u)):
 //   |ip_mfma - ip| <= g sum|x_i y_i| <= g (|x|^2 + |y|^2) / 2
@@ -795,77 +794,6 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
     }
 }
 
-// ---------------------------------------------------------------- C
-// Exact re-scan of flagged queries: every row of every probed list.
-template <bool L2>
-struct FullStream {
-    const int32_t* asg;
-    const uint32_t* list_off;
-    const uint32_t* list_len;
-    int nlist, nprobe, d, ldc, lane;
-    const float* xq;
-    const float* codes;
-    const int64_t* ids;
-    const uint32_t* lim;  // max_codes: rows scanned per probe (nullptr: all)
-    const uint8_t* sel;   // IDSelector mask of the arena rows (nullptr: all)
-    template <class F>
-    __device__ __forceinline__ void for_each(F f) const {
-        for (int r = 0; r < nprobe; r++) {
-            const int lst = asg[r];
-            if (lst < 0 || lst >= nlist) continue;
-            const int len = (int)(lim ? min(lim[r], list_len[lst]) : list_len[lst]);
-            for (int v0 = 0; v0 < len; v0 += 64) {
-                float k1 = WS_INF;
-                long long k2 = WS_NOID, rank = 0;
-                bool ok = v0 + lane < len &&
-                          (!sel || sel[(int64_t)list_off[lst] + v0 + lane]);
-                if (ok) {
-                    const int64_t grow = (int64_t)list_off[lst] + v0 + lane;
-                    const float* yr = codes + grow * ldc;
-                    const float dis = L2 ? ref_l2(xq, yr, d) : ref_ip(xq, yr, d);
-                    to_key(L2 ? 1 : 0, dis, (long long)ids[grow], k1, k2);
-                    ok = key_admissible(k1);
-                    rank = ((long long)r << 32) | (uint32_t)(v0 + lane);
-                }
-                f(ok, k1, k2, rank);
-            }
-        }
-    }
-};
-
-template <bool L2>
-__global__ __launch_bounds__(64) void k_ivf_exact_fallback(
-        const uint32_t* __restrict__ flags, const int32_t* __restrict__ assign,
-        const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
-        const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
-        const int64_t* __restrict__ ids, int d, int nprobe, int k,
-        const uint32_t* __restrict__ lim, const uint8_t* __restrict__ sel,
-        float* __restrict__ D, int64_t* __restrict__ I) {
-    const int64_t q = blockIdx.x;
-    if (flags[q] == 0u) return;
-    FullStream<L2> st{assign + q * nprobe, list_off, list_len, nlist, nprobe, d, ldc,
-                      (int)threadIdx.x, x + q * ldx, codes, ids,
-                      lim ? lim + q * nprobe : nullptr, sel};
-    exact_topk_resolve(st, k, L2 ? 1 : 0, (int)threadIdx.x, true, D + q * k, I + q * k);
-}
-
-void ivf_exact_fallback(const uint32_t* flags, const int32_t* assign, const uint32_t* list_off,
-                        const uint32_t* list_len, int nlist, const float* x, int ldx,
-                        const float* codes, int ldc, const int64_t* ids, int d, int64_t n,
-                        int nprobe, int k, int metric_l2, const uint32_t* lim,
-                        const uint8_t* sel, float* D, int64_t* I, hipStream_t s) {
-    if (n <= 0) return;
-    if (metric_l2)
-        k_ivf_exact_fallback<true><<<dim3((unsigned)n), dim3(64), 0, s>>>(
-                flags, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, nprobe, k,
-                lim, sel, D, I);
-    else
-        k_ivf_exact_fallback<false><<<dim3((unsigned)n), dim3(64), 0, s>>>(
-                flags, assign, list_off, list_len, nlist, x, ldx, codes, ldc, ids, d, nprobe, k,
-                lim, sel, D, I);
-    HIP_LAUNCH_CHECK();
-}
-
 // ---------------------------------------------------------------- host
 void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* list_len,
                     int nlist, float* out, hipStream_t s) {
@@ -1066,77 +994,6 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 #undef LAUNCH_B
 #undef DISPATCH
     }
-}
-
-namespace {
-// IVF-PQ range scan (faiss/IndexIVFPQ.cpp:1254-1279 scan_codes_range with
-// RangeSearchResults :780-799): one wave per (query, probe), 64 rows per
-// step, every code evaluated by pq_exact (the reference table arithmetic,
-// bit-exact with the k-NN path) and kept when dis < radius.  Pass 1 counts,
-// pass 2 writes in row order (see kernels_range.hip for the Flat twin).
-template <int PQD, bool FILL>
-__global__ __launch_bounds__(64) void k_ivfpq_range(
-        const float* __restrict__ x, int ldx, const int32_t* __restrict__ assign, int np,
-        PQArgs pa, const int64_t* __restrict__ ids, const uint32_t* __restrict__ list_off,
-        const uint32_t* __restrict__ list_len, int nlist, float radius,
-        const uint8_t* __restrict__ selm, uint32_t* __restrict__ counts,
-        const uint64_t* __restrict__ offsets, float* __restrict__ outD,
-        int64_t* __restrict__ outI) {
-    const int64_t qp = blockIdx.x;
-    const int64_t q = qp / np;
-    const int lane = threadIdx.x;
-    const int32_t key = assign[qp];
-    uint32_t cnt = 0;
-    if (key >= 0 && key < nlist) {
-        const uint32_t off = list_off[key], len = list_len[key];
-        const float* xq = x + q * (int64_t)ldx;
-        const float d0 = pa.table1 ? pa.cdis[qp] : 0.f;
-        const uint64_t base = FILL ? offsets[qp] : 0;
-        const uint64_t below = (1ull << lane) - 1ull;
-        for (uint32_t r0 = 0; r0 < len; r0 += 64) {
-            const uint32_t r = r0 + lane;
-            bool hit = false;
-            float dis = 0.f;
-            if (r < len && (!selm || selm[(uint64_t)off + r])) {
-                dis = pq_exact<PQD>(pa, xq, off + r, (uint32_t)key, d0);
-                hit = dis < radius;
-            }
-            const uint64_t m = __ballot(hit);
-            if (FILL && hit) {
-                const uint64_t o = base + cnt + (uint32_t)__popcll(m & below);
-                outD[o] = dis;
-                outI[o] = ids[(uint64_t)off + r];
-            }
-            cnt += (uint32_t)__popcll(m);
-        }
-    }
-    if (!FILL && lane == 0) counts[qp] = cnt;
-}
-}  // namespace
-
-void ivfpq_range(const float* x, int64_t n, int ldx, const int32_t* assign, int np,
-                 const PQArgs& pa, int dsub, const int64_t* ids, const uint32_t* list_off,
-                 const uint32_t* list_len, int nlist, float radius, const uint8_t* selm,
-                 uint32_t* counts, const uint64_t* offsets, float* outD, int64_t* outI,
-                 hipStream_t s) {
-    if (n <= 0 || np <= 0) return;
-    const dim3 grid((unsigned)(n * np)), block(64);
-#define PQR_LAUNCH(DS, F)                                                                     \
-    k_ivfpq_range<DS, F><<<grid, block, 0, s>>>(x, ldx, assign, np, pa, ids, list_off,        \
-                                                list_len, nlist, radius, selm, counts,        \
-                                                offsets, outD, outI)
-#define PQR_DISPATCH(DS)                                  \
-    do {                                                  \
-        if (offsets) PQR_LAUNCH(DS, true);                \
-        else PQR_LAUNCH(DS, false);                       \
-    } while (0)
-    if (dsub == 2) PQR_DISPATCH(2);
-    else if (dsub == 4) PQR_DISPATCH(4);
-    else if (dsub == 8) PQR_DISPATCH(8);
-    else FAISS_THROW_MSG("ivfpq_range: dsub must be 2, 4 or 8");
-    HIP_LAUNCH_CHECK();
-#undef PQR_DISPATCH
-#undef PQR_LAUNCH
 }
 
 // IVF-PQ re-rank: the Flat re-rank's certified candidate selection with the

@@ -52,7 +52,8 @@ __global__ __launch_bounds__(64) void k_ivf_range(
             if (FILL && hit) {
                 const uint64_t o = base + cnt + (uint32_t)__popcll(m & below);
                 outD[o] = dis;
-                outI[o] = ids[(uint64_t)off + r];
+                // ids == nullptr: store_pairs, lo_build(list_no, offset)
+                outI[o] = ids ? ids[(uint64_t)off + r] : (((int64_t)key << 32) | (int64_t)r);
             }
             cnt += (uint32_t)__popcll(m);
         }

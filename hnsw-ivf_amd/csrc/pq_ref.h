@@ -25,6 +25,27 @@
 namespace faiss_amd {
 namespace kern {
 
+// fvec_L2sqr / fvec_inner_product / fvec_norm_L2sqr order (ref_arith.h) with
+// scalar loads, for rows without 16-B alignment (PQ sub-vectors)
+template <bool L2>
+__device__ __forceinline__ float ref_dist_s(const float* __restrict__ x,
+                                            const float* __restrict__ y, int d) {
+    float c[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int n8 = d & ~7;
+    for (int i = 0; i < n8; i += 8)
+#pragma unroll
+        for (int j = 0; j < 8; j++) c[j] = ref_term_fma<L2>(x[i + j], y[i + j], c[j]);
+    float r = ((c[0] + c[4]) + (c[2] + c[6])) + ((c[1] + c[5]) + (c[3] + c[7]));
+    int i = n8;
+    if (d - n8 >= 4) {
+        r = r + ((ref_term<L2>(x[i], y[i]) + ref_term<L2>(x[i + 2], y[i + 2])) +
+                 (ref_term<L2>(x[i + 1], y[i + 1]) + ref_term<L2>(x[i + 3], y[i + 3])));
+        i += 4;
+    }
+    for (; i < d; i++) r = ref_term_fma<L2>(x[i], y[i], r);
+    return r;
+}
+
 template <bool L2>
 __device__ __forceinline__ float ny_entry(const float* __restrict__ x, const float* __restrict__ y,
                                           int dsub) {
@@ -46,23 +67,8 @@ __device__ __forceinline__ float ny_entry(const float* __restrict__ x, const flo
                        ref_term<L2>(x[8 + j], y[8 + j]);
             return (a[0] + a[2]) + (a[1] + a[3]);
         }
-        default: {
-            // fvec_L2sqr / fvec_inner_product order on unaligned rows
-            float c[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            const int n8 = dsub & ~7;
-            for (int i = 0; i < n8; i += 8)
-#pragma unroll
-                for (int j = 0; j < 8; j++) c[j] = ref_term_fma<L2>(x[i + j], y[i + j], c[j]);
-            float r = ((c[0] + c[4]) + (c[2] + c[6])) + ((c[1] + c[5]) + (c[3] + c[7]));
-            int i = n8;
-            if (dsub - n8 >= 4) {
-                r = r + ((ref_term<L2>(x[i], y[i]) + ref_term<L2>(x[i + 2], y[i + 2])) +
-                         (ref_term<L2>(x[i + 1], y[i + 1]) + ref_term<L2>(x[i + 3], y[i + 3])));
-                i += 4;
-            }
-            for (; i < dsub; i++) r = ref_term_fma<L2>(x[i], y[i], r);
-            return r;
-        }
+        default:
+            return ref_dist_s<L2>(x, y, dsub);
     }
 }
 

@@ -281,7 +281,8 @@ struct IndexHNSW : Index {
     template <class OutIdx>
     void hnsw_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
                      const SearchParameters* params, hipStream_t stream) const;
-    mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, s_visited_, d_stats_;
+    mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, s_visited_, d_stats_,
+            s_flags_;
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
 };
@@ -386,17 +387,19 @@ struct IndexIVF : Index {
                                   QueryLatencyStats* per_query_stats) const;
     // device form (int32 assignments).  lim (optional, max_codes): rows of
     // each (query, probe) list scanned, from apply_max_codes
+    // store_pairs: labels are lo_build(list, offset) (faiss/IndexIVF.h:108-118)
     virtual void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k,
                                            int nprobe, const int32_t* assign,
                                            const float* centroid_dis, float* distances,
                                            idx_t* labels, hipStream_t stream,
                                            const uint32_t* lim = nullptr,
-                                           const uint8_t* sel = nullptr) const = 0;
+                                           const uint8_t* sel = nullptr,
+                                           bool store_pairs = false) const = 0;
     // range scan of device-resident queries / assignments into host results
     void range_device(idx_t n, const float* x, int ldx, int np, const int32_t* assign,
                       const float* cdis, float radius, const uint8_t* sel,
-                      RangeSearchResult* result,
-                      IndexIVFStats* stats, hipStream_t s) const;
+                      RangeSearchResult* result, IndexIVFStats* stats, hipStream_t s,
+                      bool store_pairs = false) const;
     // IDSelector of the call -> arena-row membership mask (index scratch),
     // nullptr when there is none (faiss/IndexIVF.cpp:418-430)
     const uint8_t* apply_selector(const SearchParameters* params, hipStream_t stream) const;
@@ -421,6 +424,16 @@ struct IndexIVF : Index {
 
    protected:
     virtual void upload_extra() const {}
+    // general exact scan (kernels_exact.hip): any k <= 2048, any nprobe,
+    // store_pairs; the reference's results bit for bit
+    void exact_scan_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
+                           const int32_t* assign, const float* centroid_dis, float* distances,
+                           idx_t* labels, hipStream_t stream, const uint32_t* lim,
+                           const uint8_t* sel, bool store_pairs) const;
+    // the index-type part of the exact scan's arguments (codes / PQ tables)
+    virtual void exact_args(void* args) const = 0;
+    mutable uint32_t max_list_len_ = 0;
+    mutable DeviceBuffer s_ex_eoff_, s_ex_tot_, s_ex_keys_, s_ex_rows_;
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
     // arena
@@ -441,7 +454,7 @@ struct IndexIVF : Index {
     virtual void range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
                               const float* cdis, int np, float radius, const uint8_t* sel,
                               uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
-                              hipStream_t s) const;
+                              bool store_pairs, hipStream_t s) const;
 
    private:
     idx_t search_chunk(idx_t n, size_t np, idx_t k) const;
@@ -453,25 +466,27 @@ struct IndexIVF : Index {
 struct IndexIVFFlat : IndexIVF {
     IndexIVFFlat(Index* quantizer, size_t d, size_t nlist, MetricType metric = METRIC_L2);
     // scan algorithm: 0 = auto (MFMA filter + exact re-rank when eligible),
-    // 1 = direct exact VALU scan.  Both give identical results.
+    // 1 = the general exact scan (kernels_exact.hip).  Both give identical
+    // results.
     int scan_mode = 0;
     void encode_vectors(idx_t n, const float* x, const idx_t* list_nos,
                         uint8_t* codes) const override;
     void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
                                    const int32_t* assign, const float* centroid_dis,
                                    float* distances, idx_t* labels, hipStream_t stream,
-                                   const uint32_t* lim = nullptr,
-                                   const uint8_t* sel = nullptr) const override;
+                                   const uint32_t* lim = nullptr, const uint8_t* sel = nullptr,
+                                   bool store_pairs = false) const override;
     void reconstruct(idx_t key, float* recons) const override;
 
    protected:
     void upload_extra() const override;
+    void exact_args(void* args) const override;
     // one pass of the range scan (counts when offs == nullptr, else fill);
     // cdis = coarse distances [n][np] on the device (PQ table 1 dis0)
     virtual void range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
                               const float* cdis, int np, float radius, const uint8_t* sel,
                               uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
-                              hipStream_t s) const override;
+                              bool store_pairs, hipStream_t s) const override;
     mutable DeviceBuffer d_ynorm_, d_ynmax_, d_cbf_, d_rres_, d_rmax_, s_part_, s_flags_;
     mutable int obits_ = 4;
 };
@@ -497,20 +512,21 @@ struct IndexIVFPQ : IndexIVF {
     void search_preassigned_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
                                    const int32_t* assign, const float* centroid_dis,
                                    float* distances, idx_t* labels, hipStream_t stream,
-                                   const uint32_t* lim = nullptr,
-                                   const uint8_t* sel = nullptr) const override;
+                                   const uint32_t* lim = nullptr, const uint8_t* sel = nullptr,
+                                   bool store_pairs = false) const override;
     // faiss/IndexIVFPQ.cpp:364-459: choose 0/1 like the reference (the GPU
     // path uses per-code terms either way)
     void precompute_table();
 
    protected:
     void upload_extra() const override;
+    void exact_args(void* args) const override;
     // one pass of the range scan (counts when offs == nullptr, else fill);
     // cdis = coarse distances [n][np] on the device (PQ table 1 dis0)
     virtual void range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
                               const float* cdis, int np, float radius, const uint8_t* sel,
                               uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
-                              hipStream_t s) const override;
+                              bool store_pairs, hipStream_t s) const override;
     mutable DeviceBuffer d_pq_, d_terms_, d_cent_;
     // list-centric MFMA scan (kernels_pq_mfma.hip): bf16 decode table, per
     // row |y_R| and bf16 residual norm, per list maxima, |y_C| per list

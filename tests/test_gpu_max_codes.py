@@ -116,7 +116,14 @@ def test_parallel_mode(amd, orc, flat_ivf):
     try:
         D3, I3 = flat_ivf.search(xq, 10)
         assert_same_results(D3, I3, D0, I0)
-        flat_ivf.parallel_mode = 1
+        # modes 1 / 2 (probe-parallel in the reference) give mode 0's
+        # distances (tests/test_index_accuracy.py:47-60); the GPU computes
+        # them as mode 0
+        for pm in (1, 2):
+            flat_ivf.parallel_mode = pm
+            Dp, Ip = flat_ivf.search(xq, 10)
+            assert_same_results(Dp, Ip, D0, I0)
+        flat_ivf.parallel_mode = 1024  # PARALLEL_MODE_NO_HEAP_INIT: not offered
         with pytest.raises(amd.FaissError, match="parallel_mode"):
             flat_ivf.search(xq, 10)
     finally:

@@ -176,10 +176,22 @@ def test_range_search_pq_bit_exact(amd, orc, pq_ix, table):
     check_equal(got_sel, ref.range_search_preassigned(xq, r, Iq, selmask=mask, coarse_dis=Dq))
 
 
-def test_range_search_pq_ip_not_supported(amd, orc, gpu):
+def test_range_search_pq_ip(amd, orc, gpu):
+    """IVF-PQ inner-product range search (dis > radius) equals the oracle
+    restatement (pinned to the reference in tests/test_ref_fixtures.py)"""
     xb = rand(orc, 3000, D_, 100)
     idx = amd.index_factory(D_, "IVF16,PQ8", amd.METRIC_INNER_PRODUCT)
     idx.train(xb)
     idx.add(xb)
-    with pytest.raises(amd.FaissError):
-        idx.range_search(xb[:5], 1.0)
+    idx.nprobe = 4
+    xq = xb[:20]
+    ref = orc.IVFOracle.from_index(idx)
+    q = amd.IndexFlat(D_, amd.METRIC_INNER_PRODUCT)
+    q.add(idx.quantizer.xb)
+    Dq, Iq = q.search(xq, 4)
+    radius = float(np.median(ref.search_preassigned(xq, 10, Iq, Dq)[0][:, 5]))
+    lims, D, I = idx.range_search(xq, radius)
+    lr, Dr, Ir = ref.range_search_preassigned(xq, radius, Iq, coarse_dis=Dq)
+    np.testing.assert_array_equal(lims, lr)
+    np.testing.assert_array_equal(I, Ir)
+    np.testing.assert_array_equal(D, Dr)
