@@ -1,0 +1,84 @@
+"""Every BASELINE.json config at its own geometry on the HIP path, checked
+against the oracle restatement (itself pinned to the reference library in
+tests/test_ref_fixtures.py).
+
+  c2  IVF4096,Flat d=128, nb = 1M, nq = 10k, nprobe 32        (full size)
+  c3  IVF4096,PQ32x8 d=128, nb = 1M, nq = 10k, nprobe 32      (full size)
+  c4  IVF16384_HNSW32,Flat d=128, efSearch 16 / 64 / 128, nprobe 64
+      (quantizer geometry of c4; nb = 1M of its 10M, nq = 2000)
+  c5  IVF65536,PQ48 d=96, nprobe 64 (one shard's geometry; nb = 2M of the
+      12.5M of an 8-GPU shard, nq = 2000)
+Ids and distances must be equal bit for bit (data: faiss float_rand streams,
+xb seed 1234, xq seed 5678, as bench.py).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def build(amd, desc, d, nb, ntrain, seed=1234):
+    xb = amd.float_rand(nb * d, seed).reshape(nb, d)
+    idx = amd.index_factory(d, desc)
+    idx.train(xb[:ntrain])
+    idx.add(xb)
+    return idx
+
+
+def check(D, I, Dr, Ir, what):
+    bad = np.nonzero((I != Ir).any(axis=1))[0]
+    assert bad.size == 0, f"{what}: {bad.size} queries differ, first {bad[:4]}"
+    assert np.array_equal(D, Dr), f"{what}: max |dD| {np.abs(D - Dr).max()}"
+
+
+def test_c2_ivf4096_flat_full(amd, orc, gpu):
+    d, nq = 128, 10_000
+    idx = build(amd, "IVF4096,Flat", d, 1_000_000, 200_000)
+    idx.nprobe = 32
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    D, I = idx.search(xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, 32, nslices=1)
+    check(D, I, Dr, Ir, "c2")
+
+
+def test_c3_ivf4096_pq32_full(amd, orc, gpu):
+    d, nq = 128, 10_000
+    idx = build(amd, "IVF4096,PQ32", d, 1_000_000, 200_000)
+    assert idx.use_precomputed_table == 1  # 4096 x 32 x 256 x 4 B <= 2 GiB
+    idx.nprobe = 32
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    D, I = idx.search(xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, 32, nslices=1)
+    check(D, I, Dr, Ir, "c3")
+
+
+@pytest.fixture(scope="module")
+def c4_index(amd):
+    return build(amd, "IVF16384_HNSW32,Flat", 128, 1_000_000, 638_976)
+
+
+@pytest.mark.parametrize("ef", [16, 64, 128])
+def test_c4_hnsw32_ivf16384(amd, orc, gpu, c4_index, ef):
+    d, nq = 128, 2000
+    idx = c4_index
+    idx.nprobe = 64
+    amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", ef)
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    D, I = idx.search(xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, 64, efSearch=ef, nslices=1)
+    check(D, I, Dr, Ir, f"c4 efSearch {ef}")
+
+
+def test_c5_ivf65536_pq48_shard(amd, orc, gpu):
+    d, nq = 96, 2000
+    idx = build(amd, "IVF65536,PQ48", d, 2_000_000, 65536 * 16)
+    assert idx.use_precomputed_table == 0  # 65536 x 48 x 256 x 4 B > 2 GiB
+    idx.nprobe = 64
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    D, I = idx.search(xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, 64, nslices=1)
+    check(D, I, Dr, Ir, "c5")

@@ -79,8 +79,8 @@ def test_cfg1_lowlevel_decomposition(amd, orc, cfg1):
     assert_same_results(Dq, Iq, Dqr, Iqr)
 
 
-@pytest.mark.parametrize("nprobe", [1, 3, 17, 64])
-@pytest.mark.parametrize("k", [1, 5, 37, 64])
+@pytest.mark.parametrize("nprobe", [1, 3, 17, 64, 100, 256])
+@pytest.mark.parametrize("k", [1, 5, 37, 64, 100, 1024])
 def test_ivfflat_nprobe_k_grid(amd, orc, cfg1, nprobe, k):
     idx, xb, xq = cfg1
     idx.nprobe = nprobe
@@ -91,13 +91,17 @@ def test_ivfflat_nprobe_k_grid(amd, orc, cfg1, nprobe, k):
 
 
 def test_ivfflat_exhaustive_equals_exact(amd, orc, cfg1):
+    """nprobe = nlist visits every list: the result is the exact k-NN of the
+    whole base, as a flat index (direct form of fvec_L2sqr) computes it"""
     idx, xb, xq = cfg1
-    idx.nprobe = 256 if False else 64  # nprobe <= 64 on this path
+    idx.nprobe = idx.nlist
     q = xq[:50]
     D, I = idx.search(q, 10)
     ref = orc.IVFOracle.from_index(idx)
-    Dr, Ir, _, _ = ref.search(q, 10, 64, nslices=1)
+    Dr, Ir, _, _ = ref.search(q, 10, idx.nlist, nslices=1)
     assert_same_results(D, I, Dr, Ir)
+    De, Ie = orc.knn(q, xb, 10, metric=1, blas_form=False)
+    assert_same_results(D, I, De, Ie)
 
 
 def test_ivfflat_edge_cases(amd, orc, gpu):
