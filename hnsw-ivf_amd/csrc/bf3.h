@@ -21,7 +21,8 @@ namespace kern {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int BQ = 64;    // queries per work item
+constexpr int BQ = 64;    // queries per work item (IVF-PQ filter)
+constexpr int FQ = 128;   // queries per work item (IVF-Flat filter)
 constexpr int BV = 64;    // database rows per tile
 constexpr int BDM = 128;  // max padded dim (multiple of 16)
 

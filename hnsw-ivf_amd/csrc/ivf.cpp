@@ -149,8 +149,9 @@ void IndexIVF::reset() {
     dirty_ = true;
 }
 
-// Arena upload: lists packed contiguously, each list start aligned to 16
-// rows; rows padded to the device stride; ids / owning list per row.
+// Arena upload: lists packed contiguously, each list start and extent aligned
+// to ARENA_ALIGN (64) rows = one filter tile; rows padded to the device
+// stride; ids / owning list per row (~0 for padding rows).
 void IndexIVF::sync_device() const {
     quantizer->sync_device();
     std::lock_guard<std::recursive_mutex> g(mu_);
@@ -165,7 +166,7 @@ void IndexIVF::sync_device() const {
     for (size_t l = 0; l < nlist; l++) {
         off[l] = (uint32_t)rows;
         len[l] = (uint32_t)invlists->list_size(l);
-        rows += roundup(len[l], 16);
+        rows += roundup(len[l], kern::ARENA_ALIGN);
         FAISS_THROW_IF_NOT_MSG(rows < (1ull << 32), "arena larger than 2^32 rows");
     }
     off[nlist] = (uint32_t)rows;
@@ -231,7 +232,7 @@ void IndexIVF::sync_device() const {
         };
         for (size_t l = 0; l < nlist; l++) {
             put_rows(invlists->get_codes(l), len[l]);
-            put_rows(nullptr, roundup(len[l], 16) - len[l]);
+            put_rows(nullptr, roundup(len[l], kern::ARENA_ALIGN) - len[l]);
         }
         if (rows == 0) put_rows(nullptr, 1);
         flush();
@@ -573,8 +574,10 @@ void IndexIVFFlat::upload_extra() const {
     const int l = (int)roundup((size_t)d, 4);
     d_ynorm_.reserve(sizeof(float) * std::max<size_t>(arena_rows_, 1));
     d_ynmax_.reserve(sizeof(float) * std::max<size_t>(nlist, 1));
-    if (arena_rows_ > 0)
+    if (arena_rows_ > 0) {
         kern::row_norms(d_codes_.as<float>(), arena_rows_, d, l, d_ynorm_.as<float>(), s);
+        kern::pad_rows_inf(d_ynorm_.as<float>(), d_row_list_.as<uint32_t>(), arena_rows_, s);
+    }
     kern::ivf_list_ynmax(d_ynorm_.as<float>(), d_list_off_.as<uint32_t>(),
                          d_list_len_.as<uint32_t>(), (int)nlist, d_ynmax_.as<float>(), s);
     // bf16 hi/lo image of the arena for the MFMA filter (same bytes as f32)
@@ -585,6 +588,11 @@ void IndexIVFFlat::upload_extra() const {
         d_rres_.reserve(sizeof(float) * std::max<size_t>(arena_rows_, 1));
         d_rmax_.reserve(sizeof(float) * std::max<size_t>(nlist, 1));
         kern::row_resnorm_bf16(d_codes_.as<float>(), arena_rows_, d, l, d_rres_.as<float>(), s);
+        // the streamed filter's image: bf16 hi + norm per row (2 DB + 16 bytes)
+        const int DBs = kern::bf3_db_host(d) / 2 * 2;
+        d_cbs_.reserve(std::max<size_t>(arena_rows_, 1) * (2 * (size_t)DBs + 16));
+        kern::split_bf16_stream(d_codes_.as<float>(), arena_rows_, d, l, DBs,
+                                d_ynorm_.as<float>(), d_row_list_.as<uint32_t>(), d_cbs_.ptr, s);
         kern::ivf_list_ynmax(d_rres_.as<float>(), d_list_off_.as<uint32_t>(),
                              d_list_len_.as<uint32_t>(), (int)nlist, d_rmax_.as<float>(), s);
         size_t mx = 0;
@@ -611,7 +619,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
         return;
     }
     std::lock_guard<std::recursive_mutex> g(mu_);
-    const int QT = 64;
+    const int QT = kern::IVF_FLAT_QT;
     const int l = (int)roundup((size_t)d, 4);
     uint32_t* counts_next = nullptr;
     uint32_t* counts = bucket_counts(s, &counts_next);
@@ -647,7 +655,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
                              d_list_len_.as<uint32_t>(), (int)nlist, d, obits_, n, np, (int)k, l2,
                              b, max_items, s_part_.as<uint32_t>(), s_pk2_.as<kern::ProbeRec>(),
                              dbg ? s_flags_.as<uint32_t>() : nullptr, distances, labels, &ktimes,
-                             s);
+                             s, kern::ARENA_ALIGN, d_cbs_.ptr);
     if (dbg) {
         uint32_t st[4];
         HIP_CHECK(hipMemcpyAsync(st, s_flags_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));

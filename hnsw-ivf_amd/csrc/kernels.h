@@ -214,6 +214,13 @@ void select_rows_exact(const float* D, int64_t nx, int64_t ny, int64_t ldD, int 
 // stats[0] += non-empty lists visited, stats[1] += codes scanned (device)
 void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_len, int nlist,
                      const uint32_t* lim, unsigned long long* stats, hipStream_t s);
+// list starts (and list extents) in the arena are aligned to this many rows
+// (one filter tile), padding rows zero with row_list == ~0
+constexpr int ARENA_ALIGN = 64;
+// padding rows (row_list == ~0) get +inf in v (the streamed filter's norms)
+void pad_rows_inf(float* v, const uint32_t* row_list, int64_t rows, hipStream_t s);
+// queries per work item of the IVF-Flat MFMA filter (bf3.h FQ)
+constexpr int IVF_FLAT_QT = 128;
 // upper bound on the number of work items (grid size without a host sync)
 inline int64_t ivf_max_items(int64_t n, int nprobe, int nlist, int QT) {
     return (n * nprobe + QT - 1) / QT + nlist;
@@ -244,7 +251,12 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         const uint32_t* list_off, const uint32_t* list_len, int nlist, int d,
                         int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
                         int64_t max_items, uint32_t* keys, ProbeRec* recs, uint32_t* stats,
-                        float* D, int64_t* I, KernelTimes* kt, hipStream_t s);
+                        float* D, int64_t* I, KernelTimes* kt, hipStream_t s,
+                        int list_align = 16, const void* cbs = nullptr);
+// stream image of the arena for the streamed filter: per row bf16(code) (DB
+// dims) + fp32 norm (+inf for padding rows) + 12 zero bytes = 2 DB + 16 bytes
+void split_bf16_stream(const float* codes, int64_t rows, int d, int ldc, int DB,
+                       const float* ynorm, const uint32_t* row_list, void* out, hipStream_t s);
 // ---------------- IVF-PQ ----------------
 // term[v] = sum_m (||c_{m,code}||^2 + 2 <yC_m, c_{m,code}>) for every arena row
 void ivfpq_terms(const uint8_t* codes, const uint32_t* row_list, int64_t nrows,

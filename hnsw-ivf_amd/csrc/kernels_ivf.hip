@@ -296,9 +296,6 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
     }
 }
 
-// ---------------------------------------------------------------- scan
-constexpr int SQT = 64;   // queries per work item
-constexpr int SVT = 32;   // codes per tile (8 reference-order partial sums per pair)
 
 }  // namespace kern
 }  // namespace faiss_amd

@@ -44,6 +44,8 @@
 namespace faiss_amd {
 namespace kern {
 
+static_assert(FQ == IVF_FLAT_QT, "host and filter must agree on the work-item width");
+
 
 // ---------------------------------------------------------------- A
 // Filter on bf16x3 MFMA (v_mfma_f32_32x32x16_bf16).  Every f32 value is
@@ -114,23 +116,23 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     // two code tiles (double buffer), row stride CSB bytes = (Y3 ? 4 : 2) * DB + 16
     __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * BV * ((Y3 ? 4 : 2) * 16 * NS + 16)];
     __shared__ __attribute__((aligned(16))) float ynt[2][BV];  // row norm (L2) / bias (IP)
-    __shared__ uint32_t ent_s[BQ];
-    __shared__ int32_t qrow_s[BQ];
-    __shared__ float bnd_s[BQ][4];
+    __shared__ uint32_t ent_s[FQ];
+    __shared__ int32_t qrow_s[FQ];
+    __shared__ float bnd_s[FQ][4];
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t xcd = blockIdx.x & 7u, rest = blockIdx.x >> 3;
     const uint32_t item = 4u * ((rest >> 2) * 8u + xcd) + (rest & 3u);
     // one round trip: the item count, the item's descriptor and its entries
-    // (fixed stride BQ) are independent loads
+    // (fixed stride FQ) are independent loads
     const uint32_t nitems = item_off[nlist];
     const uint32_t it = item < max_items ? item : 0u;
     const ItemDesc dsc = item_desc[it];
-    const uint32_t e_raw = t < BQ ? item_entries[(size_t)it * BQ + t] : 0u;
+    const uint32_t e_raw = t < FQ ? item_entries[(size_t)it * FQ + t] : 0u;
     if (item >= nitems) return;
     const int l = (int)dsc.l;
     const int nQ = (int)dsc.nq;
-    if (t < BQ) {
+    if (t < FQ) {
         const uint32_t e = t < nQ ? e_raw : 0u;
         ent_s[t] = e;
         qrow_s[t] = t < nQ ? (int32_t)(e / (uint32_t)nprobe) : -1;
@@ -141,11 +143,11 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     constexpr int CSB = (Y3 ? 4 : 2) * DB + 16;  // LDS row stride (bytes)
     constexpr int RU = (Y3 ? DB / 4 : DB / 8);   // uint4 staged per code row
     constexpr int PF = (BV * RU + 255) / 256;    // uint4 per thread per tile
-    const int bi = w >> 1, bj = w & 1;
+    // wave w owns query columns 32w .. 32w + 31 and both 32-row halves bi of
+    // every tile: thread (li, lh) keeps streams slot = 2 bi + lh of query qloc
     const int li = lane & 31, lh = lane >> 5;
-    const int slot = 2 * bi + lh;    // this thread's share of its query's codes
-    const int qloc = 32 * bj + li;   // this thread's query (0..63)
-    const bool active = 32 * bj < nQ;  // wave-uniform
+    const int qloc = 32 * w + li;     // this thread's query (0..127)
+    const bool active = 32 * w < nQ;  // wave-uniform
     const float* ynl = ynorm + row0;
 
     // ---- code tiles: global -> registers -> LDS (+ the tile's row norms)
@@ -208,8 +210,9 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     __syncthreads();
     const unsigned long long ft1 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
 
-    ThreadQueue32<KT> tq;
-    tq.init();
+    ThreadQueue32<KT> tq[2];
+    tq[0].init();
+    tq[1].init();
     const uint32_t lowmask = (1u << obits) - 1u;
 
     for (int v0 = 0, tile = 0; v0 < len; v0 += BV, tile++) {
@@ -221,19 +224,25 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
             if (v0 + 2 * BV < len) fetch(v0 + 2 * BV);
         }
         if (active) {
-            // norms / biases of this lane's 16 rows: 32bi + 4lh + 8g + (0..3)
-            float4 yq[4];
-#pragma unroll
-            for (int g = 0; g < 4; g++) yq[g] = *(const float4*)(&ynt[buf][32 * bi + 4 * lh + 8 * g]);
-            const uint8_t* arow = tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh;
-            const floatx16 acc = Y3 ? bf3_block<NS>(arow, bh, bl) : bf2_block<NS>(arow, bh, bl);
             const uint32_t ordbase = (uint32_t)tile << 4;
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int g = r >> 2, c = r & 3;
-                const float yv = c == 0 ? yq[g].x : c == 1 ? yq[g].y : c == 2 ? yq[g].z : yq[g].w;
-                const float a = L2 ? fmaf(-2.f, acc[r], xn + yv) : yv - acc[r];
-                tq.push(key_encode<L2>(a, lowmask, ordbase | (uint32_t)r));
+            for (int bi = 0; bi < 2; bi++) {
+                // norms / biases of this lane's 16 rows: 32bi + 4lh + 8g + (0..3)
+                float4 yq[4];
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+                    yq[g] = *(const float4*)(&ynt[buf][32 * bi + 4 * lh + 8 * g]);
+                const uint8_t* arow = tiles + buf * BV * CSB + (32 * bi + li) * CSB + 16 * lh;
+                const floatx16 acc =
+                        Y3 ? bf3_block<NS>(arow, bh, bl) : bf2_block<NS>(arow, bh, bl);
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int g = r >> 2, c = r & 3;
+                    const float yv =
+                            c == 0 ? yq[g].x : c == 1 ? yq[g].y : c == 2 ? yq[g].z : yq[g].w;
+                    const float a = L2 ? fmaf(-2.f, acc[r], xn + yv) : yv - acc[r];
+                    tq[bi].push(key_encode<L2>(a, lowmask, ordbase | (uint32_t)r));
+                }
             }
         }
         __syncthreads();
@@ -242,35 +251,44 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
     // ---- outputs
     const unsigned long long ft2 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const bool qvalid = qloc < nQ;
-    const uint32_t last = tq.q[KT - 1];
-    float bnd = WS_INF;  // lower bound of every dropped candidate (none: +inf)
-    if (last != 0xffffffffu) {
-        const uint32_t ord = last & lowmask;
-        const int r = (int)(ord & 15u);
-        const int row = (int)((ord >> 4) * BV) + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-        // a padding row in the last slot: every real row of this stream is kept
-        if (row < len) bnd = key_decode_lo<L2>(last, lowmask);
+#pragma unroll
+    for (int bi = 0; bi < 2; bi++) {
+        const uint32_t last = tq[bi].q[KT - 1];
+        float bnd = WS_INF;  // lower bound of every dropped candidate (none: +inf)
+        if (last != 0xffffffffu) {
+            const uint32_t ord = last & lowmask;
+            const int r = (int)(ord & 15u);
+            const int row =
+                    (int)((ord >> 4) * BV) + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
+            // a padding row in the last slot: every real row of this stream is kept
+            if (row < len) bnd = key_decode_lo<L2>(last, lowmask);
+        }
+        bnd_s[qloc][2 * bi + lh] = bnd;
     }
-    bnd_s[qloc][slot] = bnd;
     __syncthreads();
     if (qvalid) {
         // raw 32-bit keys (the re-rank decodes the approx bracket and the row)
         const int64_t e = ent_s[qloc];
         // max_codes: only a prefix of the list is scanned for this query
         const uint32_t elen = lim ? min((uint32_t)len, lim[e]) : (uint32_t)len;
-        uint32_t* ko = keys + e * (4 * KT) + slot * KT;
 #pragma unroll
-        for (int i = 0; i < KT; i++) {
-            const uint32_t key = tq.q[i];
-            const uint32_t ord = key & lowmask;
-            const int r = (int)(ord & 15u);
-            const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-            if constexpr (HS)
-                ko[i] = (key != 0xffffffffu && row < elen && sel[row0 + row]) ? key : 0xffffffffu;
-            else
-                ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
+        for (int bi = 0; bi < 2; bi++) {
+            const int slot = 2 * bi + lh;
+            uint32_t* ko = keys + e * (4 * KT) + slot * KT;
+#pragma unroll
+            for (int i = 0; i < KT; i++) {
+                const uint32_t key = tq[bi].q[i];
+                const uint32_t ord = key & lowmask;
+                const int r = (int)(ord & 15u);
+                const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
+                if constexpr (HS)
+                    ko[i] = (key != 0xffffffffu && row < elen && sel[row0 + row]) ? key
+                                                                                   : 0xffffffffu;
+                else
+                    ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
+            }
         }
-        if (slot == 0) {
+        if (lh == 0) {
             // the list's largest margin bounds every kept row's margin:
             // Y3: coef (x^2 + y^2); bf16x2: Cauchy-Schwarz on the code
             // rounding residual, 2 (2 |x| |y - yh| + coef (x^2 + y^2))
@@ -299,6 +317,237 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
         ftrace[8 * item + 5] = ftb;
         ftrace[8 * item + 6] = (unsigned long long)len | ((unsigned long long)nQ << 32);
     }
+}
+
+// ---------------------------------------------------------------- A'
+// The bf16x2 filter with its code tiles streamed global -> LDS by
+// global_load_lds (no register staging), three LDS tile buffers and counted
+// vmcnt waits: tile j + 2 is in flight while tiles j and j + 1 are computed,
+// with one raw s_barrier per tile.  Same work item, math, keys and records
+// as k_ivf_bf3_filter (the re-rank reads them unchanged).
+// Source: the "stream image" of the arena, one SR = 2 DB + 16 byte row per
+// code: bf16(code) hi part, then the row's fp32 norm (+inf for padding rows)
+// and 12 zero bytes (split_bf16_stream).  Lists are aligned to BV rows, so a
+// tile never leaves its list: padding rows' keys sort after every real
+// candidate and the epilogue drops them by row index.  The LDS image is the
+// rows back to back (glds writes 1 KB blocks linearly); the 16-B tail makes
+// the row stride 4 banks mod 64, so the 16 rows of a ds_read_b128 quarter
+// hit distinct banks without a swizzle.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {  // s_waitcnt vmcnt(N) alone
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <bool L2, int KT, int NS>
+__global__ __launch_bounds__(256, 3) void k_ivf_bf2_stream(
+        const float* __restrict__ x, int ldx, int d, const uint8_t* __restrict__ cbs,
+        const float* __restrict__ ynmax, const float* __restrict__ rmax, int nprobe, float coef,
+        int obits, const uint32_t* __restrict__ item_off, const ItemDesc* __restrict__ item_desc,
+        const uint32_t* __restrict__ item_entries, uint32_t max_items, int nlist,
+        const uint32_t* __restrict__ lim, uint32_t* __restrict__ keys,
+        ProbeRec* __restrict__ recs) {
+    constexpr int DB = 16 * NS;          // bf16 per code row
+    constexpr int SR = 2 * DB + 16;      // bytes per stream-image row
+    constexpr int TB = BV * SR;          // bytes per tile (a multiple of 1 KB)
+    static_assert(TB % 1024 == 0, "tile = whole 1 KB glds blocks");
+    constexpr int NG = TB / 1024;        // glds blocks per tile
+    constexpr int G0 = (NG + 3) / 4;     // blocks of wave 0 (waves w: blocks w, w+4, ...)
+    constexpr int G1 = (NG + 2) / 4;
+    constexpr int G2 = (NG + 1) / 4;
+    constexpr int G3 = NG / 4;
+    constexpr int NB = 3;                // LDS tile buffers
+    // all LDS in one array (a second __shared__ object can make hipcc wait
+    // vmcnt(0) before the tile reads): NB tiles | bounds [FQ][4]
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NB * TB + FQ * 4 * 4];
+    uint8_t* tiles = smem;
+    float* bnd_s = (float*)(smem + NB * TB);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t xcd = blockIdx.x & 7u, rest = blockIdx.x >> 3;
+    const uint32_t item = 4u * ((rest >> 2) * 8u + xcd) + (rest & 3u);
+    const uint32_t nitems = item_off[nlist];
+    const uint32_t it = item < max_items ? item : 0u;
+    const ItemDesc dsc = item_desc[it];
+    const int li = lane & 31, lh = lane >> 5;
+    const int qloc = 32 * w + li;  // this thread's query (0..127)
+    const uint32_t my_e = item_entries[(size_t)it * FQ + qloc];
+    if (item >= nitems) return;
+    const int l = (int)dsc.l;
+    const int nQ = (int)dsc.nq;
+    const int len = (int)dsc.len;
+    const int64_t row0 = dsc.off;
+    const int ntile = (len + BV - 1) / BV;
+    const bool active = 32 * w < nQ;  // wave-uniform
+    const bool qvalid = qloc < nQ;
+
+    // glds of tile j into buffer b: the tile's rows are contiguous in the
+    // stream image and in LDS; wave w copies 1 KB blocks w, w + 4, ...
+    auto issue = [&](int j, int b) {
+        const uint8_t* src = cbs + (row0 + (int64_t)j * BV) * SR + 16 * lane;
+        uint8_t* dst = tiles + b * TB;
+#pragma unroll
+        for (int g = 0; g < G0; g++) {
+            const int blk = w + 4 * g;
+            if (g < G3 || blk < NG)  // wave-uniform
+                __builtin_amdgcn_global_load_lds(
+                        (const void*)(src + blk * 1024),
+                        (__attribute__((address_space(3))) void*)(dst + blk * 1024), 16, 0, 0);
+        }
+    };
+    // wait until at most `tiles_ahead` tiles of this wave's glds are pending
+    auto wait_tiles = [&](int tiles_ahead) {
+        if (tiles_ahead == 0) {
+            wait_vmcnt<0>();
+        } else if (w == 0) {
+            wait_vmcnt<G0>();
+        } else if (w == 1) {
+            wait_vmcnt<G1>();
+        } else if (w == 2) {
+            wait_vmcnt<G2>();
+        } else {
+            wait_vmcnt<G3>();
+        }
+    };
+    issue(0, 0);
+    if (ntile > 1) issue(1, 1);
+
+    // query fragments (B operand): registers for the whole work item
+    bf16x8 bh[NS], bl[NS];
+    float xn = 0.f;
+    if (active)
+        load_query_frags<NS>(x, ldx, d, qvalid ? (int32_t)(my_e / (uint32_t)nprobe) : -1, lh, bh,
+                             bl, xn);
+
+    ThreadQueue32<KT> tq[2];
+    tq[0].init();
+    tq[1].init();
+    const uint32_t lowmask = (1u << obits) - 1u;
+    int b = 0;  // buffer of tile j
+    for (int j = 0; j < ntile; j++) {
+        // tile j landed (this wave's part); tile j + 1 may still be in flight
+        wait_tiles(j + 1 < ntile ? 1 : 0);
+        __builtin_amdgcn_s_barrier();  // every wave's part; tile j - 1 consumed
+        if (j + 2 < ntile) issue(j + 2, b == 0 ? 2 : b - 1);  // the buffer of tile j - 1
+        if (active) {
+            const uint32_t ordbase = (uint32_t)j << 4;
+            const uint8_t* T = tiles + b * TB;
+#pragma unroll
+            for (int bi = 0; bi < 2; bi++) {
+                const uint8_t* arow = T + (32 * bi + li) * SR + 16 * lh;
+                bf16x8 ah[NS];
+#pragma unroll
+                for (int s = 0; s < NS; s++) ah[s] = *(const bf16x8*)(arow + 32 * s);
+                floatx16 acc;
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[r] = 0.f;
+#pragma unroll
+                for (int s = 0; s < NS; s++) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
+                }
+                // this lane's 16 rows: 32 bi + 4 lh + 8 g + c (norm at byte 2 DB)
+                const uint8_t* nrow = T + (32 * bi + 4 * lh) * SR + 2 * DB;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int g = r >> 2, c = r & 3;
+                    const float yv0 = *(const float*)(nrow + (8 * g + c) * SR);
+                    // IP: bias 0 for real rows, +inf for padding
+                    const float yv = L2 ? yv0 : (yv0 < WS_INF ? 0.f : WS_INF);
+                    const float a = L2 ? fmaf(-2.f, acc[r], xn + yv) : yv - acc[r];
+                    tq[bi].push(key_encode<L2>(a, lowmask, ordbase | (uint32_t)r));
+                }
+                // keep the two blocks' live ranges apart (register pressure)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        b = b == 2 ? 0 : b + 1;
+    }
+
+    // ---- outputs (no glds in flight: plain barriers from here)
+#pragma unroll
+    for (int bi = 0; bi < 2; bi++) {
+        const uint32_t last = tq[bi].q[KT - 1];
+        float bnd = WS_INF;  // lower bound of every dropped candidate (none: +inf)
+        if (last != 0xffffffffu) {
+            const uint32_t ord = last & lowmask;
+            const int r = (int)(ord & 15u);
+            const int row = (int)((ord >> 4) * BV) + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
+            if (row < len) bnd = key_decode_lo<L2>(last, lowmask);
+        }
+        bnd_s[qloc * 4 + 2 * bi + lh] = bnd;
+    }
+    __syncthreads();
+    if (qvalid) {
+        const int64_t e = my_e;
+        const uint32_t elen = lim ? min((uint32_t)len, lim[e]) : (uint32_t)len;
+#pragma unroll
+        for (int bi = 0; bi < 2; bi++) {
+            uint32_t* ko = keys + e * (4 * KT) + (2 * bi + lh) * KT;
+#pragma unroll
+            for (int i = 0; i < KT; i++) {
+                const uint32_t key = tq[bi].q[i];
+                const uint32_t ord = key & lowmask;
+                const int r = (int)(ord & 15u);
+                const uint32_t row = (ord >> 4) * BV + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
+                ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
+            }
+        }
+        if (lh == 0) {
+            const float mmax =
+                    2.f * (2.f * sqrtf(xn) * rmax[l] + coef * (xn + ynmax[l])) + 1e-30f;
+            ProbeRec pr;
+#pragma unroll
+            for (int sl = 0; sl < 4; sl++) {
+                const float bb = bnd_s[qloc * 4 + sl];
+                pr.pb[sl] = bb < WS_INF ? bb - mmax : WS_INF;
+            }
+            pr.mmax = mmax;
+            pr.off = (uint32_t)row0;
+            pr.len = elen;
+            pr.pad = 0u;
+            recs[e] = pr;
+        }
+    }
+}
+
+// stream image row r: bf16(code) for dims < d (zero beyond, DB dims), then
+// the fp32 norm (+inf for padding rows, row_list == ~0) and 12 zero bytes
+__global__ void k_split_stream(const float* __restrict__ codes, int64_t rows, int d, int ldc,
+                               int DB, const float* __restrict__ ynorm,
+                               const uint32_t* __restrict__ row_list, uint8_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int per = DB + 8;  // bf16 slots per row (the last 8 = the 16-B tail)
+    if (i >= rows * per) return;
+    const int64_t r = i / per;
+    const int j = (int)(i - r * per);
+    uint8_t* row = out + r * (int64_t)(2 * DB + 16);
+    if (j < DB) {
+        const float v = j < d ? codes[r * ldc + j] : 0.f;
+        ((__bf16*)row)[j] = (__bf16)v;
+    } else if (j == DB) {
+        *(float*)(row + 2 * DB) = row_list[r] == 0xffffffffu ? WS_INF : ynorm[r];
+    } else if (j > DB + 1) {
+        ((uint16_t*)row)[DB + (j - DB)] = 0;  // bytes 2 DB + 4 .. 2 DB + 15
+    }
+}
+void split_bf16_stream(const float* codes, int64_t rows, int d, int ldc, int DB,
+                       const float* ynorm, const uint32_t* row_list, void* out, hipStream_t s) {
+    if (rows <= 0) return;
+    const int64_t tot = rows * (DB + 8);
+    k_split_stream<<<dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, s>>>(
+            codes, rows, d, ldc, DB, ynorm, row_list, (uint8_t*)out);
+    HIP_LAUNCH_CHECK();
+}
+
+__global__ void k_pad_rows_inf(float* __restrict__ v, const uint32_t* __restrict__ row_list,
+                               int64_t rows) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < rows && row_list[i] == 0xffffffffu) v[i] = WS_INF;
+}
+void pad_rows_inf(float* v, const uint32_t* row_list, int64_t rows, hipStream_t s) {
+    if (rows <= 0) return;
+    k_pad_rows_inf<<<dim3((unsigned)cdiv(rows, 256)), dim3(256), 0, s>>>(v, row_list, rows);
+    HIP_LAUNCH_CHECK();
 }
 
 // per-list max row norm (margin of dropped candidates)
@@ -866,8 +1115,10 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         const uint32_t* list_off, const uint32_t* list_len, int nlist, int d,
                         int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
                         int64_t max_items, uint32_t* keys, ProbeRec* recs, uint32_t* stats,
-                        float* D, int64_t* I, KernelTimes* kt, hipStream_t s) {
+                        float* D, int64_t* I, KernelTimes* kt, hipStream_t s, int list_align,
+                        const void* cbs) {
     if (n <= 0) return;
+    const bool aligned_lists = list_align % BV == 0 && cbs != nullptr;
     const int KE = ivf_mfma_kq(k, d);
     FAISS_THROW_IF_NOT(KE > 0);
     FAISS_THROW_IF_NOT(ldc % 4 == 0);
@@ -901,11 +1152,22 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         ftrace = ftrace_buf;
     }
     const float coef = (float)(y3 ? ivf_bf3_coef(d) : ivf_bf2_coef(d));
+    // streamed (glds) bf16x2 filter: the default; the register-staged kernel
+    // serves bf16x3, IDSelectors and the per-item trace
+    // (FAISS_AMD_IVF_FILTER=staged forces it)
+    const char* fenv = getenv("FAISS_AMD_IVF_FILTER");
+    const bool stream_ok = aligned_lists && !y3 && !b.sel && !ftrace && d <= BDM &&
+                           !(fenv && !strcmp(fenv, "staged"));
     {
         ScopedKernelTimer tm(kt, "ivf_flat_scan", 0.0, s);
 #define LAUNCH_NS(L2V, KTV, NSV)                                                              \
     do {                                                                                      \
-        if (b.sel)                                                                            \
+        if (stream_ok)                                                                        \
+            k_ivf_bf2_stream<L2V, KTV, NSV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(       \
+                    x, ldx, d, (const uint8_t*)cbs, ynmax, rmax, nprobe, coef, obits,         \
+                    b.item_off, b.item_desc, b.item_entries, (uint32_t)max_items, nlist,      \
+                    b.lim, keys, recs);                                                       \
+        else if (b.sel)                                                                       \
             k_ivf_bf3_filter<L2V, KTV, NSV, false, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \

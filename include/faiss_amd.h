@@ -487,7 +487,7 @@ struct IndexIVFFlat : IndexIVF {
                               const float* cdis, int np, float radius, const uint8_t* sel,
                               uint32_t* counts, const uint64_t* offs, float* D, idx_t* I,
                               bool store_pairs, hipStream_t s) const override;
-    mutable DeviceBuffer d_ynorm_, d_ynmax_, d_cbf_, d_rres_, d_rmax_, s_part_, s_flags_;
+    mutable DeviceBuffer d_ynorm_, d_ynmax_, d_cbf_, d_cbs_, d_rres_, d_rmax_, s_part_, s_flags_;
     mutable int obits_ = 4;
 };
 

@@ -11,7 +11,7 @@ f = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
 if marker is None:  # the step's last kernel: the IVF re-rank (MFMA paths) or the PQ scan
     names = [r["Kernel_Name"] for r in rows]
-    marker = next(m for m in ("k_ivf_rerank", "k_ivfpq_scan", "k_ivf_exact_fallback")
+    marker = next(m for m in ("k_ivf_rerank", "k_ex_select", "k_ivfpq_scan")
                   if any(m in n for n in names))
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
 # the bench's timed steps run back to back: take the consecutive pair of
