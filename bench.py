@@ -51,7 +51,7 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector == fp32 MFMA peak
 PEAK_HBM_GBS = 8000.0
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 # dominant kernel per workload (device symbol substring) for the PMC traffic
-DOMINANT = {"flat": "k_ivf_bf3_filter", "pq": "k_ivfpq_scan", "pqm": "k_ivfpq_filter"}
+DOMINANT = {"flat": "k_ivf_bf2_stream", "pq": "k_ivfpq_scan", "pqm": "k_ivfpq_filter"}
 
 
 def pmc_traffic(config, kernel_sub):

@@ -60,6 +60,17 @@ __device__ __forceinline__ uint32_t key_encode(float a, uint32_t lowmask, uint32
     const uint32_t bits = L2 ? __float_as_uint(fmaxf(a, 0.f)) : ordered_f32(a);
     return (bits & ~lowmask) | ord;
 }
+// key_encode in two steps for the filters' inner loop: the clamped / folded
+// value bits, then the ordinal inserted by one v_bfi_b32 (ord < 2^obits)
+template <bool L2>
+__device__ __forceinline__ uint32_t key_bits(float a) {
+    return L2 ? __float_as_uint(fmaxf(a, 0.f)) : ordered_f32(a);
+}
+__device__ __forceinline__ uint32_t key_insert(uint32_t bits, uint32_t lowmask, uint32_t ord) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(lowmask), "s"(ord), "v"(bits));
+    return r;
+}
 template <bool L2>
 __device__ __forceinline__ float key_decode_lo(uint32_t key, uint32_t lowmask) {
     return L2 ? __uint_as_float(key & ~lowmask) : unordered_f32(key & ~lowmask);
@@ -84,12 +95,10 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& l
 // to roundup(d, 4) <= ldx); dims >= d are zeroed.  qr < 0 (an unused column,
 // whose results are discarded) reads row 0.
 template <int NS>
-__device__ __forceinline__ void load_query_frags(const float* __restrict__ x, int ldx, int d,
-                                                 int qr, int lh, bf16x8 (&bh)[NS],
-                                                 bf16x8 (&bl)[NS], float& xn) {
+__device__ __forceinline__ void query_raw_load(const float* __restrict__ x, int ldx, int d, int qr,
+                                               int lh, float4 (&raw)[2 * NS]) {
     const float* xr = x + (int64_t)(qr < 0 ? 0 : qr) * ldx;
     const int d4 = (d + 3) & ~3;
-    float4 raw[2 * NS];
 #pragma unroll
     for (int s = 0; s < NS; s++)
 #pragma unroll
@@ -98,6 +107,11 @@ __device__ __forceinline__ void load_query_frags(const float* __restrict__ x, in
             // clamped address: every load is unconditional (no branches)
             raw[2 * s + u] = *(const float4*)(xr + min(kk, d4 - 4));
         }
+}
+template <int NS>
+__device__ __forceinline__ void query_frags_from_raw(const float4 (&raw)[2 * NS], int d, int lh,
+                                                     bf16x8 (&bh)[NS], bf16x8 (&bl)[NS],
+                                                     float& xn) {
     xn = 0.f;
 #pragma unroll
     for (int s = 0; s < NS; s++) {
@@ -110,6 +124,14 @@ __device__ __forceinline__ void load_query_frags(const float* __restrict__ x, in
         for (int j = 0; j < 8; j++) xn = fmaf(v[j], v[j], xn);
     }
     xn += __shfl_xor(xn, 32);
+}
+template <int NS>
+__device__ __forceinline__ void load_query_frags(const float* __restrict__ x, int ldx, int d,
+                                                 int qr, int lh, bf16x8 (&bh)[NS],
+                                                 bf16x8 (&bl)[NS], float& xn) {
+    float4 raw[2 * NS];
+    query_raw_load<NS>(x, ldx, d, qr, lh, raw);
+    query_frags_from_raw<NS>(raw, d, lh, bh, bl, xn);
 }
 
 // One 32x32 block: A = 32 database rows (hi/lo image in LDS, this lane's row

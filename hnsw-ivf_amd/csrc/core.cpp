@@ -168,6 +168,9 @@ void IndexFlat::sync_device() const {
             s_tile_.reserve(sizeof(float) * ntotal);
             kern::row_resnorm_bf16(d_xb_.as<float>(), ntotal, d, l, s_tile_.as<float>(), s);
             kern::array_max(s_tile_.as<float>(), ntotal, d_cnmax_.as<float>() + 1, s);
+            d_cst_.reserve(kern::coarse_stream_image_bytes(ntotal, d));
+            kern::coarse_stream_image(d_xb_.as<float>(), ntotal, d, l, d_norms_.as<float>(),
+                                      d_cst_.ptr, s);
         }
     }
     HIP_CHECK(hipStreamSynchronize(s));
@@ -246,7 +249,8 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
                                  d_xb_.as<float>(), l, d_cbf_.ptr, d_norms_.as<float>(),
                                  d_cnmax_.as<float>(), (int)ny, d, k, metric_l2,
                                  s_cand_i_.as<uint32_t>(), s_tile_.as<float>(), distances + q0 * k,
-                                 o32 ? o32 + q0 * k : nullptr, o64 ? o64 + q0 * k : nullptr, s);
+                                 o32 ? o32 + q0 * k : nullptr, o64 ? o64 + q0 * k : nullptr, s,
+                                 d_cst_.ptr);
         }
         return;
     }

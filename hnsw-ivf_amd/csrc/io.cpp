@@ -59,9 +59,55 @@ std::string fourcc_str(uint32_t h) {
     return s;
 }
 
+// A file written next to its target and renamed over it on commit(): saving
+// an index back to the file it was mapped from (IO_FLAG_MMAP, or an ilod data
+// file) must not truncate the mapping it is reading the lists through (the
+// old inode stays alive while mapped).  Removed again when not committed.
+struct AtomicFile {
+    std::string target, tmp;
+    FILE* f = nullptr;
+    explicit AtomicFile(const std::string& path) : target(path) {
+        tmp = path + ".tmpXXXXXX";
+        int fd = mkstemp(&tmp[0]);
+        FAISS_THROW_IF_NOT_MSG(fd >= 0, "could not open " + path + " for writing: " +
+                                                strerror(errno));
+        f = fdopen(fd, "wb");
+        if (!f) {
+            close(fd);
+            unlink(tmp.c_str());
+            FAISS_THROW_MSG("could not open " + path + " for writing");
+        }
+    }
+    AtomicFile(const AtomicFile&) = delete;
+    AtomicFile& operator=(const AtomicFile&) = delete;
+    // flush and close; the data is complete under the temporary name
+    void finish() {
+        if (!f) return;
+        const bool ok = fflush(f) == 0 && !ferror(f);
+        const bool closed = fclose(f) == 0;
+        f = nullptr;
+        FAISS_THROW_IF_NOT_MSG(ok && closed, "write error on " + target);
+    }
+    void commit() {
+        finish();
+        // mkstemp creates 0600; give the file the usual umask-derived mode
+        const mode_t um = umask(0);
+        umask(um);
+        chmod(tmp.c_str(), 0666 & ~um);
+        FAISS_THROW_IF_NOT_MSG(rename(tmp.c_str(), target.c_str()) == 0,
+                               "could not rename onto " + target + ": " + strerror(errno));
+        tmp.clear();
+    }
+    ~AtomicFile() {
+        if (f) fclose(f);
+        if (!tmp.empty()) unlink(tmp.c_str());
+    }
+};
+
 struct Writer {
     FILE* f;
     const char* ondisk_fname = nullptr;  // write_index_ondisk: lists go to this file
+    AtomicFile* ondisk_file = nullptr;   // ... written through this (renamed by the caller)
     void bytes(const void* p, size_t n) {
         if (n && fwrite(p, 1, n, f) != n) FAISS_THROW_MSG("write error");
     }
@@ -152,26 +198,20 @@ void write_ilod(const ArrayInvertedLists* il, Writer& w, const std::string& fnam
 void write_invlists(const ArrayInvertedLists* il, Writer& w) {
     if (w.ondisk_fname) {
         // data file: per non-empty list codes[size*code_size] then ids[size]
-        FILE* df = fopen(w.ondisk_fname, "wb");
-        FAISS_THROW_IF_NOT_MSG(df, std::string("could not open ") + w.ondisk_fname);
-        Writer dw{df};
+        FAISS_THROW_IF_NOT(w.ondisk_file && w.ondisk_file->f);
+        Writer dw{w.ondisk_file->f};
         std::vector<size_t> lists(3 * il->nlist, 0);
         size_t o = 0;
-        try {
-            for (size_t l = 0; l < il->nlist; l++) {
-                const size_t n = il->list_size(l);
-                lists[3 * l] = lists[3 * l + 1] = n;
-                lists[3 * l + 2] = o;
-                if (!n) continue;
-                dw.bytes(il->get_codes(l), n * il->code_size);
-                dw.bytes(il->get_ids(l), n * sizeof(idx_t));
-                o += n * (il->code_size + sizeof(idx_t));
-            }
-        } catch (...) {
-            fclose(df);
-            throw;
+        for (size_t l = 0; l < il->nlist; l++) {
+            const size_t n = il->list_size(l);
+            lists[3 * l] = lists[3 * l + 1] = n;
+            lists[3 * l + 2] = o;
+            if (!n) continue;
+            dw.bytes(il->get_codes(l), n * il->code_size);
+            dw.bytes(il->get_ids(l), n * sizeof(idx_t));
+            o += n * (il->code_size + sizeof(idx_t));
         }
-        fclose(df);
+        w.ondisk_file->finish();
         write_ilod(il, w, w.ondisk_fname, lists, o);
         return;
     }
@@ -302,7 +342,8 @@ void read_invlists(ArrayInvertedLists* il, Reader& r, size_t nlist, size_t code_
             const size_t size = lists[3 * l], cap = lists[3 * l + 1], o = lists[3 * l + 2];
             FAISS_THROW_IF_NOT_MSG(size <= cap, "ilod: list size > capacity");
             if (!size) continue;
-            FAISS_THROW_IF_NOT_MSG(o + cap * (cs + sizeof(idx_t)) <= m->size,
+            // overflow-safe: o + cap * (cs + 8) <= size without wrapping
+            FAISS_THROW_IF_NOT_MSG(o <= m->size && cap <= (m->size - o) / (cs + sizeof(idx_t)),
                                    "ilod: list extends past the end of the data file");
             il->map_sizes[l] = size;
             il->map_codes[l] = m->ptr + o;
@@ -340,8 +381,9 @@ void read_invlists(ArrayInvertedLists* il, Reader& r, size_t nlist, size_t code_
         il->map_ids.assign(nl, nullptr);
         il->map_sizes = sizes;
         for (size_t i = 0; i < nl; i++) {
+            FAISS_THROW_IF_NOT_MSG(o <= m->size && sizes[i] <= (m->size - o) / (cs + sizeof(idx_t)),
+                                   "read error: truncated index file");
             const size_t bytes = sizes[i] * (cs + sizeof(idx_t));
-            FAISS_THROW_IF_NOT_MSG(o + bytes <= m->size, "read error: truncated index file");
             il->map_codes[i] = m->ptr + o;
             il->map_ids[i] = (const idx_t*)(m->ptr + o + sizes[i] * cs);
             o += bytes;
@@ -500,27 +542,20 @@ void write_index(const Index* idx, FILE* f) {
 void write_index_ondisk(const Index* idx, const char* fname, const char* lists_fname) {
     FAISS_THROW_IF_NOT_MSG(dynamic_cast<const IndexIVF*>(idx),
                            "write_index_ondisk: only IVF indexes have inverted lists");
-    FILE* f = fopen(fname, "wb");
-    FAISS_THROW_IF_NOT_MSG(f, std::string("could not open ") + fname + " for writing");
-    try {
-        Writer w{f, lists_fname};
-        write_index_impl(idx, w);
-    } catch (...) {
-        fclose(f);
-        throw;
-    }
-    fclose(f);
+    // both files are written under temporary names and renamed at the end,
+    // so neither truncates a mapping the lists are read from
+    AtomicFile df(lists_fname);
+    AtomicFile f(fname);
+    Writer w{f.f, lists_fname, &df};
+    write_index_impl(idx, w);
+    f.finish();
+    df.commit();
+    f.commit();
 }
 void write_index(const Index* idx, const char* fname) {
-    FILE* f = fopen(fname, "wb");
-    FAISS_THROW_IF_NOT_MSG(f, std::string("could not open ") + fname + " for writing");
-    try {
-        write_index(idx, f);
-    } catch (...) {
-        fclose(f);
-        throw;
-    }
-    fclose(f);
+    AtomicFile f(fname);
+    write_index(idx, f.f);
+    f.commit();
 }
 Index* read_index(FILE* f, int io_flags) {
     Reader r{f, ""};

@@ -257,12 +257,21 @@ void IndexIVF::sync_device() const {
 
 uint32_t* IndexIVF::bucket_counts(hipStream_t s, uint32_t** next) const {
     // two halves of nlist counters; a (re)allocation starts both at zero
+    // (re)zeroed as well when the previous call did not reach flip_counts()
+    // (an exception between the two left a half dirty) or ran on another
+    // stream (whose scan may still be zeroing the half used now)
     const size_t need = sizeof(uint32_t) * 2 * std::max<size_t>(nlist, 1);
-    if (!s_counts_.ptr || s_counts_.bytes < need) {
+    const bool fresh = !s_counts_.ptr || s_counts_.bytes < need;
+    if (fresh || counts_pending_ || s != counts_stream_) {
+        if (!fresh && s != counts_stream_ && counts_stream_valid_)
+            HIP_CHECK(hipStreamSynchronize(counts_stream_));
         s_counts_.reserve(need);
         HIP_CHECK(hipMemsetAsync(s_counts_.ptr, 0, need, s));
         counts_parity_ = 0;
     }
+    counts_stream_ = s;
+    counts_stream_valid_ = true;
+    counts_pending_ = true;  // until flip_counts()
     uint32_t* base = s_counts_.as<uint32_t>();
     *next = base + (size_t)(1 - counts_parity_) * nlist;
     return base + (size_t)counts_parity_ * nlist;
@@ -642,6 +651,8 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     s_ient_.reserve(sizeof(uint32_t) * max_items * QT);
     b.item_desc = s_idesc_.as<kern::ItemDesc>();
     b.item_entries = s_ient_.as<uint32_t>();
+    s_ictr_.reserve(16);
+    b.item_ctr = s_ictr_.as<uint32_t>();
     kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), d_list_off_.as<uint32_t>(),
                      (int)nlist, QT, b, s);
     flip_counts();

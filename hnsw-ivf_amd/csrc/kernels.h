@@ -49,7 +49,13 @@ CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k);
 void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, const float* xnorm,
                     const float* cent, int ldc, const void* cbf, const float* cnorm,
                     const float* cnmax, int nlist, int d, int k, int metric_l2, uint32_t* keys,
-                    float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s);
+                    float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s,
+                    const void* cst = nullptr);
+// the streamed coarse filter's image of the centroids: per row bf16 hi | lo
+// (bf3_db(d) dims each) | fp32 norm | 12 B, padded to 64 rows (+inf norms)
+void coarse_stream_image(const float* codes, int64_t rows, int d, int ldc, const float* norms,
+                         void* out, hipStream_t s);
+size_t coarse_stream_image_bytes(int64_t rows, int d);
 void array_max(const float* a, int64_t n, float* out, hipStream_t s);
 
 // k smallest (L2) / largest (IP) per row of D, ties by column index,
@@ -105,6 +111,7 @@ struct IVFBuckets {
     uint32_t* cursor;      // [n * nprobe]: slot of each entry in its bucket
     uint32_t* entries;     // [n * nprobe], entry = q * nprobe + rank
     uint32_t* item_list = nullptr;  // [max_items]: list of each work item
+    uint32_t* item_ctr = nullptr;   // [1]: zeroed by the scan (persistent filter's counter)
     // optional (MFMA filter path): per work item its descriptor and its
     // entries at a fixed stride of QT (so a work item's first loads do not
     // depend on each other)

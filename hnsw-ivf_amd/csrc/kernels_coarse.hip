@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <vector>
 
 #include "bf3.h"
 #include "common.h"
@@ -195,6 +196,219 @@ __global__ __launch_bounds__(256, 2) void k_coarse_bf3_filter(
             bnd = key_decode_lo<L2>(last, lowmask);
         pbs[(q * nsplit + sp) * 4 + slot] = bnd < WS_INF ? bnd - M : WS_INF;
     }
+}
+
+// Streamed form (the default): 128 queries x one split per work group, the
+// split's 64-centroid tiles copied global -> LDS by global_load_lds from the
+// coarse stream image (per centroid: bf16 hi | bf16 lo | fp32 norm | 12 B; the
+// image is padded to 64 rows with +inf-norm rows), two tile buffers, one raw
+// barrier per tile (the IVF-Flat filter's k_ivf_bf2_stream pattern, here with
+// bf16x3 blocks).  Work groups are ordered split-major per XCD (split s on
+// XCD s mod 8, every query block of a split on the same XCD): a split's tiles
+// are read from HBM once per XCD and then served from its L2.  Same keys and
+// dropped bounds as k_coarse_bf3_filter; the 4 thread streams of a (query,
+// split) are slot = 2 bi + lh.
+template <int N>
+__device__ __forceinline__ void cwait_vmcnt() {  // s_waitcnt vmcnt(N) alone
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <bool L2, int KT, int NS>
+__global__ __launch_bounds__(256, 2) void k_coarse_stream(
+        const float* __restrict__ x, int ldx, int64_t n, int d, const uint8_t* __restrict__ cst,
+        const float* __restrict__ xnorm, int nlist, int nsplit, int split_len, int nqb,
+        float coef, const float* __restrict__ cnmax_p, int obits, uint32_t* __restrict__ keys,
+        float* __restrict__ pbs, unsigned long long* __restrict__ trace) {
+    // FAISS_AMD_COARSE_TRACE: per work group (wave 0) s_memtime stamps —
+    // [0] start, [1] query fragments loaded, then per tile j: [2 + 2j] before
+    // the tile wait, [3 + 2j] after its barrier
+    unsigned long long* tr = (trace && threadIdx.x == 0) ? trace + 160ull * blockIdx.x : nullptr;
+    if (tr) tr[0] = __builtin_amdgcn_s_memtime();
+    constexpr int DB = 16 * NS;       // bf16 per part
+    constexpr int SR = 4 * DB + 16;   // bytes per image row: hi | lo | norm | pad
+    constexpr int TB = BV * SR;       // bytes per tile (whole KB)
+    static_assert(TB % 1024 == 0, "tile = whole 1 KB glds blocks");
+    constexpr int NG = TB / 1024;
+    constexpr int G0 = (NG + 3) / 4;
+    constexpr int G3 = NG / 4;
+    __shared__ __attribute__((aligned(16))) uint8_t tiles[2 * TB];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    // split-major per XCD: blocks b = 8 m + xcd, m = j * nqb + qb, split
+    // 8 j + xcd (nsplit a multiple of 8) — or block = sp * nqb + qb otherwise
+    int sp, qb;
+    if ((nsplit & 7) == 0) {
+        const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
+        sp = 8 * (m / nqb) + xcd;
+        qb = m % nqb;
+    } else {
+        sp = blockIdx.x / nqb;
+        qb = blockIdx.x % nqb;
+    }
+    const int c0 = sp * split_len;
+    const int len = min(split_len, nlist - c0);
+    const int ntile = (len + BV - 1) / BV;
+    const int qloc = 32 * w + li;
+    const int64_t q = (int64_t)qb * 128 + qloc;
+    const bool active = (int64_t)qb * 128 + 32 * w < n;  // wave-uniform
+
+    auto issue = [&](int j, int b) {
+        const uint8_t* src = cst + ((int64_t)c0 + (int64_t)j * BV) * SR + 16 * lane;
+        uint8_t* dst = tiles + b * TB;
+#pragma unroll
+        for (int g = 0; g < G0; g++) {
+            const int blk = w + 4 * g;
+            if (g < G3 || blk < NG)
+                __builtin_amdgcn_global_load_lds(
+                        (const void*)(src + blk * 1024),
+                        (__attribute__((address_space(3))) void*)(dst + blk * 1024), 16, 0, 0);
+        }
+    };
+    issue(0, 0);
+    bf16x8 bh[NS], bl[NS];
+    float xn_approx;
+    if (active) load_query_frags<NS>(x, ldx, d, q < n ? (int)q : -1, lh, bh, bl, xn_approx);
+    const float xn = (active && q < n) ? xnorm[q] : 0.f;  // the reference-order norm
+    if (tr) tr[1] = __builtin_amdgcn_s_memtime();
+
+    ThreadQueue32<KT> tq[2];
+    tq[0].init();
+    tq[1].init();
+    const uint32_t lowmask = (1u << obits) - 1u;
+    // the 16 norms of block bi of tile T: rows 32 bi + 4 lh + 8 g + c
+    auto norms = [&](const uint8_t* T, int bi, float (&nv)[16]) {
+        const uint8_t* nrow = T + (32 * bi + 4 * lh) * SR + 4 * DB;
+#pragma unroll
+        for (int r = 0; r < 16; r++) nv[r] = *(const float*)(nrow + (8 * (r >> 2) + (r & 3)) * SR);
+    };
+    auto push1 = [&](ThreadQueue32<KT>& pq, float accr, float yv0, uint32_t ord) {
+        const float yv = L2 ? yv0 : (yv0 < WS_INF ? 0.f : WS_INF);  // IP: padding +inf
+        // L2: clamped at 0 inside key_bits, as the reference clamps
+        const float a = L2 ? fmaf(-2.f, accr, xn + yv) : yv - accr;
+        pq.push(key_insert(key_bits<L2>(a), lowmask, ord));
+    };
+    // bf16x3 MFMAs of block bi of tile T with the 16 pushes of the previous
+    // block interleaved between its k-steps (their VALU issues in the MFMA
+    // gaps of this wave instead of after the chain)
+    auto mfma_push = [&](const uint8_t* T, int bi, const floatx16& pacc, const float (&pn)[16],
+                         const uint8_t* pnT, uint32_t pord, ThreadQueue32<KT>& pq) {
+        const uint8_t* arow = T + (32 * bi + li) * SR + 16 * lh;
+        bf16x8 ah[NS], al[NS];
+#pragma unroll
+        for (int s2 = 0; s2 < NS; s2++) {
+            ah[s2] = *(const bf16x8*)(arow + 32 * s2);
+            al[s2] = *(const bf16x8*)(arow + 2 * DB + 32 * s2);
+        }
+        floatx16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc[r] = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < NS; s2++) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s2], bh[s2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s2], bl[s2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s2], bh[s2], acc, 0, 0, 0);
+#pragma unroll
+            for (int r = 16 * s2 / NS; r < 16 * (s2 + 1) / NS; r++)
+                push1(pq, pacc[r],
+                      pnT ? *(const float*)(pnT + (8 * (r >> 2) + (r & 3)) * SR) : pn[r],
+                      pord | (uint32_t)r);
+        }
+        return acc;
+    };
+    // software pipeline over blocks: phase A = MFMAs of (tile j, block 1) +
+    // pushes of (j, 0); phase B = MFMAs of (j + 1, 0) + pushes of (j, 1).
+    // The norms of a block are read with its MFMAs (its buffer is refilled
+    // before its pushes may run).
+    floatx16 acc0, acc1;
+    float n1[16];
+    cwait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // tile 0 (every wave's part)
+    if (ntile > 1) issue(1, 1);
+    if (active) {
+        acc0 = bf3_block<NS>(tiles + (0 * SR) + li * SR + 16 * lh, bh, bl);
+    }
+    int b = 0;
+    for (int j = 0; j < ntile; j++) {
+        const uint8_t* T = tiles + b * TB;
+        const uint32_t ordbase = (uint32_t)j << 4;
+        if (active) {
+            // (block 0's norms straight from LDS: tile j stays until the barrier)
+            acc1 = mfma_push(T, 1, acc0, n1, T + 4 * lh * SR + 4 * DB, ordbase, tq[0]);
+            norms(T, 1, n1);
+        }
+        if (j + 1 < ntile) {
+            if (tr && j < 78) tr[2 + 2 * j] = __builtin_amdgcn_s_memtime();
+            cwait_vmcnt<0>();  // tile j + 1 (this wave's part)
+            __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0): tile j read
+            __builtin_amdgcn_s_barrier();  // every wave: tile j + 1 landed, tile j consumed
+            if (tr && j < 78) tr[3 + 2 * j] = __builtin_amdgcn_s_memtime();
+            if (j + 2 < ntile) issue(j + 2, b);
+            const uint8_t* T1 = tiles + (b ^ 1) * TB;
+            if (active) {
+                acc0 = mfma_push(T1, 0, acc1, n1, nullptr, ordbase, tq[1]);
+            }
+        } else if (active) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) push1(tq[1], acc1[r], n1[r], ordbase | (uint32_t)r);
+        }
+        b ^= 1;
+    }
+    if (active && q < n) {
+        const float M = coarse_margin(xn, cnmax_p, coef, true);
+        const int E1 = 4 * KT;
+#pragma unroll
+        for (int bi = 0; bi < 2; bi++) {
+            const int slot = 2 * bi + lh;
+            uint32_t* ko = keys + (q * nsplit + sp) * E1 + slot * KT;
+#pragma unroll
+            for (int i = 0; i < KT; i++) {
+                const uint32_t key = tq[bi].q[i];
+                const uint32_t row = ivf_key_row(key, lowmask, slot);
+                ko[i] = (key != 0xffffffffu && row < (uint32_t)len) ? key : 0xffffffffu;
+            }
+            const uint32_t last = tq[bi].q[KT - 1];
+            float bnd = WS_INF;
+            if (last != 0xffffffffu && ivf_key_row(last, lowmask, slot) < (uint32_t)len)
+                bnd = key_decode_lo<L2>(last, lowmask);
+            pbs[(q * nsplit + sp) * 4 + slot] = bnd < WS_INF ? bnd - M : WS_INF;
+        }
+    }
+}
+
+// coarse stream image: row r < rows = bf16 hi | bf16 lo of the centroid (DB
+// dims each, zero past d) | its norm | 12 zero bytes; rows past `rows` (up to
+// the 64-row padding) are zero with a +inf norm
+__global__ void k_coarse_image(const float* __restrict__ codes, int64_t rows, int64_t rows_pad,
+                               int d, int ldc, int DB, const float* __restrict__ norms,
+                               uint8_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int per = DB + 4;  // slots per row: DB (hi, lo) pairs, norm, 3 pad words
+    if (i >= rows_pad * per) return;
+    const int64_t r = i / per;
+    const int j = (int)(i - r * per);
+    uint8_t* row = out + r * (int64_t)(4 * DB + 16);
+    if (j < DB) {
+        const float v = (r < rows && j < d) ? codes[r * ldc + j] : 0.f;
+        const __bf16 h = (__bf16)v;
+        ((__bf16*)row)[j] = h;
+        ((__bf16*)row)[DB + j] = (__bf16)(v - (float)h);
+    } else {
+        float* tail = (float*)(row + 4 * DB);
+        tail[j - DB] = j == DB ? (r < rows ? norms[r] : WS_INF) : 0.f;
+    }
+}
+void coarse_stream_image(const float* codes, int64_t rows, int d, int ldc, const float* norms,
+                         void* out, hipStream_t s) {
+    const int DB = bf3_db(d);
+    const int64_t rows_pad = (int64_t)roundup((size_t)std::max<int64_t>(rows, 1), BV);
+    const int64_t tot = rows_pad * (DB + 4);
+    k_coarse_image<<<dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, s>>>(
+            codes, rows, rows_pad, d, ldc, DB, norms, (uint8_t*)out);
+    HIP_LAUNCH_CHECK();
+}
+size_t coarse_stream_image_bytes(int64_t rows, int d) {
+    return (size_t)roundup((size_t)std::max<int64_t>(rows, 1), BV) * (4 * bf3_db(d) + 16);
 }
 
 constexpr int CR_CAP = 512;
@@ -455,7 +669,8 @@ CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k) {
 void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, const float* xnorm,
                     const float* cent, int ldc, const void* cbf, const float* cnorm,
                     const float* cnmax, int nlist, int d, int k, int metric_l2, uint32_t* keys,
-                    float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s) {
+                    float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s,
+                    const void* cst) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(p.ok);
     static uint32_t* stats = nullptr;  // FAISS_AMD_IVF_STATS debug counters
@@ -472,12 +687,33 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     const char* prec = getenv("FAISS_AMD_COARSE_PREC");
     const bool y3 = !(prec && !strcmp(prec, "bf16x2"));
     const float coef = (float)(y3 ? ivf_bf3_coef(d) : ivf_bf2_coef(d));
-    const int64_t nqb = (int64_t)cdiv((size_t)n, BQ);
+    // streamed bf16x3 kernel (default when the image exists;
+    // FAISS_AMD_COARSE=staged: the register-staged one)
+    const char* cenv = getenv("FAISS_AMD_COARSE");
+    const bool stream = cst && y3 && !(cenv && !strcmp(cenv, "staged"));
+    static unsigned long long* ctrace_buf = nullptr;
+    static int64_t ctrace_n = 0;
+    const char* ctr = getenv("FAISS_AMD_COARSE_TRACE");
+    unsigned long long* ctrace = nullptr;
+    const int64_t nqb = (int64_t)cdiv((size_t)n, stream ? 128 : BQ);
     const int64_t grid = nqb * p.nsplit;
     FAISS_THROW_IF_NOT(grid < (1ll << 31));
+    if (ctr && stream) {
+        if (ctrace_n < grid) {
+            if (ctrace_buf) HIP_CHECK(hipFree(ctrace_buf));
+            HIP_CHECK(hipMalloc(&ctrace_buf, 160 * 8 * grid));
+            ctrace_n = grid;
+        }
+        HIP_CHECK(hipMemsetAsync(ctrace_buf, 0, 160 * 8 * grid, s));
+        ctrace = ctrace_buf;
+    }
 #define LAUNCH_NS(L2V, KTV, NSV)                                                              \
     do {                                                                                      \
-        if (y3)                                                                               \
+        if (stream)                                                                           \
+            k_coarse_stream<L2V, KTV, NSV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(        \
+                    x, ldx, n, d, (const uint8_t*)cst, xnorm, nlist, p.nsplit, p.split_len,   \
+                    (int)nqb, coef, cnmax, p.obits, keys, pbs, ctrace);                       \
+        else if (y3)                                                                          \
             k_coarse_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, n, d, (const __bf16*)cbf, cnorm, xnorm, nlist, p.nsplit,          \
                     p.split_len, coef, cnmax, p.obits, keys, pbs);                            \
@@ -505,6 +741,15 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
 #undef LAUNCH_A
 #undef LAUNCH_NS
     HIP_LAUNCH_CHECK();
+    if (ctrace) {
+        std::vector<unsigned long long> h(160 * grid);
+        HIP_CHECK(hipMemcpyAsync(h.data(), ctrace, 160 * 8 * grid, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        if (FILE* f = fopen(ctr, "wb")) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+        }
+    }
     const int E = p.entries;
     const int V = E <= 64 ? 1 : E <= 128 ? 2 : E <= 256 ? 4 : E <= 512 ? 8 : 16;
     FAISS_THROW_IF_NOT(E <= 1024 && V <= p.kt);

@@ -94,7 +94,8 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
                                                       uint32_t* __restrict__ bucket_off,
                                                       uint32_t* __restrict__ item_off,
                                                       uint32_t* __restrict__ item_list,
-                                                      uint32_t* __restrict__ zero_next) {
+                                                      uint32_t* __restrict__ zero_next,
+                                                      uint32_t* __restrict__ item_ctr) {
     __shared__ uint32_t wb[16], wi[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint32_t carry_b = 0, carry_i = 0;
@@ -152,6 +153,7 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
     if (t == 0) {
         bucket_off[nlist] = carry_b;
         item_off[nlist] = carry_i;
+        if (item_ctr) *item_ctr = 0u;  // the persistent filter's work counter
     }
 }
 
@@ -285,7 +287,7 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
         HIP_LAUNCH_CHECK();
     }
     k_bucket_scan<<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off, b.item_off,
-                                                 b.item_list, b.counts_next);
+                                                 b.item_list, b.counts_next, b.item_ctr);
     HIP_LAUNCH_CHECK();
     if (total > 0) {
         k_bucket_fill<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(

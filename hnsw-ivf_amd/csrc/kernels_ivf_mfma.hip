@@ -321,10 +321,13 @@ __global__ __launch_bounds__(256, Y3 ? 2 : 3) void k_ivf_bf3_filter(
 
 // ---------------------------------------------------------------- A'
 // The bf16x2 filter with its code tiles streamed global -> LDS by
-// global_load_lds (no register staging), three LDS tile buffers and counted
-// vmcnt waits: tile j + 2 is in flight while tiles j and j + 1 are computed,
-// with one raw s_barrier per tile.  Same work item, math, keys and records
-// as k_ivf_bf3_filter (the re-rank reads them unchanged).
+// global_load_lds (no register staging) and one raw s_barrier per tile.  NB
+// LDS tile buffers: NB = 2 (used: 35 KB, 4 work groups per CU) keeps tile
+// j + 1 in flight while tile j is computed; NB = 3 (3 groups per CU, counted
+// vmcnt waits) tile j + 2 — measured equal or slower on c2 (the loaded
+// latency of the work item's first loads, not the tile stream, bounds it).
+// Same work item, math, keys and records as k_ivf_bf3_filter (the re-rank
+// reads them unchanged).
 // Source: the "stream image" of the arena, one SR = 2 DB + 16 byte row per
 // code: bf16(code) hi part, then the row's fp32 norm (+inf for padding rows)
 // and 12 zero bytes (split_bf16_stream).  Lists are aligned to BV rows, so a
@@ -338,15 +341,19 @@ __device__ __forceinline__ void wait_vmcnt() {  // s_waitcnt vmcnt(N) alone
     static_assert(N >= 0 && N < 64, "vmcnt range");
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
+__device__ __forceinline__ void wait_lgkmcnt0() {  // s_waitcnt lgkmcnt(0) alone
+    __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
+}
 
-template <bool L2, int KT, int NS>
-__global__ __launch_bounds__(256, 3) void k_ivf_bf2_stream(
+template <bool L2, int KT, int NS, bool PIPE>
+__global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
         const float* __restrict__ x, int ldx, int d, const uint8_t* __restrict__ cbs,
         const float* __restrict__ ynmax, const float* __restrict__ rmax, int nprobe, float coef,
         int obits, const uint32_t* __restrict__ item_off, const ItemDesc* __restrict__ item_desc,
         const uint32_t* __restrict__ item_entries, uint32_t max_items, int nlist,
         const uint32_t* __restrict__ lim, uint32_t* __restrict__ keys,
-        ProbeRec* __restrict__ recs) {
+        ProbeRec* __restrict__ recs, unsigned long long* __restrict__ ftrace) {
+    const unsigned long long ft0 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     constexpr int DB = 16 * NS;          // bf16 per code row
     constexpr int SR = 2 * DB + 16;      // bytes per stream-image row
     constexpr int TB = BV * SR;          // bytes per tile (a multiple of 1 KB)
@@ -356,12 +363,14 @@ __global__ __launch_bounds__(256, 3) void k_ivf_bf2_stream(
     constexpr int G1 = (NG + 2) / 4;
     constexpr int G2 = (NG + 1) / 4;
     constexpr int G3 = NG / 4;
-    constexpr int NB = 3;                // LDS tile buffers
+    constexpr int NB = 2;
+    static_assert(FQ * 4 * 4 <= TB, "bounds fit in a tile buffer");
     // all LDS in one array (a second __shared__ object can make hipcc wait
-    // vmcnt(0) before the tile reads): NB tiles | bounds [FQ][4]
-    __shared__ __attribute__((aligned(16))) uint8_t smem[NB * TB + FQ * 4 * 4];
+    // vmcnt(0) before the tile reads): 2 tiles; after the loop tile buffer 0
+    // holds the bounds [FQ][4].
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NB * TB];
     uint8_t* tiles = smem;
-    float* bnd_s = (float*)(smem + NB * TB);
+    float* bnd_s = (float*)smem;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t xcd = blockIdx.x & 7u, rest = blockIdx.x >> 3;
     const uint32_t item = 4u * ((rest >> 2) * 8u + xcd) + (rest & 3u);
@@ -396,7 +405,7 @@ __global__ __launch_bounds__(256, 3) void k_ivf_bf2_stream(
     };
     // wait until at most `tiles_ahead` tiles of this wave's glds are pending
     auto wait_tiles = [&](int tiles_ahead) {
-        if (tiles_ahead == 0) {
+        if (NB == 2 || tiles_ahead == 0) {
             wait_vmcnt<0>();
         } else if (w == 0) {
             wait_vmcnt<G0>();
@@ -409,7 +418,10 @@ __global__ __launch_bounds__(256, 3) void k_ivf_bf2_stream(
         }
     };
     issue(0, 0);
-    if (ntile > 1) issue(1, 1);
+    if (NB == 3 && ntile > 1) issue(1, 1);
+    // epilogue operands, loaded now (their latency hides under the loop)
+    const float rmax_l = rmax[l], ynmax_l = ynmax[l];
+    const uint32_t lim_e = (lim && qvalid) ? lim[my_e] : 0xffffffffu;
 
     // query fragments (B operand): registers for the whole work item
     bf16x8 bh[NS], bl[NS];
@@ -422,48 +434,128 @@ __global__ __launch_bounds__(256, 3) void k_ivf_bf2_stream(
     tq[0].init();
     tq[1].init();
     const uint32_t lowmask = (1u << obits) - 1u;
-    int b = 0;  // buffer of tile j
-    for (int j = 0; j < ntile; j++) {
-        // tile j landed (this wave's part); tile j + 1 may still be in flight
-        wait_tiles(j + 1 < ntile ? 1 : 0);
-        __builtin_amdgcn_s_barrier();  // every wave's part; tile j - 1 consumed
-        if (j + 2 < ntile) issue(j + 2, b == 0 ? 2 : b - 1);  // the buffer of tile j - 1
-        if (active) {
-            const uint32_t ordbase = (uint32_t)j << 4;
-            const uint8_t* T = tiles + b * TB;
+    const unsigned long long ft1 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    // the 16 norms of block bi of tile T: rows 32 bi + 4 lh + 8 g + c
+    auto norms = [&](const uint8_t* T, int bi, float (&nv)[16]) {
+        const uint8_t* nrow = T + (32 * bi + 4 * lh) * SR + 2 * DB;
 #pragma unroll
-            for (int bi = 0; bi < 2; bi++) {
-                const uint8_t* arow = T + (32 * bi + li) * SR + 16 * lh;
-                bf16x8 ah[NS];
+        for (int r = 0; r < 16; r++) nv[r] = *(const float*)(nrow + (8 * (r >> 2) + (r & 3)) * SR);
+    };
+    auto push1 = [&](ThreadQueue32<KT>& pq, float accr, float yv0, uint32_t ord) {
+        const float yv = L2 ? yv0 : (yv0 < WS_INF ? 0.f : WS_INF);  // IP: padding +inf
+        const float a = L2 ? fmaf(-2.f, accr, xn + yv) : yv - accr;
+        pq.push(key_insert(key_bits<L2>(a), lowmask, ord));
+    };
+    // MFMAs of block bi of tile T with the previous block's 16 pushes
+    // interleaved between its k-steps (their VALU issues in this wave's MFMA
+    // gaps instead of after the chain)
+    auto mfma_push = [&](const uint8_t* T, int bi, const floatx16& pacc, const float (&pn)[16],
+                         const uint8_t* pnT, uint32_t pord, ThreadQueue32<KT>& pq) {
+        const uint8_t* arow = T + (32 * bi + li) * SR + 16 * lh;
+        bf16x8 ah[NS];
 #pragma unroll
-                for (int s = 0; s < NS; s++) ah[s] = *(const bf16x8*)(arow + 32 * s);
-                floatx16 acc;
+        for (int s2 = 0; s2 < NS; s2++) ah[s2] = *(const bf16x8*)(arow + 32 * s2);
+        floatx16 acc;
 #pragma unroll
-                for (int r = 0; r < 16; r++) acc[r] = 0.f;
+        for (int r = 0; r < 16; r++) acc[r] = 0.f;
 #pragma unroll
-                for (int s = 0; s < NS; s++) {
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
-                }
-                // this lane's 16 rows: 32 bi + 4 lh + 8 g + c (norm at byte 2 DB)
-                const uint8_t* nrow = T + (32 * bi + 4 * lh) * SR + 2 * DB;
+        for (int s2 = 0; s2 < NS; s2++) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s2], bl[s2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s2], bh[s2], acc, 0, 0, 0);
 #pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int g = r >> 2, c = r & 3;
-                    const float yv0 = *(const float*)(nrow + (8 * g + c) * SR);
-                    // IP: bias 0 for real rows, +inf for padding
-                    const float yv = L2 ? yv0 : (yv0 < WS_INF ? 0.f : WS_INF);
-                    const float a = L2 ? fmaf(-2.f, acc[r], xn + yv) : yv - acc[r];
-                    tq[bi].push(key_encode<L2>(a, lowmask, ordbase | (uint32_t)r));
-                }
-                // keep the two blocks' live ranges apart (register pressure)
-                __builtin_amdgcn_sched_barrier(0);
-            }
+            for (int r = 16 * s2 / NS; r < 16 * (s2 + 1) / NS; r++)
+                push1(pq, pacc[r],
+                      pnT ? *(const float*)(pnT + (8 * (r >> 2) + (r & 3)) * SR) : pn[r],
+                      pord | (uint32_t)r);
         }
-        b = b == 2 ? 0 : b + 1;
+        return acc;
+    };
+    if constexpr (PIPE) {
+        // software pipeline over blocks: phase A = MFMAs of (tile j, block 1)
+        // + pushes of (j, 0); phase B = MFMAs of (j + 1, 0) + pushes of (j, 1).
+        // A block's norms are read with its MFMAs (its buffer is refilled
+        // before its pushes run).
+        floatx16 acc0, acc1;
+        float n1[16];
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // tile 0 (every wave's part)
+        if (ntile > 1) issue(1, 1);
+        if (active) {
+            acc0 = bf2_block<NS>(tiles + li * SR + 16 * lh, bh, bl);
+        }
+        int b = 0;
+        for (int j = 0; j < ntile; j++) {
+            const uint8_t* T = tiles + b * TB;
+            const uint32_t ordbase = (uint32_t)j << 4;
+            if (active) {
+                // (block 0's norms straight from LDS: tile j stays until the barrier)
+                acc1 = mfma_push(T, 1, acc0, n1, T + 4 * lh * SR + 2 * DB, ordbase, tq[0]);
+                norms(T, 1, n1);
+            }
+            if (j + 1 < ntile) {
+                wait_vmcnt<0>();  // tile j + 1 (this wave's part)
+                wait_lgkmcnt0();  // this wave's reads of tile j
+                __builtin_amdgcn_s_barrier();  // tile j + 1 landed, tile j consumed
+                if (j + 2 < ntile) issue(j + 2, b);
+                const uint8_t* T1 = tiles + (b ^ 1) * TB;
+                if (active) {
+                    acc0 = mfma_push(T1, 0, acc1, n1, nullptr, ordbase, tq[1]);
+                }
+            } else if (active) {
+#pragma unroll
+                for (int r = 0; r < 16; r++) push1(tq[1], acc1[r], n1[r], ordbase | (uint32_t)r);
+            }
+            b ^= 1;
+        }
+    } else {
+        int b = 0;  // buffer of tile j
+        for (int j = 0; j < ntile; j++) {
+            // tile j landed (this wave's part); with NB = 3 tile j + 1 may still
+            // be in flight
+            wait_tiles(j + 1 < ntile ? 1 : 0);
+            __builtin_amdgcn_s_barrier();  // every wave's part; tile j - 1 consumed
+            if (j + NB - 1 < ntile) issue(j + NB - 1, b == 0 ? NB - 1 : b - 1);  // tile j - 1's buffer
+
+
+            if (active) {
+                const uint32_t ordbase = (uint32_t)j << 4;
+                const uint8_t* T = tiles + b * TB;
+#pragma unroll
+                for (int bi = 0; bi < 2; bi++) {
+                    const uint8_t* arow = T + (32 * bi + li) * SR + 16 * lh;
+                    bf16x8 ah[NS];
+#pragma unroll
+                    for (int s = 0; s < NS; s++) ah[s] = *(const bf16x8*)(arow + 32 * s);
+                    floatx16 acc;
+#pragma unroll
+                    for (int r = 0; r < 16; r++) acc[r] = 0.f;
+#pragma unroll
+                    for (int s = 0; s < NS; s++) {
+                        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
+                    }
+                    // this lane's 16 rows: 32 bi + 4 lh + 8 g + c (norm at byte 2 DB)
+                    const uint8_t* nrow = T + (32 * bi + 4 * lh) * SR + 2 * DB;
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const int g = r >> 2, c = r & 3;
+                        const float yv0 = *(const float*)(nrow + (8 * g + c) * SR);
+                        // IP: bias 0 for real rows, +inf for padding
+                        const float yv = L2 ? yv0 : (yv0 < WS_INF ? 0.f : WS_INF);
+                        const float a = L2 ? fmaf(-2.f, acc[r], xn + yv) : yv - acc[r];
+                        tq[bi].push(key_insert(key_bits<L2>(a), lowmask, ordbase | (uint32_t)r));
+                    }
+                    // keep the two blocks' live ranges apart (register pressure)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            b = b == NB - 1 ? 0 : b + 1;
+        }
     }
 
+    const unsigned long long ft2 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     // ---- outputs (no glds in flight: plain barriers from here)
+    __syncthreads();  // every wave is done with the tiles: bounds reuse buffer 0
 #pragma unroll
     for (int bi = 0; bi < 2; bi++) {
         const uint32_t last = tq[bi].q[KT - 1];
@@ -479,7 +571,7 @@ __global__ __launch_bounds__(256, 3) void k_ivf_bf2_stream(
     __syncthreads();
     if (qvalid) {
         const int64_t e = my_e;
-        const uint32_t elen = lim ? min((uint32_t)len, lim[e]) : (uint32_t)len;
+        const uint32_t elen = min((uint32_t)len, lim_e);
 #pragma unroll
         for (int bi = 0; bi < 2; bi++) {
             uint32_t* ko = keys + e * (4 * KT) + (2 * bi + lh) * KT;
@@ -494,7 +586,7 @@ __global__ __launch_bounds__(256, 3) void k_ivf_bf2_stream(
         }
         if (lh == 0) {
             const float mmax =
-                    2.f * (2.f * sqrtf(xn) * rmax[l] + coef * (xn + ynmax[l])) + 1e-30f;
+                    2.f * (2.f * sqrtf(xn) * rmax_l + coef * (xn + ynmax_l)) + 1e-30f;
             ProbeRec pr;
 #pragma unroll
             for (int sl = 0; sl < 4; sl++) {
@@ -507,6 +599,17 @@ __global__ __launch_bounds__(256, 3) void k_ivf_bf2_stream(
             pr.pad = 0u;
             recs[e] = pr;
         }
+    }
+    if (ftrace && t == 0) {  // per-item timestamps (FAISS_AMD_FILTER_TRACE)
+        ftrace[8 * item + 0] = ft0;
+        ftrace[8 * item + 1] = ft1;
+        ftrace[8 * item + 2] = ft2;
+        ftrace[8 * item + 3] = __builtin_amdgcn_s_memrealtime();
+        // HW_ID (wave, simd, cu, sh, se) and XCC_ID registers
+        ftrace[8 * item + 4] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                               ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+        ftrace[8 * item + 5] = (unsigned long long)l;
+        ftrace[8 * item + 6] = (unsigned long long)len | ((unsigned long long)nQ << 32);
     }
 }
 
@@ -1156,17 +1259,22 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     // serves bf16x3, IDSelectors and the per-item trace
     // (FAISS_AMD_IVF_FILTER=staged forces it)
     const char* fenv = getenv("FAISS_AMD_IVF_FILTER");
-    const bool stream_ok = aligned_lists && !y3 && !b.sel && !ftrace && d <= BDM &&
+    const bool stream_ok = aligned_lists && !y3 && !b.sel && d <= BDM &&
                            !(fenv && !strcmp(fenv, "staged"));
+    // block-pipelined streamed filter (3 groups per CU) unless
+    // FAISS_AMD_IVF_PIPE=0 (the sequential form, 4 groups per CU)
+    const char* penv = getenv("FAISS_AMD_IVF_PIPE");
+    const bool spipe = !(penv && !strcmp(penv, "0"));
     {
         ScopedKernelTimer tm(kt, "ivf_flat_scan", 0.0, s);
 #define LAUNCH_NS(L2V, KTV, NSV)                                                              \
     do {                                                                                      \
         if (stream_ok)                                                                        \
-            k_ivf_bf2_stream<L2V, KTV, NSV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(       \
+            (spipe ? k_ivf_bf2_stream<L2V, KTV, NSV, true>                                   \
+                   : k_ivf_bf2_stream<L2V, KTV, NSV, false>)<<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const uint8_t*)cbs, ynmax, rmax, nprobe, coef, obits,         \
                     b.item_off, b.item_desc, b.item_entries, (uint32_t)max_items, nlist,      \
-                    b.lim, keys, recs);                                                       \
+                    b.lim, keys, recs, ftrace);                                               \
         else if (b.sel)                                                                       \
             k_ivf_bf3_filter<L2V, KTV, NSV, false, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \

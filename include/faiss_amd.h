@@ -219,7 +219,7 @@ struct IndexFlat : Index {
     template <class OutIdx>
     void knn_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
                     hipStream_t stream) const;
-    mutable DeviceBuffer d_xb_, d_norms_, d_cbf_, d_cnmax_;
+    mutable DeviceBuffer d_xb_, d_norms_, d_cbf_, d_cnmax_, d_cst_;
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
     mutable DeviceBuffer s_xn_, s_tile_, s_cand_d_, s_cand_i_;
@@ -440,6 +440,7 @@ struct IndexIVF : Index {
     mutable DeviceBuffer d_codes_, d_ids_, d_list_off_, d_list_len_, d_row_list_;
     mutable size_t arena_rows_ = 0;
     // scratch
+    mutable DeviceBuffer s_ictr_;
     mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_counts_, s_boff_, s_ioff_, s_cur_, s_ent_,
             s_pk1_, s_pk2_, s_q_;
     mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_,
@@ -447,7 +448,12 @@ struct IndexIVF : Index {
     // bucket counts of this call (zero) and the half the call's scan clears
     // for the next one; flip_counts() after the bucket kernels are queued
     uint32_t* bucket_counts(hipStream_t s, uint32_t** next) const;
-    void flip_counts() const { counts_parity_ ^= 1; }
+    void flip_counts() const {
+        counts_parity_ ^= 1;
+        counts_pending_ = false;
+    }
+    mutable bool counts_pending_ = false, counts_stream_valid_ = false;
+    mutable hipStream_t counts_stream_ = nullptr;
     mutable int counts_parity_ = 0;
     // one pass of the range scan (counts when offs == nullptr, else fill);
     // cdis = coarse distances [n][np] on the device (PQ table 1 dis0)

@@ -107,3 +107,64 @@ def test_ilod_read_write_roundtrip(amd, tmp_path):
     data.write_bytes(bytes(blob[:len(blob) // 2]))
     with pytest.raises(amd.FaissError):
         amd.read_index(fn)
+
+
+def test_mmap_index_resaved_in_place(amd, tmp_path):
+    """write_index onto the very file the lists are mapped from (IO_FLAG_MMAP)
+    must not truncate the mapping under the index: the file is written under
+    a temporary name and renamed over the target."""
+    sizes, codes, ids = lists_data(seed=6)
+    raw = ivf_prefix(sum(sizes)) + ilar_bytes(sizes, codes, ids)
+    fn = tmp_path / "m.index"
+    fn.write_bytes(raw)
+    idx = amd.read_index(fn, amd.IO_FLAG_MMAP)
+    amd.write_index(idx, fn)
+    assert fn.read_bytes() == raw
+    check_lists(idx, sizes, codes, ids)  # still reads through the old mapping
+    amd.write_index(idx, fn)
+    assert fn.read_bytes() == raw
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["m.index"]  # no temporaries left
+
+
+def test_ilod_data_file_rewritten_in_place(amd, tmp_path):
+    """write_index_ondisk with the data file the lists are mapped from"""
+    sizes, codes, ids = lists_data(seed=7)
+    raw = ivf_prefix(sum(sizes)) + ilar_bytes(sizes, codes, ids)
+    fn = tmp_path / "a.index"
+    fn.write_bytes(raw)
+    data = tmp_path / "lists.ivfdata"
+    amd.write_index_ondisk(amd.read_index(fn), tmp_path / "o.index", data)
+    idx = amd.read_index(tmp_path / "o.index")
+    check_lists(idx, sizes, codes, ids)
+    amd.write_index_ondisk(idx, tmp_path / "o.index", data)
+    check_lists(idx, sizes, codes, ids)
+    check_lists(amd.read_index(tmp_path / "o.index"), sizes, codes, ids)
+
+
+def test_corrupt_list_extents_rejected(amd, tmp_path):
+    """list sizes / capacities whose byte extent wraps around size_t"""
+    sizes, codes, ids = lists_data(seed=8)
+    cs = 4 * D
+    # ilar mapped: a size of 2^61 (times cs + 8 = 40 wraps to a small number)
+    bad = list(sizes)
+    bad[2] = 1 << 61
+    raw = ivf_prefix(sum(sizes)) + ilar_bytes(sizes, codes, ids)
+    lo = raw.index(b"full") + 12
+    raw = raw[:lo] + b"".join(struct.pack("<Q", n) for n in bad) + raw[lo + 8 * NLIST:]
+    fn = tmp_path / "w.index"
+    fn.write_bytes(raw)
+    with pytest.raises(amd.FaissError):
+        amd.read_index(fn, amd.IO_FLAG_MMAP)
+    # ilod: capacity 2^61 with size 1
+    data = tmp_path / "d.ivfdata"
+    data.write_bytes(bytes(4 * (cs + 8)))
+    name = str(data).encode()
+    meta = b"ilod" + struct.pack("<QQQ", NLIST, cs, NLIST)
+    meta += b"".join(struct.pack("<QQQ", *t) for t in
+                     [(1, 1 << 61, 0)] + [(0, 0, 0)] * (NLIST - 1))
+    meta += struct.pack("<Q", 0) + struct.pack("<Q", len(name)) + name
+    meta += struct.pack("<Q", 4 * (cs + 8))
+    fo = tmp_path / "w2.index"
+    fo.write_bytes(ivf_prefix(1) + meta)
+    with pytest.raises(amd.FaissError):
+        amd.read_index(fo)
