@@ -181,6 +181,10 @@ def _declare(L):
         "faiss_amd_IndexShardsIVF_new": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_int, C.c_int]),
         "faiss_amd_IndexShardsIVF_add_shard": (C.c_int, [_P, _P]),
         "faiss_amd_IndexShardsIVF_count": (C.c_int, [_P]),
+        "faiss_amd_IndexShardsIVF_shard": (C.c_int, [_P, C.c_int, C.POINTER(_P)]),
+        "faiss_amd_IndexIVF_copy_subset_to": (C.c_int, [_P, _P, C.c_int, C.c_int64, C.c_int64,
+                                                        C.POINTER(C.c_size_t)]),
+        "faiss_amd_index_ivf_to_shards": (C.c_int, [_P, C.c_int, C.c_int, _P, C.POINTER(_P)]),
         "faiss_write_index": (C.c_int, [_P, _P]),
         "faiss_write_index_fname": (C.c_int, [_P, C.c_char_p]),
         "faiss_amd_write_index_ondisk": (C.c_int, [_P, C.c_char_p, C.c_char_p]),
@@ -625,7 +629,8 @@ class IndexIVFPQ(IndexIVF):
 
 
 class IndexShardsIVF(IndexIVF):
-    """faiss/IndexShardsIVF.h: shards sharing one coarse quantizer (one device)."""
+    """faiss/IndexShardsIVF.h: shards sharing one coarse quantizer; shards on
+    other devices than the quantizer are searched over RCCL (shards.cpp)."""
 
     def __init__(self, quantizer, nlist, threaded=False, successive_ids=True):
         p = C.c_void_p()
@@ -641,6 +646,12 @@ class IndexShardsIVF(IndexIVF):
 
     def count(self):
         return lib().faiss_amd_IndexShardsIVF_count(self.h)
+
+    def shard(self, i):
+        """Shard i (a view owned by this index)."""
+        s = C.c_void_p()
+        _check(lib().faiss_amd_IndexShardsIVF_shard(self.h, i, C.byref(s)))
+        return _wrap(s, owner=self)
 
 
 class IDSelector:
@@ -863,3 +874,29 @@ def _shards_init_from(self, h, owner):
 
 
 IndexShardsIVF._init_from = _shards_init_from
+
+# faiss/invlists/InvertedLists.h:36-43
+SUBSET_TYPE_ID_RANGE, SUBSET_TYPE_ID_MOD, SUBSET_TYPE_ELEMENT_RANGE = 0, 1, 2
+SUBSET_TYPE_INVLIST_FRACTION, SUBSET_TYPE_INVLIST = 3, 4
+
+
+def copy_subset_to(src, dst, subset_type, a1, a2):
+    """IndexIVF::copy_subset_to (faiss/IndexIVF.cpp:1732-1739): entries of
+    src selected by (subset_type, a1, a2) appended to dst; returns the count."""
+    n = C.c_size_t()
+    _check(lib().faiss_amd_IndexIVF_copy_subset_to(src.h, dst.h, int(subset_type), int(a1),
+                                                    int(a2), C.byref(n)))
+    return n.value
+
+
+def index_ivf_to_shards(src, nshard, shard_type=1, devices=None):
+    """GpuCloner.cpp:283-420 for IVF: nshard shards of src (shard_type 1 id
+    modulo, 2 id range, 4 list range), shard i on devices[i]."""
+    p = C.c_void_p()
+    dv = None
+    if devices is not None:
+        dv = (C.c_int * nshard)(*[int(x) for x in devices])
+    _check(lib().faiss_amd_index_ivf_to_shards(src.h, int(nshard), int(shard_type),
+                                                C.cast(dv, C.c_void_p) if dv is not None else None,
+                                                C.byref(p)))
+    return _wrap(p)

@@ -489,6 +489,29 @@ int faiss_amd_IndexShardsIVF_count(const FaissIndexShardsIVF* index) {
     auto s = dynamic_cast<const IndexShardsIVF*>(IX(index));
     return s ? (int)s->shards.size() : 0;
 }
+int faiss_amd_IndexShardsIVF_shard(const FaissIndexShardsIVF* index, int i, FaissIndex** p_shard) {
+    C_TRY auto s = dynamic_cast<const IndexShardsIVF*>(IX(index));
+    FAISS_THROW_IF_NOT_MSG(s, "not an IndexShardsIVF");
+    FAISS_THROW_IF_NOT(i >= 0 && i < (int)s->shards.size());
+    *p_shard = FX(s->shards[i]);
+    C_CATCH
+}
+int faiss_amd_IndexIVF_copy_subset_to(const FaissIndex* src, FaissIndex* dst, int subset_type,
+                                      idx_t a1, idx_t a2, size_t* n_added) {
+    C_TRY auto a = dynamic_cast<const IndexIVF*>(IX(src));
+    auto b = dynamic_cast<IndexIVF*>(IX(dst));
+    FAISS_THROW_IF_NOT_MSG(a && b, "copy_subset_to: both indexes must be IndexIVF");
+    const size_t n = ivf_copy_subset_to(a, b, subset_type, a1, a2);
+    if (n_added) *n_added = n;
+    C_CATCH
+}
+int faiss_amd_index_ivf_to_shards(const FaissIndex* src, int nshard, int shard_type,
+                                  const int* devices, FaissIndexShardsIVF** p_index) {
+    C_TRY auto a = dynamic_cast<const IndexIVF*>(IX(src));
+    FAISS_THROW_IF_NOT_MSG(a, "index_ivf_to_shards: not an IndexIVF");
+    *p_index = FX(index_ivf_to_shards(a, nshard, shard_type, devices));
+    C_CATCH
+}
 
 // ---------------- range search
 static RangeSearchResult* RSR(FaissRangeSearchResult* p) {

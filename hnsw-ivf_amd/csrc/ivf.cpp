@@ -976,21 +976,6 @@ void IndexIVFPQ::exact_args(void* p) const {
 }
 
 // ---------------------------------------------------------------- shards
-IndexShardsIVF::IndexShardsIVF(Index* q, size_t nl, bool th, bool succ)
-        : Index(q->d, q->metric_type), quantizer(q), nlist(nl), threaded(th),
-          successive_ids(succ) {
-    device = q->device;
-    is_trained = q->is_trained && (size_t)q->ntotal == nlist;
-}
-
-void IndexShardsIVF::add_shard(IndexIVF* idx) {
-    FAISS_THROW_IF_NOT(idx && idx->d == d && idx->nlist == nlist);
-    FAISS_THROW_IF_NOT_MSG(idx->device == device, "in-process shards must share the device; "
-                                                  "use one process per GPU for multi-GPU");
-    shards.push_back(idx);
-    ntotal += idx->ntotal;
-}
-
 void IndexShardsIVF::train(idx_t n, const float* x) {
     // faiss/IndexShardsIVF.cpp:44-86: train the common quantizer, copy to shards
     std::vector<float> cent((size_t)nlist * d);
@@ -1047,6 +1032,10 @@ void IndexShardsIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, fl
     FAISS_THROW_IF_NOT(ns > 0);
     DevGuard dg(device);
     std::lock_guard<std::recursive_mutex> g(mu_);
+    if (multi_device()) {
+        search_multi(n, x, ldx, k, distances, labels, params, np, s);
+        return;
+    }
     s_cd_.reserve(sizeof(float) * n * np);
     s_ci_.reserve(sizeof(int32_t) * n * np);
     s_all_d_.reserve(sizeof(float) * ns * n * k);

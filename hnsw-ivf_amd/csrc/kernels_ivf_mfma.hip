@@ -712,11 +712,14 @@ __device__ __forceinline__ float eval_rows64(const float* xr /* LDS copy of the 
     const int d4 = (d + 3) >> 2;  // float4 per row actually read
     const unsigned long long vm = __ballot(valid);
     float out = 0.f;
-#pragma unroll 1
-    for (int p = 0; p < 4; p++) {
-        if (((vm >> (16 * p)) & 0xffffull) == 0ull) continue;
-        // ---- stage: row 2t + (lane >> 5), float4 column lane & 31
-        float4 v[8];
+    // passes with rows, in order; the next pass's rows are loaded (into the
+    // registers the LDS staging just freed) while this one is evaluated
+    auto next_pass = [&](int p) {
+        while (p < 4 && ((vm >> (16 * p)) & 0xffffull) == 0ull) p++;
+        return p;
+    };
+    float4 v[8];
+    auto load = [&](int p) {
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             const int row = 2 * t + (lane >> 5), c4 = lane & 31;
@@ -725,12 +728,23 @@ __device__ __forceinline__ float eval_rows64(const float* xr /* LDS copy of the 
             v[t] = (rv && c4 < d4) ? *(const float4*)(codes + (int64_t)rg * ldc + 4 * c4)
                                    : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+    };
+    int p = next_pass(0);
+    if (p < 4) load(p);
+#pragma unroll 1
+    while (p < 4) {
+        // ---- stage: row 2t + (lane >> 5), float4 column lane & 31
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             const int row = 2 * t + (lane >> 5), c4 = lane & 31;
             *(float4*)(stage + row * RR_RS + 4 * c4) = v[t];
         }
-        __syncthreads();  // one wave per block: orders the staging before the reads
+        // one wave per block: orders the staging before the reads (LDS only:
+        // the next pass's loads stay in flight)
+        __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        const int pn = next_pass(p + 1);
+        if (pn < 4) load(pn);
         // ---- evaluate
         const float* yj = stage + g * RR_RS + 2 * jp;
         const float* xj = xr + 2 * jp;
@@ -763,7 +777,10 @@ __device__ __forceinline__ float eval_rows64(const float* xr /* LDS copy of the 
         }
         const float got = __shfl(r, 4 * (lane & 15));
         if ((lane >> 4) == p) out = got;
-        __syncthreads();  // the next pass overwrites the staging rows
+        // the next pass overwrites the staging rows
+        __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        p = pn;
     }
     return out;
 }
@@ -1122,6 +1139,34 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
             }
         }
         t_e = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        if constexpr (NB > 1) {
+            // only keys <= U can be in the top k (at least k kept entries have
+            // exact keys <= their ub' <= U; boundary ties are <= U too): the
+            // order-preserving compaction of those (failing streams add whole
+            // slots of rows, most of them far above U) ranks in one batch
+            float* ck1 = stg[w];
+            long long* ck2 = reinterpret_cast<long long*>(stg[w] + 64 * NB);
+            int m = 0;
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                const bool in = 64 * b + lane < ns && k1[b] < WS_INF && k1[b] <= U;
+                const unsigned long long bm = __ballot(in);
+                const int pos = m + __popcll(bm & ((1ull << lane) - 1ull));
+                if (in) {
+                    ck1[pos] = k1[b];
+                    ck2[pos] = k2[b];
+                }
+                m += __popcll(bm);
+            }
+            if (m <= 64) {
+                __syncthreads();  // one wave per block
+                float c1[1] = {lane < m ? ck1[lane] : WS_INF};
+                long long c2[1] = {lane < m ? ck2[lane] : WS_NOID};
+                __syncthreads();
+                return exact_topk_small<1>(c1, c2, m, k, L2 ? 1 : 0, lane, valid, D + q * k,
+                                           I + q * k);
+            }
+        }
         return exact_topk_small<NB>(k1, k2, ns, k, L2 ? 1 : 0, lane, valid, D + q * k,
                                     I + q * k);
     };

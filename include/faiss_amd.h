@@ -335,6 +335,10 @@ struct ArrayInvertedLists {
     void reset();
 };
 
+struct IndexIVF;
+size_t ivf_copy_subset_to(const IndexIVF* src, IndexIVF* dst, int subset_type, idx_t a1,
+                          idx_t a2);
+
 struct IndexIVF : Index {
     Index* quantizer = nullptr;
     bool own_fields = false;
@@ -432,6 +436,7 @@ struct IndexIVF : Index {
                            const uint8_t* sel, bool store_pairs) const;
     // the index-type part of the exact scan's arguments (codes / PQ tables)
     virtual void exact_args(void* args) const = 0;
+    friend size_t ivf_copy_subset_to(const IndexIVF*, IndexIVF*, int, idx_t, idx_t);
     mutable uint32_t max_list_len_ = 0;
     mutable DeviceBuffer s_ex_eoff_, s_ex_tot_, s_ex_keys_, s_ex_rows_;
     mutable bool dirty_ = true;
@@ -549,8 +554,14 @@ struct IndexShardsIVF : Index {
     size_t nlist = 0;
     bool threaded = false, successive_ids = true;
     std::vector<IndexIVF*> shards;
+    // shards (and the quantizer, owned by shard 0) deleted with this object
+    // (index_ivf_to_shards)
+    bool own_shards = false;
     IndexShardsIVF(Index* quantizer, size_t nlist, bool threaded = false,
                    bool successive_ids = true);
+    ~IndexShardsIVF() override;
+    // shards may live on other devices than the quantizer: the search then
+    // runs as one RCCL communicator over the devices (shards.cpp)
     void add_shard(IndexIVF* idx);
     void add(idx_t n, const float* x) override;
     void add_with_ids(idx_t n, const float* x, const idx_t* xids) override;
@@ -561,10 +572,41 @@ struct IndexShardsIVF : Index {
     void reset() override;
     size_t nprobe = 1;
 
+    // true when some shard is on another device than the quantizer (or
+    // FAISS_AMD_SHARDS_RCCL=1): search over RCCL
+    bool multi_device() const;
+
    private:
     mutable std::recursive_mutex mu_;
     mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_all_d_, s_all_i_;
+    struct MultiDev;
+    mutable std::unique_ptr<MultiDev> md_;
+    void search_multi(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                      idx_t* labels, const SearchParametersIVF* params, size_t np,
+                      hipStream_t s) const;
 };
+
+// faiss/invlists/InvertedLists.h:36-43 subset types of copy_subset_to
+enum SubsetType {
+    SUBSET_TYPE_ID_RANGE = 0,
+    SUBSET_TYPE_ID_MOD = 1,
+    SUBSET_TYPE_ELEMENT_RANGE = 2,
+    SUBSET_TYPE_INVLIST_FRACTION = 3,
+    SUBSET_TYPE_INVLIST = 4,
+};
+// faiss/IndexIVF.cpp:1732-1739 + faiss/invlists/InvertedLists.cpp:91-175:
+// append the entries of src selected by (subset_type, a1, a2) to dst's lists
+// (same nlist / code_size); returns the number added (dst->ntotal grows)
+size_t ivf_copy_subset_to(const IndexIVF* src, IndexIVF* dst, int subset_type, idx_t a1,
+                          idx_t a2);
+// faiss/gpu/GpuCloner.cpp:283-317 + :319-420 (IVF part of
+// clone_Index_to_shards): nshard copies of src with empty lists (through
+// write_index / read_index), shard i on devices[i], holding the entries of
+// shard_type 1 (id % nshard == i), 2 (ids in [i ntotal / n, (i+1) ntotal / n))
+// or 4 (lists [i nlist / n, (i+1) nlist / n)); ids are kept (successive_ids
+// false).  The result owns its shards.
+IndexShardsIVF* index_ivf_to_shards(const IndexIVF* src, int nshard, int shard_type,
+                                    const int* devices);
 
 // ---------------------------------------------------------------- misc
 // GPU k-means (faiss/Clustering.h:23-59 defaults); assignment on the GPU

@@ -358,6 +358,32 @@ int faiss_amd_IndexShardsIVF_new(
         int successive_ids);
 int faiss_amd_IndexShardsIVF_add_shard(FaissIndexShardsIVF* index, FaissIndex* shard);
 int faiss_amd_IndexShardsIVF_count(const FaissIndexShardsIVF* index);
+/* borrowed pointer to shard i (owned by the shards index or the caller) */
+int faiss_amd_IndexShardsIVF_shard(const FaissIndexShardsIVF* index, int i,
+                                   FaissIndex** p_shard);
+/* faiss/IndexIVF.h:393-402 IndexIVF::copy_subset_to
+ * (faiss/invlists/InvertedLists.cpp:91-175): append to dst the entries of src
+ * selected by subset_type 0 = ids in [a1, a2), 1 = id % a1 == a2,
+ * 2 = element range [a1, a2) of the running total, 3 = fraction a2 / a1 of
+ * every list, 4 = lists [a1, a2).  Host lists; n_added may be NULL. */
+int faiss_amd_IndexIVF_copy_subset_to(
+        const FaissIndex* src,
+        FaissIndex* dst,
+        int subset_type,
+        idx_t a1,
+        idx_t a2,
+        size_t* n_added);
+/* faiss/gpu/GpuCloner.cpp:283-420 (ToGpuClonerMultiple::clone_Index_to_shards
+ * of an IVF index): nshard copies of src, shard i on devices[i] (NULL: src's
+ * device) holding shard_type 1 (id % nshard == i), 2 (id range) or 4 (list
+ * range).  Shards on several devices are searched over RCCL.  The result owns
+ * its shards; free it with faiss_Index_free. */
+int faiss_amd_index_ivf_to_shards(
+        const FaissIndex* src,
+        int nshard,
+        int shard_type,
+        const int* devices,
+        FaissIndexShardsIVF** p_index);
 
 /* ---------------- range search (c_api/impl/AuxIndexStructures_c.h:20-50,
  * c_api/Index_c.h:148-153, c_api/IndexIVF_c.h range_search_preassigned) ----
