@@ -19,7 +19,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libfaiss_amd.so")
+LIB_PATH = os.environ.get("FAISS_AMD_LIB") or os.path.join(_HERE, "lib", "libfaiss_amd.so")
 
 METRIC_INNER_PRODUCT = 0
 METRIC_L2 = 1

@@ -134,6 +134,26 @@ __device__ __forceinline__ void load_query_frags(const float* __restrict__ x, in
     query_frags_from_raw<NS>(raw, d, lh, bh, bl, xn);
 }
 
+// Query image (k_query_prep): per query the B fragments load_query_frags
+// builds — bf16 hi then bf16 lo, each 16 NS values in dim order (64 NS bytes
+// per query) — and its |x|^2 (same order, same bits).  A filter work group
+// then reads its fragments with 2 NS 16-byte loads instead of splitting the
+// fp32 row itself (~6 VALU per dim, repeated by every work group that sees
+// the query: once per probed list item, once per coarse split).
+template <int NS>
+__device__ __forceinline__ void load_query_image(const uint8_t* __restrict__ qimg,
+                                                 const float* __restrict__ qxn, int qr, int lh,
+                                                 bf16x8 (&bh)[NS], bf16x8 (&bl)[NS], float& xn) {
+    const int q = qr < 0 ? 0 : qr;
+    const uint8_t* row = qimg + (int64_t)q * (64 * NS) + 16 * lh;
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        bh[s] = *(const bf16x8*)(row + 32 * s);
+        bl[s] = *(const bf16x8*)(row + 32 * NS + 32 * s);
+    }
+    xn = qxn ? qxn[q] : 0.f;
+}
+
 // One 32x32 block: A = 32 database rows (hi/lo image in LDS, this lane's row
 // pointer `arow` already offset by 16 * lh bytes), B = the register query
 // fragments.  acc[r] = row (r&3)+8(r>>2)+4lh, col li.

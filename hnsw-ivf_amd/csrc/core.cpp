@@ -181,6 +181,10 @@ const float* IndexFlat::device_vectors() const {
     sync_device();
     return d_xb_.as<float>();
 }
+const void* IndexFlat::prepared_query_image(const float* x, idx_t n, int ldx) const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    return (x && x == qimg_x_ && n == qimg_n_ && ldx == qimg_ldx_) ? s_qimg_.ptr : nullptr;
+}
 const float* IndexFlat::device_norms() const {
     sync_device();
     return d_norms_.as<float>();
@@ -193,6 +197,7 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
                            kern::kMaxKExact);
     sync_device();
     std::lock_guard<std::recursive_mutex> g(mu_);
+    qimg_x_ = nullptr;  // set again below if this call prepares the image
     const int l = ld();
     const int metric_l2 = metric_type == METRIC_L2;
     if (k > kern::kMaxK) {
@@ -236,7 +241,20 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
                     ? kern::CoarsePlan{}
                     : kern::coarse_bf3_plan(n, (int)ny, d, k);
     if (plan.ok) {
-        kern::row_norms(x, n, d, ldx, s_xn_.as<float>(), s);
+        // the streamed filter reads prepared query fragments (one launch with
+        // the reference-order norms)
+        const bool qi = d_cst_.ptr != nullptr && ldx % 4 == 0;
+        if (qi) {
+            const size_t ib = kern::query_image_bytes(n, d);
+            s_qimg_.reserve(ib + sizeof(float) * n);
+            kern::query_prep(x, n, ldx, d, s_xn_.as<float>(), s_qimg_.ptr,
+                             (float*)((uint8_t*)s_qimg_.ptr + ib), s);
+            qimg_x_ = x;
+            qimg_n_ = n;
+            qimg_ldx_ = ldx;
+        } else {
+            kern::row_norms(x, n, d, ldx, s_xn_.as<float>(), s);
+        }
         const size_t per_q = (size_t)plan.entries * 4 + plan.nsplit * 16;
         const idx_t qchunk = std::max<idx_t>(64, (idx_t)(((size_t)256 << 20) / per_q) / 64 * 64);
         const idx_t qc = std::min<idx_t>(qchunk, n);
@@ -250,7 +268,9 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
                                  d_cnmax_.as<float>(), (int)ny, d, k, metric_l2,
                                  s_cand_i_.as<uint32_t>(), s_tile_.as<float>(), distances + q0 * k,
                                  o32 ? o32 + q0 * k : nullptr, o64 ? o64 + q0 * k : nullptr, s,
-                                 d_cst_.ptr);
+                                 d_cst_.ptr,
+                                 qi ? (const uint8_t*)s_qimg_.ptr + q0 * kern::query_image_bytes(1, d)
+                                    : nullptr);
         }
         return;
     }

@@ -363,6 +363,13 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
                         params ? params->quantizer_params : nullptr, s);
         const uint32_t* lim = nullptr;
         const int32_t* asg = apply_max_codes(nq, (int)np, s_ci_.as<int32_t>(), mc, &lim, s);
+        // the flat quantizer's prepared query image serves the list filter too
+        struct Reset {
+            const void*& p;
+            ~Reset() { p = nullptr; }
+        } reset{shared_qimg_};
+        if (auto* qf = dynamic_cast<const IndexFlat*>(quantizer))
+            shared_qimg_ = qf->d == d ? qf->prepared_query_image(x + q0 * ldx, nq, ldx) : nullptr;
         search_preassigned_device(nq, x + q0 * ldx, ldx, k, (int)np, asg, s_cd_.as<float>(),
                                   distances + q0 * k, labels + q0 * k, s, lim, selm);
     }
@@ -660,13 +667,17 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(n, 4));
     const bool dbg = getenv("FAISS_AMD_IVF_STATS") != nullptr;
     if (dbg) HIP_CHECK(hipMemsetAsync(s_flags_.ptr, 0, 4 * sizeof(uint32_t), s));
+    // query image + |x|^2: the quantizer's when this is search()'s chunk
+    const void* qready = shared_qimg_;
+    if (!qready) s_q_.reserve(kern::query_image_bytes(n, d) + sizeof(float) * n);
     kern::ivf_flat_scan_mfma(x, ldx, d_codes_.as<float>(), l, d_cbf_.ptr, d_ids_.as<int64_t>(),
                              d_ynorm_.as<float>(), d_ynmax_.as<float>(), d_rres_.as<float>(),
                              d_rmax_.as<float>(), d_list_off_.as<uint32_t>(),
                              d_list_len_.as<uint32_t>(), (int)nlist, d, obits_, n, np, (int)k, l2,
                              b, max_items, s_part_.as<uint32_t>(), s_pk2_.as<kern::ProbeRec>(),
                              dbg ? s_flags_.as<uint32_t>() : nullptr, distances, labels, &ktimes,
-                             s, kern::ARENA_ALIGN, d_cbs_.ptr);
+                             s, kern::ARENA_ALIGN, d_cbs_.ptr,
+                             qready ? const_cast<void*>(qready) : s_q_.ptr, qready != nullptr);
     if (dbg) {
         uint32_t st[4];
         HIP_CHECK(hipMemcpyAsync(st, s_flags_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));

@@ -11,6 +11,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 
 #include "common.h"
@@ -50,7 +51,16 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
                     const float* cent, int ldc, const void* cbf, const float* cnorm,
                     const float* cnmax, int nlist, int d, int k, int metric_l2, uint32_t* keys,
                     float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s,
-                    const void* cst = nullptr);
+                    const void* cst = nullptr, const void* qimg = nullptr);
+// Query preparation for the MFMA filters (one launch): the reference-order
+// norms ref_norms[i] = fvec_norm_L2sqr(x_i) (skipped when null) and the query
+// image of bf3.h load_query_image — qimg [n][64 NS] bytes (NS = bf3_db(d)/16)
+// and qxn [n] (skipped when null).  d <= BDM.
+void query_prep(const float* x, int64_t n, int ldx, int d, float* ref_norms, void* qimg,
+                float* qxn, hipStream_t s);
+inline size_t query_image_bytes(int64_t n, int d) {
+    return (size_t)std::max<int64_t>(n, 1) * 4 * ((d + 31) / 32 * 32);
+}
 // the streamed coarse filter's image of the centroids: per row bf16 hi | lo
 // (bf3_db(d) dims each) | fp32 norm | 12 B, padded to 64 rows (+inf norms)
 void coarse_stream_image(const float* codes, int64_t rows, int d, int ldc, const float* norms,
@@ -259,7 +269,9 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
                         int64_t max_items, uint32_t* keys, ProbeRec* recs, uint32_t* stats,
                         float* D, int64_t* I, KernelTimes* kt, hipStream_t s,
-                        int list_align = 16, const void* cbs = nullptr);
+                        int list_align = 16, const void* cbs = nullptr,
+                        void* qscratch = nullptr,  // query_image_bytes(n, d) + 4 n bytes
+                        bool qready = false);      // qscratch already holds x's image
 // stream image of the arena for the streamed filter: per row bf16(code) (DB
 // dims) + fp32 norm (+inf for padding rows) + 12 zero bytes = 2 DB + 16 bytes
 void split_bf16_stream(const float* codes, int64_t rows, int d, int ldc, int DB,

@@ -219,7 +219,8 @@ __global__ __launch_bounds__(256, 2) void k_coarse_stream(
         const float* __restrict__ x, int ldx, int64_t n, int d, const uint8_t* __restrict__ cst,
         const float* __restrict__ xnorm, int nlist, int nsplit, int split_len, int nqb,
         float coef, const float* __restrict__ cnmax_p, int obits, uint32_t* __restrict__ keys,
-        float* __restrict__ pbs, unsigned long long* __restrict__ trace) {
+        float* __restrict__ pbs, unsigned long long* __restrict__ trace,
+        const uint8_t* __restrict__ qimg) {
     // FAISS_AMD_COARSE_TRACE: per work group (wave 0) s_memtime stamps —
     // [0] start, [1] query fragments loaded, then per tile j: [2 + 2j] before
     // the tile wait, [3 + 2j] after its barrier
@@ -268,7 +269,12 @@ __global__ __launch_bounds__(256, 2) void k_coarse_stream(
     issue(0, 0);
     bf16x8 bh[NS], bl[NS];
     float xn_approx;
-    if (active) load_query_frags<NS>(x, ldx, d, q < n ? (int)q : -1, lh, bh, bl, xn_approx);
+    if (active) {
+        if (qimg)  // fragments prepared once per query (k_query_prep)
+            load_query_image<NS>(qimg, nullptr, q < n ? (int)q : -1, lh, bh, bl, xn_approx);
+        else
+            load_query_frags<NS>(x, ldx, d, q < n ? (int)q : -1, lh, bh, bl, xn_approx);
+    }
     const float xn = (active && q < n) ? xnorm[q] : 0.f;  // the reference-order norm
     if (tr) tr[1] = __builtin_amdgcn_s_memtime();
 
@@ -411,6 +417,48 @@ size_t coarse_stream_image_bytes(int64_t rows, int d) {
     return (size_t)roundup((size_t)std::max<int64_t>(rows, 1), BV) * (4 * bf3_db(d) + 16);
 }
 
+// Query preparation: 32 queries per 64-lane block, lane (li, lh) builds the
+// fragments load_query_frags would build for query li (lh = which 8-dim half
+// of each 16-dim step) and stores them in the query image; lanes lh == 0
+// also write |x|^2 (the fragments' order) and the reference-order norm.
+template <int NS>
+__global__ __launch_bounds__(64) void k_query_prep(const float* __restrict__ x, int64_t n,
+                                                   int ldx, int d, float* __restrict__ ref_norms,
+                                                   uint8_t* __restrict__ qimg,
+                                                   float* __restrict__ qxn) {
+    const int lane = threadIdx.x, li = lane & 31, lh = lane >> 5;
+    const int64_t q = (int64_t)blockIdx.x * 32 + li;
+    const int qr = q < n ? (int)q : -1;
+    bf16x8 bh[NS], bl[NS];
+    float xn;
+    load_query_frags<NS>(x, ldx, d, qr, lh, bh, bl, xn);  // every lane: the shfl pairs halves
+    if (qr < 0) return;
+    uint8_t* row = qimg + q * (64 * NS) + 16 * lh;
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        *(bf16x8*)(row + 32 * s) = bh[s];
+        *(bf16x8*)(row + 32 * NS + 32 * s) = bl[s];
+    }
+    if (lh == 0) {
+        if (qxn) qxn[q] = xn;
+        if (ref_norms) ref_norms[q] = ref_norm(x + q * ldx, d);
+    }
+}
+
+void query_prep(const float* x, int64_t n, int ldx, int d, float* ref_norms, void* qimg,
+                float* qxn, hipStream_t s) {
+    if (n <= 0) return;
+    FAISS_THROW_IF_NOT(ldx % 4 == 0 && bf3_db(d) <= BDM && qimg != nullptr);
+    const int NS = bf3_db(d) / 16;
+    const dim3 grid((unsigned)cdiv(n, 32)), blk(64);
+    uint8_t* qi = (uint8_t*)qimg;
+    if (NS == 2) k_query_prep<2><<<grid, blk, 0, s>>>(x, n, ldx, d, ref_norms, qi, qxn);
+    else if (NS == 4) k_query_prep<4><<<grid, blk, 0, s>>>(x, n, ldx, d, ref_norms, qi, qxn);
+    else if (NS == 6) k_query_prep<6><<<grid, blk, 0, s>>>(x, n, ldx, d, ref_norms, qi, qxn);
+    else k_query_prep<8><<<grid, blk, 0, s>>>(x, n, ldx, d, ref_norms, qi, qxn);
+    HIP_LAUNCH_CHECK();
+}
+
 constexpr int CR_CAP = 512;
 
 // exact coarse distance of centroid j (the fixed BLAS-form order: sequential
@@ -499,7 +547,10 @@ struct CoarseStream {
 // not fail, plus every centroid of the failing streams; exact evaluation and a
 // rank-based top-k (exact_topk_resolve when a tie crosses the boundary).
 template <bool L2, class OutIdx, int V>
-__global__ __launch_bounds__(64, 4) void k_coarse_rerank(
+#ifndef CR_WAVES
+#define CR_WAVES 4  // waves per SIMD the re-rank is compiled for (tuning)
+#endif
+__global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
         const uint32_t* __restrict__ keys, const float* __restrict__ pbs,
         const float* __restrict__ x, int ldx, const float* __restrict__ xnorm,
         const float* __restrict__ cent, int ldc, const float* __restrict__ cnorm,
@@ -640,19 +691,54 @@ CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k) {
     CoarsePlan p{};
     if (n < 20 || nlist <= 0 || k < 1 || k > kMaxK || bf3_db(d) > BDM)
         return p;
-    // splits of >= 512 centroids: enough work items to fill the chip, at most
-    // 16 (the re-rank keeps one thread stream per lane)
+    // At most 16 splits (the re-rank keeps one thread stream per lane).
     // Each of the 4 * nsplit thread streams keeps KT keys; it "fails" (is
     // re-scanned exactly) when more than KT of the top-k + margin fall in it.
     // With lam = k / (4 nsplit) expected members per stream, KT = 4 / 8 / 16
     // for lam <= 1/4 / 2 / 4 keeps the Poisson tail below ~1e-3 per query.
-    int nsplit = std::max(1, std::min(16, nlist / 512));
-    while (nsplit > 1 && k > 16 * nsplit) nsplit >>= 1;
-    const double lam = (double)k / (4.0 * nsplit);
-    if (lam > 4.0) return p;
-    const int kt = lam <= 0.25 ? 4 : lam <= 2.0 ? 8 : 16;
-    const int split_len = (int)roundup(cdiv((size_t)nlist, (size_t)nsplit), BV);
-    nsplit = (int)cdiv((size_t)nlist, (size_t)split_len);
+    //
+    // The split count sets the grid: cdiv(n, 128) query blocks x nsplit work
+    // groups, two resident per CU (k_coarse_stream's two 64-centroid tile
+    // buffers).  The kernel's time is (rounds of resident groups) x (tiles
+    // per group) x (per-tile cost, growing with KT), so the split count is
+    // the one minimising that product — e.g. c2 (10k queries, 4096
+    // centroids): 6 splits of 11 tiles in one round instead of 8 splits of 8
+    // tiles in two.  When the centroid image exceeds one XCD's L2, split
+    // counts that are not a multiple of 8 lose the split-major XCD order
+    // (each split read from HBM once per XCD) and are charged for it.
+    int ncu = 256, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+        ncu = 256;
+    (void)hipGetLastError();
+    const int64_t nqb = (int64_t)cdiv((size_t)n, 128);
+    const int64_t slots = 2 * (int64_t)ncu;
+    const bool big_image = coarse_stream_image_bytes(nlist, d) > ((size_t)4 << 20);
+    int nsplit = 0, kt = 0, split_len = 0;
+    double best = 0.0;
+    const char* nsenv = getenv("FAISS_AMD_COARSE_NSPLIT");  // forces the split count (tuning)
+    const int ns_force = nsenv ? atoi(nsenv) : 0;
+    for (int ns = 1; ns <= std::min(16, std::max(1, nlist / BV)); ns++) {
+        if (ns_force > 0 && ns != ns_force) continue;
+        if (k > 16 * ns) continue;
+        const double lam = (double)k / (4.0 * ns);
+        if (lam > 4.0) continue;
+        const int kt1 = lam <= 0.25 ? 4 : lam <= 2.0 ? 8 : 16;
+        const int sl = (int)roundup(cdiv((size_t)nlist, (size_t)ns), BV);
+        const int nsp = (int)cdiv((size_t)nlist, (size_t)sl);
+        if ((size_t)sl > ((size_t)BV << 10)) continue;  // ordinals: 4 + log2(tiles) <= 14 bits
+        const int64_t rounds = (int64_t)cdiv((size_t)(nqb * nsp), (size_t)slots);
+        double cost = (double)rounds * (double)cdiv((size_t)sl, BV) * (kt1 + 12);
+        if (big_image && nsp % 8 != 0) cost *= 1.15;
+        if (nsplit == 0 || cost < best) {
+            best = cost;
+            nsplit = nsp;
+            kt = kt1;
+            split_len = sl;
+        }
+    }
+    if (nsplit == 0) return p;
     const int tiles = (int)cdiv((size_t)split_len, BV);
     int b = 0;
     while ((1 << b) < tiles) b++;
@@ -670,7 +756,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
                     const float* cent, int ldc, const void* cbf, const float* cnorm,
                     const float* cnmax, int nlist, int d, int k, int metric_l2, uint32_t* keys,
                     float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s,
-                    const void* cst) {
+                    const void* cst, const void* qimg) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(p.ok);
     static uint32_t* stats = nullptr;  // FAISS_AMD_IVF_STATS debug counters
@@ -712,7 +798,8 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
         if (stream)                                                                           \
             k_coarse_stream<L2V, KTV, NSV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(        \
                     x, ldx, n, d, (const uint8_t*)cst, xnorm, nlist, p.nsplit, p.split_len,   \
-                    (int)nqb, coef, cnmax, p.obits, keys, pbs, ctrace);                       \
+                    (int)nqb, coef, cnmax, p.obits, keys, pbs, ctrace,                        \
+                    (const uint8_t*)qimg);                                                    \
         else if (y3)                                                                          \
             k_coarse_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, n, d, (const __bf16*)cbf, cnorm, xnorm, nlist, p.nsplit,          \

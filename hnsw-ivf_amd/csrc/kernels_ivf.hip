@@ -15,6 +15,8 @@
 // second kernel merges the nprobe partial lists of each query.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 
 #include <cfloat>
@@ -42,8 +44,8 @@ __global__ void k_bucket_count(const int32_t* __restrict__ assign, int64_t total
 // Same with a block-local LDS histogram (nlist <= BC_MAXL): BC_PER entries
 // per thread take their slot from an LDS atomic, then one global atomic per
 // non-empty bin reserves the block's range of each bucket.
-constexpr int BC_PER = 16;
 constexpr int BC_MAXL = 16384;
+template <int BC_PER>
 __global__ __launch_bounds__(1024) void k_bucket_count_lds(const int32_t* __restrict__ assign,
                                                            int64_t total,
                                                            const uint32_t* __restrict__ list_len,
@@ -281,9 +283,20 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
     if (!b.counts_next) HIP_CHECK(hipMemsetAsync(b.counts, 0, sizeof(uint32_t) * nlist, s));
     if (total > 0) {
         const int nr = (int)cdiv(nlist, BC_MAXL);  // list ranges (LDS histogram each)
-        k_bucket_count_lds<<<dim3((unsigned)cdiv(total, 1024 * BC_PER), (unsigned)nr), dim3(1024),
-                             sizeof(uint32_t) * std::min(nlist, BC_MAXL), s>>>(
-                assign, total, list_len, nlist, b.counts, b.cursor);
+        // entries per thread: enough work groups to spread the histogram
+        // merge's global atomics over the chip (FAISS_AMD_BC_PER: tuning)
+        const char* pe = getenv("FAISS_AMD_BC_PER");
+        const int per = pe ? atoi(pe) : 4;
+        const size_t lds = sizeof(uint32_t) * std::min(nlist, BC_MAXL);
+#define BCL(P)                                                                              \
+    k_bucket_count_lds<P><<<dim3((unsigned)cdiv(total, 1024 * P), (unsigned)nr), dim3(1024), \
+                            lds, s>>>(assign, total, list_len, nlist, b.counts, b.cursor)
+        if (per >= 16) BCL(16);
+        else if (per >= 8) BCL(8);
+        else if (per >= 4) BCL(4);
+        else if (per >= 2) BCL(2);
+        else BCL(1);
+#undef BCL
         HIP_LAUNCH_CHECK();
     }
     k_bucket_scan<<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off, b.item_off,

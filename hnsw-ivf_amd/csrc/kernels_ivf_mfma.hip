@@ -352,7 +352,8 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
         int obits, const uint32_t* __restrict__ item_off, const ItemDesc* __restrict__ item_desc,
         const uint32_t* __restrict__ item_entries, uint32_t max_items, int nlist,
         const uint32_t* __restrict__ lim, uint32_t* __restrict__ keys,
-        ProbeRec* __restrict__ recs, unsigned long long* __restrict__ ftrace) {
+        ProbeRec* __restrict__ recs, unsigned long long* __restrict__ ftrace,
+        const uint8_t* __restrict__ qimg, const float* __restrict__ qxn) {
     const unsigned long long ft0 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     constexpr int DB = 16 * NS;          // bf16 per code row
     constexpr int SR = 2 * DB + 16;      // bytes per stream-image row
@@ -426,9 +427,13 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
     // query fragments (B operand): registers for the whole work item
     bf16x8 bh[NS], bl[NS];
     float xn = 0.f;
-    if (active)
-        load_query_frags<NS>(x, ldx, d, qvalid ? (int32_t)(my_e / (uint32_t)nprobe) : -1, lh, bh,
-                             bl, xn);
+    if (active) {
+        const int32_t qr = qvalid ? (int32_t)(my_e / (uint32_t)nprobe) : -1;
+        if (qimg)  // fragments prepared once per query (k_query_prep)
+            load_query_image<NS>(qimg, qxn, qr, lh, bh, bl, xn);
+        else
+            load_query_frags<NS>(x, ldx, d, qr, lh, bh, bl, xn);
+    }
 
     ThreadQueue32<KT> tq[2];
     tq[0].init();
@@ -1264,7 +1269,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
                         int64_t max_items, uint32_t* keys, ProbeRec* recs, uint32_t* stats,
                         float* D, int64_t* I, KernelTimes* kt, hipStream_t s, int list_align,
-                        const void* cbs) {
+                        const void* cbs, void* qscratch, bool qready) {
     if (n <= 0) return;
     const bool aligned_lists = list_align % BV == 0 && cbs != nullptr;
     const int KE = ivf_mfma_kq(k, d);
@@ -1312,6 +1317,15 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     // selection)
     const char* penv = getenv("FAISS_AMD_IVF_PIPE");
     const bool spipe = penv && !strcmp(penv, "1");
+    // the streamed filter reads prepared query fragments: one k_query_prep
+    // launch instead of every work item splitting its queries' fp32 rows
+    const uint8_t* qimg = nullptr;
+    const float* qxn = nullptr;
+    if (stream_ok && qscratch && ldx % 4 == 0) {
+        qimg = (const uint8_t*)qscratch;
+        qxn = (const float*)((uint8_t*)qscratch + query_image_bytes(n, d));
+        if (!qready) query_prep(x, n, ldx, d, nullptr, qscratch, (float*)qxn, s);
+    }
     {
         ScopedKernelTimer tm(kt, "ivf_flat_scan", 0.0, s);
 #define LAUNCH_NS(L2V, KTV, NSV)                                                              \
@@ -1321,7 +1335,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                    : k_ivf_bf2_stream<L2V, KTV, NSV, false>)<<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const uint8_t*)cbs, ynmax, rmax, nprobe, coef, obits,         \
                     b.item_off, b.item_desc, b.item_entries, (uint32_t)max_items, nlist,      \
-                    b.lim, keys, recs, ftrace);                                               \
+                    b.lim, keys, recs, ftrace, qimg, qxn);                                    \
         else if (b.sel)                                                                       \
             k_ivf_bf3_filter<L2V, KTV, NSV, false, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \

@@ -214,15 +214,23 @@ struct IndexFlat : Index {
 
     const float* device_vectors() const;  // [ntotal][ld]
     const float* device_norms() const;
+    // The query image (kernels.h query_prep: bf16 fragments, then |x|^2 at
+    // byte query_image_bytes(n, d)) the last assign / search prepared, if it
+    // was prepared for exactly (x, n, ldx); else null.  IndexIVF::search
+    // hands it to its list filter so a batch is prepared once.
+    const void* prepared_query_image(const float* x, idx_t n, int ldx) const;
 
    private:
     template <class OutIdx>
     void knn_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
                     hipStream_t stream) const;
+    mutable const float* qimg_x_ = nullptr;
+    mutable idx_t qimg_n_ = 0;
+    mutable int qimg_ldx_ = 0;
     mutable DeviceBuffer d_xb_, d_norms_, d_cbf_, d_cnmax_, d_cst_;
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
-    mutable DeviceBuffer s_xn_, s_tile_, s_cand_d_, s_cand_i_;
+    mutable DeviceBuffer s_xn_, s_tile_, s_cand_d_, s_cand_i_, s_qimg_;
 };
 struct IndexFlatL2 : IndexFlat {
     explicit IndexFlatL2(idx_t d = 0) : IndexFlat(d, METRIC_L2) {}
@@ -448,6 +456,9 @@ struct IndexIVF : Index {
     mutable DeviceBuffer s_ictr_;
     mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_counts_, s_boff_, s_ioff_, s_cur_, s_ent_,
             s_pk1_, s_pk2_, s_q_;
+    // query image prepared by the flat quantizer for the chunk search() is
+    // scanning (IndexFlat::prepared_query_image), null outside that call
+    mutable const void* shared_qimg_ = nullptr;
     mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_,
             s_selmask_;
     // bucket counts of this call (zero) and the half the call's scan clears
