@@ -23,6 +23,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
 
 #include "common.h"
 #include "kernels.h"
@@ -41,11 +45,14 @@ __device__ __forceinline__ float l2_row(const float* __restrict__ qs, const floa
 
 // merge a sorted 64-batch into a sorted 128-queue (c0: positions 0..63,
 // c1: 64..127), keeping the 128 smallest.
-__device__ __forceinline__ void merge128(float& d0, long long& i0, float& d1, long long& i1,
-                                         float bd, long long bi, int lane) {
+// Returns the smallest distance it discarded (+inf when none).
+__device__ __forceinline__ float merge128(float& d0, long long& i0, float& d1, long long& i1,
+                                          float bd, long long bi, int lane) {
     float rd = __shfl(bd, 63 - lane);
     long long ri = shfl_ll(bi, 63 - lane);
+    float disc = rd;
     if (key_less(rd, ri, d1, i1)) {
+        disc = d1;
         d1 = rd;
         i1 = ri;
     }
@@ -60,6 +67,70 @@ __device__ __forceinline__ void merge128(float& d0, long long& i0, float& d1, lo
         cas_lane(d0, i0, j, (lane & j) == 0);
         cas_lane(d1, i1, j, (lane & j) == 0);
     }
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) disc = fminf(disc, __shfl_xor(disc, j));
+    return disc;
+}
+// wave_merge64 (wave_select.h) that also returns the smallest distance it
+// discarded (+inf when none)
+__device__ __forceinline__ float merge64_disc(float& qd, long long& qi, float cd, long long ci,
+                                              int lane) {
+    const float rd = __shfl(cd, 63 - lane);
+    const long long ri = shfl_ll(ci, 63 - lane);
+    float disc = rd;
+    if (key_less(rd, ri, qd, qi)) {
+        disc = qd;
+        qd = rd;
+        qi = ri;
+    }
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) cas_lane(qd, qi, j, (lane & j) == 0);
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) disc = fminf(disc, __shfl_xor(disc, j));
+    return disc;
+}
+
+// Move the lanes with `sel` to lanes 0..m-1 (order kept) and give the others
+// (+inf, NOID); returns m.  One ds_permute per 32-bit word: every lane pushes
+// its key to its destination (a permutation of the 64 lanes).
+__device__ __forceinline__ int wave_compact(float& d, long long& i, bool sel, int lane) {
+    const unsigned long long bm = __ballot(sel);
+    const int m = __popcll(bm);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int dst = sel ? __popcll(bm & lt) : m + __popcll(~bm & lt);
+    const int a = dst << 2;
+    d = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(d)));
+    const int lo = __builtin_amdgcn_ds_permute(a, (int)(i & 0xffffffffLL));
+    const int hi = __builtin_amdgcn_ds_permute(a, (int)(i >> 32));
+    i = ((long long)hi << 32) | (unsigned int)lo;
+    if (lane >= m) {
+        d = WS_INF;
+        i = WS_NOID;
+    }
+    return m;
+}
+
+// ascending bitonic sort of lanes [0, W) (W a power of two); lanes >= W hold
+// (+inf, NOID), so the whole wave ends sorted
+template <int W>
+__device__ __forceinline__ void wave_sort_w(float& d, long long& i, int lane) {
+#pragma unroll
+    for (int k = 2; k <= W; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) cas_lane(d, i, j, ((lane & j) == 0) == ((lane & k) == 0));
+    }
+}
+// sort a batch whose real keys are compacted to lanes 0..m-1: the narrowest
+// network that covers them (a hop rarely brings more than a few keys that can
+// enter a queue, so most batches need 1-3 stages instead of 21)
+__device__ __forceinline__ void wave_sort_m(float& d, long long& i, int lane, int m) {
+    if (m <= 1) return;
+    if (m <= 2) wave_sort_w<2>(d, i, lane);
+    else if (m <= 4) wave_sort_w<4>(d, i, lane);
+    else if (m <= 8) wave_sort_w<8>(d, i, lane);
+    else if (m <= 16) wave_sort_w<16>(d, i, lane);
+    else if (m <= 32) wave_sort_w<32>(d, i, lane);
+    else wave_sort_w<64>(d, i, lane);
 }
 
 template <bool LDS_VISITED>
@@ -160,6 +231,10 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
             float d0v = pos < 64 ? __shfl(c0d, pos) : __shfl(c1d, pos - 64);
             long long k0v = pos < 64 ? shfl_ll(c0i, pos) : shfl_ll(c1i, pos - 64);
             const int v0 = (int)(k0v >> 1);
+            // pop_min among equal alive minima picks by heap slot in the
+            // reference (MinimaxHeap::pop_min): an order the batched queue
+            // does not keep
+            tie |= __popcll(__ballot(a0 && c0d == d0v)) + __popcll(__ballot(a1 && c1d == d0v)) > 1;
             if (pos < 64) {
                 if (lane == pos) c0i &= ~1ll;
             } else {
@@ -206,26 +281,50 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
                 const float eth = ef <= 64 ? __shfl(c0d, ef - 1) : __shfl(c1d, ef - 65);
                 tie |= __ballot(fresh && (dis == kth || dis == eth)) != 0ull;
             }
-            // result heap: k smallest (dis, id) of the union, strict admission
+            // result heap: k smallest (dis, id) of the union, strict admission;
+            // only keys below the current k-th can enter: they are compacted
+            // and sorted by the narrowest network that holds them
             {
-                float cd = (fresh && dis < FLT_MAX) ? dis : WS_INF;
-                long long ci = (fresh && dis < FLT_MAX) ? (long long)v : WS_NOID;
-                wave_offer_q(res_d, res_i, cd, ci, k, lane);
-                const float rn = __shfl(res_d, (lane + 1) & 63);
-                tie |= __ballot(lane + 1 < k && res_d < WS_INF && res_d == rn) != 0ull;
+                const float thr_d = __shfl(res_d, k - 1);
+                const long long thr_i = shfl_ll(res_i, k - 1);
+                const bool pass = fresh && dis < FLT_MAX && key_less(dis, (long long)v, thr_d, thr_i);
+                float cd = pass ? dis : WS_INF;
+                long long ci = pass ? (long long)v : WS_NOID;
+                const int m = wave_compact(cd, ci, pass, lane);
+                if (m > 0) {
+                    wave_sort_m(cd, ci, lane, m);
+                    const float disc = merge64_disc(res_d, res_i, cd, ci, lane);
+                    // the sequential heap's strict admission against a
+                    // threshold that moves within the batch and the union's
+                    // (dis, id) order differ only when the k-th kept and the
+                    // best dropped distance are equal
+                    const float kd = __shfl(res_d, k - 1);
+                    const float nd = k < 64 ? __shfl(res_d, k) : disc;
+                    tie |= nd < WS_INF && kd == nd;
+                }
             }
-            // candidate heap: ef smallest of the union (dead slots included)
+            // candidate heap: ef smallest of the union (dead slots included);
+            // a key above the ef-th kept slot would land past ef (positions
+            // never read), so only the ones below it are merged
             {
-                float cd = fresh ? dis : WS_INF;
-                long long ci = fresh ? (((long long)v << 1) | 1) : WS_NOID;
-                wave_sort64(cd, ci, lane);
-                merge128(c0d, c0i, c1d, c1i, cd, ci, lane);
-                // equal neighbours among the kept positions (sorted queue)
-                const float n0 = __shfl(c0d, (lane + 1) & 63), n1 = __shfl(c1d, (lane + 1) & 63);
-                const float nx = lane < 63 ? n0 : __shfl(c1d, 0);
-                const bool e0 = lane + 1 < ef && c0d < WS_INF && c0d == nx;
-                const bool e1 = 65 + lane < ef && lane < 63 && c1d < WS_INF && c1d == n1;
-                tie |= __ballot(e0 || e1) != 0ull;
+                const float ed = ef <= 64 ? __shfl(c0d, ef - 1) : __shfl(c1d, ef - 65);
+                const long long ei = ef <= 64 ? shfl_ll(c0i, ef - 1) : shfl_ll(c1i, ef - 65);
+                const long long key2 = ((long long)v << 1) | 1;
+                const bool enter = fresh && key_less(dis, key2, ed, ei);
+                float cd = enter ? dis : WS_INF;
+                long long ci = enter ? key2 : WS_NOID;
+                const int m = wave_compact(cd, ci, enter, lane);
+                if (m > 0) {
+                    wave_sort_m(cd, ci, lane, m);
+                    const float disc = merge128(c0d, c0i, c1d, c1i, cd, ci, lane);
+                    // MinimaxHeap::push drops v >= max and evicts the max
+                    // with popped slots at id -1: only an equal distance at
+                    // the ef boundary can make the kept sets differ
+                    const float ld = ef <= 64 ? __shfl(c0d, ef - 1) : __shfl(c1d, ef - 65);
+                    const float nd = ef < 64 ? __shfl(c0d, ef)
+                                     : ef < 128 ? __shfl(c1d, ef - 64) : disc;
+                    tie |= nd < WS_INF && ld == nd;
+                }
             }
         }
     }
@@ -452,23 +551,30 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
                 break;
             }
             // neighbours of v0 in stored order; visited test-and-set in order
+            // (the ids are loaded by all lanes at once; the stored-order
+            // test-and-set is restated in parallel: neighbour j is fresh when
+            // its bit was clear before this hop and no earlier neighbour of the
+            // list is the same node; the fresh ones keep their stored order)
             const uint64_t o = g.offsets[v0];
             const int b = g.cum_nb[0], e = g.cum_nb[1];
             const int cnt = e - b;
-            if (lane == 0) {
-                int nf = 0;
-                for (int j = 0; j < cnt; j++) {
-                    const int32_t v1 = g.neighbors[o + b + j];
-                    if (v1 < 0) break;
-                    const uint32_t bit = 1u << (v1 & 31);
-                    const uint32_t old = vis[v1 >> 5];
-                    vis[v1 >> 5] = old | bit;
-                    if (!(old & bit)) fi[nf++] = v1;
-                }
-                sh[2] = nf;
+            int nf;
+            {
+                const int32_t v1 = lane < cnt ? g.neighbors[o + b + lane] : -1;
+                const unsigned long long neg =
+                        __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
+                const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
+                const bool live = lane < jmax;
+                bool fresh = live && !((vis[v1 >> 5] >> (v1 & 31)) & 1u);
+                for (int i = 0; i < jmax; i++)  // a node listed twice: the first is the visit
+                    fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
+                __syncthreads();  // every lane read the bits before any is set
+                if (fresh) atomicOr(&vis[v1 >> 5], 1u << (v1 & 31));
+                const unsigned long long fm = __ballot(fresh);
+                nf = __popcll(fm);
+                if (fresh) fi[__popcll(fm & ((1ull << lane) - 1ull))] = v1;
             }
             __syncthreads();
-            const int nf = sh[2];
             if (lane < nf) fd[lane] = l2_row(qs, g.storage + (int64_t)fi[lane] * g.ld, g.d);
             st_ndis += (uint32_t)nf;
             st_nhops += 1;
@@ -534,6 +640,253 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
     }
 }
 
+// The same sequential search for ef, k <= 64 with both heaps in registers:
+// slot s of a heap is lane s's register, and the reference's sift loops
+// (hx_push / hx_pop / hx_replace_top, index for index) run in scalar control
+// flow over v_readlane and a lane-select write — a few cycles per level instead of two
+// dependent LDS round trips, which is what paced the LDS form (a query is one
+// wave running ~100 hops of serial heap updates).
+namespace {
+struct LaneHeap {
+    float v;    // this lane's slot: distance
+    int32_t i;  // id
+    __device__ __forceinline__ float rv(int s) const {
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), s));
+    }
+    __device__ __forceinline__ int32_t ri(int s) const { return __builtin_amdgcn_readlane(i, s); }
+    __device__ __forceinline__ void w(int s, float val, int32_t id) {
+        const bool me = (int)threadIdx.x == s;  // one wave per block
+        v = me ? val : v;
+        i = me ? id : i;
+    }
+    // 1-based positions as in faiss/utils/Heap.h; position p is slot p - 1
+    __device__ void push(int k, float val, int32_t id) {  // hx_push
+        int p = k;
+        while (p > 1) {
+            const int f = p >> 1;
+            const float fv = rv(f - 1);
+            const int32_t fi = ri(f - 1);
+            if (!cmp2_gt(val, fv, id, fi)) break;
+            w(p - 1, fv, fi);
+            p = f;
+        }
+        w(p - 1, val, id);
+    }
+    __device__ int sift(int k, float val, int32_t id) {  // hx_pop / hx_replace_top loop
+        int p = 1;
+        for (;;) {
+            const int p1 = p << 1, p2 = p1 + 1;
+            if (p1 > k) break;
+            const float v1 = rv(p1 - 1);
+            const int32_t i1 = ri(p1 - 1);
+            if (p2 == k + 1) {
+                if (cmp2_gt(val, v1, id, i1)) break;
+                w(p - 1, v1, i1);
+                p = p1;
+                continue;
+            }
+            const float v2 = rv(p2 - 1);
+            const int32_t i2 = ri(p2 - 1);
+            if (cmp2_gt(v1, v2, i1, i2)) {
+                if (cmp2_gt(val, v1, id, i1)) break;
+                w(p - 1, v1, i1);
+                p = p1;
+            } else {
+                if (cmp2_gt(val, v2, id, i2)) break;
+                w(p - 1, v2, i2);
+                p = p2;
+            }
+        }
+        return p;
+    }
+    __device__ void pop(int k) {  // hx_pop: the top leaves, slot k - 1 is stale
+        const int p = sift(k, rv(k - 1), ri(k - 1));
+        w(p - 1, rv(k - 1), ri(k - 1));
+    }
+    __device__ void replace_top(int k, float val, int32_t id) {
+        const int p = sift(k, val, id);
+        w(p - 1, val, id);
+    }
+};
+}  // namespace
+
+template <bool LDS_VISITED>
+__global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float* __restrict__ x,
+                                                       int ldx, int64_t n, int k, int efSearch,
+                                                       int ef, float* __restrict__ D,
+                                                       int64_t* __restrict__ I,
+                                                       int32_t* __restrict__ I32,
+                                                       uint32_t* __restrict__ vis_global,
+                                                       int64_t vwords,
+                                                       unsigned long long* __restrict__ stats,
+                                                       const uint32_t* __restrict__ only) {
+    const int64_t q = blockIdx.x;
+    if (only && only[q] == 0u) return;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* qs = sm;  // [ld]
+    uint32_t* vis = LDS_VISITED ? (uint32_t*)(sm + g.ld) : vis_global + blockIdx.x * vwords;
+    const int lane = threadIdx.x;
+    for (int j = lane; j < g.ld; j += 64) qs[j] = j < g.d ? x[q * ldx + j] : 0.f;
+    for (int64_t w = lane; w < vwords; w += 64) vis[w] = 0u;
+    LaneHeap C, R;  // MinimaxHeap candidates (size hk <= ef), results (k, heapified)
+    C.v = FLT_MAX;
+    C.i = -1;
+    R.v = FLT_MAX;  // heap_heapify<CMax> (Heap.h:316-339)
+    R.i = -1;
+    __syncthreads();
+    uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0;
+    if (g.entry_point >= 0) {
+        // ---- greedy descent (HNSW.cpp:852-924), as in k_hnsw_search
+        int nearest = g.entry_point;
+        float d_nearest = l2_row(qs, g.storage + (int64_t)nearest * g.ld, g.d);
+        for (int level = g.max_level; level >= 1; level--) {
+            for (;;) {
+                const uint64_t o = g.offsets[nearest];
+                const int b = g.cum_nb[level], e = g.cum_nb[level + 1];
+                const int cnt = e - b;
+                int v = lane < cnt ? g.neighbors[o + b + lane] : -1;
+                unsigned long long neg =
+                        __ballot(lane < cnt && v < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
+                const int first_neg = neg ? __ffsll((long long)neg) - 1 : 64;
+                float dis = WS_INF;
+                if (lane < first_neg) dis = l2_row(qs, g.storage + (int64_t)v * g.ld, g.d);
+                st_ndis += (uint32_t)min(first_neg, 64);
+                st_nhops += 1;
+                float md = dis;
+                int ml = lane;
+#pragma unroll
+                for (int m = 32; m > 0; m >>= 1) {
+                    const float od = __shfl_xor(md, m);
+                    const int ol = __shfl_xor(ml, m);
+                    if (od < md || (od == md && ol < ml)) {
+                        md = od;
+                        ml = ol;
+                    }
+                }
+                if (md < d_nearest) {
+                    d_nearest = md;
+                    nearest = __shfl(v, ml);
+                } else {
+                    break;
+                }
+            }
+        }
+        // ---- level 0: MinimaxHeap candidates(ef) seeded with the entry
+        int hk = 0, nvalid = 1;
+        C.push(++hk, d_nearest, nearest);
+        {  // search_from_candidates (:624-637): the seeds enter the results
+            float threshold = R.rv(0);
+            for (int s = 0; s < hk; s++) {
+                const int32_t v1 = C.ri(s);
+                const float dd = C.rv(s);
+                if (dd < threshold && R.rv(0) > dd) {
+                    R.replace_top(k, dd, v1);
+                    threshold = R.rv(0);
+                }
+                if (lane == 0) vis[v1 >> 5] |= 1u << (v1 & 31);
+            }
+        }
+        __syncthreads();
+        for (;;) {
+            if (nvalid <= 0) {  // candidates.size() == 0
+                st_n2 = 1;
+                break;
+            }
+            // pop_min (:1299-1330): smallest alive dis, highest slot among ties
+            float bd = FLT_MAX;
+            int bp = -1;
+            if (lane < hk && C.i != -1) {
+                bd = C.v;
+                bp = lane;
+            }
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) {
+                const float od = __shfl_xor(bd, m);
+                const int op = __shfl_xor(bp, m);
+                if (op >= 0 && (bp < 0 || od < bd || (od == bd && op > bp))) {
+                    bd = od;
+                    bp = op;
+                }
+            }
+            bp = __builtin_amdgcn_readfirstlane(bp);
+            const int32_t v0 = C.ri(bp);
+            const float d0 = bd;
+            // count_below(d0): every slot, dead ones included
+            const int nb = __popcll(__ballot(lane < hk && C.v < d0));
+            C.i = lane == bp ? -1 : C.i;
+            nvalid--;
+            if (nb >= efSearch) {
+                st_n2 = nvalid == 0 ? 1u : 0u;
+                break;
+            }
+            // neighbours of v0 in stored order (parallel test-and-set, as in
+            // k_hnsw_exact), fresh ones compacted to lanes 0..nf-1
+            const uint64_t o = g.offsets[v0];
+            const int b = g.cum_nb[0], e = g.cum_nb[1];
+            const int cnt = e - b;
+            const int32_t v1 = lane < cnt ? g.neighbors[o + b + lane] : -1;
+            const unsigned long long neg =
+                    __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
+            const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
+            bool fresh = lane < jmax && !((vis[v1 >> 5] >> (v1 & 31)) & 1u);
+            for (int i = 0; i < jmax; i++)
+                fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
+            __syncthreads();
+            if (fresh) atomicOr(&vis[v1 >> 5], 1u << (v1 & 31));
+            const unsigned long long fm = __ballot(fresh);
+            const int nf = __popcll(fm);
+            const unsigned long long lt = (1ull << lane) - 1ull;
+            const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
+            const int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
+            const float fdis = lane < nf ? l2_row(qs, g.storage + (int64_t)fv * g.ld, g.d) : 0.f;
+            st_ndis += (uint32_t)nf;
+            st_nhops += 1;
+            float threshold = R.rv(0);
+            for (int t = 0; t < nf; t++) {
+                const int32_t vt = __builtin_amdgcn_readlane(fv, t);
+                const float dis = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), t));
+                // add_to_heap (:678-689)
+                if (dis < threshold && R.rv(0) > dis) {
+                    R.replace_top(k, dis, vt);
+                    threshold = R.rv(0);
+                }
+                // MinimaxHeap::push (:1096-1107)
+                if (hk == ef) {
+                    if (dis >= C.rv(0)) continue;
+                    if (C.ri(0) != -1) --nvalid;
+                    C.pop(hk--);
+                }
+                C.push(++hk, dis, vt);
+                ++nvalid;
+            }
+        }
+    }
+    if (stats && lane == 0 && g.entry_point >= 0) {
+        atomicAdd(&stats[0], 1ull);
+        atomicAdd(&stats[1], (unsigned long long)st_n2);
+        atomicAdd(&stats[2], (unsigned long long)st_ndis);
+        atomicAdd(&stats[3], (unsigned long long)st_nhops);
+    }
+    // heap_reorder<CMax> (Heap.h:421-450), then the memmove to the front
+    int ii = 0;
+    for (int s = 0; s < k; s++) {
+        const float val = R.rv(0);
+        const int32_t id = R.ri(0);
+        R.pop(k - s);
+        R.w(k - ii - 1, val, id);
+        if (id != -1) ii++;
+    }
+    const float ov = __shfl(R.v, min(k - ii + lane, 63));
+    const int32_t oi = __shfl(R.i, min(k - ii + lane, 63));
+    if (lane < k) {
+        const float dv = lane < ii ? ov : FLT_MAX;
+        const int32_t iv = lane < ii ? oi : -1;
+        if (D) D[q * k + lane] = dv;
+        if (I) I[q * k + lane] = iv;
+        if (I32) I32[q * k + lane] = iv;
+    }
+}
+
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
@@ -551,11 +904,22 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
     const bool x_lds_vis = lds_x + vwords * 4 <= 64 * 1024;
     FAISS_THROW_IF_NOT_FMT(lds_x <= 64 * 1024, "max(efSearch, k) = %d too large for LDS", ef);
     const bool lds_vis = vwords * 4 <= 64 * 1024;
-    if ((batched && !lds_vis) || (!x_lds_vis)) {
+    if (!lds_vis || !x_lds_vis) {
         FAISS_THROW_IF_NOT(visited_scratch != nullptr);
         HIP_CHECK(hipMemsetAsync(visited_scratch, 0, sizeof(uint32_t) * vwords * n, s));
     }
     auto exact = [&](const uint32_t* only) {
+        if (ef <= 64 && k <= 64) {  // register heaps
+            if (lds_vis)
+                k_hnsw_exact_reg<true><<<dim3((unsigned)n), dim3(64), lds_q + vwords * 4, s>>>(
+                        g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only);
+            else
+                k_hnsw_exact_reg<false><<<dim3((unsigned)n), dim3(64), lds_q, s>>>(
+                        g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
+                        only);
+            HIP_LAUNCH_CHECK();
+            return;
+        }
         if (x_lds_vis)
             k_hnsw_exact<true><<<dim3((unsigned)n), dim3(64), lds_x + vwords * 4, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only);
@@ -565,7 +929,9 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
                     only);
         HIP_LAUNCH_CHECK();
     };
-    if (!batched) {
+    // FAISS_AMD_HNSW_EXACT=1: every query through the sequential kernel (tests)
+    const char* xenv = getenv("FAISS_AMD_HNSW_EXACT");
+    if (!batched || (xenv && !strcmp(xenv, "1"))) {
         exact(nullptr);
         return;
     }
@@ -579,6 +945,15 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
     }
     HIP_LAUNCH_CHECK();
     if (flags) {
+        if (getenv("FAISS_AMD_HNSW_STATS")) {  // debug: how many queries tie (synchronises)
+            std::vector<uint32_t> h((size_t)n);
+            HIP_CHECK(hipMemcpyAsync(h.data(), flags, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            size_t c = 0;
+            for (uint32_t f : h) c += f != 0u;
+            fprintf(stderr, "[faiss_amd] hnsw: %zu of %lld queries flagged for the sequential kernel\n",
+                    c, (long long)n);
+        }
         // the flagged queries again, sequentially; the visited scratch of a
         // flagged query is reset by the kernel itself
         exact(flags);

@@ -140,7 +140,10 @@ def test_gpu_add_path_equals_reference(amd, gpu, tag):
 
 @pytest.mark.parametrize("ef", [16, 64, 200])
 @pytest.mark.parametrize("nprobe", [8, 100])
-def test_gpu_hnsw_ivf_equals_reference(amd, gpu, ef, nprobe):
+@pytest.mark.parametrize("path_", ["batched", "sequential"])
+def test_gpu_hnsw_ivf_equals_reference(amd, gpu, monkeypatch, ef, nprobe, path_):
+    if path_ == "sequential":
+        monkeypatch.setenv("FAISS_AMD_HNSW_EXACT", "1")
     idx = amd.read_index(path("hnswivf"))
     q = idx.quantizer
     q.efSearch = ef
@@ -155,8 +158,12 @@ def test_gpu_hnsw_ivf_equals_reference(amd, gpu, ef, nprobe):
 
 @pytest.mark.parametrize("ef", [8, 32, 200])
 @pytest.mark.parametrize("k", [1, 10, 40])
-def test_gpu_hnsw_duplicates_equal_reference(amd, gpu, ef, k):
-    """exact distance ties in the MinimaxHeap and the result heap"""
+@pytest.mark.parametrize("path_", ["batched", "sequential"])
+def test_gpu_hnsw_duplicates_equal_reference(amd, gpu, monkeypatch, ef, k, path_):
+    """exact distance ties in the MinimaxHeap and the result heap; the
+    sequential kernel (register heaps for ef, k <= 64) on every query too"""
+    if path_ == "sequential":
+        monkeypatch.setenv("FAISS_AMD_HNSW_EXACT", "1")
     idx = amd.read_index(path("hnsw_dup"))
     idx.efSearch = ef
     D, I = idx.search(FX["hnsw_dup_xq"], k)
