@@ -686,106 +686,69 @@ __global__ void k_list_max(const float* __restrict__ yn, const uint32_t* __restr
 //   2. the survivors' rows and ids.
 // Invalid / empty probes carry empty entries (k_bucket_fill), so neither the
 // assignment nor the list geometry arrays are read.
-// Exact distances: 4 lanes per row (ref_arith.h order, see eval_rows64).
+// Exact distances: 4 lanes per row (ref_arith.h order, see eval_rows64_direct).
 constexpr int RR_CAP = 512;
 constexpr int RR_XM = BDM / 8;
 constexpr int RR_W = 1;  // waves (queries) per block: one, for fine-grained packing
 // (the re-rank's barriers sit in wave-uniform branches: one wave per block)
 static_assert(RR_W == 1, "k_ivf_rerank assumes one wave per block");
 
-// exact reference-order distance of the row `grow` each lane names (valid
-// lanes only); 16 rows per pass, 4 lanes per row: lane j' of a row owns the
-// reference's partial sums c[2j'] and c[2j'+1] (dims 8m + 2j' + {0,1}), so a
-// pass is one round trip of 16 float2 loads per lane
-constexpr int RR_RS = BDM + 4;  // LDS row stride (floats) of the staged rows
-
-// exact reference-order distance of the row `grow` each lane names (valid
-// lanes only), 16 rows per pass:
-//  1. the pass's rows are staged into LDS with coalesced 16-B loads (32
-//     lanes per 512-B row, whole cache lines per request);
-//  2. 4 lanes per row evaluate it: lane j' owns the reference's partial sums
-//     c[2j'] and c[2j'+1] (dims 8m + 2j' + {0,1}); x_j = c_j + c_{j+4},
-//     then (x0 + x2) + (x1 + x3) (ref_arith.h order), then the epilogue dims.
+// Exact reference-order distance of the row `grow` each lane names (valid
+// lanes only), 16 rows per pass, 4 lanes per row: lane j' of row g owns the
+// reference's partial sums c[2j'] and c[2j'+1] (dims 8m + 2j' + {0,1}) and
+// loads those float2 pairs straight from the arena — one load instruction
+// covers 16 rows x 32 contiguous bytes, the 4 lanes of a row complete its
+// cache lines.  x_j = c_j + c_{j+4}, then (x0 + x2) + (x1 + x3) (ref_arith.h
+// order), then the epilogue dims.  No LDS staging and no barriers: the
+// kernel's LDS is the candidate list only, so 4 waves per SIMD fit (3 with
+// staged rows; c2 re-rank 69 -> 57 us).
 template <bool L2>
-__device__ __forceinline__ float eval_rows64(const float* xr /* LDS copy of the query */,
-                                             float* stage /* LDS [16][RR_RS] */,
-                                             const float* __restrict__ xq,
-                                             const float* __restrict__ codes, int ldc, int d,
-                                             uint32_t grow, bool valid, int lane) {
+__device__ __forceinline__ float eval_rows64_direct(const float* xr /* LDS copy of the query */,
+                                                    const float* __restrict__ xq,
+                                                    const float* __restrict__ codes, int ldc,
+                                                    int d, uint32_t grow, bool valid, int lane) {
     const int g = lane >> 2, jp = lane & 3;
     const int n8 = d & ~7, nm = n8 >> 3;
-    const int d4 = (d + 3) >> 2;  // float4 per row actually read
     const unsigned long long vm = __ballot(valid);
     float out = 0.f;
-    // passes with rows, in order; the next pass's rows are loaded (into the
-    // registers the LDS staging just freed) while this one is evaluated
-    auto next_pass = [&](int p) {
-        while (p < 4 && ((vm >> (16 * p)) & 0xffffull) == 0ull) p++;
-        return p;
-    };
-    float4 v[8];
-    auto load = [&](int p) {
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const int row = 2 * t + (lane >> 5), c4 = lane & 31;
-            const uint32_t rg = __shfl(grow, 16 * p + row);
-            const bool rv = (vm >> (16 * p + row)) & 1ull;
-            v[t] = (rv && c4 < d4) ? *(const float4*)(codes + (int64_t)rg * ldc + 4 * c4)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
-    int p = next_pass(0);
-    if (p < 4) load(p);
 #pragma unroll 1
-    while (p < 4) {
-        // ---- stage: row 2t + (lane >> 5), float4 column lane & 31
+    for (int p = 0; p < 4; p++) {
+        if (((vm >> (16 * p)) & 0xffffull) == 0ull) continue;  // wave-uniform
+        const uint32_t rg = __shfl(grow, 16 * p + g);
+        const bool rv = (vm >> (16 * p + g)) & 1ull;
+        const float* yr = codes + (int64_t)(rv ? rg : 0u) * ldc;
+        float2 yv[RR_XM];
 #pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const int row = 2 * t + (lane >> 5), c4 = lane & 31;
-            *(float4*)(stage + row * RR_RS + 4 * c4) = v[t];
-        }
-        // one wave per block: orders the staging before the reads (LDS only:
-        // the next pass's loads stay in flight)
-        __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-        const int pn = next_pass(p + 1);
-        if (pn < 4) load(pn);
-        // ---- evaluate
-        const float* yj = stage + g * RR_RS + 2 * jp;
+        for (int m = 0; m < RR_XM; m++)
+            yv[m] = m < nm ? *(const float2*)(yr + 8 * m + 2 * jp) : make_float2(0.f, 0.f);
         const float* xj = xr + 2 * jp;
         float ca = 0.f, cb = 0.f;
 #pragma unroll
         for (int m = 0; m < RR_XM; m++) {
             const float2 xv = *(const float2*)(xj + 8 * m);
-            const float2 yv = *(const float2*)(yj + 8 * m);
-            const float ta = ref_term_fma<L2>(xv.x, yv.x, ca);
-            const float tb = ref_term_fma<L2>(xv.y, yv.y, cb);
+            const float ta = ref_term_fma<L2>(xv.x, yv[m].x, ca);
+            const float tb = ref_term_fma<L2>(xv.y, yv[m].y, cb);
             ca = m < nm ? ta : ca;
             cb = m < nm ? tb : cb;
         }
         ca += __shfl_xor(ca, 2);
         cb += __shfl_xor(cb, 2);
-        ca += __shfl_xor(ca, 1);  // lane 0: x0 + x2
-        cb += __shfl_xor(cb, 1);  // lane 0: x1 + x3
+        ca += __shfl_xor(ca, 1);  // x0 + x2
+        cb += __shfl_xor(cb, 1);  // x1 + x3
         float r = ca + cb;
         if (n8 < d) {
-            const float* y = stage + g * RR_RS;
             int i = n8;
             if (d - n8 >= 4) {
-                const float e0 = ref_term<L2>(xq[n8], y[n8]), e1 = ref_term<L2>(xq[n8 + 1], y[n8 + 1]);
-                const float e2 = ref_term<L2>(xq[n8 + 2], y[n8 + 2]);
-                const float e3 = ref_term<L2>(xq[n8 + 3], y[n8 + 3]);
+                const float e0 = ref_term<L2>(xq[n8], yr[n8]), e1 = ref_term<L2>(xq[n8 + 1], yr[n8 + 1]);
+                const float e2 = ref_term<L2>(xq[n8 + 2], yr[n8 + 2]);
+                const float e3 = ref_term<L2>(xq[n8 + 3], yr[n8 + 3]);
                 r = r + ((e0 + e2) + (e1 + e3));
                 i += 4;
             }
-            for (; i < d; i++) r = ref_term_fma<L2>(xq[i], y[i], r);
+            for (; i < d; i++) r = ref_term_fma<L2>(xq[i], yr[i], r);
         }
         const float got = __shfl(r, 4 * (lane & 15));
         if ((lane >> 4) == p) out = got;
-        // the next pass overwrites the staging rows
-        __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-        p = pn;
     }
     return out;
 }
@@ -856,7 +819,6 @@ struct RerankStream {
     const float* xq;
     const float* codes;
     const float* xs;  // LDS copy of the query (first d & ~7 dims)
-    float* stage;     // LDS staging rows of the evaluator
     int ldc, d, lane, nsv, KE, KT, E;
     uint32_t lowmask;
     bool overflow;  // candidate list did not fit: re-derive it from global
@@ -880,7 +842,7 @@ struct RerankStream {
             const float d0 = __shfl(my_d0, r);
             dis = ok ? pq_exact<PQD>(pa, xs, grow, l, d0) : 0.f;
         } else {
-            dis = eval_rows64<L2>(xs, stage, xq, codes, ldc, d, grow, ok, lane);
+            dis = eval_rows64_direct<L2>(xs, xq, codes, ldc, d, grow, ok, lane);
         }
         k1 = WS_INF;
         k2 = WS_NOID;
@@ -959,7 +921,8 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
     __shared__ uint32_t surv[RR_W][RR_CAP];
     __shared__ uint16_t sprobe[RR_W][RR_CAP];
     __shared__ __attribute__((aligned(16))) float xsh[RR_W][BDM];
-    __shared__ __attribute__((aligned(16))) float stg[RR_W][16 * RR_RS];
+    // scratch of the small-batch compaction (64 NB keys + labels, NB <= 4)
+    __shared__ __attribute__((aligned(16))) float stg[RR_W][64 * 4 * 3];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t q0 = (int64_t)blockIdx.x * RR_W + w;
     const bool valid = q0 < n;
@@ -1105,7 +1068,6 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
     st.xq = xq;
     st.codes = codes;
     st.xs = xsh[w];
-    st.stage = stg[w];
     st.ldc = ldc;
     st.d = d;
     st.lane = lane;
