@@ -6,10 +6,14 @@ nprobe=32; 1/2/4/8 GPUs.  One step = one batched search of nq=10k synthetic
 uniform queries (faiss float_rand, seed 5678) against IVF4096,Flat over 1M
 synthetic vectors (float_rand seed 1234), k=10, inputs resident in HBM.
 
-N=1: the whole path (coarse fp32-MFMA quantizer + list-centric scan + merge)
-through faiss_amd_Index_search_device.  N>1 (torch.distributed.run, one rank
-per GPU, RCCL): the 1M-vector index is sharded by id modulo N, every rank
-brings its own 10k queries (weak scaling in queries), see hnsw-ivf_amd/dist.py.
+N=1: the whole path (query prep + bf16x3-MFMA coarse filter + exact re-rank +
+list-centric bf16x2-MFMA scan + exact re-rank) through
+faiss_amd_Index_search_device.  N>1 (torch.distributed.run, one rank per GPU):
+c1-c4 are one-GPU configs, so every rank serves its own 10k queries from a
+replica of the whole index (weak scaling, no collective on the data path;
+--shard instead shards the index by id modulo N and runs the IndexShardsIVF
+exchange of hnsw-ivf_amd/dist.py over RCCL); c5 is the sharded config: the
+100M set is split by id modulo N and the 100k queries are exchanged.
 """
 from __future__ import annotations
 
@@ -164,6 +168,9 @@ def main():
     ap.add_argument("--recall-queries", type=int, default=1000)
     ap.add_argument("--shard-of", type=int, default=0,
                     help="c5: build one rank's share of a run over this many GPUs")
+    ap.add_argument("--shard", action="store_true",
+                    help="c1-c4 at N > 1: shard the index by id %% N over RCCL "
+                         "(IndexShardsIVF exchange) instead of one replica per GPU")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -171,12 +178,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}"
-    torch.cuda.set_device(local_rank)
+    # c1-c4 at N > 1 are replicas: their only collectives are the timing
+    # barrier and max (gloo, host side); sharded runs exchange device tensors
+    # over RCCL.  (local_rank % devices: a rehearsal of N ranks on fewer GPUs)
+    replicas = world > 1 and not cfg.get("sharded", False) and not args.shard
+    gpu = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if replicas:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
     amd = ge.load_package()
-    amd.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    amd.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     stream = torch.cuda.current_stream().cuda_stream
 
     d, nb, nq, k, nprobe = cfg["d"], cfg["nb"], cfg["nq"], cfg["k"], cfg["nprobe"]
@@ -188,6 +203,9 @@ def main():
     index = amd.index_factory(d, cfg["desc"])
     sharded = cfg.get("sharded", False)
     nshard = max(world, args.shard_of) if sharded else world
+    # c1-c4 name one GPU; at N > 1 each GPU serves its own queries from a
+    # replica of the whole index (independent units, no collective) unless
+    # --shard asks for the IndexShardsIVF exchange.  c5 is the sharded config.
     if sharded:
         # rows of the float_rand(nb * d, 1234) set, generated shard-wise and
         # added in chunks (no host image of the whole shard)
@@ -219,7 +237,8 @@ def main():
     else:
         xb = amd.float_rand(nb * d, 1234).reshape(nb, d)
         index.train(xb[:cfg["ntrain"]])
-        ids = np.arange(rank, nb, world, dtype=np.int64)
+        ids = (np.arange(nb, dtype=np.int64) if world == 1 or replicas
+               else np.arange(rank, nb, world, dtype=np.int64))
         index.add_with_ids(xb[ids], ids)
     index.nprobe = nprobe
     if "efSearch" in cfg:
@@ -232,7 +251,7 @@ def main():
     D_t = torch.empty((nq, k), dtype=torch.float32, device=dev)
     I_t = torch.empty((nq, k), dtype=torch.int64, device=dev)
 
-    if world == 1:
+    if world == 1 or replicas:
         def step():
             index.search_device(nq, x_t.data_ptr(), k, D_t.data_ptr(), I_t.data_ptr(), stream)
     else:
@@ -278,7 +297,7 @@ def main():
     elapsed = time.perf_counter() - t1
     amd.set_kernel_timing(False)
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if replicas else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed / args.steps * 1e3
@@ -298,7 +317,7 @@ def main():
     scan_ms = float(np.sum(scan)) / args.steps if scan else float("nan")
     # algorithmic work of one scan launch: sum over (query, probe) of the
     # probed list length x per-candidate cost (Flat: 3*d flops; PQ: M bytes)
-    nq_launch = nq * world
+    nq_launch = nq if replicas else nq * world
     cd_h = torch.empty((nq, nprobe), dtype=torch.float32, device=dev)
     ci_h = torch.empty((nq, nprobe), dtype=torch.int32, device=dev)
     index.quantize_device(nq, x_t.data_ptr(), nprobe, cd_h.data_ptr(), ci_h.data_ptr(), stream)
@@ -346,7 +365,7 @@ def main():
         dpad = -(-d // 32) * 32
         lists = np.unique(ci_h.cpu().numpy().astype(np.int64))
         lists = lists[lists >= 0]
-        work = float(sizes[lists].sum()) * (2.0 * dpad + 8.0) * world
+        work = float(sizes[lists].sum()) * (2.0 * dpad + 8.0) * (1 if replicas else world)
         achieved = work / (scan_ms * 1e-3) / 1e9
         flops = cands * nprod * 2.0 * dpad
         mfma_tf = flops / (scan_ms * 1e-3) / 1e12
@@ -411,10 +430,13 @@ def main():
             "value": qps, "unit": "queries/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            # "weak": every GPU brings its own nq queries (replicas / --shard);
+            # "strong": c5's 100M set and 100k queries split over the GPUs
             "config": {"workload": cfg["workload"], "d": d, "nb": nb, "vectors_per_gpu": len(ids),
                        "nq_per_gpu": nq,
                        "nprobe": nprobe, "k": k, "global_batch": nq * world,
-                       "parallelism": f"shards{world}" if world > 1 else "single",
+                       "parallelism": (f"replicas{world}" if replicas else
+                                       f"shards{world}" if world > 1 else "single"),
                        "recall_at_10": recall, "candidates_per_query": cand_per_q},
             "roofline": roofline,
             "cpu_baseline": cpu,
