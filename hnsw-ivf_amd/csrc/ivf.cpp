@@ -934,13 +934,24 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         s_pflags_.reserve(4 * sizeof(uint32_t));
         if (dbg) HIP_CHECK(hipMemsetAsync(s_pflags_.ptr, 0, 4 * sizeof(uint32_t), s));
         int KT = 0;
+        // query image: the flat quantizer's when this is search()'s chunk,
+        // else prepared here (one launch instead of a split per work item)
+        const void* qimg = shared_qimg_;
+        if (!qimg && ldx % 4 == 0) {
+            s_q_.reserve(kern::query_image_bytes(n, d) + sizeof(float) * n);
+            kern::query_prep(x, n, ldx, d, nullptr, s_q_.ptr,
+                             (float*)((uint8_t*)s_q_.ptr + kern::query_image_bytes(n, d)), s);
+            qimg = s_q_.ptr;
+        }
+        const float* qxn =
+                qimg ? (const float*)((const uint8_t*)qimg + kern::query_image_bytes(n, d)) : nullptr;
         {
             ScopedKernelTimer tm(&ktimes, "ivfpq_filter", 0.0, s);
             kern::ivfpq_filter(x, ldx, d, (int)pq.M, d_dec_.ptr, d_codes_.as<uint8_t>(),
                                d_terms_.as<float>(), centroid_dis, d_cnorm_.as<float>(),
                                d_lrmax_.as<float>(), d_lRmax_.as<float>(), (int)nlist, n, np,
                                (int)k, pq_obits_, b, mi, s_pkeys_.as<uint32_t>(),
-                               s_precs_.as<kern::ProbeRec>(), &KT, s);
+                               s_precs_.as<kern::ProbeRec>(), &KT, s, qimg, qxn);
         }
         {
             ScopedKernelTimer tm(&ktimes, "ivfpq_rerank", 0.0, s);

@@ -175,7 +175,8 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
                   const float* terms, const float* cdis, const float* cnorm, const float* lrmax,
                   const float* lRmax, int nlist, int64_t n, int nprobe, int k, int obits,
                   const IVFBuckets& b, int64_t max_items, uint32_t* keys, ProbeRec* recs,
-                  int* kt_out, hipStream_t s);
+                  int* kt_out, hipStream_t s,
+                  const void* qimg = nullptr, const float* qxn = nullptr);
 void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx, int d,
                   const int64_t* ids, const PQArgs& pa, int dsub, int64_t n, int nprobe, int KT,
                   int obits, int k, const uint8_t* sel, float* D, int64_t* I, uint32_t* stats,

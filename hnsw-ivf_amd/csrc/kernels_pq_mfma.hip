@@ -144,7 +144,8 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
         float coef, int obits, const uint32_t* __restrict__ item_off,
         const ItemDesc* __restrict__ item_desc, const uint32_t* __restrict__ item_entries,
         const uint32_t* __restrict__ lim, const uint8_t* __restrict__ sel,
-        uint32_t* __restrict__ keys, ProbeRec* __restrict__ recs) {
+        uint32_t* __restrict__ keys, ProbeRec* __restrict__ recs,
+        const uint8_t* __restrict__ qimg, const float* __restrict__ qxn) {
     constexpr int D = 16 * NS;
     constexpr int M = D / DSUB;
     constexpr int CS = (M + 3) & ~3;  // code stride (bytes)
@@ -231,7 +232,10 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
         bf16x8 bh[NS], bl[NS];
         float xn = 0.f, base = 0.f;
         if (active) {
-            load_query_frags<NS>(x, ldx, D, qrow_s[qloc], lh, bh, bl, xn);
+            if (qimg)  // fragments prepared once per query (k_query_prep)
+                load_query_image<NS>(qimg, qxn, qrow_s[qloc], lh, bh, bl, xn);
+            else
+                load_query_frags<NS>(x, ldx, D, qrow_s[qloc], lh, bh, bl, xn);
             base = cdis[ent_s[qloc]];
         }
         ThreadQueue32<KT> tq;
@@ -326,7 +330,7 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
                   const float* terms, const float* cdis, const float* cnorm, const float* lrmax,
                   const float* lRmax, int nlist, int64_t n, int nprobe, int k, int obits,
                   const IVFBuckets& b, int64_t max_items, uint32_t* keys, ProbeRec* recs,
-                  int* kt_out, hipStream_t s) {
+                  int* kt_out, hipStream_t s, const void* qimg, const float* qxn) {
     FAISS_THROW_IF_NOT(ivfpq_mfma_eligible(d, M, k, nprobe));
     FAISS_THROW_IF_NOT(b.item_desc && b.item_entries);
     FAISS_THROW_IF_NOT(obits >= 4 && obits <= 14);
@@ -357,7 +361,7 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
         kfn<<<dim3((unsigned)grid), dim3(256), lds, s>>>(                                      \
                 x, ldx, (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, nlist,    \
                 nprobe, coef, obits, b.item_off, b.item_desc, b.item_entries, b.lim, b.sel,    \
-                keys, recs);                                                                   \
+                keys, recs, (const uint8_t*)qimg, qxn);                                        \
         HIP_LAUNCH_CHECK();                                                                    \
         return;                                                                                \
     }
