@@ -354,6 +354,24 @@ void IndexHNSW::sync_device() const {
     HIP_CHECK(hipMemcpyAsync(d_cum_.ptr, hnsw.cum_nneighbor_per_level.data(),
                              sizeof(int32_t) * hnsw.cum_nneighbor_per_level.size(),
                              hipMemcpyHostToDevice, s));
+    // regular level-0 table [ntotal][nb_neighbors(0)] (a copy of each node's
+    // level-0 slice): the level-0 hop then loads its neighbour ids without
+    // first loading offsets[v].  Kept when it costs at most 1 GiB of HBM.
+    std::vector<int32_t> nb0;
+    const size_t c0 = hnsw.cum_nneighbor_per_level.size() >= 2 ? (size_t)hnsw.nb_neighbors(0) : 0;
+    nb0_stride_ = 0;
+    if (c0 > 0 && !hnsw.levels.empty() &&
+        hnsw.levels.size() * c0 * sizeof(int32_t) <= ((size_t)1 << 30)) {
+        const size_t nn = hnsw.levels.size();
+        const size_t b0 = (size_t)hnsw.cum_nneighbor_per_level[0];
+        nb0.resize(nn * c0);
+        for (size_t v = 0; v < nn; v++)
+            memcpy(&nb0[v * c0], &hnsw.neighbors[hnsw.offsets[v] + b0], c0 * sizeof(int32_t));
+        d_nb0_.reserve(sizeof(int32_t) * nb0.size());
+        HIP_CHECK(hipMemcpyAsync(d_nb0_.ptr, nb0.data(), sizeof(int32_t) * nb0.size(),
+                                 hipMemcpyHostToDevice, s));
+        nb0_stride_ = (int)c0;
+    }
     HIP_CHECK(hipStreamSynchronize(s));
     dirty_ = false;
 }
@@ -381,6 +399,8 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
     gd.offsets = d_offsets_.as<uint64_t>();
     gd.neighbors = d_neighbors_.as<int32_t>();
     gd.cum_nb = d_cum_.as<int32_t>();
+    gd.nb0 = nb0_stride_ > 0 ? d_nb0_.as<int32_t>() : nullptr;
+    gd.nb0_stride = nb0_stride_;
     gd.nlevels_cum = (int)hnsw.cum_nneighbor_per_level.size();
     gd.entry_point = ntotal > 0 ? hnsw.entry_point : -1;
     gd.max_level = hnsw.max_level;

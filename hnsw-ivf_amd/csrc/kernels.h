@@ -299,6 +299,11 @@ struct HNSWDevice {
     const uint64_t* offsets;  // [ntotal+1]
     const int32_t* neighbors;
     const int32_t* cum_nb;    // cum_nneighbor_per_level
+    // level-0 neighbours of node v at nb0[v * nb0_stride + j] (a regular copy
+    // of the level-0 slices of `neighbors`, so a level-0 hop needs no offsets
+    // load); null: read them through offsets
+    const int32_t* nb0;
+    int nb0_stride;
     int nlevels_cum;
     int entry_point;
     int max_level;

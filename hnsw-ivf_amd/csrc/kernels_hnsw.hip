@@ -251,11 +251,12 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
                 st_n2 = (__ballot(b0) | __ballot(b1)) == 0ull ? 1u : 0u;
                 break;
             }
-            // neighbours of v0 at level 0
-            const uint64_t o = g.offsets[v0];
-            const int b = g.cum_nb[0], e = g.cum_nb[1];
-            const int cnt = e - b;
-            int v = lane < cnt ? g.neighbors[o + b + lane] : -1;
+            // neighbours of v0 at level 0 (the regular table: no offsets load)
+            const int cnt = g.cum_nb[1] - g.cum_nb[0];
+            int v = -1;
+            if (lane < cnt)
+                v = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
+                          : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
             unsigned long long neg = __ballot(lane < cnt && v < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
             const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
             bool fresh = false;
@@ -555,12 +556,13 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
             // test-and-set is restated in parallel: neighbour j is fresh when
             // its bit was clear before this hop and no earlier neighbour of the
             // list is the same node; the fresh ones keep their stored order)
-            const uint64_t o = g.offsets[v0];
-            const int b = g.cum_nb[0], e = g.cum_nb[1];
-            const int cnt = e - b;
+            const int cnt = g.cum_nb[1] - g.cum_nb[0];
             int nf;
             {
-                const int32_t v1 = lane < cnt ? g.neighbors[o + b + lane] : -1;
+                int32_t v1 = -1;
+                if (lane < cnt)
+                    v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
+                               : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
                 const unsigned long long neg =
                         __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
                 const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
@@ -821,10 +823,11 @@ __global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float
             }
             // neighbours of v0 in stored order (parallel test-and-set, as in
             // k_hnsw_exact), fresh ones compacted to lanes 0..nf-1
-            const uint64_t o = g.offsets[v0];
-            const int b = g.cum_nb[0], e = g.cum_nb[1];
-            const int cnt = e - b;
-            const int32_t v1 = lane < cnt ? g.neighbors[o + b + lane] : -1;
+            const int cnt = g.cum_nb[1] - g.cum_nb[0];
+            int32_t v1 = -1;
+            if (lane < cnt)
+                v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
+                           : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
             const unsigned long long neg =
                     __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
             const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;

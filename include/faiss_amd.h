@@ -289,8 +289,9 @@ struct IndexHNSW : Index {
     template <class OutIdx>
     void hnsw_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
                      const SearchParameters* params, hipStream_t stream) const;
-    mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, s_visited_, d_stats_,
+    mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, d_nb0_, s_visited_, d_stats_,
             s_flags_;
+    mutable int nb0_stride_ = 0;  // level-0 table width (0: not built)
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
 };
