@@ -155,7 +155,8 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
 
     float res_d = WS_INF;
     long long res_i = WS_NOID;
-    bool tie = false;  // an exact distance tie where the batched form may differ
+    uint32_t tie = 0u;  // exact distance ties where the batched form may differ (reason bits)
+    float rdisc = WS_INF;  // smallest distance the result heap ever turned away
     // HNSWStats (faiss/impl/HNSW.h:234-246): n1, n2, ndis, nhops of this query
     uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0;
     if (g.entry_point >= 0) {
@@ -234,7 +235,8 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
             // pop_min among equal alive minima picks by heap slot in the
             // reference (MinimaxHeap::pop_min): an order the batched queue
             // does not keep
-            tie |= __popcll(__ballot(a0 && c0d == d0v)) + __popcll(__ballot(a1 && c1d == d0v)) > 1;
+            if (__popcll(__ballot(a0 && c0d == d0v)) + __popcll(__ballot(a1 && c1d == d0v)) > 1)
+                tie |= 1u;  // pop order
             if (pos < 64) {
                 if (lane == pos) c0i &= ~1ll;
             } else {
@@ -278,9 +280,8 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
             // kept candidates (checked after the merge below), flags the query
             // for the sequential kernel (k_hnsw_exact).
             {
-                const float kth = __shfl(res_d, k - 1);
                 const float eth = ef <= 64 ? __shfl(c0d, ef - 1) : __shfl(c1d, ef - 65);
-                tie |= __ballot(fresh && (dis == kth || dis == eth)) != 0ull;
+                if (__ballot(fresh && dis == eth) != 0ull) tie |= 2u;  // push at the max
             }
             // result heap: k smallest (dis, id) of the union, strict admission;
             // only keys below the current k-th can enter: they are compacted
@@ -291,17 +292,19 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
                 const bool pass = fresh && dis < FLT_MAX && key_less(dis, (long long)v, thr_d, thr_i);
                 float cd = pass ? dis : WS_INF;
                 long long ci = pass ? (long long)v : WS_NOID;
+                // the result heap never steers the traversal (only the
+                // candidate heap does), so the strict-admission / (dis, id)
+                // difference can only show in the final set: it is checked
+                // once, after the search, against the smallest distance the
+                // heap ever turned away (rejected entrants, evicted keys)
+                float rej = (fresh && !pass && dis < FLT_MAX) ? dis : WS_INF;
+#pragma unroll
+                for (int j = 32; j > 0; j >>= 1) rej = fminf(rej, __shfl_xor(rej, j));
+                rdisc = fminf(rdisc, rej);
                 const int m = wave_compact(cd, ci, pass, lane);
                 if (m > 0) {
                     wave_sort_m(cd, ci, lane, m);
-                    const float disc = merge64_disc(res_d, res_i, cd, ci, lane);
-                    // the sequential heap's strict admission against a
-                    // threshold that moves within the batch and the union's
-                    // (dis, id) order differ only when the k-th kept and the
-                    // best dropped distance are equal
-                    const float kd = __shfl(res_d, k - 1);
-                    const float nd = k < 64 ? __shfl(res_d, k) : disc;
-                    tie |= nd < WS_INF && kd == nd;
+                    rdisc = fminf(rdisc, merge64_disc(res_d, res_i, cd, ci, lane));
                 }
             }
             // candidate heap: ef smallest of the union (dead slots included);
@@ -324,12 +327,19 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
                     const float ld = ef <= 64 ? __shfl(c0d, ef - 1) : __shfl(c1d, ef - 65);
                     const float nd = ef < 64 ? __shfl(c0d, ef)
                                      : ef < 128 ? __shfl(c1d, ef - 64) : disc;
-                    tie |= nd < WS_INF && ld == nd;
+                    if (nd < WS_INF && ld == nd) tie |= 4u;  // candidate boundary
                 }
             }
         }
     }
-    if (tie_flags && lane == 0) tie_flags[q] = tie ? 1u : 0u;
+    {
+        // the final k-set equals the sequential heap's unless its k-th
+        // distance is shared by a key it turned away (or kept past k)
+        const float kd = __shfl(res_d, k - 1);
+        const float nd = fminf(rdisc, k < 64 ? __shfl(res_d, k) : WS_INF);
+        if (nd < WS_INF && kd == nd) tie |= 8u;  // result boundary
+    }
+    if (tie_flags && lane == 0) tie_flags[q] = tie;
     if (tie && tie_flags) return;  // the sequential kernel redoes this query
     if (stats && lane == 0 && g.entry_point >= 0) {
         atomicAdd(&stats[0], 1ull);
@@ -952,10 +962,16 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
             std::vector<uint32_t> h((size_t)n);
             HIP_CHECK(hipMemcpyAsync(h.data(), flags, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
             HIP_CHECK(hipStreamSynchronize(s));
-            size_t c = 0;
-            for (uint32_t f : h) c += f != 0u;
-            fprintf(stderr, "[faiss_amd] hnsw: %zu of %lld queries flagged for the sequential kernel\n",
-                    c, (long long)n);
+            size_t c = 0, r[4] = {0, 0, 0, 0};
+            for (uint32_t f : h) {
+                c += f != 0u;
+                for (int b = 0; b < 4; b++) r[b] += (f >> b) & 1u;
+            }
+            fprintf(stderr,
+                    "[faiss_amd] hnsw: %zu of %lld queries flagged for the sequential kernel "
+                    "(pop order %zu, push at the max %zu, candidate boundary %zu, result "
+                    "boundary %zu)\n",
+                    c, (long long)n, r[0], r[1], r[2], r[3]);
         }
         // the flagged queries again, sequentially; the visited scratch of a
         // flagged query is reset by the kernel itself
