@@ -628,7 +628,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     int mode = scan_mode;
     if (env && !strcmp(env, "exact")) mode = 1;
     if (env && !strcmp(env, "mfma")) mode = 0;
-    const int KQ = obits_ <= 14 ? kern::ivf_mfma_kq((int)k, d) : 0;
+    const int KQ = obits_ <= 14 ? kern::ivf_mfma_kq((int)k, d, np) : 0;
     if (mode != 0 || KQ <= 0 || np > kern::kMaxK || store_pairs) {
         exact_scan_device(n, x, ldx, k, np, assign, cdis, distances, labels, s, lim, sel,
                           store_pairs);
@@ -916,7 +916,7 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         b.counts_next = counts_next;
         b.lim = lim;
         b.sel = sel;
-        const int KE = kern::ivf_mfma_kq((int)k, d);
+        const int KE = kern::ivf_mfma_kq((int)k, d, np);
         s_pkeys_.reserve(sizeof(uint32_t) * n * np * KE);
         s_precs_.reserve(sizeof(kern::ProbeRec) * n * np);
         b.mark_keys = s_pkeys_.as<uint32_t>();

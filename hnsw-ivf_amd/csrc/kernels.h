@@ -248,7 +248,7 @@ inline int64_t ivf_max_items(int64_t n, int nprobe, int nlist, int QT) {
 // results are identical to the general exact scan (ivf_exact_search).
 // ivf_mfma_kq = entries kept per (query, list); 0 = not eligible
 // (k > 32 or roundup(d, 16) > 128).
-int ivf_mfma_kq(int k, int d);
+int ivf_mfma_kq(int k, int d, int nprobe = 0);
 int ivf_bf3_obits(uint32_t max_list_len);
 // padded dim of the bf16 hi/lo images (multiple of 32)
 constexpr int BDM_HOST = 128;  // bf3.h BDM: max padded dim of the MFMA paths

@@ -1167,10 +1167,14 @@ void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* l
     HIP_LAUNCH_CHECK();
 }
 
-int ivf_mfma_kq(int k, int dp) {
-    // entries kept per (query, list) = 4 threads x KT
+int ivf_mfma_kq(int k, int dp, int nprobe) {
+    // entries kept per (query, list) = 4 threads x KT.  A thread stream that
+    // drops a key which may reach the top-k "fails" and is re-scanned whole by
+    // the re-rank; with few probes the top-k crowds into the query's nearest
+    // lists (c1: k = 10 over 8 probes), so nprobe < k keeps 8 per stream.
     if (bf3_db(dp) > BDM || k > 32) return 0;
-    return 4 * (k <= 2 ? 2 : k <= 12 ? 4 : 8);
+    const int kt = k <= 2 ? 2 : k <= 12 ? 4 : 8;
+    return 4 * (nprobe > 0 && nprobe < k ? 8 : kt);
 }
 
 int ivf_bf3_obits(uint32_t max_list_len) {
@@ -1234,7 +1238,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         const void* cbs, void* qscratch, bool qready) {
     if (n <= 0) return;
     const bool aligned_lists = list_align % BV == 0 && cbs != nullptr;
-    const int KE = ivf_mfma_kq(k, d);
+    const int KE = ivf_mfma_kq(k, d, nprobe);
     FAISS_THROW_IF_NOT(KE > 0);
     FAISS_THROW_IF_NOT(ldc % 4 == 0);
     FAISS_THROW_IF_NOT(nprobe <= 64);

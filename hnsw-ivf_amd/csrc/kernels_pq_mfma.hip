@@ -334,7 +334,7 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
     FAISS_THROW_IF_NOT(ivfpq_mfma_eligible(d, M, k, nprobe));
     FAISS_THROW_IF_NOT(b.item_desc && b.item_entries);
     FAISS_THROW_IF_NOT(obits >= 4 && obits <= 14);
-    const int KE = ivf_mfma_kq(k, d);
+    const int KE = ivf_mfma_kq(k, d, nprobe);
     FAISS_THROW_IF_NOT(KE > 0);
     *kt_out = KE / 4;
     const int dsub = d / M, NS = d / 16;
