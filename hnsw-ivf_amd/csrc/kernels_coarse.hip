@@ -556,8 +556,12 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
         const float* __restrict__ cent, int ldc, const float* __restrict__ cnorm,
         const float* __restrict__ cnmax_p, float coef, int y3, int64_t n, int d, int nlist,
         int nsplit, int split_len, int KT, int obits, int k, float* __restrict__ D,
-        OutIdx* __restrict__ I, uint32_t* __restrict__ stats) {
+        OutIdx* __restrict__ I, uint32_t* __restrict__ stats,
+        unsigned long long* __restrict__ trace) {
+    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ uint32_t surv[CR_CAP];
+    __shared__ float ck1[256];      // compaction scratch of the small-batch select
+    __shared__ long long ck2[256];
     __shared__ __attribute__((aligned(16))) float xsh[BDM];
     const int lane = threadIdx.x;
     const int64_t q0 = blockIdx.x;
@@ -583,6 +587,7 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
     for (int i = 0; i < V; i++)
         ub[i] = kv[i] != 0xffffffffu ? key_decode_hi<L2>(kv[i], lowmask) + M : WS_INF;
     float U = wave_kth_smallest<V>(ub, k);
+    const unsigned long long t_u = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (!(U <= WS_INF)) U = WS_INF;
     const unsigned long long fmask = __ballot(my_pb < WS_INF && my_pb <= U);
     const int lst = has ? lane * V / KT : 0;  // this lane's stream (V <= KT)
@@ -621,6 +626,7 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
         }
     }
     __syncthreads();  // one wave per block: the LDS query and candidate list
+    const unsigned long long t_c = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     CoarseStream<L2> st;
     st.surv = surv;
     st.keys = kq;
@@ -643,6 +649,7 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
     st.overflow = ns > CR_CAP;
     st.fmask = fmask;
     bool done = false;
+    unsigned long long t_e = 0ull;
     auto small = [&](auto nbc) {
         constexpr int NB = decltype(nbc)::value;
         float k1[NB];
@@ -656,6 +663,33 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
                 k2[b] = WS_NOID;
             }
         }
+        if (trace) t_e = __builtin_amdgcn_s_memrealtime();
+        if constexpr (NB > 1) {
+            // only keys <= U can be in the top k (at least k candidates have
+            // exact keys <= their ub <= U): a failing split adds a whole
+            // split of candidates, most far above U; the order-preserving
+            // compaction of the others ranks in one batch (as k_ivf_rerank)
+            int m = 0;
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                const bool in = 64 * b + lane < ns && k1[b] < WS_INF && k1[b] <= U;
+                const unsigned long long bm = __ballot(in);
+                const int pos = m + __popcll(bm & ((1ull << lane) - 1ull));
+                if (in) {
+                    ck1[pos] = k1[b];
+                    ck2[pos] = k2[b];
+                }
+                m += __popcll(bm);
+            }
+            if (m <= 64) {
+                __syncthreads();  // one wave per block
+                float c1[1] = {lane < m ? ck1[lane] : WS_INF};
+                long long c2[1] = {lane < m ? ck2[lane] : WS_NOID};
+                __syncthreads();
+                return exact_topk_small<1, OutIdx>(c1, c2, m, k, L2 ? 1 : 0, lane, valid,
+                                                   D + q * k, I + q * k);
+            }
+        }
         return exact_topk_small<NB, OutIdx>(k1, k2, ns, k, L2 ? 1 : 0, lane, valid, D + q * k,
                                             I + q * k);
     };
@@ -663,6 +697,14 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
     else if (ns <= 128) done = small(std::integral_constant<int, 2>());
     else if (ns <= 256) done = small(std::integral_constant<int, 4>());
     if (!done) exact_topk_resolve(st, k, L2 ? 1 : 0, lane, valid, D + q * k, I + q * k);
+    if (trace && valid && lane == 0) {  // FAISS_AMD_CRERANK_TRACE (scripts/rtrace_summary.py)
+        trace[8 * q + 0] = t_start;
+        trace[8 * q + 1] = __builtin_amdgcn_s_memrealtime();
+        trace[8 * q + 2] = (unsigned long long)ns | ((unsigned long long)__popcll(fmask) << 32);
+        trace[8 * q + 3] = t_u;
+        trace[8 * q + 4] = t_c;
+        trace[8 * q + 5] = t_e;
+    }
     if (stats && valid && lane == 0) {
         atomicAdd(&stats[0], (uint32_t)min(ns, CR_CAP));
         atomicAdd(&stats[1], (uint32_t)__popcll(fmask));
@@ -844,7 +886,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     k_coarse_rerank<L2V, OT, VV><<<dim3((unsigned)n), dim3(64), 0, s>>>(                       \
             keys, pbs, x, ldx, xnorm, cent, ldc, cnorm, cnmax, coef, y3 ? 1 : 0, n, d, nlist,  \
             p.nsplit,                                                                           \
-            p.split_len, p.kt, p.obits, k, D, OUT, st_ptr)
+            p.split_len, p.kt, p.obits, k, D, OUT, st_ptr, crtrace)
 #define LAUNCH_RV(L2V, OT, OUT)                  \
     do {                                         \
         if (V == 1) LAUNCH_R(L2V, OT, OUT, 1);   \
@@ -854,6 +896,20 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
         else LAUNCH_R(L2V, OT, OUT, 16);         \
     } while (0)
     uint32_t* const st_ptr = dbg ? stats : nullptr;
+    // FAISS_AMD_CRERANK_TRACE=<file>: per-query wave stamps (profiling only)
+    static unsigned long long* crtrace_buf = nullptr;
+    static int64_t crtrace_n = 0;
+    const char* crt = getenv("FAISS_AMD_CRERANK_TRACE");
+    unsigned long long* crtrace = nullptr;
+    if (crt) {
+        if (crtrace_n < n) {
+            if (crtrace_buf) HIP_CHECK(hipFree(crtrace_buf));
+            HIP_CHECK(hipMalloc(&crtrace_buf, 64 * n));
+            crtrace_n = n;
+        }
+        HIP_CHECK(hipMemsetAsync(crtrace_buf, 0, 64 * n, s));
+        crtrace = crtrace_buf;
+    }
     if (metric_l2) {
         if (I32) LAUNCH_RV(true, int32_t, I32);
         else LAUNCH_RV(true, int64_t, I64);
@@ -863,6 +919,15 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     }
 #undef LAUNCH_RV
 #undef LAUNCH_R
+    if (crtrace) {
+        std::vector<unsigned long long> h(8 * n);
+        HIP_CHECK(hipMemcpyAsync(h.data(), crtrace, 64 * n, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        if (FILE* f = fopen(crt, "wb")) {
+            fwrite(h.data(), 64, n, f);
+            fclose(f);
+        }
+    }
     if (dbg) {
         uint32_t h[4];
         HIP_CHECK(hipMemcpyAsync(h, stats, 16, hipMemcpyDeviceToHost, s));
