@@ -10,7 +10,7 @@ for v in $VARIANTS; do
   name=${v%%:*}; rest=${v#*:}; lib=${rest%%:*}; envs=${rest#*:}
   envargs=$(echo "$envs" | tr ',' ' ')
   rm -rf gpurun_out/ab_$name
-  env $envargs ${lib:+FAISS_AMD_LIB=$PWD/$lib} timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ab_$name -o run --output-format csv -- python bench.py --config ${CFG:-c2} --steps ${STEPS:-20} --warmup 2 --no-cpu-baseline --recall-queries 0 > gpurun_out/ab_$name.json 2> gpurun_out/ab_$name.err
+  env $envargs ${lib:+FAISS_AMD_LIB=$PWD/$lib} timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ab_$name -o run --output-format csv -- python bench.py --config ${CFG:-c2} --steps ${STEPS:-20} --warmup 2 --no-cpu-baseline --recall-queries 0 ${AB_ARGS:-} > gpurun_out/ab_$name.json 2> gpurun_out/ab_$name.err
   rc=$?; echo "== $name rc=$rc $(python -c "import json;d=json.load(open('gpurun_out/ab_$name.json'));print(d['value'],d['ms_per_step'])" 2>/dev/null)"
   [ "$rc" -eq 0 ] || exit $rc
   python scripts/step_kernels.py gpurun_out/ab_$name 2>&1 | tail -12
