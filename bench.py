@@ -8,18 +8,29 @@ synthetic vectors (float_rand seed 1234), k=10, inputs resident in HBM.
 
 N=1: the whole path (query prep + bf16x3-MFMA coarse filter + exact re-rank +
 list-centric bf16x2-MFMA scan + exact re-rank) through
-faiss_amd_Index_search_device.  N>1 (torch.distributed.run, one rank per GPU):
-c1-c4 are one-GPU configs, so every rank serves its own 10k queries from a
-replica of the whole index (weak scaling, no collective on the data path;
---shard instead shards the index by id modulo N and runs the IndexShardsIVF
-exchange of hnsw-ivf_amd/dist.py over RCCL); c5 is the sharded config: the
-100M set is split by id modulo N and the 100k queries are exchanged.
+faiss_amd_Index_search_device.
+
+N>1 (torch.distributed.run, one rank per GPU, torch.distributed over RCCL):
+  c1-c4 name one GPU, so `value` is N replicas of the whole index, each rank
+  serving its own 10k queries (weak scaling, no data-path collective).  Beside
+  it the line carries `rccl_shards`: the same index sharded by id modulo N
+  (faiss GPU shard_type 1) with the IndexShardsIVF exchange of
+  hnsw-ivf_amd/dist.py (all_gather of queries + coarse results, all_to_all of
+  per-shard top-k, device merge), every rank again bringing 10k queries.
+  `--shard` makes the sharded form the `value`.
+  c5 is the sharded config: the 100M set is split by id modulo N and the
+  100k queries of the batch are split over the ranks (nq / N each, strong
+  scaling: the total work is fixed); `--weak` instead has every rank bring
+  100k queries (global batch N x 100k, labelled weak).
+
+The line names the step's dominant kernel (largest per-step time, HIP events
+on the launch stream) and prices it against its roofline; every kernel stage
+above 10 % of the step is listed with its own time and fraction.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -44,9 +55,10 @@ CONFIGS = {
                nb=10_000_000, nq=10_000, nlist=16384, nprobe=64, k=10, ntrain=638_976,
                efSearch=64),
     # BASELINE.json configs[4]: IndexShardsIVF, 100M vectors d=96 split over
-    # the N ranks (ids == rank mod N, faiss GPU shard_type 1): every rank
-    # holds 100M / N vectors and serves all 100k queries (strong scaling);
-    # --shard-of 8 with --gpus 1 builds one rank's share of an 8-GPU run.
+    # the N ranks (ids == rank mod N, faiss GPU shard_type 1); the 100k
+    # queries of a step are split over the ranks (strong scaling).  --shard-of
+    # 8 with --gpus 1 builds one rank's share of an 8-GPU run (12.5M vectors)
+    # and serves the whole 100k batch on it.
     "c5": dict(workload="IVF65536,PQ48 over 100M", desc="IVF65536,PQ48", d=96,
                nb=100_000_000, sharded=True, nq=100_000, nlist=65536, nprobe=64, k=10,
                ntrain=65536 * 39),
@@ -54,18 +66,21 @@ CONFIGS = {
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector == fp32 MFMA peak
 PEAK_HBM_GBS = 8000.0
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
-# dominant kernel per workload (device symbol substring) for the PMC traffic
-DOMINANT = {"flat": "k_ivf_bf2_stream", "pq": "k_ivfpq_scan", "pqm": "k_ivfpq_filter"}
+# kernel stage (library timer name) -> device symbol substring of its kernel
+# in the committed rocprofv3 PMC summaries
+PMC_SYMBOL = {"ivf_flat_scan": "k_ivf_bf2_stream", "ivfpq_filter": "k_ivfpq_filter",
+              "coarse_filter": "k_coarse_stream", "hnsw_search": "k_hnsw_search",
+              "ivf_rerank": "k_ivf_rerank", "coarse_rerank": "k_coarse_rerank"}
 
 
 def pmc_traffic(config, kernel_sub):
-    """HBM bytes per launch of the dominant kernel from the newest committed
-    rocprofv3 --pmc summary for this workload (profiles/rNN_<config>_pmc.json,
-    written by scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950
-    correction + WRITE_SIZE, separate passes)."""
+    """HBM bytes per launch of a kernel from the newest committed rocprofv3
+    --pmc summary for this workload (profiles/rNN_<config>_pmc.json, written
+    by scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950 correction +
+    WRITE_SIZE, separate passes)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")))
-    if not files:
+    if not files or not kernel_sub:
         return None, None
     with open(files[-1]) as f:
         summ = json.load(f)
@@ -157,6 +172,59 @@ def cpu_baseline(args, cfg, amd, index, xq, I_gpu, k, nprobe):
             "one_thread": {"value": n1 / t1, "unit": "queries/s", "queries": n1}}
 
 
+def kernel_breakdown(index, steps):
+    """{stage: ms per step} from the library's HIP-event timers."""
+    out = {}
+    for nm, ms, _ in index.kernel_times():
+        out[nm] = out.get(nm, 0.0) + ms
+    return {nm: ms / max(steps, 1) for nm, ms in out.items()}
+
+
+def kernel_roofline(name, ms, work, config):
+    """Roofline of one kernel stage from its per-step time and algorithmic
+    work (work: dict of the step's quantities, see main)."""
+    t = ms * 1e-3
+    r = None
+    if name == "ivf_flat_scan":
+        # one pass over the rows of every distinct probed list: bf16 hi of
+        # the dims (padded to 32) + |y|^2 + residual bound = 2 dpad + 8 bytes
+        b = work["flat_rows"] * work["flat_row_bytes"]
+        r = {"bound": "hbm", "achieved": b / t / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+             "algorithmic_bytes_per_step": b, "bytes_per_row": work["flat_row_bytes"],
+             "mfma_dtype": "bf16", "mfma_flops_per_step": work["flat_flops"],
+             "mfma_tflops": work["flat_flops"] / t / 1e12,
+             "mfma_frac": work["flat_flops"] / t / 1e12 / PEAK_BF16_TFLOPS}
+    elif name == "ivfpq_filter":
+        # codes decoded to bf16 and multiplied against the queries' hi + lo
+        # split: 2 products of 2 dpad flops per candidate
+        f = work["cands"] * 4.0 * work["dpad16"]
+        r = {"bound": "mfma", "achieved": f / t / 1e12, "peak": PEAK_BF16_TFLOPS,
+             "unit": "TFLOP/s", "mfma_dtype": "bf16", "algorithmic_flops_per_step": f,
+             "flops_per_candidate": 4 * work["dpad16"],
+             "streamed_code_bytes_per_step": work["cands"] * work.get("M", 0),
+             "streamed_code_gbs": work["cands"] * work.get("M", 0) / t / 1e9}
+    elif name == "coarse_filter":
+        # bf16x3 x.c of every (query, centroid): 3 products of 2 dpad flops
+        f = work["nq_coarse"] * work["nlist"] * 6.0 * work["dpad16"]
+        r = {"bound": "mfma", "achieved": f / t / 1e12, "peak": PEAK_BF16_TFLOPS,
+             "unit": "TFLOP/s", "mfma_dtype": "bf16", "algorithmic_flops_per_step": f,
+             "flops_per_query_centroid": 6 * work["dpad16"]}
+    elif name == "hnsw_search" and work.get("hnsw_ndis"):
+        # every distance reads one fp32 vector of the graph's storage
+        b = work["hnsw_ndis"] * 4.0 * work["d"]
+        r = {"bound": "hbm", "achieved": b / t / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+             "algorithmic_bytes_per_step": b, "hnsw_ndis_per_step": work["hnsw_ndis"]}
+    if r is None:
+        return None
+    r["frac"] = r["achieved"] / r["peak"]
+    traffic, src = pmc_traffic(config, PMC_SYMBOL.get(name))
+    r["traffic"] = traffic
+    if traffic is not None:
+        r["traffic_source"] = src
+        r["traffic_unit"] = "bytes/launch"
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -169,8 +237,12 @@ def main():
     ap.add_argument("--shard-of", type=int, default=0,
                     help="c5: build one rank's share of a run over this many GPUs")
     ap.add_argument("--shard", action="store_true",
-                    help="c1-c4 at N > 1: shard the index by id %% N over RCCL "
-                         "(IndexShardsIVF exchange) instead of one replica per GPU")
+                    help="c1-c4 at N > 1: the IndexShardsIVF exchange over RCCL is the "
+                         "value (instead of one replica per GPU)")
+    ap.add_argument("--no-shard-figure", action="store_true",
+                    help="c1-c4 at N > 1: skip the rccl_shards figure beside the replicas")
+    ap.add_argument("--weak", action="store_true",
+                    help="c5: every rank brings nq queries (global batch N x nq)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -178,34 +250,47 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}"
-    # c1-c4 at N > 1 are replicas: their only collectives are the timing
-    # barrier and max (gloo, host side); sharded runs exchange device tensors
-    # over RCCL.  (local_rank % devices: a rehearsal of N ranks on fewer GPUs)
-    replicas = world > 1 and not cfg.get("sharded", False) and not args.shard
+    sharded = cfg.get("sharded", False)
+    replicas = world > 1 and not sharded and not args.shard
+    # (local_rank % devices: a rehearsal of N ranks on fewer GPUs)
     gpu = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        if replicas:
-            dist.init_process_group("gloo")
+        # RCCL; FAISS_AMD_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs
+        # (RCCL refuses two ranks on one device)
+        be = os.environ.get("FAISS_AMD_BENCH_BACKEND", "nccl")
+        if be == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            dist.init_process_group(be)
     amd = ge.load_package()
     amd.set_device(gpu)
-    dev = torch.device("cuda", gpu)
     stream = torch.cuda.current_stream().cuda_stream
 
     d, nb, nq, k, nprobe = cfg["d"], cfg["nb"], cfg["nq"], cfg["k"], cfg["nprobe"]
-    qseed = 5678 + 7919 * rank
-    xq = amd.float_rand(nq * d, qseed).reshape(nq, d)
-    nr = min(args.recall_queries, nq) if rank == 0 else 0
-    gt_run = None  # sharded: exact top-k of the shard, merged chunk by chunk
+    # ---- queries: c5 (strong) splits the batch of nq over the ranks; the
+    # other forms give every rank its own nq queries
+    strong = sharded and not args.weak
+    if strong:
+        assert nq % world == 0, f"nq={nq} does not split over {world} ranks"
+        nq_loc = nq // world
+        xq_glob = amd.float_rand(nq * d, 5678).reshape(nq, d)
+        xq = np.ascontiguousarray(xq_glob[rank * nq_loc:(rank + 1) * nq_loc])
+        nq_glob = nq
+    else:
+        nq_loc = nq
+        xq = amd.float_rand(nq * d, 5678 + 7919 * rank).reshape(nq, d)
+        nq_glob = nq * world
+    # recall queries: the first of rank 0's (every rank of a sharded run
+    # computes its shard's exact top-k for them; rank 0 merges)
+    nr = min(args.recall_queries, nq_loc)
+    xr = amd.float_rand(nr * d, 5678).reshape(nr, d) if nr else None
+    gt_run = None
     t0 = time.time()
     index = amd.index_factory(d, cfg["desc"])
-    sharded = cfg.get("sharded", False)
     nshard = max(world, args.shard_of) if sharded else world
-    # c1-c4 name one GPU; at N > 1 each GPU serves its own queries from a
-    # replica of the whole index (independent units, no collective) unless
-    # --shard asks for the IndexShardsIVF exchange.  c5 is the sharded config.
+    xb = None
     if sharded:
         # rows of the float_rand(nb * d, 1234) set, generated shard-wise and
         # added in chunks (no host image of the whole shard)
@@ -225,7 +310,7 @@ def main():
             if nr:
                 gt = amd.IndexFlatL2(d)
                 gt.add(xc)
-                Dg, Ig = gt.search(xq[:nr], k)
+                Dg, Ig = gt.search(xr, k)
                 Ig = np.where(Ig >= 0, cid[np.maximum(Ig, 0)], -1)
                 if gt_run is not None:
                     Dg, Ig = amd.merge_knn_results(np.stack([gt_run[0], Dg]),
@@ -248,144 +333,153 @@ def main():
         f"{time.time() - t0:.1f}s")
 
     x_t = torch.from_numpy(xq).to(dev)
-    D_t = torch.empty((nq, k), dtype=torch.float32, device=dev)
-    I_t = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    D_t = torch.empty((nq_loc, k), dtype=torch.float32, device=dev)
+    I_t = torch.empty((nq_loc, k), dtype=torch.int64, device=dev)
+    hdist = ge.load_package_module("dist")
 
-    if world == 1 or replicas:
-        def step():
-            index.search_device(nq, x_t.data_ptr(), k, D_t.data_ptr(), I_t.data_ptr(), stream)
-    else:
-        hdist = __import__("hnsw_ivf_amd.dist", fromlist=["sharded_search"])
-        cd_t = torch.empty((nq, nprobe), dtype=torch.float32, device=dev)
-        ci_t = torch.empty((nq, nprobe), dtype=torch.int32, device=dev)
-        Ds_t = torch.empty((world * nq, k), dtype=torch.float32, device=dev)
-        Is_t = torch.empty((world * nq, k), dtype=torch.int64, device=dev)
+    def sharded_step_fn(ix):
+        """IndexShardsIVF exchange (dist.py) with `ix` as this rank's shard."""
+        cd_t = torch.empty((nq_loc, nprobe), dtype=torch.float32, device=dev)
+        ci_t = torch.empty((nq_loc, nprobe), dtype=torch.int32, device=dev)
+        Ds_t = torch.empty((world * nq_loc, k), dtype=torch.float32, device=dev)
+        Is_t = torch.empty((world * nq_loc, k), dtype=torch.int64, device=dev)
 
         def quantize(x):
-            index.quantize_device(nq, x.data_ptr(), nprobe, cd_t.data_ptr(), ci_t.data_ptr(),
-                                  stream)
+            ix.quantize_device(nq_loc, x.data_ptr(), nprobe, cd_t.data_ptr(), ci_t.data_ptr(),
+                               stream)
             return cd_t, ci_t
 
         def search_pre(xa, ca, cda):
-            index.search_preassigned_device(world * nq, xa.data_ptr(), k, nprobe, ca.data_ptr(),
-                                            cda.data_ptr(), Ds_t.data_ptr(), Is_t.data_ptr(),
-                                            stream)
+            ix.search_preassigned_device(world * nq_loc, xa.data_ptr(), k, nprobe,
+                                         ca.data_ptr(), cda.data_ptr(), Ds_t.data_ptr(),
+                                         Is_t.data_ptr(), stream)
             return Ds_t, Is_t
 
         def merge(Dr, Ir):
-            amd.merge_knn_results_device(nq, k, world, Dr.data_ptr(), Ir.data_ptr(),
+            amd.merge_knn_results_device(nq_loc, k, world, Dr.data_ptr(), Ir.data_ptr(),
                                          D_t.data_ptr(), I_t.data_ptr(), amd.METRIC_L2, stream)
             return D_t, I_t
 
+        return lambda: hdist.sharded_search(x_t, k, quantize, search_pre, merge)
+
+    if world == 1 or replicas:
         def step():
-            hdist.sharded_search(x_t, k, quantize, search_pre, merge)
+            index.search_device(nq_loc, x_t.data_ptr(), k, D_t.data_ptr(), I_t.data_ptr(),
+                                stream)
+    else:
+        step = sharded_step_fn(index)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    amd.set_kernel_timing(True)
-    index.reset_kernel_times()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t1
-    amd.set_kernel_timing(False)
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if replicas else dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    def run_timed(step_fn, ix, steps, warmup):
+        """warmup steps (the first untimed; the rest with every kernel stage
+        timed: the per-step breakdown), then exactly `steps` steps between a
+        barrier + synchronize on both sides, with only the dominant stage
+        timed.  Returns (max elapsed over ranks, breakdown, dominant stage,
+        its ms per step in the timed region)."""
+        step_fn()
+        torch.cuda.synchronize()
+        nb_steps = max(1, warmup - 1)
+        amd.set_kernel_timing(True)
+        ix.reset_kernel_times()
+        for _ in range(nb_steps):
+            step_fn()
+        torch.cuda.synchronize()
+        brk = kernel_breakdown(ix, nb_steps)
+        dom = max(brk, key=brk.get) if brk else None
+        amd.set_kernel_timing(True, only=dom)
+        ix.reset_kernel_times()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            step_fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t1
+        amd.set_kernel_timing(False)
+        dom_ms = kernel_breakdown(ix, steps).get(dom, float("nan")) if dom else float("nan")
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el, brk, dom, dom_ms
+
+    elapsed, brk, dom, dom_ms = run_timed(step, index, args.steps, args.warmup)
     ms_per_step = elapsed / args.steps * 1e3
-    qps = world * nq * args.steps / elapsed
+    qps = nq_glob * args.steps / elapsed
 
-    # ---- dominant kernel: HIP events over the timed region (lib-side)
-    kt = index.kernel_times()
-    scan_name = "ivfpq_scan" if "PQ" in cfg["desc"] else "ivf_flat_scan"
-    pq_mfma = any(nm == "ivfpq_filter" for (nm, _, _) in kt)
-    if pq_mfma:
-        scan_name = "ivfpq_filter"  # list-centric bf16 MFMA filter over decoded codes
-    scan = [ms for (nm, ms, _) in kt if nm == scan_name]
-    # a step may launch the kernel more than once (query chunks): the per-step
-    # kernel time is the sum over the step's launches, priced against the
-    # step's whole algorithmic work
-    launches_per_step = len(scan) / args.steps if scan else 0.0
-    scan_ms = float(np.sum(scan)) / args.steps if scan else float("nan")
-    # algorithmic work of one scan launch: sum over (query, probe) of the
-    # probed list length x per-candidate cost (Flat: 3*d flops; PQ: M bytes)
-    nq_launch = nq if replicas else nq * world
-    cd_h = torch.empty((nq, nprobe), dtype=torch.float32, device=dev)
-    ci_h = torch.empty((nq, nprobe), dtype=torch.int32, device=dev)
-    index.quantize_device(nq, x_t.data_ptr(), nprobe, cd_h.data_ptr(), ci_h.data_ptr(), stream)
+    # ---- the step's algorithmic work (this rank), for the roofline models
+    cd_h = torch.empty((nq_loc, nprobe), dtype=torch.float32, device=dev)
+    ci_h = torch.empty((nq_loc, nprobe), dtype=torch.int32, device=dev)
+    index.quantize_device(nq_loc, x_t.data_ptr(), nprobe, cd_h.data_ptr(), ci_h.data_ptr(),
+                          stream)
     torch.cuda.synchronize()
     sizes = np.array([index.get_list_size(l) for l in range(index.nlist)], dtype=np.int64)
-    cand_per_q = float(sizes[ci_h.cpu().numpy().astype(np.int64)].sum()) / nq
-    cands = cand_per_q * nq_launch
-    is_pq = "PQ" in cfg["desc"]
-    traffic, traffic_src = pmc_traffic(
-        args.config, DOMINANT["pqm" if pq_mfma else "pq" if is_pq else "flat"])
-    if is_pq and not pq_mfma:
-        M = index.pq_info()["M"]
-        work = cands * M  # code bytes streamed (LUT-gather bound)
-        achieved = work / (scan_ms * 1e-3) / 1e9
-        roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                    "kernel": scan_name, "kernel_ms_per_step": scan_ms,
-                    "launches_per_step": launches_per_step,
-                    "algorithmic_bytes_per_step": work}
-    elif is_pq:
-        # IVF-PQ on the list-centric filter: codes are decoded to bf16 and
-        # multiplied against the queries' bf16 hi + lo split (2 MFMA passes),
-        # 2 * 2d bf16 flops per candidate, priced against the dense bf16 peak;
-        # the streamed-code model (M bytes per candidate) is reported beside it
-        M = index.pq_info()["M"]
-        dpad = -(-d // 16) * 16
-        work = cands * 2 * 2.0 * dpad
-        achieved = work / (scan_ms * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
-                    "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
-                    "kernel": scan_name, "kernel_ms_per_step": scan_ms,
-                    "launches_per_step": launches_per_step, "mfma_dtype": "bf16",
-                    "algorithmic_flops_per_step": work, "flops_per_candidate": 4 * dpad,
-                    "streamed_code_bytes_per_step": cands * M,
-                    "streamed_code_gbs": cands * M / (scan_ms * 1e-3) / 1e9}
-    else:
-        # The list-centric filter streams, once per probed list, the bf16 hi
-        # image of the rows (2 B/dim, dims padded to 32) plus two fp32 norms
-        # per row (|y|^2 and the bf16 residual bound): its algorithmic bytes.
-        # Its bf16 MFMA work (codes hi x queries hi+lo = 2 products of 2*dpad
-        # flops per candidate) would take less time at the dense bf16 peak
-        # than these bytes at the HBM peak, so HBM is the binding roofline;
-        # the MFMA fraction is reported beside it.
-        nprod = 3 if os.environ.get("FAISS_AMD_IVF_PREC") == "bf16x3" else 2
-        dpad = -(-d // 32) * 32
-        lists = np.unique(ci_h.cpu().numpy().astype(np.int64))
-        lists = lists[lists >= 0]
-        work = float(sizes[lists].sum()) * (2.0 * dpad + 8.0) * (1 if replicas else world)
-        achieved = work / (scan_ms * 1e-3) / 1e9
-        flops = cands * nprod * 2.0 * dpad
-        mfma_tf = flops / (scan_ms * 1e-3) / 1e12
-        roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                    "kernel": scan_name, "kernel_ms_per_step": scan_ms,
-                    "launches_per_step": launches_per_step,
-                    "algorithmic_bytes_per_step": work,
-                    "bytes_per_row": 2 * dpad + 8,
-                    "mfma_dtype": "bf16", "mfma_flops_per_step": flops,
-                    "mfma_tflops": mfma_tf, "mfma_frac": mfma_tf / PEAK_BF16_TFLOPS,
-                    "fp32_equivalent_tflops": cands * 3.0 * d / (scan_ms * 1e-3) / 1e12}
-    if traffic is not None:
-        # HBM bytes per launch from rocprofv3 PMC (committed summary), scaled
-        # to the step's launches like `achieved`, and the bandwidth they imply
-        # at the live kernel time
-        roofline["traffic"] = traffic * launches_per_step
-        roofline["traffic_source"] = traffic_src
-        roofline["traffic_unit"] = "bytes/step"
-        roofline["traffic_gbs"] = traffic * launches_per_step / (scan_ms * 1e-3) / 1e9
+    ci_np = ci_h.cpu().numpy().astype(np.int64)
+    cand_per_q = float(sizes[ci_np].sum()) / nq_loc
+    scan_q = nq_loc if (world == 1 or replicas) else nq_glob  # queries this rank's scan sees
+    dpad16 = -(-d // 16) * 16
+    dpad32 = -(-d // 32) * 32
+    lists = np.unique(ci_np)
+    lists = lists[lists >= 0]
+    work = {"cands": cand_per_q * scan_q, "dpad16": dpad16, "d": d, "nlist": cfg["nlist"],
+            "nq_coarse": nq_loc,
+            # distinct lists of this rank's own batch (the scan of a sharded
+            # step sees every rank's: at least these)
+            "flat_rows": float(sizes[lists].sum()), "flat_row_bytes": 2 * dpad32 + 8,
+            "flat_flops": cand_per_q * scan_q * 2 * 2.0 * dpad32}
+    if "PQ" in cfg["desc"]:
+        work["M"] = index.pq_info()["M"]
+    if "efSearch" in cfg:
+        hs = amd.cvar.hnsw_stats
+        index.fold_device_stats()
+        hs.reset()
+        step()
+        torch.cuda.synchronize()
+        index.fold_device_stats()
+        work["hnsw_ndis"] = float(amd.cvar.hnsw_stats.ndis)
+    kernels = []
+    for nm, ms in sorted(brk.items(), key=lambda kv: -kv[1]):
+        if ms < 0.1 * ms_per_step and nm != dom:
+            continue
+        ent = {"name": nm, "ms_per_step": ms, "frac_of_step": ms / ms_per_step}
+        rf = kernel_roofline(nm, ms, work, args.config)
+        if rf is not None:
+            ent["roofline_frac"] = rf["frac"]
+            ent["bound"] = rf["bound"]
+        kernels.append(ent)
+    roofline = kernel_roofline(dom, dom_ms, work, args.config) if dom else None
+    if roofline is None and dom:
+        roofline = {"bound": "latency", "achieved": None, "peak": None, "unit": None,
+                    "frac": None, "traffic": None}
+    if roofline is not None:
+        roofline["kernel"] = dom
+        roofline["kernel_ms_per_step"] = dom_ms
+        roofline["kernel_frac_of_step"] = dom_ms / ms_per_step
+        roofline["timing"] = ("HIP events around the stage's launches on its stream, "
+                              "every timed step (only this stage timed)")
+
+    # ---- c1-c4 at N > 1: the RCCL shard exchange beside the replicas
+    shard_fig = None
+    if replicas and not args.no_shard_figure and nb <= 2_000_000:
+        shards = amd.index_ivf_to_shards(index, world, 1, devices=[gpu] * world)
+        local = shards.shard(rank)
+        local.nprobe = nprobe
+        local.sync_device()
+        sstep = sharded_step_fn(local)
+        el2, brk2, dom2, dom2_ms = run_timed(sstep, local, args.steps, args.warmup)
+        xbytes = nq_loc * (4 * d + 8 * nprobe)  # queries + coarse (f32 dis, i32 list)
+        shard_fig = {
+            "value": nq_glob * args.steps / el2, "unit": "queries/s",
+            "ms_per_step": el2 / args.steps * 1e3, "global_batch": nq_glob,
+            "scaling": "weak", "partition": "id % N (faiss GPU shard_type 1)",
+            "vectors_per_gpu": int(local.ntotal),
+            "collectives": "all_gather(queries, coarse dis, coarse ids) + "
+                           "all_to_all(per-shard top-k) over RCCL",
+            "bytes_out_per_rank": world * xbytes, "bytes_back_per_rank": world * nq_loc * k * 12,
+            "dominant_kernel": dom2, "dominant_ms_per_step": dom2_ms}
+        del local, shards
 
     # ---- PCIe-inclusive rate (host buffers through faiss_Index_search: query
     # upload + result download); reported beside `value`, never as it
@@ -397,22 +491,38 @@ def main():
         for _ in range(nh):
             index.search(xq, k)
         th = time.perf_counter() - th
-        pcie = {"value": nq * nh / th, "unit": "queries/s", "ms_per_step": th / nh * 1e3,
+        pcie = {"value": nq_loc * nh / th, "unit": "queries/s", "ms_per_step": th / nh * 1e3,
                 "what": "faiss_Index_search on host buffers (H2D queries + search + D2H results)"}
 
-    # ---- recall@10 of this rank's queries vs exact search (subset; for
-    # sharded configs against the rank's own shard)
+    # ---- recall@10 of rank 0's first queries vs exact search
     recall = None
     if nr:
-        I_t2 = I_t.cpu().numpy()
+        step()
+        torch.cuda.synchronize()
+        I_res = I_t.cpu().numpy()[:nr]
         if sharded:
-            Igt = gt_run[1]
+            # every rank's shard ground truth, merged on rank 0
+            Dg = torch.from_numpy(np.ascontiguousarray(gt_run[0])).to(dev)
+            Ig = torch.from_numpy(np.ascontiguousarray(gt_run[1])).to(dev)
+            if world > 1:
+                Dl = [torch.empty_like(Dg) for _ in range(world)]
+                Il = [torch.empty_like(Ig) for _ in range(world)]
+                dist.all_gather(Dl, Dg)
+                dist.all_gather(Il, Ig)
+                _, Igt = amd.merge_knn_results(np.stack([t.cpu().numpy() for t in Dl]),
+                                               np.stack([t.cpu().numpy() for t in Il]))
+            else:
+                Igt = gt_run[1]
+            gt_note = ("exact top-k over all ranks' shards" if world > 1 or not args.shard_of
+                       else f"exact top-k over this rank's 1/{nshard} shard")
         else:
             gt = amd.IndexFlatL2(d)
             gt.add(xb)
-            _, Igt = gt.search(xq[:nr], k)
+            _, Igt = gt.search(xr, k)
             del gt
-        recall = float(np.mean([len(set(a) & set(b)) / k for a, b in zip(I_t2[:nr], Igt)]))
+            gt_note = "exact top-k over the whole set"
+        if rank == 0:
+            recall = float(np.mean([len(set(a) & set(b)) / k for a, b in zip(I_res, Igt)]))
 
     # ---- CPU baseline, rank 0, N=1: the reference's own IndexIVF::search
     # (oracle/_ref/libfaissfull.so, compiled from /root/reference here and
@@ -424,24 +534,31 @@ def main():
         cpu = cpu_baseline(args, cfg, amd, index, xq, I_t.cpu().numpy(), k, nprobe)
 
     if rank == 0:
+        par = (f"replicas{world}" if replicas else
+               f"shards{world}" if world > 1 else "single")
         out = {
             "metric": "queries/sec @ recall@10, IVF4096 d=128 nq=10k nprobe=32; 1/2/4/8 GPUs"
             if args.config == "c2" else f"queries/sec, {cfg['workload']}",
             "value": qps, "unit": "queries/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            # "weak": every GPU brings its own nq queries (replicas / --shard);
-            # "strong": c5's 100M set and 100k queries split over the GPUs
-            "config": {"workload": cfg["workload"], "d": d, "nb": nb, "vectors_per_gpu": len(ids),
-                       "nq_per_gpu": nq,
-                       "nprobe": nprobe, "k": k, "global_batch": nq * world,
-                       "parallelism": (f"replicas{world}" if replicas else
-                                       f"shards{world}" if world > 1 else "single"),
-                       "recall_at_10": recall, "candidates_per_query": cand_per_q},
+            # "weak": every GPU brings its own nq queries (replicas / --shard /
+            # c5 --weak); "strong": c5's 100M set and 100k-query batch split
+            # over the GPUs
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": cfg["workload"], "d": d, "nb": nb,
+                       "vectors_per_gpu": len(ids), "nq_per_gpu": nq_loc,
+                       "nprobe": nprobe, "k": k, "global_batch": nq_glob,
+                       "parallelism": par, "recall_at_10": recall,
+                       "recall_ground_truth": gt_note if nr else None,
+                       "candidates_per_query": cand_per_q},
             "roofline": roofline,
+            "kernels": kernels,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
         }
+        if shard_fig is not None:
+            out["rccl_shards"] = shard_fig
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -203,6 +203,7 @@ def _declare(L):
         "faiss_amd_IndexIVF_quantize_device": (C.c_int, [_P, _I64, _P, C.c_int, _P, _P, _P]),
         "faiss_amd_merge_knn_results_device": (C.c_int, [C.c_size_t, C.c_size_t, C.c_int, _P, _P, _P, _P, C.c_int, _P]),
         "faiss_amd_set_kernel_timing": (C.c_int, [C.c_int]),
+        "faiss_amd_set_kernel_timing_filter": (C.c_int, [C.c_char_p]),
         "faiss_amd_Index_type": (C.c_char_p, [_P]),
         "faiss_amd_reset_kernel_times": (C.c_int, [_P]),
         "faiss_amd_float_rand": (C.c_int, [_P, C.c_size_t, C.c_int64]),
@@ -863,7 +864,10 @@ def set_device(dev):
     _check(lib().faiss_amd_set_device(int(dev)))
 
 
-def set_kernel_timing(enable=True):
+def set_kernel_timing(enable=True, only=None):
+    """HIP-event timing of the kernel stages of later searches; `only`
+    restricts it to the stage of that name (kernel_times() names)."""
+    _check(lib().faiss_amd_set_kernel_timing_filter(only.encode() if only else None))
     _check(lib().faiss_amd_set_kernel_timing(int(bool(enable))))
 
 

@@ -687,8 +687,8 @@ int faiss_amd_IndexIVF_search_preassigned_device(const FaissIndexIVF* index, idx
     FAISS_THROW_IF_NOT(nprobe > 0 && (size_t)nprobe <= ix->nlist);
     ensure_hip();
     ix->sync_device();
-    ix->search_preassigned_device(n, x_dev, ldx_of(ix), k, nprobe, assign_dev, cdis_dev, d_dev,
-                                  l_dev, pick_stream(ix, stream));
+    ix->search_preassigned_device_ordered(n, x_dev, ldx_of(ix), k, nprobe, assign_dev, cdis_dev,
+                                          d_dev, l_dev, pick_stream(ix, stream));
     C_CATCH
 }
 int faiss_amd_IndexIVF_quantize_device(const FaissIndexIVF* index, idx_t n, const float* x_dev,
@@ -714,6 +714,10 @@ int faiss_amd_merge_knn_results_device(size_t n, size_t k, int nshard, const flo
 }
 int faiss_amd_set_kernel_timing(int enable) {
     C_TRY set_kernel_timing_enabled(enable != 0);
+    C_CATCH
+}
+int faiss_amd_set_kernel_timing_filter(const char* name) {
+    C_TRY set_kernel_timing_filter(name);
     C_CATCH
 }
 int faiss_amd_last_kernel_times(const FaissIndex* index, int* n_kernels, char* names,

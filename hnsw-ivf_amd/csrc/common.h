@@ -133,6 +133,31 @@ DeviceContext& device_context(int device);
 int current_device();  // device selected by faiss_amd_set_device for this thread
 void ensure_hip();     // throws a FaissException when no HIP device is usable
 
+// Device order between calls that share an index's scratch buffers but run
+// on different streams: a device entry point calls enter(s) first (s waits
+// for the event the previous call recorded on its stream) and leave(s) after
+// its last launch.  Same-stream calls are ordered by the stream itself.
+struct StreamOrder {
+    hipStream_t last = nullptr;
+    hipEvent_t ev = nullptr;
+    bool valid = false;
+    StreamOrder() = default;
+    StreamOrder(const StreamOrder&) = delete;
+    StreamOrder& operator=(const StreamOrder&) = delete;
+    void enter(hipStream_t s) {
+        if (valid && last != s) HIP_CHECK(hipStreamWaitEvent(s, ev, 0));
+    }
+    void leave(hipStream_t s) {
+        if (!ev) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(ev, s));
+        last = s;
+        valid = true;
+    }
+    ~StreamOrder() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
+
 // Kernel-time recorder (HIP events) used by bench.py for the roofline line.
 // Events are recorded on the launch stream without synchronising; elapsed
 // times are resolved lazily when queried.
@@ -160,6 +185,9 @@ struct KernelTimes {
 };
 bool kernel_timing_enabled();
 void set_kernel_timing_enabled(bool);
+// only the kernel stage of this name is timed (nullptr / "": all of them)
+void set_kernel_timing_filter(const char* name);
+bool kernel_timing_wants(const char* name);
 
 // Brackets a launch with HIP events when timing is enabled.
 struct ScopedKernelTimer {
@@ -168,7 +196,7 @@ struct ScopedKernelTimer {
     hipEvent_t a = nullptr, b = nullptr;
     ScopedKernelTimer(KernelTimes* s, const char* name, double units, hipStream_t st)
             : sink(s), stream(st) {
-        if (sink && kernel_timing_enabled()) {
+        if (sink && kernel_timing_wants(name)) {
             HIP_CHECK(hipEventCreate(&a));
             HIP_CHECK(hipEventCreate(&b));
             HIP_CHECK(hipEventRecord(a, stream));

@@ -55,6 +55,19 @@ int current_device() { return tl_device; }
 void set_current_device(int d) { tl_device = d; }
 bool kernel_timing_enabled() { return g_timing; }
 void set_kernel_timing_enabled(bool b) { g_timing = b; }
+namespace {
+std::mutex g_timing_mu;
+std::string g_timing_only;  // empty: every timed kernel
+}  // namespace
+void set_kernel_timing_filter(const char* name) {
+    std::lock_guard<std::mutex> g(g_timing_mu);
+    g_timing_only = name ? name : "";
+}
+bool kernel_timing_wants(const char* name) {
+    if (!g_timing) return false;
+    std::lock_guard<std::mutex> g(g_timing_mu);
+    return g_timing_only.empty() || g_timing_only == name;
+}
 
 struct DeviceGuard {
     int prev = 0;
@@ -181,9 +194,8 @@ const float* IndexFlat::device_vectors() const {
     sync_device();
     return d_xb_.as<float>();
 }
-const void* IndexFlat::prepared_query_image(const float* x, idx_t n, int ldx) const {
-    std::lock_guard<std::recursive_mutex> g(mu_);
-    return (x && x == qimg_x_ && n == qimg_n_ && ldx == qimg_ldx_) ? s_qimg_.ptr : nullptr;
+size_t IndexFlat::query_image_size(idx_t n) const {
+    return kern::query_image_bytes(n, d) + sizeof(float) * n;
 }
 const float* IndexFlat::device_norms() const {
     sync_device();
@@ -191,13 +203,24 @@ const float* IndexFlat::device_norms() const {
 }
 
 template <class OutIdx>
-void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* distances,
-                           OutIdx* labels, hipStream_t s) const {
+bool IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* distances,
+                           OutIdx* labels, hipStream_t s, void* qimg_out, idx_t batch_n) const {
     FAISS_THROW_IF_NOT_FMT(k >= 1 && k <= kern::kMaxKExact, "k = %d must be in [1, %d]", k,
                            kern::kMaxKExact);
     sync_device();
     std::lock_guard<std::recursive_mutex> g(mu_);
-    qimg_x_ = nullptr;  // set again below if this call prepares the image
+    order_.enter(s);
+    // faiss/utils/distances.cpp:807-823: batches below
+    // distance_compute_blas_threshold (20) take the direct form
+    const bool direct = (batch_n >= 0 ? batch_n : n) < 20;
+    const bool img = knn_impl<OutIdx>(n, x, ldx, k, distances, labels, s, qimg_out, direct);
+    order_.leave(s);
+    return img;
+}
+
+template <class OutIdx>
+bool IndexFlat::knn_impl(idx_t n, const float* x, int ldx, int k, float* distances,
+                         OutIdx* labels, hipStream_t s, void* qimg_out, bool direct) const {
     const int l = ld();
     const int metric_l2 = metric_type == METRIC_L2;
     if (k > kern::kMaxK) {
@@ -214,7 +237,7 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
         ScopedKernelTimer tm(&ktimes, "flat_distance+select_exact", 2.0 * n * ntotal * d, s);
         for (idx_t q0 = 0; q0 < n; q0 += qc) {
             const idx_t nq = std::min(qc, n - q0);
-            if (ntotal > 0 && n < 20)
+            if (ntotal > 0 && direct)
                 kern::direct_distances(x + q0 * ldx, nq, ldx, d_xb_.as<float>(), ntotal, l, d,
                                        metric_l2, s_tile_.as<float>(), ntotal, s);
             else if (ntotal > 0)
@@ -226,7 +249,7 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
                                             metric_l2, 0, distances + q0 * k, labels + q0 * k, k,
                                             s);
         }
-        return;
+        return false;
     }
     constexpr bool i32 = sizeof(OutIdx) == 4;
     int32_t* o32 = i32 ? (int32_t*)labels : nullptr;
@@ -237,21 +260,21 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
     // f32 tile + select below (FAISS_AMD_COARSE=f32 forces the latter)
     const char* cenv = getenv("FAISS_AMD_COARSE");
     const kern::CoarsePlan plan =
-            (cenv && !strcmp(cenv, "f32")) || ny > (1 << 20) || d_cbf_.ptr == nullptr
+            (cenv && !strcmp(cenv, "f32")) || ny > (1 << 20) || d_cbf_.ptr == nullptr || direct
                     ? kern::CoarsePlan{}
                     : kern::coarse_bf3_plan(n, (int)ny, d, k);
     if (plan.ok) {
         // the streamed filter reads prepared query fragments (one launch with
         // the reference-order norms)
         const bool qi = d_cst_.ptr != nullptr && ldx % 4 == 0;
+        void* qimg = nullptr;
         if (qi) {
             const size_t ib = kern::query_image_bytes(n, d);
-            s_qimg_.reserve(ib + sizeof(float) * n);
-            kern::query_prep(x, n, ldx, d, s_xn_.as<float>(), s_qimg_.ptr,
-                             (float*)((uint8_t*)s_qimg_.ptr + ib), s);
-            qimg_x_ = x;
-            qimg_n_ = n;
-            qimg_ldx_ = ldx;
+            if (!qimg_out) s_qimg_.reserve(ib + sizeof(float) * n);
+            qimg = qimg_out ? qimg_out : s_qimg_.ptr;
+            ScopedKernelTimer tq(&ktimes, "query_prep", 0.0, s);
+            kern::query_prep(x, n, ldx, d, s_xn_.as<float>(), qimg, (float*)((uint8_t*)qimg + ib),
+                             s);
         } else {
             kern::row_norms(x, n, d, ldx, s_xn_.as<float>(), s);
         }
@@ -260,7 +283,6 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
         const idx_t qc = std::min<idx_t>(qchunk, n);
         s_cand_i_.reserve(sizeof(uint32_t) * qc * plan.entries);  // raw filter keys
         s_tile_.reserve(sizeof(float) * qc * plan.nsplit * 4);    // per-stream dropped bounds
-        ScopedKernelTimer tm(&ktimes, "coarse_bf3", 2.0 * n * ny * d, s);
         for (idx_t q0 = 0; q0 < n; q0 += qc) {
             const idx_t nq = std::min(qc, n - q0);
             kern::coarse_bf3_knn(plan, x + q0 * ldx, nq, ldx, s_xn_.as<float>() + q0,
@@ -269,10 +291,11 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
                                  s_cand_i_.as<uint32_t>(), s_tile_.as<float>(), distances + q0 * k,
                                  o32 ? o32 + q0 * k : nullptr, o64 ? o64 + q0 * k : nullptr, s,
                                  d_cst_.ptr,
-                                 qi ? (const uint8_t*)s_qimg_.ptr + q0 * kern::query_image_bytes(1, d)
-                                    : nullptr);
+                                 qi ? (const uint8_t*)qimg + q0 * kern::query_image_bytes(1, d)
+                                    : nullptr,
+                                 &ktimes);
         }
-        return;
+        return qi && qimg_out;
     }
     if (metric_l2) kern::row_norms(x, n, d, ldx, s_xn_.as<float>(), s);
     const idx_t Yc = std::min<idx_t>(std::max<idx_t>(ny, 1), 1 << 20);
@@ -295,7 +318,7 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
         if (nyc == 1) {
             // faiss/utils/distances.cpp:807-823: blocks of fewer than
             // distance_compute_blas_threshold (20) queries take the direct form
-            if (ny > 0 && n < 20)
+            if (ny > 0 && direct)
                 kern::direct_distances(xq, nq, ldx, d_xb_.as<float>(), ny, l, d, metric_l2,
                                        s_tile_.as<float>(), ny, s);
             else if (ny > 0)
@@ -312,7 +335,7 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
         } else {
             for (idx_t c = 0; c < nyc; c++) {
                 const idx_t y0 = c * Yc, nyy = std::min(Yc, ny - y0);
-                if (n < 20)
+                if (direct)
                     kern::direct_distances(xq, nq, ldx, d_xb_.as<float>() + y0 * l, nyy, l, d,
                                            metric_l2, s_tile_.as<float>(), nyy, s);
                 else
@@ -328,6 +351,7 @@ void IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* dista
                              o64 + q0 * k, s);
         }
     }
+    return false;
 }
 
 void IndexFlat::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
@@ -343,6 +367,19 @@ void IndexFlat::assign_device(idx_t n, const float* x, int ldx, int k, float* di
                               int32_t* labels, const SearchParameters*, hipStream_t s) const {
     DeviceGuard g(device);
     knn_device<int32_t>(n, x, ldx, k, distances, labels, s);
+}
+
+void IndexFlat::assign_device_slice(idx_t n, const float* x, int ldx, int k, float* distances,
+                                    int32_t* labels, const SearchParameters*, hipStream_t s,
+                                    idx_t batch_n) const {
+    DeviceGuard g(device);
+    knn_device<int32_t>(n, x, ldx, k, distances, labels, s, nullptr, batch_n);
+}
+
+bool IndexFlat::assign_device_qimg(idx_t n, const float* x, int ldx, int k, float* distances,
+                                   int32_t* labels, void* qimg, hipStream_t s) const {
+    DeviceGuard g(device);
+    return knn_device<int32_t>(n, x, ldx, k, distances, labels, s, qimg);
 }
 
 // ---------------------------------------------------------------- k-means

@@ -422,13 +422,13 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
                              : n;
     if (scratch) s_visited_.reserve(sizeof(uint32_t) * vwords * qc);
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(qc, 1));
-    ScopedKernelTimer tm(&ktimes, "hnsw_search", 0.0, s);
     for (idx_t q0 = 0; q0 < n; q0 += qc) {
         const idx_t nq = std::min(qc, n - q0);
         kern::hnsw_search(gd, x + q0 * ldx, ldx, nq, k, efSearch, distances + q0 * k,
                           i32 ? nullptr : (int64_t*)labels + q0 * k,
                           i32 ? (int32_t*)labels + q0 * k : nullptr, s_visited_.as<uint32_t>(),
-                          vwords, d_stats_.as<unsigned long long>(), s_flags_.as<uint32_t>(), s);
+                          vwords, d_stats_.as<unsigned long long>(), s_flags_.as<uint32_t>(), s,
+                          &ktimes);
     }
 }
 

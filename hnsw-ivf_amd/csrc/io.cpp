@@ -25,6 +25,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -63,24 +64,42 @@ std::string fourcc_str(uint32_t h) {
 // an index back to the file it was mapped from (IO_FLAG_MMAP, or an ilod data
 // file) must not truncate the mapping it is reading the lists through (the
 // old inode stays alive while mapped).  Removed again when not committed.
+// Only an existing regular file is replaced this way (through a symlink, the
+// file it names, keeping its mode); a new name, a FIFO, a device such as
+// /dev/stdout, or a directory where no temporary can be created is written in
+// place, as fopen(path, "wb") would.
 struct AtomicFile {
     std::string target, tmp;
     FILE* f = nullptr;
+    bool used = false;  // write_index_ondisk: the list data went through this file
+    mode_t mode = 0;
     explicit AtomicFile(const std::string& path) : target(path) {
-        tmp = path + ".tmpXXXXXX";
-        int fd = mkstemp(&tmp[0]);
-        FAISS_THROW_IF_NOT_MSG(fd >= 0, "could not open " + path + " for writing: " +
-                                                strerror(errno));
-        f = fdopen(fd, "wb");
-        if (!f) {
-            close(fd);
-            unlink(tmp.c_str());
-            FAISS_THROW_MSG("could not open " + path + " for writing");
+        struct stat st;
+        if (stat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode)) {
+            if (char* rp = realpath(path.c_str(), nullptr)) {
+                target = rp;
+                free(rp);
+            }
+            mode = st.st_mode & 07777;
+            tmp = target + ".tmpXXXXXX";
+            const int fd = mkstemp(&tmp[0]);
+            if (fd >= 0) {
+                f = fdopen(fd, "wb");
+                if (!f) {
+                    close(fd);
+                    unlink(tmp.c_str());
+                    FAISS_THROW_MSG("could not open " + path + " for writing");
+                }
+                return;
+            }
+            tmp.clear();  // no temporary beside it: write in place
         }
+        f = fopen(path.c_str(), "wb");
+        FAISS_THROW_IF_NOT_MSG(f, "could not open " + path + " for writing: " + strerror(errno));
     }
     AtomicFile(const AtomicFile&) = delete;
     AtomicFile& operator=(const AtomicFile&) = delete;
-    // flush and close; the data is complete under the temporary name
+    // flush and close; the data is complete (under the temporary name)
     void finish() {
         if (!f) return;
         const bool ok = fflush(f) == 0 && !ferror(f);
@@ -90,10 +109,8 @@ struct AtomicFile {
     }
     void commit() {
         finish();
-        // mkstemp creates 0600; give the file the usual umask-derived mode
-        const mode_t um = umask(0);
-        umask(um);
-        chmod(tmp.c_str(), 0666 & ~um);
+        if (tmp.empty()) return;  // written in place
+        chmod(tmp.c_str(), mode);  // mkstemp creates 0600: the replaced file's mode
         FAISS_THROW_IF_NOT_MSG(rename(tmp.c_str(), target.c_str()) == 0,
                                "could not rename onto " + target + ": " + strerror(errno));
         tmp.clear();
@@ -199,6 +216,7 @@ void write_invlists(const ArrayInvertedLists* il, Writer& w) {
     if (w.ondisk_fname) {
         // data file: per non-empty list codes[size*code_size] then ids[size]
         FAISS_THROW_IF_NOT(w.ondisk_file && w.ondisk_file->f);
+        w.ondisk_file->used = true;
         Writer dw{w.ondisk_file->f};
         std::vector<size_t> lists(3 * il->nlist, 0);
         size_t o = 0;
@@ -549,6 +567,7 @@ void write_index_ondisk(const Index* idx, const char* fname, const char* lists_f
     Writer w{f.f, lists_fname, &df};
     write_index_impl(idx, w);
     f.finish();
+    FAISS_THROW_IF_NOT_MSG(df.used, "write_index_ondisk: no inverted lists were written");
     df.commit();
     f.commit();
 }

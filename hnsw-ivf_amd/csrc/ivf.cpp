@@ -355,24 +355,45 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     // entry points (search / search_stats / search_preassigned) only
     const idx_t qchunk = search_chunk(n, np, k);
     std::lock_guard<std::recursive_mutex> g(mu_);
+    order_.enter(s);
     s_cd_.reserve(sizeof(float) * qchunk * np);
     s_ci_.reserve(sizeof(int32_t) * qchunk * np);
+    // a flat quantizer prepares the query image into this index's scratch, on
+    // this stream, and the list filter reads it from there
+    const auto* qf = dynamic_cast<const IndexFlat*>(quantizer);
+    if (qf && qf->d == d) s_q_.reserve(qf->query_image_size(qchunk));
     for (idx_t q0 = 0; q0 < n; q0 += qchunk) {
         const idx_t nq = std::min(qchunk, n - q0);
-        quantize_device(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(), s_ci_.as<int32_t>(),
-                        params ? params->quantizer_params : nullptr, s);
-        const uint32_t* lim = nullptr;
-        const int32_t* asg = apply_max_codes(nq, (int)np, s_ci_.as<int32_t>(), mc, &lim, s);
-        // the flat quantizer's prepared query image serves the list filter too
         struct Reset {
             const void*& p;
             ~Reset() { p = nullptr; }
         } reset{shared_qimg_};
-        if (auto* qf = dynamic_cast<const IndexFlat*>(quantizer))
-            shared_qimg_ = qf->d == d ? qf->prepared_query_image(x + q0 * ldx, nq, ldx) : nullptr;
+        if (qf && qf->d == d) {
+            if (qf->assign_device_qimg(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
+                                       s_ci_.as<int32_t>(), s_q_.ptr, s))
+                shared_qimg_ = s_q_.ptr;
+        } else {
+            quantize_device(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
+                            s_ci_.as<int32_t>(), params ? params->quantizer_params : nullptr, s);
+        }
+        const uint32_t* lim = nullptr;
+        const int32_t* asg = apply_max_codes(nq, (int)np, s_ci_.as<int32_t>(), mc, &lim, s);
         search_preassigned_device(nq, x + q0 * ldx, ldx, k, (int)np, asg, s_cd_.as<float>(),
                                   distances + q0 * k, labels + q0 * k, s, lim, selm);
     }
+    order_.leave(s);
+}
+
+void IndexIVF::search_preassigned_device_ordered(idx_t n, const float* x, int ldx, idx_t k,
+                                                 int np, const int32_t* assign,
+                                                 const float* cdis, float* distances,
+                                                 idx_t* labels, hipStream_t s) const {
+    DevGuard dg(device);
+    sync_device();
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    order_.enter(s);
+    search_preassigned_device(n, x, ldx, k, np, assign, cdis, distances, labels, s);
+    order_.leave(s);
 }
 
 void IndexIVF::search_preassigned(idx_t n, const float* x, idx_t k, const idx_t* assign,
@@ -660,8 +681,11 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     b.item_entries = s_ient_.as<uint32_t>();
     s_ictr_.reserve(16);
     b.item_ctr = s_ictr_.as<uint32_t>();
-    kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), d_list_off_.as<uint32_t>(),
-                     (int)nlist, QT, b, s);
+    {
+        ScopedKernelTimer tb(&ktimes, "ivf_bucket", 0.0, s);
+        kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), d_list_off_.as<uint32_t>(),
+                         (int)nlist, QT, b, s);
+    }
     flip_counts();
     const bool l2 = metric_type == METRIC_L2;
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(n, 4));
@@ -704,7 +728,7 @@ void IndexIVF::exact_scan_device(idx_t n, const float* x, int ldx, idx_t k, int 
                            (long long)k, kern::kMaxKExact);
     std::lock_guard<std::recursive_mutex> g(mu_);
     int64_t cap = 0;
-    const idx_t qc = kern::ivf_exact_chunk(n, np, max_list_len_, (int64_t)arena_rows_, &cap);
+    const idx_t qc = kern::ivf_exact_chunk(n, np, max_list_len_, &cap);
     s_ex_eoff_.reserve(sizeof(uint32_t) * qc * np);
     s_ex_tot_.reserve(sizeof(uint32_t) * qc);
     s_ex_keys_.reserve(sizeof(uint32_t) * qc * cap);
@@ -927,8 +951,11 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         s_ient_.reserve(sizeof(uint32_t) * mi * QT);
         b.item_desc = s_idesc_.as<kern::ItemDesc>();
         b.item_entries = s_ient_.as<uint32_t>();
-        kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), d_list_off_.as<uint32_t>(),
-                         (int)nlist, QT, b, s);
+            {
+            ScopedKernelTimer tb(&ktimes, "ivf_bucket", 0.0, s);
+            kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(),
+                             d_list_off_.as<uint32_t>(), (int)nlist, QT, b, s);
+        }
         flip_counts();
         const bool dbg = getenv("FAISS_AMD_IVF_STATS") != nullptr;
         s_pflags_.reserve(4 * sizeof(uint32_t));

@@ -51,7 +51,8 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
                     const float* cent, int ldc, const void* cbf, const float* cnorm,
                     const float* cnmax, int nlist, int d, int k, int metric_l2, uint32_t* keys,
                     float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s,
-                    const void* cst = nullptr, const void* qimg = nullptr);
+                    const void* cst = nullptr, const void* qimg = nullptr,
+                    KernelTimes* kt = nullptr);
 // Query preparation for the MFMA filters (one launch): the reference-order
 // norms ref_norms[i] = fvec_norm_L2sqr(x_i) (skipped when null) and the query
 // image of bf3.h load_query_image — qimg [n][64 NS] bytes (NS = bf3_db(d)/16)
@@ -214,8 +215,7 @@ struct ExactScanArgs {
     ExactPQ pq;  // pq.M > 0: IVF-PQ
 };
 // candidates per query (cap) and queries per chunk for a 1 GiB scratch
-int64_t ivf_exact_chunk(int64_t n, int np, uint32_t max_list_len, int64_t arena_rows,
-                        int64_t* cap_out);
+int64_t ivf_exact_chunk(int64_t n, int np, uint32_t max_list_len, int64_t* cap_out);
 // eoff [n*np], total [n], keys / rows [n*cap] scratch
 void ivf_exact_search(const ExactScanArgs& a, uint32_t* eoff, uint32_t* total, uint32_t* keys,
                       uint32_t* rows, int64_t cap, float* D, int64_t* I, hipStream_t s);
@@ -317,7 +317,7 @@ struct HNSWDevice {
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
-                 hipStream_t s);
+                 hipStream_t s, KernelTimes* kt = nullptr);
 
 // IVF-Flat range search (kernels_range.hip): one wave per (query, probe).
 // offsets == nullptr: counts[q*np+p] = hits (dis < radius for L2, > for IP,

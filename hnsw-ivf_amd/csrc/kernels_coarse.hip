@@ -798,7 +798,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
                     const float* cent, int ldc, const void* cbf, const float* cnorm,
                     const float* cnmax, int nlist, int d, int k, int metric_l2, uint32_t* keys,
                     float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s,
-                    const void* cst, const void* qimg) {
+                    const void* cst, const void* qimg, KernelTimes* kt) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(p.ok);
     static uint32_t* stats = nullptr;  // FAISS_AMD_IVF_STATS debug counters
@@ -864,8 +864,11 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
         else if (p.kt == 8) LAUNCH_A(L2V, 8); \
         else LAUNCH_A(L2V, 16);            \
     } while (0)
-    if (metric_l2) DISPATCH(true);
-    else DISPATCH(false);
+    {
+        ScopedKernelTimer tm(kt, "coarse_filter", 0.0, s);
+        if (metric_l2) DISPATCH(true);
+        else DISPATCH(false);
+    }
 #undef DISPATCH
 #undef LAUNCH_A
 #undef LAUNCH_NS
@@ -910,12 +913,15 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
         HIP_CHECK(hipMemsetAsync(crtrace_buf, 0, 64 * n, s));
         crtrace = crtrace_buf;
     }
-    if (metric_l2) {
-        if (I32) LAUNCH_RV(true, int32_t, I32);
-        else LAUNCH_RV(true, int64_t, I64);
-    } else {
-        if (I32) LAUNCH_RV(false, int32_t, I32);
-        else LAUNCH_RV(false, int64_t, I64);
+    {
+        ScopedKernelTimer tm(kt, "coarse_rerank", 0.0, s);
+        if (metric_l2) {
+            if (I32) LAUNCH_RV(true, int32_t, I32);
+            else LAUNCH_RV(true, int64_t, I64);
+        } else {
+            if (I32) LAUNCH_RV(false, int32_t, I32);
+            else LAUNCH_RV(false, int64_t, I64);
+        }
     }
 #undef LAUNCH_RV
 #undef LAUNCH_R

@@ -428,10 +428,11 @@ size_t select_lds(int k) {
 
 }  // namespace
 
-int64_t ivf_exact_chunk(int64_t n, int np, uint32_t max_list_len, int64_t arena_rows,
-                        int64_t* cap_out) {
-    const int64_t cap =
-            std::max<int64_t>(1, std::min<int64_t>((int64_t)np * max_list_len, arena_rows));
+// A query's candidate slot holds every row of its probes: np * max_list_len.
+// (Not clamped to the arena size: a caller-supplied assignment may name a list
+// twice, and the reference then scans it twice.)
+int64_t ivf_exact_chunk(int64_t n, int np, uint32_t max_list_len, int64_t* cap_out) {
+    const int64_t cap = std::max<int64_t>(1, (int64_t)np * max_list_len);
     *cap_out = cap;
     const int64_t budget = (int64_t)1 << 30;  // bytes of keys + rows per chunk
     return std::max<int64_t>(1, std::min<int64_t>(n, budget / (cap * 8)));

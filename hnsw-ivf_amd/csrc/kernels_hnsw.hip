@@ -903,7 +903,7 @@ __global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
-                 hipStream_t s) {
+                 hipStream_t s, KernelTimes* kt) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_FMT(k >= 1 && k <= kMaxKExact, "k = %d must be in [1, %d]", k,
                            kMaxKExact);
@@ -922,6 +922,7 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
         HIP_CHECK(hipMemsetAsync(visited_scratch, 0, sizeof(uint32_t) * vwords * n, s));
     }
     auto exact = [&](const uint32_t* only) {
+        ScopedKernelTimer tm(kt, "hnsw_exact", 0.0, s);
         if (ef <= 64 && k <= 64) {  // register heaps
             if (lds_vis)
                 k_hnsw_exact_reg<true><<<dim3((unsigned)n), dim3(64), lds_q + vwords * 4, s>>>(
@@ -948,6 +949,8 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
         exact(nullptr);
         return;
     }
+    {
+    ScopedKernelTimer tm(kt, "hnsw_search", 0.0, s);
     if (lds_vis) {
         size_t lds = lds_q + sizeof(uint32_t) * vwords;
         k_hnsw_search<true><<<dim3((unsigned)n), dim3(64), lds, s>>>(
@@ -957,6 +960,7 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
                 g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats, flags);
     }
     HIP_LAUNCH_CHECK();
+    }
     if (flags) {
         if (getenv("FAISS_AMD_HNSW_STATS")) {  // debug: how many queries tie (synchronises)
             std::vector<uint32_t> h((size_t)n);

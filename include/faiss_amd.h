@@ -181,6 +181,15 @@ struct Index {
     virtual void assign_device(idx_t n, const float* x, int ldx, int k, float* distances,
                                int32_t* labels, const SearchParameters* params,
                                hipStream_t stream) const;
+    // assign_device of n queries that are a slice of a batch of batch_n: the
+    // computation form the reference picks by batch size (a flat quantizer's
+    // direct form below 20 queries, faiss/utils/distances.cpp:807-823) follows
+    // batch_n, so a query split over devices gives the whole batch's result
+    virtual void assign_device_slice(idx_t n, const float* x, int ldx, int k, float* distances,
+                                     int32_t* labels, const SearchParameters* params,
+                                     hipStream_t stream, idx_t batch_n) const {
+        assign_device(n, x, ldx, k, distances, labels, params, stream);
+    }
     virtual void reset() = 0;
     virtual void reconstruct(idx_t key, float* recons) const;
     // faiss/Index.h:183-196: all vectors with distance < radius (L2) or
@@ -214,19 +223,28 @@ struct IndexFlat : Index {
 
     const float* device_vectors() const;  // [ntotal][ld]
     const float* device_norms() const;
-    // The query image (kernels.h query_prep: bf16 fragments, then |x|^2 at
-    // byte query_image_bytes(n, d)) the last assign / search prepared, if it
-    // was prepared for exactly (x, n, ldx); else null.  IndexIVF::search
-    // hands it to its list filter so a batch is prepared once.
-    const void* prepared_query_image(const float* x, idx_t n, int ldx) const;
+    // assign_device that also leaves the batch's query image (kernels.h
+    // query_prep: bf16 fragments, then |x|^2 at byte query_image_bytes(n, d))
+    // in the caller's buffer `qimg` (query_image_bytes(n, d) + 4 n bytes), on
+    // the caller's stream, so IndexIVF::search hands it to its list filter
+    // and a batch is prepared once.  Returns false when the coarse plan does
+    // not prepare an image (the buffer is then untouched).
+    bool assign_device_qimg(idx_t n, const float* x, int ldx, int k, float* distances,
+                            int32_t* labels, void* qimg, hipStream_t stream) const;
+    void assign_device_slice(idx_t n, const float* x, int ldx, int k, float* distances,
+                             int32_t* labels, const SearchParameters* params, hipStream_t stream,
+                             idx_t batch_n) const override;
+    // bytes of the query image assign_device_qimg writes for n queries
+    size_t query_image_size(idx_t n) const;
 
    private:
     template <class OutIdx>
-    void knn_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
-                    hipStream_t stream) const;
-    mutable const float* qimg_x_ = nullptr;
-    mutable idx_t qimg_n_ = 0;
-    mutable int qimg_ldx_ = 0;
+    bool knn_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
+                    hipStream_t stream, void* qimg_out = nullptr, idx_t batch_n = -1) const;
+    template <class OutIdx>
+    bool knn_impl(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
+                  hipStream_t stream, void* qimg_out, bool direct) const;
+    mutable StreamOrder order_;
     mutable DeviceBuffer d_xb_, d_norms_, d_cbf_, d_cnmax_, d_cst_;
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
@@ -408,6 +426,13 @@ struct IndexIVF : Index {
                                            const uint32_t* lim = nullptr,
                                            const uint8_t* sel = nullptr,
                                            bool store_pairs = false) const = 0;
+    // search_preassigned_device as a public device entry point: calls on
+    // different streams are put in device order (they share this index's
+    // scratch buffers)
+    void search_preassigned_device_ordered(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
+                                           const int32_t* assign, const float* centroid_dis,
+                                           float* distances, idx_t* labels,
+                                           hipStream_t stream) const;
     // range scan of device-resident queries / assignments into host results
     void range_device(idx_t n, const float* x, int ldx, int np, const int32_t* assign,
                       const float* cdis, float radius, const uint8_t* sel,
@@ -457,9 +482,11 @@ struct IndexIVF : Index {
     mutable DeviceBuffer s_ictr_;
     mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_counts_, s_boff_, s_ioff_, s_cur_, s_ent_,
             s_pk1_, s_pk2_, s_q_;
-    // query image prepared by the flat quantizer for the chunk search() is
-    // scanning (IndexFlat::prepared_query_image), null outside that call
+    // query image the flat quantizer prepared into s_q_ for the chunk
+    // search() is scanning (IndexFlat::assign_device_qimg), null outside it
     mutable const void* shared_qimg_ = nullptr;
+    // device order of calls on different streams sharing this index's scratch
+    mutable StreamOrder order_;
     mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_,
             s_selmask_;
     // bucket counts of this call (zero) and the half the call's scan clears

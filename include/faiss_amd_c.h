@@ -510,6 +510,8 @@ int faiss_amd_merge_knn_results_device(
 /* timing of the dominant kernel in the last search on this index: number of
  * launches and summed milliseconds (HIP events, only when enabled) */
 int faiss_amd_set_kernel_timing(int enable);
+/* time only the kernel stage of this name (NULL or "": every stage) */
+int faiss_amd_set_kernel_timing_filter(const char* name);
 int faiss_amd_last_kernel_times(
         const FaissIndex* index,
         int* n_kernels,

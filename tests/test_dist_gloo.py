@@ -2,8 +2,14 @@
 
 gloo stands in for RCCL; the per-shard search and the merge are the CPU
 oracle (faiss IndexShardsIVF semantics, faiss/IndexShardsIVF.cpp:158-245).
-Each rank holds the vectors with id % world == rank and brings its own
-queries; the merged result must equal the unsharded search of those queries.
+Each rank holds the vectors with id % world == rank.  Two batch forms:
+  weak   — every rank brings its own queries; the merged result must equal
+           the unsharded search of those queries;
+  strong — one global batch split over the ranks (bench.py c5): each rank
+           quantizes its slice in the form the whole batch's size decides
+           (BLAS form from 20 queries, faiss/utils/distances.cpp:807-823) and
+           the rank outputs, concatenated, equal the unsharded search of the
+           whole batch — also when a slice is below 20 queries.
 """
 import os
 import socket
@@ -37,7 +43,7 @@ def _shard_oracle(orc, xb, cent, ids):
     return orc.IVFOracle(D_, NLIST, 1, off, codes, ids[order], cent)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mode="weak", nq_glob=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -49,10 +55,17 @@ def _worker(rank, world, port, out_dir):
         ids = np.arange(NB, dtype=np.int64)
         mine = ids % world == rank
         shard = _shard_oracle(orc, xb[mine], cent, ids[mine])
-        xq = orc.float_rand(NQ * D_, 5678 + 7919 * rank).reshape(NQ, D_)
+        if mode == "strong":
+            xg = orc.float_rand(nq_glob * D_, 5678).reshape(nq_glob, D_)
+            s = nq_glob // world
+            xq = np.ascontiguousarray(xg[rank * s:(rank + 1) * s])
+            blas = nq_glob >= 20  # the form of the whole batch
+        else:
+            xq = orc.float_rand(NQ * D_, 5678 + 7919 * rank).reshape(NQ, D_)
+            blas = True
 
         def quantize(x):
-            cd, ci = orc.knn(x.numpy(), cent, NPROBE, blas_form=True, nthreads=1)
+            cd, ci = orc.knn(x.numpy(), cent, NPROBE, blas_form=blas, nthreads=1)
             return torch.from_numpy(cd), torch.from_numpy(ci.astype(np.int32))
 
         def search_pre(xa, ca, cda):
@@ -80,3 +93,20 @@ def test_sharded_search_equals_unsharded(tmp_path, orc):
         cd, ci = orc.knn(z["xq"], xb[:NLIST], NPROBE, blas_form=True, nthreads=1)
         Dr, Ir = full.search_preassigned(z["xq"], K, ci, cd, nthreads=1)
         assert np.array_equal(z["I"], Ir) and np.array_equal(z["D"], Dr)
+
+
+@pytest.mark.parametrize("nq_glob", [30, 128])
+def test_sharded_search_strong_split(tmp_path, orc, nq_glob):
+    """c5's form: one batch of nq_glob queries split over the ranks (15 per
+    rank at nq_glob = 30: slices below the BLAS threshold, the batch above)."""
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), "strong", nq_glob),
+             nprocs=world, join=True)
+    xb = orc.float_rand(NB * D_, 1234).reshape(NB, D_)
+    full = _shard_oracle(orc, xb, xb[:NLIST].copy(), np.arange(NB, dtype=np.int64))
+    xg = orc.float_rand(nq_glob * D_, 5678).reshape(nq_glob, D_)
+    cd, ci = orc.knn(xg, xb[:NLIST], NPROBE, blas_form=True, nthreads=1)
+    Dr, Ir = full.search_preassigned(xg, K, ci, cd, nthreads=1)
+    z = [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
+    assert np.array_equal(np.concatenate([t["I"] for t in z]), Ir)
+    assert np.array_equal(np.concatenate([t["D"] for t in z]), Dr)

@@ -291,3 +291,29 @@ def test_ivf_many_lists_bucketing(amd, orc, gpu):
     ref = orc.IVFOracle.from_index(idx)
     Dr, Ir = ref.search_preassigned(xq, 10, Iq, Dq)
     assert_same_results(D, I, Dr, Ir)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("desc", ["Flat", "PQ4"])
+@pytest.mark.parametrize("k", [10, 100])
+def test_preassigned_duplicate_probes(amd, orc, gpu, desc, k):
+    """A caller-supplied assignment may name a list more than once; the
+    reference then scans it once per probe (faiss/IndexIVF.cpp:595-631).
+    Every probe naming the same list makes a query's candidates outnumber the
+    arena's rows (the exact path's per-query slot must still hold them)."""
+    d, nb, nlist, nq, np_ = 16, 1200, 4, 40, 8
+    xb = rand(orc, nb, d, 81)
+    idx = amd.index_factory(d, f"IVF{nlist},{desc}")
+    idx.train(xb)
+    idx.add(xb)
+    xq = rand(orc, nq, d, 82)
+    Dq, Iq = idx.quantizer.search(xq, nlist)
+    keys = np.repeat(Iq[:, :1], np_, axis=1)          # the nearest list, 8 times
+    keys[nq // 2:, 1::2] = Iq[nq // 2:, 1:2]           # half the queries: two lists
+    by_list = np.empty_like(Dq)
+    np.put_along_axis(by_list, Iq, Dq, axis=1)        # coarse distance of every list
+    cdis = np.ascontiguousarray(np.take_along_axis(by_list, keys, axis=1), np.float32)
+    D, I = idx.search_preassigned(xq, k, keys, cdis)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir = ref.search_preassigned(xq, k, keys, cdis)
+    assert_same_results(D, I, Dr, Ir)

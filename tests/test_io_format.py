@@ -126,6 +126,38 @@ def test_mmap_index_resaved_in_place(amd, tmp_path):
     assert sorted(p.name for p in tmp_path.iterdir()) == ["m.index"]  # no temporaries left
 
 
+def test_write_keeps_symlink_and_mode(amd, tmp_path):
+    """Only an existing regular file is replaced by rename, and it keeps its
+    mode; a symlink stays a symlink (the file it names is replaced), and a
+    FIFO is written in place."""
+    import os
+    import stat
+    import threading
+    sizes, codes, ids = lists_data(seed=8)
+    raw = ivf_prefix(sum(sizes)) + ilar_bytes(sizes, codes, ids)
+    src = tmp_path / "s.index"
+    src.write_bytes(raw)
+    idx = amd.read_index(src)
+    real = tmp_path / "real.index"
+    real.write_bytes(b"old")
+    os.chmod(real, 0o640)
+    link = tmp_path / "link.index"
+    link.symlink_to(real)
+    amd.write_index(idx, link)
+    assert link.is_symlink() and real.read_bytes() == raw
+    assert stat.S_IMODE(os.stat(real).st_mode) == 0o640
+    fifo = tmp_path / "pipe"
+    os.mkfifo(fifo)
+    got = []
+    t = threading.Thread(target=lambda: got.append(open(fifo, "rb").read()))
+    t.start()
+    amd.write_index(idx, fifo)
+    t.join(30)
+    assert got == [raw] and stat.S_ISFIFO(os.stat(fifo).st_mode)
+    assert sorted(p.name for p in tmp_path.iterdir()) == [
+        "link.index", "pipe", "real.index", "s.index"]
+
+
 def test_ilod_data_file_rewritten_in_place(amd, tmp_path):
     """write_index_ondisk with the data file the lists are mapped from"""
     sizes, codes, ids = lists_data(seed=7)
