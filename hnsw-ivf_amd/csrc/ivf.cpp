@@ -256,11 +256,13 @@ void IndexIVF::sync_device() const {
 }
 
 uint32_t* IndexIVF::bucket_counts(hipStream_t s, uint32_t** next) const {
-    // two halves of nlist counters; a (re)allocation starts both at zero
-    // (re)zeroed as well when the previous call did not reach flip_counts()
-    // (an exception between the two left a half dirty) or ran on another
-    // stream (whose scan may still be zeroing the half used now)
-    const size_t need = sizeof(uint32_t) * 2 * std::max<size_t>(nlist, 1);
+    // nlist counters, zero between calls: the scan clears each count once it
+    // has read it (self-cleaning, so a captured step can be replayed).  A
+    // (re)allocation starts them at zero; they are (re)zeroed as well when
+    // the previous call did not reach flip_counts() (an exception between
+    // the two left them dirty) or ran on another stream (whose scan may still
+    // be clearing them)
+    const size_t need = sizeof(uint32_t) * std::max<size_t>(nlist, 1);
     const bool fresh = !s_counts_.ptr || s_counts_.bytes < need;
     if (fresh || counts_pending_ || s != counts_stream_) {
         if (!fresh && s != counts_stream_ && counts_stream_valid_)
@@ -273,8 +275,8 @@ uint32_t* IndexIVF::bucket_counts(hipStream_t s, uint32_t** next) const {
     counts_stream_valid_ = true;
     counts_pending_ = true;  // until flip_counts()
     uint32_t* base = s_counts_.as<uint32_t>();
-    *next = base + (size_t)(1 - counts_parity_) * nlist;
-    return base + (size_t)counts_parity_ * nlist;
+    *next = base;  // cleared by the scan that reads them
+    return base;
 }
 
 void IndexIVF::quantize_device(idx_t n, const float* x, int ldx, int np, float* coarse_dis,

@@ -134,9 +134,9 @@ struct IVFBuckets {
     uint32_t* mark_keys = nullptr;
     ProbeRec* mark_recs = nullptr;
     int mark_ke = 0;
-    // optional: the other half of a double-buffered count array.  When set,
-    // `counts` is already zero (the previous call's scan cleared it) and the
-    // scan clears counts_next for the next call, so no memset is launched.
+    // optional: the count array the scan clears after reading it (== counts:
+    // self-cleaning).  When set, `counts` is already zero (the previous
+    // call's scan cleared it), so no memset is launched.
     uint32_t* counts_next = nullptr;
     // optional (max_codes): rows of each entry's list that are scanned (a
     // prefix; probe_limits), nullptr = whole lists

@@ -109,6 +109,8 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             c[j] = l0 + j < nlist ? counts[l0 + j] : 0u;
+            // zero_next == counts: each count is cleared once read (the fill
+            // takes the bucket sizes from bucket_off)
             if (zero_next && l0 + j < nlist) zero_next[l0 + j] = 0u;
             n[j] = (c[j] + QT - 1) / QT;
             sb += c[j];
@@ -181,7 +183,7 @@ __global__ void k_bucket_fill(const int32_t* __restrict__ assign, int64_t total,
             if (p % QT == 0) {  // the item's first entry writes its descriptor
                 ItemDesc dsc;
                 dsc.l = (uint32_t)l;
-                dsc.nq = min((uint32_t)QT, counts[l] - p);
+                dsc.nq = min((uint32_t)QT, bucket_off[l + 1] - bucket_off[l] - p);
                 dsc.len = list_len[l];
                 dsc.off = list_off[l];
                 item_desc[item] = dsc;

@@ -489,8 +489,8 @@ struct IndexIVF : Index {
     mutable StreamOrder order_;
     mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_,
             s_selmask_;
-    // bucket counts of this call (zero) and the half the call's scan clears
-    // for the next one; flip_counts() after the bucket kernels are queued
+    // bucket counts of this call (zero; the call's scan clears them again);
+    // flip_counts() after the bucket kernels are queued
     uint32_t* bucket_counts(hipStream_t s, uint32_t** next) const;
     void flip_counts() const {
         counts_parity_ ^= 1;
