@@ -83,6 +83,95 @@ struct DeviceGuard {
     }
 };
 
+// ---------------------------------------------------------------- staging
+namespace {
+constexpr size_t kStageBytes = (size_t)4 << 20;  // per buffer
+bool host_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    const hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+}  // namespace
+
+HostStaging::~HostStaging() {
+    for (int b = 0; b < 2; b++) {
+        if (ev[b]) (void)hipEventDestroy(ev[b]);
+        if (buf[b]) (void)hipHostFree(buf[b]);
+    }
+}
+void HostStaging::ensure() {
+    if (cap) return;
+    for (int b = 0; b < 2; b++) {
+        HIP_CHECK(hipHostMalloc(&buf[b], kStageBytes, hipHostMallocDefault));
+        HIP_CHECK(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming));
+    }
+    cap = kStageBytes;
+}
+void HostStaging::wait(int b) {
+    if (pend[b]) HIP_CHECK(hipEventSynchronize(ev[b]));
+    pend[b] = false;
+}
+void HostStaging::upload_rows(float* dst, int ld, const float* x, int d, int64_t n,
+                              hipStream_t s) {
+    const size_t row = sizeof(float) * d;
+    if (n <= 0) return;
+    // pinned queries go straight to the DMA engine; small pageable ones are
+    // staged by HIP itself
+    if ((size_t)n * row <= ((size_t)64 << 10) || host_pinned(x)) {
+        HIP_CHECK(hipMemcpy2DAsync(dst, sizeof(float) * ld, x, row, row, n,
+                                   hipMemcpyHostToDevice, s));
+        return;
+    }
+    ensure();
+    const int64_t per = std::max<int64_t>(1, (int64_t)(cap / row));
+    int b = 0;
+    for (int64_t r0 = 0; r0 < n; r0 += per, b ^= 1) {
+        const int64_t rows = std::min(per, n - r0);
+        wait(b);  // its previous DMA has read the buffer
+        memcpy(buf[b], x + r0 * d, rows * row);
+        HIP_CHECK(hipMemcpy2DAsync(dst + r0 * ld, sizeof(float) * ld, buf[b], row, row, rows,
+                                   hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipEventRecord(ev[b], s));
+        pend[b] = true;
+    }
+}
+void HostStaging::download(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    if (host_pinned(dst)) {
+        HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        return;
+    }
+    ensure();
+    // chunk c lands in buf[c & 1]; it is copied out while chunk c + 1 moves
+    size_t off[2] = {0, 0}, len[2] = {0, 0};
+    int b = 0;
+    for (size_t o = 0; o < bytes; o += cap, b ^= 1) {
+        const size_t l = std::min(cap, bytes - o);
+        if (len[b]) {
+            wait(b);
+            memcpy((uint8_t*)dst + off[b], buf[b], len[b]);
+        } else {
+            wait(b);
+        }
+        HIP_CHECK(hipMemcpyAsync(buf[b], (const uint8_t*)src + o, l, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipEventRecord(ev[b], s));
+        pend[b] = true;
+        off[b] = o;
+        len[b] = l;
+    }
+    for (int i = 0; i < 2; i++, b ^= 1) {
+        if (!len[b]) continue;
+        wait(b);
+        memcpy((uint8_t*)dst + off[b], buf[b], len[b]);
+        len[b] = 0;
+    }
+}
+
 // ---------------------------------------------------------------- Index
 Index::Index(idx_t d_, MetricType metric) : d((int)d_), metric_type(metric) {
     device = current_device();
@@ -111,7 +200,8 @@ void Index::range_search(idx_t, const float*, float, RangeSearchResult*,
 
 hipStream_t Index::stream() const { return device_context(device).stream; }
 
-// Host entry: upload (zero-padded rows), search_device, download.
+// Host entry: upload (zero-padded rows) through the device's pinned staging
+// into this index's cached buffers, search_device, download.
 void Index::search(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
                    const SearchParameters* params) const {
     FAISS_THROW_IF_NOT(k > 0);
@@ -120,17 +210,17 @@ void Index::search(idx_t n, const float* x, idx_t k, float* distances, idx_t* la
     sync_device();
     hipStream_t s = stream();
     const int ldx = ld();
-    DeviceBuffer bx, bd, bi;
-    bx.reserve(sizeof(float) * n * ldx);
-    bd.reserve(sizeof(float) * n * k);
-    bi.reserve(sizeof(idx_t) * n * k);
-    if (ldx != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * n * ldx, s));
-    HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ldx, x, sizeof(float) * d,
-                               sizeof(float) * d, n, hipMemcpyHostToDevice, s));
-    search_device(n, bx.as<float>(), ldx, k, bd.as<float>(), bi.as<idx_t>(), params, s);
-    HIP_CHECK(hipMemcpyAsync(distances, bd.ptr, sizeof(float) * n * k, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    std::lock_guard<std::mutex> hg(host_mu_);
+    h_x_.reserve(sizeof(float) * n * ldx);
+    h_d_.reserve(sizeof(float) * n * k);
+    h_i_.reserve(sizeof(idx_t) * n * k);
+    HostStaging& st = device_context(device).staging;
+    std::lock_guard<std::mutex> sg(st.mu);
+    if (ldx != d) HIP_CHECK(hipMemsetAsync(h_x_.ptr, 0, sizeof(float) * n * ldx, s));
+    st.upload_rows(h_x_.as<float>(), ldx, x, d, n, s);
+    search_device(n, h_x_.as<float>(), ldx, k, h_d_.as<float>(), h_i_.as<idx_t>(), params, s);
+    st.download(distances, h_d_.ptr, sizeof(float) * n * k, s);
+    st.download(labels, h_i_.ptr, sizeof(idx_t) * n * k, s);
     fold_device_stats();
 }
 

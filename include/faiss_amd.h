@@ -202,6 +202,12 @@ struct Index {
 
     hipStream_t stream() const;
     int ld() const { return (int)roundup((size_t)d, 4); }
+
+   protected:
+    // host-pointer entry points: queries and results in HBM, kept between
+    // calls (one host call at a time per index)
+    mutable std::mutex host_mu_;
+    mutable DeviceBuffer h_x_, h_d_, h_i_;
 };
 
 // ---------------------------------------------------------------- flat
