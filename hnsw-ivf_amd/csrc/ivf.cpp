@@ -471,11 +471,26 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
     HIP_CHECK(hipMemsetAsync(s_stats_.ptr, 0, 2 * sizeof(unsigned long long), s));
     StageEvents ev;
     hipEvent_t e0 = ev.mark(s);
+    // per query: the device clock where its result is emitted, against
+    // stamps at the scan's start and end (calibrated by e0 / e1)
+    struct ResetQ {
+        unsigned long long*& p;
+        ~ResetQ() { p = nullptr; }
+    } reset_q{qdone_};
+    if (per_query_stats) {
+        s_qdone_.reserve(sizeof(unsigned long long) * n);
+        HIP_CHECK(hipMemsetAsync(s_qdone_.ptr, 0, sizeof(unsigned long long) * n, s));
+        s_stamps_.reserve(sizeof(unsigned long long) * 2);
+        kern::device_stamp(s_stamps_.as<unsigned long long>(), s);
+        qdone_ = s_qdone_.as<unsigned long long>();
+    }
     const uint32_t* lim = nullptr;
     const int32_t* asg = apply_max_codes(n, (int)np, ba.as<int32_t>(), mc, &lim, s);
     const uint8_t* selm = apply_selector(params, s);
     search_preassigned_device(n, bx.as<float>(), ldx, k, (int)np, asg, bc.as<float>(),
                               bd.as<float>(), bi.as<idx_t>(), s, lim, selm, store_pairs);
+    qdone_ = nullptr;
+    if (per_query_stats) kern::device_stamp(s_stamps_.as<unsigned long long>() + 1, s);
     hipEvent_t e1 = ev.mark(s);
     kern::ivf_visit_stats(asg, n * (int64_t)np, d_list_len_.as<uint32_t>(), (int)nlist, lim,
                           s_stats_.as<unsigned long long>(), s);
@@ -490,7 +505,16 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
     out->ndis += st[1];
     if (per_query_stats) {
         const double scan_us = StageEvents::ms(e0, e1) * 1e3;
-        for (idx_t i = 0; i < n; i++) per_query_stats[i].list_scan_us = scan_us;
+        std::vector<unsigned long long> qd((size_t)n), sp(2);
+        HIP_CHECK(hipMemcpy(qd.data(), s_qdone_.ptr, sizeof(unsigned long long) * n,
+                            hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(sp.data(), s_stamps_.ptr, 2 * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost));
+        const double ticks = (double)(sp[1] - sp[0]);
+        const double us_per_tick = ticks > 0 ? scan_us / ticks : 0.01;
+        for (idx_t i = 0; i < n; i++)
+            per_query_stats[i].list_scan_us =
+                    qd[i] >= sp[0] ? (double)(qd[i] - sp[0]) * us_per_tick : scan_us;
     }
 }
 
@@ -545,17 +569,39 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
     StageEvents ev;
     std::vector<hipEvent_t> marks;
     const uint8_t* selm = apply_selector(params, s);
-    for (idx_t q0 = 0; q0 < n; q0 += qchunk) {
+    // search_stats: device-clock stamps (s_memrealtime) at the batch's first
+    // and last stage boundary (their HIP events calibrate the clock), at each
+    // chunk's scan start, and per query where its result is emitted
+    const idx_t nch = (n + qchunk - 1) / qchunk;
+    unsigned long long* stamps = nullptr;
+    if (per_query_stats) {
+        s_qdone_.reserve(sizeof(unsigned long long) * n);
+        HIP_CHECK(hipMemsetAsync(s_qdone_.ptr, 0, sizeof(unsigned long long) * n, s));
+        s_stamps_.reserve(sizeof(unsigned long long) * (nch + 2));
+        stamps = s_stamps_.as<unsigned long long>();
+    }
+    struct ResetQ {
+        unsigned long long*& p;
+        ~ResetQ() { p = nullptr; }
+    } reset_q{qdone_};
+    for (idx_t q0 = 0, c = 0; q0 < n; q0 += qchunk, c++) {
         const idx_t nq = std::min(qchunk, n - q0);
         marks.push_back(ev.mark(s));
+        if (stamps && c == 0) kern::device_stamp(stamps, s);
         quantize_device(nq, bx.as<float>() + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
                         s_ci_.as<int32_t>(), params ? params->quantizer_params : nullptr, s);
         marks.push_back(ev.mark(s));
+        if (stamps) {
+            kern::device_stamp(stamps + 2 + c, s);
+            qdone_ = s_qdone_.as<unsigned long long>() + q0;
+        }
         const uint32_t* lim = nullptr;
         const int32_t* asg = apply_max_codes(nq, (int)np, s_ci_.as<int32_t>(), mc, &lim, s);
         search_preassigned_device(nq, bx.as<float>() + q0 * ldx, ldx, k, (int)np, asg,
                                   s_cd_.as<float>(), bd.as<float>() + q0 * k,
                                   bi.as<idx_t>() + q0 * k, s, lim, selm);
+        qdone_ = nullptr;
+        if (stamps && q0 + nq == n) kern::device_stamp(stamps + 1, s);
         marks.push_back(ev.mark(s));
         kern::ivf_visit_stats(asg, nq * (int64_t)np, d_list_len_.as<uint32_t>(), (int)nlist,
                               lim, s_stats_.as<unsigned long long>(), s);
@@ -579,11 +625,29 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
         indexIVF_stats.search_time += qms + sms;
     }
     if (per_query_stats) {
-        const double qus = qms * 1e3 / n, sus = sms * 1e3;
-        for (idx_t i = 0; i < n; i++) {
-            per_query_stats[i].quantization_us = qus;
-            per_query_stats[i].list_scan_us = sus;
-            per_query_stats[i].total_us = qus + sus;
+        // faiss/IndexIVF.cpp:760-777, 1062-1107: quantization_us is the
+        // coarse stage's time amortised over the chunk's queries;
+        // list_scan_us runs from the chunk's scan start to the query's
+        // result on the device clock (its completion latency in the batch)
+        std::vector<unsigned long long> qd((size_t)n), sp((size_t)nch + 2);
+        HIP_CHECK(hipMemcpy(qd.data(), s_qdone_.ptr, sizeof(unsigned long long) * n,
+                            hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(sp.data(), s_stamps_.ptr, sizeof(unsigned long long) * (nch + 2),
+                            hipMemcpyDeviceToHost));
+        const double span_us = StageEvents::ms(marks.front(), marks.back()) * 1e3;
+        const double ticks = (double)(sp[1] - sp[0]);
+        const double us_per_tick = ticks > 0 ? span_us / ticks : 0.01;  // 100 MHz nominal
+        for (idx_t q0 = 0, c = 0; q0 < n; q0 += qchunk, c++) {
+            const idx_t nq = std::min(qchunk, n - q0);
+            const double qus = StageEvents::ms(marks[3 * c], marks[3 * c + 1]) * 1e3 / nq;
+            const double sus_all = StageEvents::ms(marks[3 * c + 1], marks[3 * c + 2]) * 1e3;
+            for (idx_t i = q0; i < q0 + nq; i++) {
+                double sus = qd[i] >= sp[2 + c] ? (double)(qd[i] - sp[2 + c]) * us_per_tick
+                                                : sus_all;
+                per_query_stats[i].quantization_us = qus;
+                per_query_stats[i].list_scan_us = sus;
+                per_query_stats[i].total_us = qus + sus;
+            }
         }
     }
 }
@@ -705,7 +769,8 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
                              b, max_items, s_part_.as<uint32_t>(), s_pk2_.as<kern::ProbeRec>(),
                              dbg ? s_flags_.as<uint32_t>() : nullptr, distances, labels, &ktimes,
                              s, kern::ARENA_ALIGN, d_cbs_.ptr,
-                             qready ? const_cast<void*>(qready) : s_q_.ptr, qready != nullptr);
+                             qready ? const_cast<void*>(qready) : s_q_.ptr, qready != nullptr,
+                             qdone_);
     if (dbg) {
         uint32_t st[4];
         HIP_CHECK(hipMemcpyAsync(st, s_flags_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
@@ -758,6 +823,7 @@ void IndexIVF::exact_scan_device(idx_t n, const float* x, int ldx, idx_t k, int 
         a.assign = assign + q0 * np;
         a.cdis = cdis ? cdis + q0 * np : nullptr;
         a.lim = lim ? lim + q0 * np : nullptr;
+        a.qdone = qdone_ ? qdone_ + q0 : nullptr;
         kern::ivf_exact_search(a, s_ex_eoff_.as<uint32_t>(), s_ex_tot_.as<uint32_t>(),
                                s_ex_keys_.as<uint32_t>(), s_ex_rows_.as<uint32_t>(), cap,
                                distances + q0 * k, labels + q0 * k, s);
@@ -998,7 +1064,7 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
             kern::ivfpq_rerank(s_pkeys_.as<uint32_t>(), s_precs_.as<kern::ProbeRec>(), x, ldx, d,
                                d_ids_.as<int64_t>(), pa, (int)pq.dsub, n, np, KT, pq_obits_,
                                (int)k, sel, distances, labels,
-                               dbg ? s_pflags_.as<uint32_t>() : nullptr, s);
+                               dbg ? s_pflags_.as<uint32_t>() : nullptr, s, qdone_);
         }
         if (dbg) {
             uint32_t st[4];

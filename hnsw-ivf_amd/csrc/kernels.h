@@ -181,7 +181,9 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
 void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx, int d,
                   const int64_t* ids, const PQArgs& pa, int dsub, int64_t n, int nprobe, int KT,
                   int obits, int k, const uint8_t* sel, float* D, int64_t* I, uint32_t* stats,
-                  hipStream_t s);
+                  hipStream_t s, unsigned long long* qdone = nullptr);
+// the device clock (s_memrealtime) into *out, in stream order
+void device_stamp(unsigned long long* out, hipStream_t s);
 
 // ---------------- general exact path (kernels_exact.hip) ----------------
 // IVF-PQ tables of the exact scan (QueryTables semantics)
@@ -196,6 +198,7 @@ struct ExactPQ {
     int cs = 0;                      // code stride (bytes)
 };
 struct ExactScanArgs {
+    unsigned long long* qdone = nullptr;  // per query completion stamps (search_stats)
     const float* x = nullptr;  // [n][ldx] queries of the chunk
     int ldx = 0, d = 0;
     int64_t n = 0;
@@ -272,7 +275,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         float* D, int64_t* I, KernelTimes* kt, hipStream_t s,
                         int list_align = 16, const void* cbs = nullptr,
                         void* qscratch = nullptr,  // query_image_bytes(n, d) + 4 n bytes
-                        bool qready = false);      // qscratch already holds x's image
+                        bool qready = false, unsigned long long* qdone = nullptr);      // qscratch already holds x's image
 // stream image of the arena for the streamed filter: per row bf16(code) (DB
 // dims) + fp32 norm (+inf for padding rows) + 12 zero bytes = 2 DB + 16 bytes
 void split_bf16_stream(const float* codes, int64_t rows, int d, int ldc, int DB,

@@ -256,7 +256,11 @@ struct SrcIVF {
     const uint32_t* row_list;
     const uint32_t* list_off;
     int store_pairs;
+    unsigned long long* qdone;  // per query: completion stamp (search_stats), or nullptr
     __device__ int64_t count(int64_t q) const { return total[q]; }
+    __device__ void done(int64_t q) const {
+        if (qdone) qdone[q] = __builtin_amdgcn_s_memrealtime();
+    }
     __device__ uint32_t key(int64_t q, int64_t i) const { return keys[q * cap + i]; }
     __device__ int64_t label(int64_t q, int64_t i) const {
         const uint32_t row = rows[q * cap + i];
@@ -275,6 +279,7 @@ struct SrcDense {
     __device__ int64_t count(int64_t) const { return ny; }
     __device__ uint32_t key(int64_t q, int64_t i) const { return ex_key(D[q * ldD + i], l2); }
     __device__ int64_t label(int64_t, int64_t i) const { return col0 + i; }
+    __device__ void done(int64_t) const {}
 };
 
 template <class Src, class OutIdx>
@@ -419,6 +424,7 @@ __global__ __launch_bounds__(256) void k_ex_select(Src src, int k, int l2, float
         D[q * ldo + t] = ok ? ex_dis(okey[t], l2) : (l2 ? FLT_MAX : -FLT_MAX);
         I[q * ldo + t] = ok ? (OutIdx)oid[t] : (OutIdx)-1;
     }
+    if (tid == 0) src.done(q);
 }
 
 size_t select_lds(int k) {
@@ -477,7 +483,7 @@ void ivf_exact_search(const ExactScanArgs& a, uint32_t* eoff, uint32_t* total, u
                     a.codes, a.ldc, a.sel, eoff, cap, keys, rows);
     }
     HIP_LAUNCH_CHECK();
-    SrcIVF src{keys, rows, total, cap, a.ids, a.row_list, a.list_off, a.store_pairs};
+    SrcIVF src{keys, rows, total, cap, a.ids, a.row_list, a.list_off, a.store_pairs, a.qdone};
     k_ex_select<SrcIVF, int64_t><<<dim3((unsigned)a.n), dim3(256), select_lds(a.k), s>>>(
             src, a.k, a.l2, D, I, a.k);
     HIP_LAUNCH_CHECK();

@@ -203,6 +203,12 @@ __global__ void k_bucket_fill(const int32_t* __restrict__ assign, int64_t total,
     }
 }
 
+__global__ void k_stamp(unsigned long long* out) { *out = __builtin_amdgcn_s_memrealtime(); }
+void device_stamp(unsigned long long* out, hipStream_t s) {
+    k_stamp<<<dim3(1), dim3(1), 0, s>>>(out);
+    HIP_LAUNCH_CHECK();
+}
+
 // grid-stride partial counts per thread, one atomic pair per work-group
 __global__ __launch_bounds__(256) void k_ivf_visit_stats(const int32_t* __restrict__ assign,
                                                          int64_t total,

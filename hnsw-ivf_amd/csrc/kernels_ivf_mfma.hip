@@ -916,7 +916,8 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
         const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
         const int64_t* __restrict__ ids, int d, int64_t n, int nprobe, int KT, int obits, int k,
         float* __restrict__ D, int64_t* __restrict__ I, uint32_t* __restrict__ stats,
-        unsigned long long* __restrict__ trace, PQArgs pa, const uint8_t* __restrict__ sel) {
+        unsigned long long* __restrict__ trace, PQArgs pa, const uint8_t* __restrict__ sel,
+        unsigned long long* __restrict__ qdone) {
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ uint32_t surv[RR_W][RR_CAP];
     __shared__ uint16_t sprobe[RR_W][RR_CAP];
@@ -1147,6 +1148,8 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
         atomicAdd(&stats[2], st.overflow ? 1u : 0u);
         atomicAdd(&stats[3], done ? 0u : 1u);
     }
+    // search_stats: the query's completion on the device clock
+    if (qdone && valid && lane == 0) qdone[q] = __builtin_amdgcn_s_memrealtime();
     if (trace && valid && lane == 0) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         trace[8 * q + 0] = t_start;
@@ -1237,7 +1240,8 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         int obits, int64_t n, int nprobe, int k, int metric_l2, IVFBuckets b,
                         int64_t max_items, uint32_t* keys, ProbeRec* recs, uint32_t* stats,
                         float* D, int64_t* I, KernelTimes* kt, hipStream_t s, int list_align,
-                        const void* cbs, void* qscratch, bool qready) {
+                        const void* cbs, void* qscratch, bool qready,
+                        unsigned long long* qdone) {
     if (n <= 0) return;
     const bool aligned_lists = list_align % BV == 0 && cbs != nullptr;
     const int KE = ivf_mfma_kq(k, d, nprobe);
@@ -1366,7 +1370,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 #define LAUNCH_B(L2V, VV)                                                                      \
     k_ivf_rerank<L2V, VV><<<dim3((unsigned)cdiv(n, RR_W)), dim3(64 * RR_W), 0, s>>>(           \
             keys, recs, x, ldx, codes, ldc, ids, d, n, nprobe, KE / 4, obits, k, D, I, stats,   \
-            trace, PQArgs{}, b.sel)
+            trace, PQArgs{}, b.sel, qdone)
 #define DISPATCH_V(L2V)                      \
     do {                                     \
         if (V == 2) LAUNCH_B(L2V, 2);        \
@@ -1400,7 +1404,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx, int d,
                   const int64_t* ids, const PQArgs& pa, int dsub, int64_t n, int nprobe, int KT,
                   int obits, int k, const uint8_t* sel, float* D, int64_t* I, uint32_t* stats,
-                  hipStream_t s) {
+                  hipStream_t s, unsigned long long* qdone) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(d <= BDM && d % 4 == 0);
     const int KE = 4 * KT;
@@ -1409,7 +1413,7 @@ void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, in
 #define LAUNCH_P(VV, DS)                                                                        \
     k_ivf_rerank<true, VV, DS><<<dim3((unsigned)cdiv(n, RR_W)), dim3(64 * RR_W), 0, s>>>(       \
             keys, recs, x, ldx, nullptr, 0, ids, d, n, nprobe, KT, obits, k, D, I, stats,         \
-            nullptr, pa, sel)
+            nullptr, pa, sel, qdone)
 #define DISPATCH_P(DS)                       \
     do {                                     \
         if (V == 2) LAUNCH_P(2, DS);         \

@@ -493,6 +493,11 @@ struct IndexIVF : Index {
     mutable const void* shared_qimg_ = nullptr;
     // device order of calls on different streams sharing this index's scratch
     mutable StreamOrder order_;
+    // search_stats: per-query completion stamps of the chunk being scanned
+    // (device clock, written by the kernel that emits a query's result),
+    // null outside such a call
+    mutable unsigned long long* qdone_ = nullptr;
+    mutable DeviceBuffer s_qdone_, s_stamps_;
     mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_,
             s_selmask_;
     // bucket counts of this call (zero; the call's scan clears them again);

@@ -72,6 +72,38 @@ def test_ivf_search_preassigned_stats(amd, orc, flat_ivf):
     assert g.nq == 0  # an explicit stats object receives the counts
 
 
+@pytest.mark.parametrize("desc,k", [("Flat", 10), ("Flat", 100), ("PQ8", 10)])
+def test_ivf_search_stats_per_query_latency(amd, orc, gpu, desc, k):
+    """list_scan_us is each query's own completion time in the batched scan
+    (device clock stamped where its result is emitted: the re-rank wave, or
+    the exact path's select), so the per-query values carry the spread the
+    author's harness reports as P50 / P95 / P99
+    (tutorial/cpp/benchmark-hnsw-ivf/benchmark_hnsw_ivf.cpp:400-404)."""
+    import time
+    d, nb, nlist = 32, 20000, 64
+    xb = rand(orc, nb, d, 54)
+    idx = amd.index_factory(d, f"IVF{nlist},{desc}")
+    idx.train(xb)
+    idx.add(xb)
+    idx.nprobe = 8
+    xq = rand(orc, 2000, d, 55)
+    D, I = idx.search(xq, k)
+    t = time.perf_counter()
+    D2, I2, lat = idx.search_stats(xq, k)
+    wall_us = (time.perf_counter() - t) * 1e6
+    assert_same_results(D2, I2, D, I)
+    ls = lat["list_scan_us"]
+    assert (ls > 0).all() and (ls < wall_us).all()
+    assert len(np.unique(ls)) > 100  # per-query values, not one batch figure
+    p50, p99 = np.percentile(ls, [50, 99])
+    assert p50 <= p99
+    np.testing.assert_allclose(lat["total_us"], lat["quantization_us"] + ls)
+    # search_preassigned_stats: the same per-query stamps
+    Dq, Iq = idx.quantizer.search(xq, 8)
+    _, _, lat2 = idx.search_preassigned_stats(xq, k, Iq, Dq)
+    assert (lat2["list_scan_us"] > 0).all() and len(np.unique(lat2["list_scan_us"])) > 100
+
+
 def test_ivf_stats_empty_batch(amd, flat_ivf):
     idx, _ = flat_ivf
     D, I, lat = idx.search_stats(np.zeros((0, 32), np.float32), 4)
