@@ -285,7 +285,13 @@ def main():
     # recall queries: the first of rank 0's (every rank of a sharded run
     # computes its shard's exact top-k for them; rank 0 merges)
     nr = min(args.recall_queries, nq_loc)
-    xr = amd.float_rand(nr * d, 5678).reshape(nr, d) if nr else None
+    # (float_rand's blocks depend on n: rank 0's rows are re-derived from its
+    # whole set, not from a shorter call)
+    xr = None
+    if nr:
+        xr = np.ascontiguousarray((xq_glob if strong else
+                                   xq if rank == 0 else
+                                   amd.float_rand(nq * d, 5678).reshape(nq, d))[:nr])
     gt_run = None
     t0 = time.time()
     index = amd.index_factory(d, cfg["desc"])

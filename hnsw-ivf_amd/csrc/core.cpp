@@ -85,7 +85,7 @@ struct DeviceGuard {
 
 // ---------------------------------------------------------------- staging
 namespace {
-constexpr size_t kStageBytes = (size_t)4 << 20;  // per buffer
+constexpr size_t kStageBytes = (size_t)1 << 20;  // per buffer
 bool host_pinned(const void* p) {
     hipPointerAttribute_t a;
     const hipError_t e = hipPointerGetAttributes(&a, p);
@@ -97,16 +97,30 @@ bool host_pinned(const void* p) {
 }
 }  // namespace
 
+// FAISS_AMD_STAGING=0: host buffers go to hipMemcpy directly (HIP's own
+// staging of pageable memory), for comparison
+static bool staging_enabled() {
+    const char* e = getenv("FAISS_AMD_STAGING");
+    return !(e && !strcmp(e, "0"));
+}
+
 HostStaging::~HostStaging() {
     for (int b = 0; b < 2; b++) {
         if (ev[b]) (void)hipEventDestroy(ev[b]);
-        if (buf[b]) (void)hipHostFree(buf[b]);
+        if (buf[b]) {
+            (void)hipHostUnregister(buf[b]);
+            free(buf[b]);
+        }
     }
 }
 void HostStaging::ensure() {
     if (cap) return;
+    // ordinary (CPU-cached) pages, pinned by registration: the CPU fills them
+    // at memcpy speed, the DMA engine reads them directly
     for (int b = 0; b < 2; b++) {
-        HIP_CHECK(hipHostMalloc(&buf[b], kStageBytes, hipHostMallocDefault));
+        buf[b] = aligned_alloc(4096, kStageBytes);
+        FAISS_THROW_IF_NOT_MSG(buf[b], "staging allocation failed");
+        HIP_CHECK(hipHostRegister(buf[b], kStageBytes, hipHostRegisterDefault));
         HIP_CHECK(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming));
     }
     cap = kStageBytes;
@@ -121,7 +135,7 @@ void HostStaging::upload_rows(float* dst, int ld, const float* x, int d, int64_t
     if (n <= 0) return;
     // pinned queries go straight to the DMA engine; small pageable ones are
     // staged by HIP itself
-    if ((size_t)n * row <= ((size_t)64 << 10) || host_pinned(x)) {
+    if ((size_t)n * row <= ((size_t)64 << 10) || !staging_enabled() || host_pinned(x)) {
         HIP_CHECK(hipMemcpy2DAsync(dst, sizeof(float) * ld, x, row, row, n,
                                    hipMemcpyHostToDevice, s));
         return;
@@ -141,7 +155,7 @@ void HostStaging::upload_rows(float* dst, int ld, const float* x, int d, int64_t
 }
 void HostStaging::download(void* dst, const void* src, size_t bytes, hipStream_t s) {
     if (!bytes) return;
-    if (host_pinned(dst)) {
+    if (!staging_enabled() || host_pinned(dst)) {
         HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
         return;

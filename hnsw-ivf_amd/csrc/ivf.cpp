@@ -449,6 +449,19 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
                                (long long)key, nlist);
         a32[i] = (int32_t)(key < 0 ? -1 : key);
     }
+    // a caller-supplied assignment may name a list twice for one query; the
+    // reference then scans it twice and its heap holds each such vector twice
+    // (faiss/IndexIVF.cpp:595-631).  The exact scan reproduces that; the
+    // list-centric filter assumes distinct probes.
+    bool dup = false;
+    {
+        std::vector<int32_t> row((size_t)np);
+        for (idx_t q = 0; q < n && !dup; q++) {
+            std::copy(a32.begin() + q * np, a32.begin() + (q + 1) * np, row.begin());
+            std::sort(row.begin(), row.end());
+            for (size_t j = 1; j < np && !dup; j++) dup = row[j] >= 0 && row[j] == row[j - 1];
+        }
+    }
     DevGuard dg(device);
     sync_device();
     hipStream_t s = stream();
@@ -487,8 +500,14 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
     const uint32_t* lim = nullptr;
     const int32_t* asg = apply_max_codes(n, (int)np, ba.as<int32_t>(), mc, &lim, s);
     const uint8_t* selm = apply_selector(params, s);
+    struct ResetDup {
+        bool& f;
+        ~ResetDup() { f = false; }
+    } reset_dup{dup_probes_};
+    dup_probes_ = dup;
     search_preassigned_device(n, bx.as<float>(), ldx, k, (int)np, asg, bc.as<float>(),
                               bd.as<float>(), bi.as<idx_t>(), s, lim, selm, store_pairs);
+    dup_probes_ = false;
     qdone_ = nullptr;
     if (per_query_stats) kern::device_stamp(s_stamps_.as<unsigned long long>() + 1, s);
     hipEvent_t e1 = ev.mark(s);
@@ -718,7 +737,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     if (env && !strcmp(env, "exact")) mode = 1;
     if (env && !strcmp(env, "mfma")) mode = 0;
     const int KQ = obits_ <= 14 ? kern::ivf_mfma_kq((int)k, d, np) : 0;
-    if (mode != 0 || KQ <= 0 || np > kern::kMaxK || store_pairs) {
+    if (mode != 0 || KQ <= 0 || np > kern::kMaxK || store_pairs || dup_probes_) {
         exact_scan_device(n, x, ldx, k, np, assign, cdis, distances, labels, s, lim, sel,
                           store_pairs);
         return;
@@ -995,7 +1014,7 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
     // general exact scan, which serves every other geometry)
     const char* penv = getenv("FAISS_AMD_PQ_SCAN");
     const bool force_exact = penv && !strcmp(penv, "exact");
-    if (!force_exact && !store_pairs && pq_mfma_ready_ && metric_type == METRIC_L2 &&
+    if (!force_exact && !store_pairs && !dup_probes_ && pq_mfma_ready_ && metric_type == METRIC_L2 &&
         by_residual && kern::ivfpq_mfma_eligible(d, (int)pq.M, (int)k, np)) {
         std::lock_guard<std::recursive_mutex> g(mu_);
         const int QT = 64;

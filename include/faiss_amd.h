@@ -497,6 +497,9 @@ struct IndexIVF : Index {
     // (device clock, written by the kernel that emits a query's result),
     // null outside such a call
     mutable unsigned long long* qdone_ = nullptr;
+    // search_preassigned of a caller assignment naming a list twice for a
+    // query: the exact scan (the list-centric filter assumes distinct probes)
+    mutable bool dup_probes_ = false;
     mutable DeviceBuffer s_qdone_, s_stamps_;
     mutable DeviceBuffer s_as_, s_ad_, s_stats_, s_ilist_, s_idesc_, s_ient_, s_lim_, s_alim_,
             s_selmask_;

@@ -474,7 +474,10 @@ int faiss_amd_Index_search_device(
         idx_t* labels_dev,
         void* stream);
 /* search_preassigned with device pointers; assign_dev is int32 [n*nprobe]
- * (list numbers, -1 = skip), centroid_dis_dev f32 [n*nprobe] */
+ * (list numbers, -1 = skip), centroid_dis_dev f32 [n*nprobe].  A query's
+ * probes name distinct lists here (the coarse quantizer's output does); the
+ * host entry point faiss_IndexIVF_search_preassigned also accepts a list
+ * named twice and then returns the reference's duplicated entries. */
 int faiss_amd_IndexIVF_search_preassigned_device(
         const FaissIndexIVF* index,
         idx_t n,
