@@ -123,37 +123,10 @@ struct DeviceBuffer {
     T* as() const { return reinterpret_cast<T*>(ptr); }
 };
 
-// Pinned host staging of one device for the host-pointer entry points (the
-// role of faiss GPU's searchFromCpuPaged_, faiss/gpu/GpuIndex.cu:307-333):
-// two pinned buffers, one filled by the CPU while the other's DMA runs.  A
-// caller holds `mu` for the whole upload / search / download sequence.
-struct HostStaging {
-    std::mutex mu;
-    void* buf[2] = {nullptr, nullptr};
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    bool pend[2] = {false, false};  // ev[b] recorded since buf[b] was last free
-    size_t cap = 0;                 // bytes per buffer
-    HostStaging() = default;
-    HostStaging(const HostStaging&) = delete;
-    HostStaging& operator=(const HostStaging&) = delete;
-    ~HostStaging();
-    // n rows of d floats at x (host, row stride d) into dst (device, row
-    // stride ld floats), enqueued on s; returns once x may be reused
-    void upload_rows(float* dst, int ld, const float* x, int d, int64_t n, hipStream_t s);
-    // bytes at src (device) into dst (host) after the work queued on s
-    void download(void* dst, const void* src, size_t bytes, hipStream_t s);
-
-   private:
-    void ensure();
-    void wait(int b);
-};
-
-// Per-device resources: one non-blocking stream per device, created lazily,
-// and the pinned staging of the host entry points.
+// Per-device resources: one non-blocking stream per device, created lazily.
 struct DeviceContext {
     int device = 0;
     hipStream_t stream = nullptr;
-    HostStaging staging;
 };
 
 DeviceContext& device_context(int device);

@@ -575,10 +575,9 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
     bx.reserve(sizeof(float) * n * ldx);
     bd.reserve(sizeof(float) * n * k);
     bi.reserve(sizeof(idx_t) * n * k);
-    HostStaging& stg = device_context(device).staging;
-    std::lock_guard<std::mutex> sg(stg.mu);
     if (ldx != d) HIP_CHECK(hipMemsetAsync(bx.ptr, 0, sizeof(float) * n * ldx, s));
-    stg.upload_rows(bx.as<float>(), ldx, x, d, n, s);
+    HIP_CHECK(hipMemcpy2DAsync(bx.ptr, sizeof(float) * ldx, x, sizeof(float) * d,
+                               sizeof(float) * d, n, hipMemcpyHostToDevice, s));
     const idx_t qchunk = search_chunk(n, np, k);
     std::lock_guard<std::recursive_mutex> g(mu_);
     s_cd_.reserve(sizeof(float) * qchunk * np);
@@ -626,8 +625,8 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
                               lim, s_stats_.as<unsigned long long>(), s);
     }
     unsigned long long st[2];
-    stg.download(distances, bd.ptr, sizeof(float) * n * k, s);
-    stg.download(labels, bi.ptr, sizeof(idx_t) * n * k, s);
+    HIP_CHECK(hipMemcpyAsync(distances, bd.ptr, sizeof(float) * n * k, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(st, s_stats_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     quantizer->fold_device_stats();

@@ -306,6 +306,7 @@ def test_preassigned_duplicate_probes(amd, orc, gpu, desc, k):
     idx = amd.index_factory(d, f"IVF{nlist},{desc}")
     idx.train(xb)
     idx.add(xb)
+    idx.nprobe = np_  # search_preassigned reads nprobe columns of the assignment
     xq = rand(orc, nq, d, 82)
     Dq, Iq = idx.quantizer.search(xq, nlist)
     keys = np.repeat(Iq[:, :1], np_, axis=1)          # the nearest list, 8 times
