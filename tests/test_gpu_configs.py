@@ -8,6 +8,12 @@ tests/test_ref_fixtures.py).
       (quantizer geometry of c4; nb = 1M of its 10M, nq = 2000)
   c5  IVF65536,PQ48 d=96, nprobe 64 (one shard's geometry; nb = 2M of the
       12.5M of an 8-GPU shard, nq = 2000)
+and at their real sizes (the bench's batches searched whole on the GPU, a
+subset of the queries re-derived by the oracle):
+  c4  10M vectors, the 10k-query batch, efSearch 64 (400 queries checked)
+  c5  one 12.5M-vector shard of the 100M set (ids == 0 mod 8, as bench.py
+      --shard-of 8), the 100k-query batch (400 queries checked): ~190 rows
+      per list, the PQ filter's long-list work items at full length
 Ids and distances must be equal bit for bit (data: faiss float_rand streams,
 xb seed 1234, xq seed 5678, as bench.py).
 """
@@ -82,3 +88,45 @@ def test_c5_ivf65536_pq48_shard(amd, orc, gpu):
     ref = orc.IVFOracle.from_index(idx)
     Dr, Ir, _, _ = ref.search(xq, 10, 64, nslices=1)
     check(D, I, Dr, Ir, "c5")
+
+
+def check_subset(D, I, Dr, Ir, rows, what):
+    check(D[rows], I[rows], Dr, Ir, what)
+
+
+def test_c4_full_10m(amd, orc, gpu):
+    d, nb, nq = 128, 10_000_000, 10_000
+    idx = amd.index_factory(d, "IVF16384_HNSW32,Flat")
+    xt = amd.float_rand_rows(nb, d, 1234, 0, 1, 638_976)
+    idx.train(xt)
+    del xt
+    for c0 in range(0, nb, 2_000_000):
+        idx.add(amd.float_rand_rows(nb, d, 1234, c0, 1, 2_000_000))
+    idx.nprobe = 64
+    amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", 64)
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    D, I = idx.search(xq, 10)
+    rows = np.arange(0, nq, nq // 400)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(np.ascontiguousarray(xq[rows]), 10, 64, efSearch=64, nslices=1)
+    check_subset(D, I, Dr, Ir, rows, "c4 10M efSearch 64")
+
+
+def test_c5_full_shard(amd, orc, gpu):
+    d, nb, nshard, nq = 96, 100_000_000, 8, 100_000
+    idx = amd.index_factory(d, "IVF65536,PQ48")
+    xt = amd.float_rand_rows(nb, d, 1234, 0, 1, 65536 * 16)
+    idx.train(xt)
+    del xt
+    ids = np.arange(0, nb, nshard, dtype=np.int64)
+    for c0 in range(0, len(ids), 2_500_000):
+        cid = ids[c0:c0 + 2_500_000]
+        idx.add_with_ids(amd.float_rand_rows(nb, d, 1234, c0 * nshard, nshard, len(cid)), cid)
+    assert idx.ntotal == 12_500_000
+    idx.nprobe = 64
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    D, I = idx.search(xq, 10)
+    rows = np.arange(0, nq, nq // 400)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(np.ascontiguousarray(xq[rows]), 10, 64, nslices=1)
+    check_subset(D, I, Dr, Ir, rows, "c5 12.5M shard")
