@@ -85,50 +85,47 @@ double ivfpq_mfma_coef(int d, int M) {
     return 1.02 / 65536.0 + (4.0 * d + 2.0 * M + 64.0) * u;
 }
 
-// A fragment of one lane: row `cw` (its code words), dims [16 s + 8 lh, +8)
-// decoded from the LDS table (8 / DSUB entries of DSUB bf16 each).
-template <int DSUB, int NS, int NWC>
-__device__ __forceinline__ void pq_decode_frags(const uint32_t (&cw)[NWC], int lh,
-                                                const uint8_t* __restrict__ dec,
-                                                bf16x8 (&ah)[NS]) {
+// A fragment of one lane for k-step s: row `cw` (its code words), dims
+// [16 s + 8 lh, +8) decoded from the LDS table (8 / DSUB entries of DSUB
+// bf16 each).  Decoded one k-step at a time, just before its MFMAs, so only
+// one fragment's gathers are live.
+template <int DSUB, int NWC>
+__device__ __forceinline__ bf16x8 pq_decode_frag(const uint32_t (&cw)[NWC], int lh,
+                                                 const uint8_t* __restrict__ dec, int s) {
     constexpr int E = 8 / DSUB;  // subquantizers per fragment
+    uint32_t w32[4];
 #pragma unroll
-    for (int s = 0; s < NS; s++) {
-        // subquantizers m0 .. m0 + E - 1, m0 = (16 s + 8 lh) / DSUB
-        uint32_t w32[4];
-#pragma unroll
-        for (int u = 0; u < E; u++) {
-            // byte m of the code, m = (16 s) / DSUB + lh * E + u
-            const int mb = (16 * s) / DSUB + u;  // compile-time part
-            const int m_lo = mb, m_hi = mb + E;  // lh = 0 / 1
-            const uint32_t wl = cw[m_lo >> 2], wh = cw[m_hi >> 2];
-            const uint32_t blo = (wl >> (8 * (m_lo & 3))) & 0xffu;
-            const uint32_t bhi = (wh >> (8 * (m_hi & 3))) & 0xffu;
-            const uint32_t j = lh ? bhi : blo;
-            const int m = lh ? m_hi : m_lo;
-            const uint8_t* src = dec + ((size_t)m * 256 + j) * (2 * DSUB);
-            if constexpr (DSUB == 2) {
-                w32[u] = *(const uint32_t*)src;
-            } else if constexpr (DSUB == 4) {
-                const uint2 v = *(const uint2*)src;
-                w32[2 * u] = v.x;
-                w32[2 * u + 1] = v.y;
-            } else {
-                const uint4 v = *(const uint4*)src;
-                w32[0] = v.x;
-                w32[1] = v.y;
-                w32[2] = v.z;
-                w32[3] = v.w;
-            }
+    for (int u = 0; u < E; u++) {
+        // byte m of the code, m = (16 s) / DSUB + lh * E + u
+        const int mb = (16 * s) / DSUB + u;  // compile-time part
+        const int m_lo = mb, m_hi = mb + E;  // lh = 0 / 1
+        const uint32_t wl = cw[m_lo >> 2], wh = cw[m_hi >> 2];
+        const uint32_t blo = (wl >> (8 * (m_lo & 3))) & 0xffu;
+        const uint32_t bhi = (wh >> (8 * (m_hi & 3))) & 0xffu;
+        const uint32_t j = lh ? bhi : blo;
+        const int m = lh ? m_hi : m_lo;
+        const uint8_t* src = dec + ((size_t)m * 256 + j) * (2 * DSUB);
+        if constexpr (DSUB == 2) {
+            w32[u] = *(const uint32_t*)src;
+        } else if constexpr (DSUB == 4) {
+            const uint2 v = *(const uint2*)src;
+            w32[2 * u] = v.x;
+            w32[2 * u + 1] = v.y;
+        } else {
+            const uint4 v = *(const uint4*)src;
+            w32[0] = v.x;
+            w32[1] = v.y;
+            w32[2] = v.z;
+            w32[3] = v.w;
         }
-        union {
-            uint32_t w[4];
-            bf16x8 v;
-        } cv;
-#pragma unroll
-        for (int i = 0; i < 4; i++) cv.w[i] = w32[i];
-        ah[s] = cv.v;
     }
+    union {
+        uint32_t w[4];
+        bf16x8 v;
+    } cv;
+#pragma unroll
+    for (int i = 0; i < 4; i++) cv.w[i] = w32[i];
+    return cv.v;
 }
 
 // One work item = (list, <= 64 queries); persistent work-groups walk the
@@ -136,7 +133,7 @@ __device__ __forceinline__ void pq_decode_frags(const uint32_t (&cw)[NWC], int l
 // work-group.  Wave layout, keys, streams and outputs as k_ivf_bf3_filter.
 // HS: an IDSelector mask is present (own instantiation; none on the hot path)
 template <int DSUB, int NS, int KT, bool HS>
-__global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
+__global__ __launch_bounds__(256, 3) void k_ivfpq_filter(
         const float* __restrict__ x, int ldx, const __bf16* __restrict__ dec_g,
         const uint8_t* __restrict__ codes, const float* __restrict__ terms,
         const float* __restrict__ cdis, const float* __restrict__ cnorm,
@@ -152,8 +149,6 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
     constexpr int NWC = CS / 4;
     extern __shared__ __attribute__((aligned(16))) uint8_t dec[];  // [M][256][DSUB] bf16
     __shared__ __attribute__((aligned(16))) float ynt[2][BV];      // term per row (+inf pad)
-    __shared__ uint32_t ent_s[BQ];
-    __shared__ int32_t qrow_s[BQ];
     __shared__ float bnd_s[BQ][4];
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -162,6 +157,7 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
         const uint4* src = (const uint4*)dec_g;
         for (int i = t; i < NW16; i += 256) ((uint4*)dec)[i] = src[i];
     }
+    __syncthreads();  // the decode table
     const int bi = w >> 1, bj = w & 1;
     const int li = lane & 31, lh = lane >> 5;
     const int slot = 2 * bi + lh;
@@ -169,19 +165,43 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
     const uint32_t lowmask = (1u << obits) - 1u;
     const uint32_t nitems = item_off[nlist];
 
-    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
-        const ItemDesc dsc = item_desc[it];
-        const uint32_t e_raw = t < BQ ? item_entries[(size_t)it * BQ + t] : 0u;
+    // Every global load is consumed one step after it is issued, so its
+    // latency hides under other work: the next item's descriptor and this
+    // lane's entry of it load while the current item runs, a tile's codes
+    // and terms load while the previous tile is multiplied (the terms are
+    // masked when they are stored, not when they arrive).
+    uint32_t it = blockIdx.x;
+    ItemDesc dsc{};
+    uint32_t my_e = 0u;
+    if (it < nitems) {
+        dsc = item_desc[it];
+        my_e = item_entries[(size_t)it * BQ + qloc];
+    }
+    for (; it < nitems; it += gridDim.x) {
+        const uint32_t itn = it + gridDim.x;
+        ItemDesc dscn{};
+        uint32_t my_en = 0u;
+        if (itn < nitems) {
+            dscn = item_desc[itn];
+            my_en = item_entries[(size_t)itn * BQ + qloc];
+        }
         const int l = (int)dsc.l;
         const int nQ = (int)dsc.nq;
         const int len = (int)dsc.len;
         const int64_t row0 = dsc.off;
-        if (t < BQ) {
-            const uint32_t e = t < nQ ? e_raw : 0u;
-            ent_s[t] = e;
-            qrow_s[t] = t < nQ ? (int32_t)(e / (uint32_t)nprobe) : -1;
+        const bool qvalid = qloc < nQ;
+        const bool active = 32 * bj < nQ;  // wave-uniform
+        // query fragments and coarse distance of this lane's column
+        bf16x8 bh[NS], bl[NS];
+        float xn = 0.f, base = 0.f;
+        if (active) {
+            const int32_t qr = qvalid ? (int32_t)(my_e / (uint32_t)nprobe) : -1;
+            // fragments prepared once per query (k_query_prep; the host always
+            // passes the image)
+            load_query_image<NS>(qimg, qxn, qr, lh, bh, bl, xn);
+            base = cdis[qvalid ? my_e : 0u];
         }
-        // first tile: this lane's code row and the tile's terms
+        // this lane's code row of a tile and the tile's terms (raw)
         uint32_t cw[NWC];
         auto load_codes = [&](int v0n) {
             const int r = v0n + 32 * bi + li;
@@ -200,82 +220,78 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
                 for (int i = 0; i < NWC; i++) cw[i] = *(const uint32_t*)(cp + 4 * i);
             }
         };
-        float4 tn = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 traw = make_float4(0.f, 0.f, 0.f, 0.f);
+        uchar4 mraw = make_uchar4(1, 1, 1, 1);
         auto load_terms = [&](int v0n) {
             if (t < BV / 4) {
                 const int r = 4 * t;
                 const int nvn = min(BV, len - v0n);
                 // rows < roundup(len, 16) are inside the list's arena slot
-                const float4 v = r < nvn ? *(const float4*)(terms + row0 + v0n + r)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (r < nvn) {
+                    traw = *(const float4*)(terms + row0 + v0n + r);
+                    if constexpr (HS) mraw = *(const uchar4*)(sel + row0 + v0n + r);
+                }
+            }
+        };
+        auto store_terms = [&](int buf, int v0n) {
+            if (t < BV / 4) {
+                const int r = 4 * t;
+                const int nvn = min(BV, len - v0n);
+                float4 tn;
                 if constexpr (HS) {
                     // non-members of an IDSelector are treated as padding rows
-                    uchar4 ms = make_uchar4(1, 1, 1, 1);
-                    if (r < nvn) ms = *(const uchar4*)(sel + row0 + v0n + r);
-                    tn.x = r + 0 < nvn && ms.x ? v.x : WS_INF;
-                    tn.y = r + 1 < nvn && ms.y ? v.y : WS_INF;
-                    tn.z = r + 2 < nvn && ms.z ? v.z : WS_INF;
-                    tn.w = r + 3 < nvn && ms.w ? v.w : WS_INF;
+                    tn.x = r + 0 < nvn && mraw.x ? traw.x : WS_INF;
+                    tn.y = r + 1 < nvn && mraw.y ? traw.y : WS_INF;
+                    tn.z = r + 2 < nvn && mraw.z ? traw.z : WS_INF;
+                    tn.w = r + 3 < nvn && mraw.w ? traw.w : WS_INF;
                 } else {
-                    tn.x = r + 0 < nvn ? v.x : WS_INF;
-                    tn.y = r + 1 < nvn ? v.y : WS_INF;
-                    tn.z = r + 2 < nvn ? v.z : WS_INF;
-                    tn.w = r + 3 < nvn ? v.w : WS_INF;
+                    tn.x = r + 0 < nvn ? traw.x : WS_INF;
+                    tn.y = r + 1 < nvn ? traw.y : WS_INF;
+                    tn.z = r + 2 < nvn ? traw.z : WS_INF;
+                    tn.w = r + 3 < nvn ? traw.w : WS_INF;
                 }
+                *(float4*)(&ynt[buf][4 * t]) = tn;
             }
         };
         load_codes(0);
         load_terms(0);
-        __syncthreads();  // ent_s / qrow_s (and, first time, the decode table)
-
-        const bool active = 32 * bj < nQ;
-        bf16x8 bh[NS], bl[NS];
-        float xn = 0.f, base = 0.f;
-        if (active) {
-            if (qimg)  // fragments prepared once per query (k_query_prep)
-                load_query_image<NS>(qimg, qxn, qrow_s[qloc], lh, bh, bl, xn);
-            else
-                load_query_frags<NS>(x, ldx, D, qrow_s[qloc], lh, bh, bl, xn);
-            base = cdis[ent_s[qloc]];
-        }
         ThreadQueue32<KT> tq;
         tq.init();
         for (int v0 = 0, tile = 0; v0 < len; v0 += BV, tile++) {
             const int buf = tile & 1;
-            if (t < BV / 4) *(float4*)(&ynt[buf][4 * t]) = tn;
-            bf16x8 ah[NS];
-            if (active) pq_decode_frags<DSUB, NS, NWC>(cw, lh, dec, ah);
-            if (v0 + BV < len) {
-                load_codes(v0 + BV);
-                load_terms(v0 + BV);
-            }
-            __syncthreads();
+            const bool more = v0 + BV < len;
+            store_terms(buf, v0);
+            if (more) load_terms(v0 + BV);
+            __syncthreads();  // ynt[buf]
             if (active) {
-                float4 yq[4];
-#pragma unroll
-                for (int g = 0; g < 4; g++)
-                    yq[g] = *(const float4*)(&ynt[buf][32 * bi + 4 * lh + 8 * g]);
                 floatx16 acc;
 #pragma unroll
                 for (int r = 0; r < 16; r++) acc[r] = 0.f;
 #pragma unroll
                 for (int s = 0; s < NS; s++) {
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
+                    const bf16x8 ah = pq_decode_frag<DSUB, NWC>(cw, lh, dec, s);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
                 }
+                // the next tile's code words load under this tile's MFMAs and
+                // pushes (cw is decoded)
+                if (more) load_codes(v0 + BV);
                 const uint32_t ordbase = (uint32_t)tile << 4;
 #pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int g = r >> 2, c = r & 3;
-                    const float yv = c == 0 ? yq[g].x : c == 1 ? yq[g].y : c == 2 ? yq[g].z : yq[g].w;
-                    const float a = fmaf(-2.f, acc[r], base + yv);
-                    tq.push(key_encode<true>(a, lowmask, ordbase | (uint32_t)r));
+                for (int g = 0; g < 4; g++) {
+                    const float4 yq = *(const float4*)(&ynt[buf][32 * bi + 4 * lh + 8 * g]);
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const int r = 4 * g + c;
+                        const float yv = c == 0 ? yq.x : c == 1 ? yq.y : c == 2 ? yq.z : yq.w;
+                        const float a = fmaf(-2.f, acc[r], base + yv);
+                        tq.push(key_encode<true>(a, lowmask, ordbase | (uint32_t)r));
+                    }
                 }
             }
         }
 
         // ---- outputs (as k_ivf_bf3_filter)
-        const bool qvalid = qloc < nQ;
         const uint32_t last = tq.q[KT - 1];
         float bnd = WS_INF;
         if (last != 0xffffffffu) {
@@ -285,7 +301,7 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
         bnd_s[qloc][slot] = bnd;
         __syncthreads();
         if (qvalid) {
-            const int64_t e = ent_s[qloc];
+            const int64_t e = my_e;
             const uint32_t elen = lim ? min((uint32_t)len, lim[e]) : (uint32_t)len;
             uint32_t* ko = keys + e * (4 * KT) + slot * KT;
 #pragma unroll
@@ -315,7 +331,9 @@ __global__ __launch_bounds__(256, 2) void k_ivfpq_filter(
                 recs[e] = pr;
             }
         }
-        __syncthreads();  // ent_s / bnd_s / ynt are reused by the next item
+        __syncthreads();  // bnd_s / ynt are reused by the next item
+        dsc = dscn;
+        my_e = my_en;
     }
 }
 
@@ -333,6 +351,7 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
                   int* kt_out, hipStream_t s, const void* qimg, const float* qxn) {
     FAISS_THROW_IF_NOT(ivfpq_mfma_eligible(d, M, k, nprobe));
     FAISS_THROW_IF_NOT(b.item_desc && b.item_entries);
+    FAISS_THROW_IF_NOT_MSG(qimg && qxn, "ivfpq_filter needs the prepared query image");
     FAISS_THROW_IF_NOT(obits >= 4 && obits <= 14);
     const int KE = ivf_mfma_kq(k, d, nprobe);
     FAISS_THROW_IF_NOT(KE > 0);
