@@ -298,19 +298,24 @@ def test_ivf_many_lists_bucketing(amd, orc, gpu):
 @pytest.mark.parametrize("k", [10, 100])
 def test_preassigned_duplicate_probes(amd, orc, gpu, desc, k):
     """A caller-supplied assignment may name a list more than once; the
-    reference then scans it once per probe (faiss/IndexIVF.cpp:595-631).
-    Every probe naming the same list makes a query's candidates outnumber the
-    arena's rows (the exact path's per-query slot must still hold them)."""
-    d, nb, nlist, nq, np_ = 16, 1200, 4, 40, 8
-    xb = rand(orc, nb, d, 81)
+    reference then scans it once per probe (faiss/IndexIVF.cpp:595-631) and
+    its heap holds such vectors more than once.  One list holds most of the
+    base, so a query whose probes all name it has more candidates than the
+    arena has rows (the exact path's per-query slot must still hold them)."""
+    d, nlist, nq, np_ = 16, 8, 40, 8
+    xt = rand(orc, 2000, d, 81)
     idx = amd.index_factory(d, f"IVF{nlist},{desc}")
-    idx.train(xb)
+    idx.train(xt)
+    crowd = xt[:1] + 0.01 * rand(orc, 2500, d, 83)   # ~2500 rows in one list
+    xb = np.ascontiguousarray(np.concatenate([xt[:700], crowd]), np.float32)
     idx.add(xb)
-    idx.nprobe = np_  # search_preassigned reads nprobe columns of the assignment
+    idx.nprobe = np_  # search_preassigned reads nprobe (<= nlist) columns
     xq = rand(orc, nq, d, 82)
     Dq, Iq = idx.quantizer.search(xq, nlist)
-    keys = np.repeat(Iq[:, :1], np_, axis=1)          # the nearest list, 8 times
-    keys[nq // 2:, 1::2] = Iq[nq // 2:, 1:2]           # half the queries: two lists
+    big = int(np.argmax([idx.get_list_size(l) for l in range(nlist)]))
+    assert idx.get_list_size(big) * np_ > idx.ntotal
+    keys = np.full((nq, np_), big, dtype=np.int64)     # the crowded list, 8 times
+    keys[nq // 2:, 1::2] = Iq[nq // 2:, :1]             # half the queries: two lists
     by_list = np.empty_like(Dq)
     np.put_along_axis(by_list, Iq, Dq, axis=1)        # coarse distance of every list
     cdis = np.ascontiguousarray(np.take_along_axis(by_list, keys, axis=1), np.float32)
