@@ -30,6 +30,8 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 
 #include "bf3.h"
 #include "common.h"
@@ -337,6 +339,198 @@ __global__ __launch_bounds__(256, 3) void k_ivfpq_filter(
     }
 }
 
+// Wave-independent form (the default): the same work items, keys and probe
+// records, but every wave is its own worker with no barrier after the decode
+// table is loaded.  A task is (item, query half bj): one wave, 32 query
+// columns, both 32-row blocks of every tile (thread streams slot = 2 bi + lh
+// of its queries, as above).  Each wave loads its own rows' code words and
+// the tile's terms (through a wave-private LDS slot), keeps the next tile's
+// loads in flight under the current tile's MFMAs, and assembles each query's
+// probe record itself (the two lane halves of a column hold its 4 streams).
+// Work groups of WPB waves share one decode table, so a CU holds as many
+// workers as its registers allow instead of as many 4-wave groups as its LDS
+// holds tables; waves desynchronise and hide each other's load latency.
+template <int DSUB, int NS, int KT, bool HS>
+__global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
+        const __bf16* __restrict__ dec_g, const uint8_t* __restrict__ codes,
+        const float* __restrict__ terms, const float* __restrict__ cdis,
+        const float* __restrict__ cnorm, const float* __restrict__ lrmax,
+        const float* __restrict__ lRmax, int nlist, int nprobe, float coef, int obits,
+        const uint32_t* __restrict__ item_off, const ItemDesc* __restrict__ item_desc,
+        const uint32_t* __restrict__ item_entries, const uint32_t* __restrict__ lim,
+        const uint8_t* __restrict__ sel, uint32_t* __restrict__ keys,
+        ProbeRec* __restrict__ recs, const uint8_t* __restrict__ qimg,
+        const float* __restrict__ qxn) {
+    constexpr int D = 16 * NS;
+    constexpr int M = D / DSUB;
+    constexpr int CS = (M + 3) & ~3;  // code stride (bytes)
+    constexpr int NWC = CS / 4;
+    constexpr int TBL = M * 256 * DSUB * 2;  // decode table bytes
+    extern __shared__ __attribute__((aligned(16))) uint8_t dec[];  // table | per-wave terms
+    const int nthr = blockDim.x, wpb = nthr >> 6;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    {
+        const uint4* src = (const uint4*)dec_g;
+        for (int i = t; i < TBL / 16; i += nthr) ((uint4*)dec)[i] = src[i];
+    }
+    __syncthreads();  // the decode table (the only barrier)
+    float* ynt = (float*)(dec + TBL) + w * 2 * BV;  // this wave's [2][BV] terms
+    const int li = lane & 31, lh = lane >> 5;
+    const uint32_t lowmask = (1u << obits) - 1u;
+    const uint32_t nitems = item_off[nlist];
+    const uint32_t ntask = 2u * nitems;
+    const uint32_t stride = gridDim.x * (uint32_t)wpb;
+    for (uint32_t task = blockIdx.x * (uint32_t)wpb + (uint32_t)w; task < ntask; task += stride) {
+        const uint32_t it = task >> 1;
+        const int bj = (int)(task & 1u);
+        const ItemDesc dsc = item_desc[it];
+        const int nQ = (int)dsc.nq;
+        if (32 * bj >= nQ) continue;  // wave-uniform: an item of <= 32 queries
+        const int l = (int)dsc.l;
+        const int len = (int)dsc.len;
+        const int64_t row0 = dsc.off;
+        const int qloc = 32 * bj + li;
+        const bool qvalid = qloc < nQ;
+        const uint32_t my_e = item_entries[(size_t)it * BQ + qloc];
+        // list-level margin operands (uniform)
+        const float cn_l = cnorm[l], rmax_l = lrmax[l], Rmax_l = lRmax[l];
+        bf16x8 bh[NS], bl[NS];
+        float xn = 0.f;
+        load_query_image<NS>(qimg, qxn, qvalid ? (int32_t)(my_e / (uint32_t)nprobe) : -1, lh,
+                             bh, bl, xn);
+        const float base = cdis[qvalid ? my_e : 0u];
+        const uint32_t elen = (lim && qvalid) ? min((uint32_t)len, lim[my_e]) : (uint32_t)len;
+        // code words of this lane's two rows (li, 32 + li) of a tile
+        uint32_t cw[2][NWC];
+        auto load_codes = [&](int bi, int v0n) {
+            const int r = v0n + 32 * bi + li;
+            const uint8_t* cp = codes + (row0 + (r < len ? r : 0)) * CS;
+            if constexpr (CS % 16 == 0) {
+#pragma unroll
+                for (int i = 0; i < NWC; i += 4) {
+                    const uint4 v = *(const uint4*)(cp + 4 * i);
+                    cw[bi][i] = v.x;
+                    cw[bi][i + 1] = v.y;
+                    cw[bi][i + 2] = v.z;
+                    cw[bi][i + 3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < NWC; i++) cw[bi][i] = *(const uint32_t*)(cp + 4 * i);
+            }
+        };
+        // the tile's 64 terms: lanes 0..15 load a float4 each, stored masked
+        float4 traw = make_float4(0.f, 0.f, 0.f, 0.f);
+        uchar4 mraw = make_uchar4(1, 1, 1, 1);
+        auto load_terms = [&](int v0n) {
+            const int r = 4 * lane;
+            if (lane < BV / 4 && r < len - v0n) {
+                traw = *(const float4*)(terms + row0 + v0n + r);
+                if constexpr (HS) mraw = *(const uchar4*)(sel + row0 + v0n + r);
+            }
+        };
+        auto store_terms = [&](int buf, int v0n) {
+            if (lane < BV / 4) {
+                const int r = 4 * lane;
+                const int nvn = min(BV, len - v0n);
+                float4 tn;
+                if constexpr (HS) {
+                    // non-members of an IDSelector are treated as padding rows
+                    tn.x = r + 0 < nvn && mraw.x ? traw.x : WS_INF;
+                    tn.y = r + 1 < nvn && mraw.y ? traw.y : WS_INF;
+                    tn.z = r + 2 < nvn && mraw.z ? traw.z : WS_INF;
+                    tn.w = r + 3 < nvn && mraw.w ? traw.w : WS_INF;
+                } else {
+                    tn.x = r + 0 < nvn ? traw.x : WS_INF;
+                    tn.y = r + 1 < nvn ? traw.y : WS_INF;
+                    tn.z = r + 2 < nvn ? traw.z : WS_INF;
+                    tn.w = r + 3 < nvn ? traw.w : WS_INF;
+                }
+                *(float4*)(&ynt[buf * BV + r]) = tn;
+            }
+        };
+        load_codes(0, 0);
+        load_codes(1, 0);
+        load_terms(0);
+        ThreadQueue32<KT> tq[2];
+        tq[0].init();
+        tq[1].init();
+        for (int v0 = 0, tile = 0; v0 < len; v0 += BV, tile++) {
+            const int buf = tile & 1;
+            const bool more = v0 + BV < len;
+            store_terms(buf, v0);  // (wave-private: ordered by the wave's own lgkm waits)
+            if (more) load_terms(v0 + BV);
+            const uint32_t ordbase = (uint32_t)tile << 4;
+#pragma unroll
+            for (int bi = 0; bi < 2; bi++) {
+                floatx16 acc;
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[r] = 0.f;
+#pragma unroll
+                for (int s = 0; s < NS; s++) {
+                    const bf16x8 ah = pq_decode_frag<DSUB, NWC>(cw[bi], lh, dec, s);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
+                }
+                // block bi decoded: its next code words load under the pushes
+                if (more) load_codes(bi, v0 + BV);
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const float4 yq = *(const float4*)(&ynt[buf * BV + 32 * bi + 4 * lh + 8 * g]);
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const int r = 4 * g + c;
+                        const float yv = c == 0 ? yq.x : c == 1 ? yq.y : c == 2 ? yq.z : yq.w;
+                        const float a = fmaf(-2.f, acc[r], base + yv);
+                        tq[bi].push(key_encode<true>(a, lowmask, ordbase | (uint32_t)r));
+                    }
+                }
+            }
+        }
+        // ---- outputs: this lane's two streams (slot 2 bi + lh) of query qloc
+        const float xl = sqrtf(xn);
+        const float sr = xl + cn_l + Rmax_l;
+        const float mmax = 2.f * (2.f * xl * rmax_l + coef * sr * sr) + 1e-30f;
+        float pb[2];
+#pragma unroll
+        for (int bi = 0; bi < 2; bi++) {
+            const int slot = 2 * bi + lh;
+            const uint32_t last = tq[bi].q[KT - 1];
+            float bnd = WS_INF;
+            if (last != 0xffffffffu && (int)ivf_key_row(last, lowmask, slot) < len)
+                bnd = key_decode_lo<true>(last, lowmask);
+            pb[bi] = bnd < WS_INF ? bnd - mmax : WS_INF;
+            if (qvalid) {
+                uint32_t* ko = keys + (int64_t)my_e * (4 * KT) + slot * KT;
+#pragma unroll
+                for (int i = 0; i < KT; i++) {
+                    const uint32_t key = tq[bi].q[i];
+                    const uint32_t row = ivf_key_row(key, lowmask, slot);
+                    if constexpr (HS)
+                        ko[i] = (key != 0xffffffffu && row < elen && sel[row0 + row]) ? key
+                                                                                      : 0xffffffffu;
+                    else
+                        ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
+                }
+            }
+        }
+        // slots 1 and 3 live in the other lane half of the column
+        const float pb1 = __shfl_xor(pb[0], 32), pb3 = __shfl_xor(pb[1], 32);
+        if (qvalid && lh == 0) {
+            ProbeRec pr;
+            pr.pb[0] = pb[0];
+            pr.pb[1] = pb1;
+            pr.pb[2] = pb[1];
+            pr.pb[3] = pb3;
+            pr.mmax = mmax;
+            pr.off = (uint32_t)row0;
+            pr.len = elen;
+            pr.pad = (uint32_t)l;
+            recs[my_e] = pr;
+        }
+    }
+}
+
 bool ivfpq_mfma_eligible(int d, int M, int k, int nprobe) {
     if (d % 16 != 0 || M <= 0 || d % M != 0 || k > 32 || nprobe > 64) return false;
     const int dsub = d / M, NS = d / 16;
@@ -366,6 +560,39 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
     const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / (lds + 4096))));
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(max_items, (int64_t)ncu * per_cu));
     const float coef = (float)ivfpq_mfma_coef(d, M);
+    // wave-independent kernel (default; FAISS_AMD_PQ_FILTER=wg: the 4-wave
+    // work-group form): WPB waves per group sharing one table, as many groups
+    // per CU as the LDS holds, enough waves to reach 12 per CU
+    const char* fenv = getenv("FAISS_AMD_PQ_FILTER");
+    if (!(fenv && !strcmp(fenv, "wg"))) {
+        const size_t tbl = lds;
+        const int g_lds = std::max(1, (int)((160 * 1024) / (tbl + 8 * 2 * BV * 4 + 1024)));
+        const int wpb = std::min(6, std::max(4, (12 + g_lds - 1) / g_lds));  // waves per group
+        const int groups = std::min(g_lds, std::max(1, 12 / wpb));
+        const size_t ldsw = tbl + (size_t)wpb * 2 * BV * sizeof(float);
+        const int64_t ntask = 2 * max_items;
+        const int64_t gridw = std::max<int64_t>(
+                1, std::min<int64_t>(cdiv(ntask, wpb), (int64_t)ncu * groups));
+#define PQW(DS, NSV, KTV)                                                                      \
+    if (dsub == DS && NS == NSV && KE / 4 == KTV) {                                            \
+        auto kfn = b.sel ? k_ivfpq_filter_w<DS, NSV, KTV, true>                                \
+                         : k_ivfpq_filter_w<DS, NSV, KTV, false>;                               \
+        HIP_CHECK(hipFuncSetAttribute((const void*)kfn,                                        \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsw)); \
+        kfn<<<dim3((unsigned)gridw), dim3(64 * wpb), ldsw, s>>>(                               \
+                (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, nlist, nprobe,    \
+                coef, obits, b.item_off, b.item_desc, b.item_entries, b.lim, b.sel, keys,      \
+                recs, (const uint8_t*)qimg, qxn);                                              \
+        HIP_LAUNCH_CHECK();                                                                    \
+        return;                                                                                \
+    }
+#define PQW_KT(DS, NSV) PQW(DS, NSV, 2) PQW(DS, NSV, 4) PQW(DS, NSV, 8)
+#define PQW_NS(DS) PQW_KT(DS, 4) PQW_KT(DS, 6) PQW_KT(DS, 8)
+        PQW_NS(2) PQW_NS(4) PQW_NS(8)
+#undef PQW_NS
+#undef PQW_KT
+#undef PQW
+    }
 #define PQF(DS, NSV, KTV)                                                                      \
     if (dsub == DS && NS == NSV && KE / 4 == KTV) {                                            \
         auto kfn = b.sel ? k_ivfpq_filter<DS, NSV, KTV, true>                                  \
