@@ -1025,6 +1025,8 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         s_ent_.reserve(sizeof(uint32_t) * n * np);
         kern::IVFBuckets b{counts, s_boff_.as<uint32_t>(), s_ioff_.as<uint32_t>(),
                            s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
+        s_ictr_.reserve(16);
+        b.item_ctr = s_ictr_.as<uint32_t>();  // the PQ filter's work counter
         b.counts_next = counts_next;
         b.lim = lim;
         b.sel = sel;

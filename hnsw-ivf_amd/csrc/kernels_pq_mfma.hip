@@ -360,7 +360,7 @@ __global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
         const uint32_t* __restrict__ item_entries, const uint32_t* __restrict__ lim,
         const uint8_t* __restrict__ sel, uint32_t* __restrict__ keys,
         ProbeRec* __restrict__ recs, const uint8_t* __restrict__ qimg,
-        const float* __restrict__ qxn) {
+        const float* __restrict__ qxn, uint32_t* __restrict__ task_ctr) {
     constexpr int D = 16 * NS;
     constexpr int M = D / DSUB;
     constexpr int CS = (M + 3) & ~3;  // code stride (bytes)
@@ -379,13 +379,23 @@ __global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
     const uint32_t lowmask = (1u << obits) - 1u;
     const uint32_t nitems = item_off[nlist];
     const uint32_t ntask = 2u * nitems;
-    const uint32_t stride = gridDim.x * (uint32_t)wpb;
-    for (uint32_t task = blockIdx.x * (uint32_t)wpb + (uint32_t)w; task < ntask; task += stride) {
+    // the first task of every wave is static, later ones come from a work
+    // counter (zeroed by k_bucket_scan): lists differ in length, so a static
+    // stride leaves the waves that drew long lists running alone at the end
+    const uint32_t nstatic = gridDim.x * (uint32_t)wpb;
+    for (uint32_t task = blockIdx.x * (uint32_t)wpb + (uint32_t)w; task < ntask;) {
+        // the next task, fetched now so the atomic's latency hides under this one
+        uint32_t nxt = 0u;
+        if (lane == 0) nxt = nstatic + atomicAdd(task_ctr, 1u);
+        nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt);
         const uint32_t it = task >> 1;
         const int bj = (int)(task & 1u);
         const ItemDesc dsc = item_desc[it];
         const int nQ = (int)dsc.nq;
-        if (32 * bj >= nQ) continue;  // wave-uniform: an item of <= 32 queries
+        if (32 * bj >= nQ) {  // wave-uniform: an item of <= 32 queries
+            task = nxt;
+            continue;
+        }
         const int l = (int)dsc.l;
         const int len = (int)dsc.len;
         const int64_t row0 = dsc.off;
@@ -528,6 +538,7 @@ __global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
             pr.pad = (uint32_t)l;
             recs[my_e] = pr;
         }
+        task = nxt;
     }
 }
 
@@ -564,7 +575,7 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
     // work-group form): WPB waves per group sharing one table, as many groups
     // per CU as the LDS holds, enough waves to reach 12 per CU
     const char* fenv = getenv("FAISS_AMD_PQ_FILTER");
-    if (!(fenv && !strcmp(fenv, "wg"))) {
+    if (!(fenv && !strcmp(fenv, "wg")) && b.item_ctr) {
         const size_t tbl = lds;
         const int g_lds = std::max(1, (int)((160 * 1024) / (tbl + 8 * 2 * BV * 4 + 1024)));
         const int wpb = std::min(6, std::max(4, (12 + g_lds - 1) / g_lds));  // waves per group
@@ -582,7 +593,7 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
         kfn<<<dim3((unsigned)gridw), dim3(64 * wpb), ldsw, s>>>(                               \
                 (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, nlist, nprobe,    \
                 coef, obits, b.item_off, b.item_desc, b.item_entries, b.lim, b.sel, keys,      \
-                recs, (const uint8_t*)qimg, qxn);                                              \
+                recs, (const uint8_t*)qimg, qxn, b.item_ctr);                                  \
         HIP_LAUNCH_CHECK();                                                                    \
         return;                                                                                \
     }
