@@ -214,8 +214,12 @@ __device__ __forceinline__ void cwait_vmcnt() {  // s_waitcnt vmcnt(N) alone
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
+// Work groups per CU: the two tile buffers (2 x 64 x (4 DB + 16) bytes) fit
+// three times in the LDS up to DB = 96 (d <= 96), twice at DB = 128; the
+// register budget follows (three waves per SIMD need <= 168 VGPRs, which
+// KT = 16 queues do not leave).
 template <bool L2, int KT, int NS>
-__global__ __launch_bounds__(256, 2) void k_coarse_stream(
+__global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stream(
         const float* __restrict__ x, int ldx, int64_t n, int d, const uint8_t* __restrict__ cst,
         const float* __restrict__ xnorm, int nlist, int nsplit, int split_len, int nqb,
         float coef, const float* __restrict__ cnmax_p, int obits, uint32_t* __restrict__ keys,
@@ -755,7 +759,7 @@ CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k) {
         ncu = 256;
     (void)hipGetLastError();
     const int64_t nqb = (int64_t)cdiv((size_t)n, 128);
-    const int64_t slots = 2 * (int64_t)ncu;
+
     const bool big_image = coarse_stream_image_bytes(nlist, d) > ((size_t)4 << 20);
     int nsplit = 0, kt = 0, split_len = 0;
     double best = 0.0;
@@ -770,6 +774,9 @@ CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k) {
         const int sl = (int)roundup(cdiv((size_t)nlist, (size_t)ns), BV);
         const int nsp = (int)cdiv((size_t)nlist, (size_t)sl);
         if ((size_t)sl > ((size_t)BV << 10)) continue;  // ordinals: 4 + log2(tiles) <= 14 bits
+        // resident work groups (k_coarse_stream: 3 per CU for DB <= 96 and
+        // KT <= 8, else 2)
+        const int64_t slots = (bf3_db(d) <= 96 && kt1 <= 8 ? 3 : 2) * (int64_t)ncu;
         const int64_t rounds = (int64_t)cdiv((size_t)(nqb * nsp), (size_t)slots);
         double cost = (double)rounds * (double)cdiv((size_t)sl, BV) * (kt1 + 12);
         if (big_image && nsp % 8 != 0) cost *= 1.15;

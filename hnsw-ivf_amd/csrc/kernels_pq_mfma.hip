@@ -379,15 +379,11 @@ __global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
     const uint32_t lowmask = (1u << obits) - 1u;
     const uint32_t nitems = item_off[nlist];
     const uint32_t ntask = 2u * nitems;
-    // the first task of every wave is static, later ones come from a work
-    // counter (zeroed by k_bucket_scan): lists differ in length, so a static
-    // stride leaves the waves that drew long lists running alone at the end
     const uint32_t nstatic = gridDim.x * (uint32_t)wpb;
+    // (a work counter fetched one task ahead measured slower on c3: 204 vs
+    // 170 us, same-address atomics from every wave; tasks are strided)
     for (uint32_t task = blockIdx.x * (uint32_t)wpb + (uint32_t)w; task < ntask;) {
-        // the next task, fetched now so the atomic's latency hides under this one
-        uint32_t nxt = 0u;
-        if (lane == 0) nxt = nstatic + atomicAdd(task_ctr, 1u);
-        nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt);
+        const uint32_t nxt = task + nstatic;
         const uint32_t it = task >> 1;
         const int bj = (int)(task & 1u);
         const ItemDesc dsc = item_desc[it];
