@@ -250,6 +250,17 @@ void IndexIVF::sync_device() const {
                              hipMemcpyHostToDevice, s));
     HIP_CHECK(hipMemcpyAsync(d_list_len_.ptr, len.data(), sizeof(uint32_t) * nlist,
                              hipMemcpyHostToDevice, s));
+    {
+        // work items longest list first (kern::IVFBuckets::perm)
+        std::vector<uint32_t> perm(nlist);
+        for (size_t l = 0; l < nlist; l++) perm[l] = (uint32_t)l;
+        std::stable_sort(perm.begin(), perm.end(),
+                         [&](uint32_t a, uint32_t b) { return len[a] > len[b]; });
+        d_list_perm_.reserve(sizeof(uint32_t) * std::max<size_t>(nlist, 1));
+        HIP_CHECK(hipMemcpyAsync(d_list_perm_.ptr, perm.data(), sizeof(uint32_t) * nlist,
+                                 hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));  // perm is a host temporary
+    }
     upload_extra();
     HIP_CHECK(hipStreamSynchronize(s));
     dirty_ = false;
@@ -755,6 +766,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     b.counts_next = counts_next;
     b.lim = lim;
     b.sel = sel;
+    b.perm = d_list_perm_.as<uint32_t>();
     s_part_.reserve(sizeof(uint32_t) * n * np * KQ);  // raw filter keys
     s_pk2_.reserve(sizeof(kern::ProbeRec) * n * np);  // per-probe records
     b.mark_keys = s_part_.as<uint32_t>();
@@ -1030,6 +1042,7 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         b.counts_next = counts_next;
         b.lim = lim;
         b.sel = sel;
+        b.perm = d_list_perm_.as<uint32_t>();
         const int KE = kern::ivf_mfma_kq((int)k, d, np);
         s_pkeys_.reserve(sizeof(uint32_t) * n * np * KE);
         s_precs_.reserve(sizeof(kern::ProbeRec) * n * np);

@@ -123,6 +123,10 @@ struct IVFBuckets {
     uint32_t* entries;     // [n * nprobe], entry = q * nprobe + rank
     uint32_t* item_list = nullptr;  // [max_items]: list of each work item
     uint32_t* item_ctr = nullptr;   // [1]: zeroed by the scan (persistent filter's counter)
+    // optional: lists by decreasing length; work items are numbered in this
+    // order (longest first: the filters' launch order, so the long items do
+    // not start last and set the kernel's tail)
+    const uint32_t* perm = nullptr;
     // optional (MFMA filter path): per work item its descriptor and its
     // entries at a fixed stride of QT (so a work item's first loads do not
     // depend on each other)

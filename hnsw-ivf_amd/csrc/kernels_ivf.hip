@@ -98,7 +98,8 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
                                                       uint32_t* __restrict__ item_off,
                                                       uint32_t* __restrict__ item_list,
                                                       uint32_t* __restrict__ zero_next,
-                                                      uint32_t* __restrict__ item_ctr) {
+                                                      uint32_t* __restrict__ item_ctr,
+                                                      const uint32_t* __restrict__ perm) {
     __shared__ uint32_t wb[16], wi[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint32_t carry_b = 0, carry_i = 0;
@@ -159,6 +160,48 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
         bucket_off[nlist] = carry_b;
         item_off[nlist] = carry_i;
         if (item_ctr) *item_ctr = 0u;  // the persistent filter's work counter
+    }
+    if (!perm) return;
+    // items renumbered in perm order (bucket sizes from bucket_off: the counts
+    // are cleared)
+    __syncthreads();
+    carry_i = 0;
+    for (int c0 = 0; c0 < nlist; c0 += 4096) {
+        const int i0 = c0 + 4 * t;
+        uint32_t n[4], si = 0;
+        int ls[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            ls[j] = i0 + j < nlist ? (int)perm[i0 + j] : -1;
+            n[j] = ls[j] >= 0 ? (bucket_off[ls[j] + 1] - bucket_off[ls[j]] + QT - 1) / QT : 0u;
+            si += n[j];
+        }
+        uint32_t ii = si;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t vi = __shfl_up(ii, off);
+            if (lane >= off) ii += vi;
+        }
+        if (lane == 63) wi[w] = ii;
+        __syncthreads();
+        uint32_t pi = carry_i, ti = 0;
+#pragma unroll
+        for (int v = 0; v < 16; v++) {
+            pi += v < w ? wi[v] : 0u;
+            ti += wi[v];
+        }
+        __syncthreads();
+        uint32_t ri = pi + ii - si;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (ls[j] >= 0) {
+                item_off[ls[j]] = ri;
+                if (item_list)
+                    for (uint32_t i = 0; i < n[j]; i++) item_list[ri + i] = (uint32_t)ls[j];
+            }
+            ri += n[j];
+        }
+        carry_i += ti;
     }
 }
 
@@ -314,7 +357,7 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
         }
     }
     k_bucket_scan<<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off, b.item_off,
-                                                 b.item_list, b.counts_next, b.item_ctr);
+                                                 b.item_list, b.counts_next, b.item_ctr, b.perm);
     HIP_LAUNCH_CHECK();
     if (total > 0) {
         k_bucket_fill<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(

@@ -483,6 +483,7 @@ struct IndexIVF : Index {
     mutable std::recursive_mutex mu_;
     // arena
     mutable DeviceBuffer d_codes_, d_ids_, d_list_off_, d_list_len_, d_row_list_;
+    mutable DeviceBuffer d_list_perm_;  // lists by decreasing length (work-item order)
     mutable size_t arena_rows_ = 0;
     // scratch
     mutable DeviceBuffer s_ictr_;
