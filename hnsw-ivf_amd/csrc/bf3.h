@@ -80,6 +80,55 @@ __device__ __forceinline__ float key_decode_hi(uint32_t key, uint32_t lowmask) {
     return L2 ? __uint_as_float(key | lowmask) : unordered_f32(key | lowmask);
 }
 
+// Folded L2 keys (fold image, kernels.h split_bf16_stream): the filter's
+// accumulator is acc = <x, y> - (|x|^2 + |y|^2) / 2 = -approx / 2, and the key
+// is the raw bits of acc with the ordinal in the low bits (one v_bfi_b32).
+// Negative floats order by magnitude as unsigned integers, so these keys order
+// like the approx.  acc >= 0 (approx <= 0, a near-duplicate of the query) gives
+// a pattern below 0x80000000: it sorts before every negative one, and its
+// decode is 0 (clamped) for both bounds — a valid bracket, as the approx is
+// <= 0 and every distance is >= 0 — so no clamp is needed in the hot loop.  A
+// kept pattern below 0x80000000 makes the stream's dropped bound 0, which is
+// still a lower bound of everything it dropped.  The decode brackets the
+// approx whatever the ordinal: for negative patterns, clearing the low bits
+// shrinks the magnitude (lower bound), setting them grows it (upper bound).
+__device__ __forceinline__ uint32_t fold_key_bits(float acc) { return __float_as_uint(acc); }
+// The fold key is key_insert (an inline-asm v_bfi_b32) applied straight to
+// an MFMA result register.  The compiler's hazard recognizer does not see
+// inline-asm readers of an MFMA's destination, so the caller must put
+// mfma_read_guard() between the MFMA and the first key_insert: 16 wait states
+// (the compiler itself pads this read with s_nop 11, i.e. 12) behind a
+// scheduling fence.  (Plain C, (bits & ~lowmask) | ord, is hazard-safe but
+// compiles to v_and + v_or3: two VALU per candidate instead of one.)
+__device__ __forceinline__ void mfma_read_guard() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 15" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ float fold_decode_lo(uint32_t key, uint32_t lowmask) {
+    return fmaxf(-2.f * __uint_as_float(key & ~lowmask), 0.f);
+}
+__device__ __forceinline__ float fold_decode_hi(uint32_t key, uint32_t lowmask) {
+    return fmaxf(-2.f * __uint_as_float(key | lowmask), 0.f);
+}
+// key decode of the IVF-Flat filter keys, plain or folded (runtime flag)
+template <bool L2>
+__device__ __forceinline__ float ivf_decode_lo(uint32_t key, uint32_t lowmask, bool fold) {
+    return (L2 && fold) ? fold_decode_lo(key, lowmask) : key_decode_lo<L2>(key, lowmask);
+}
+template <bool L2>
+__device__ __forceinline__ float ivf_decode_hi(uint32_t key, uint32_t lowmask, bool fold) {
+    return (L2 && fold) ? fold_decode_hi(key, lowmask) : key_decode_hi<L2>(key, lowmask);
+}
+// v = h + m + l exactly (three round-to-nearest bf16 parts: the first
+// residual has <= 16 significant bits, the second <= 8)
+__device__ __forceinline__ void split3_bf16(float v, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)v;
+    const float r1 = v - (float)h;
+    m = (__bf16)r1;
+    l = (__bf16)(r1 - (float)m);
+}
+
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& l) {
 #pragma unroll
     for (int j = 0; j < 8; j++) {

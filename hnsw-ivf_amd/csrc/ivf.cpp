@@ -725,8 +725,13 @@ void IndexIVFFlat::upload_extra() const {
         // the streamed filter's image: bf16 hi + norm per row (2 DB + 16 bytes)
         const int DBs = kern::bf3_db_host(d) / 2 * 2;
         d_cbs_.reserve(std::max<size_t>(arena_rows_, 1) * (2 * (size_t)DBs + 16));
+        // L2: the norms enter the filter's MFMA as a bias k-step (fold image;
+        // FAISS_AMD_IVF_FOLD=0 keeps the fp32-norm tail and the fma epilogue)
+        const char* fenv = getenv("FAISS_AMD_IVF_FOLD");
+        fold_ = (metric_type == METRIC_L2 && !(fenv && !strcmp(fenv, "0"))) ? 1 : 0;
         kern::split_bf16_stream(d_codes_.as<float>(), arena_rows_, d, l, DBs,
-                                d_ynorm_.as<float>(), d_row_list_.as<uint32_t>(), d_cbs_.ptr, s);
+                                d_ynorm_.as<float>(), d_row_list_.as<uint32_t>(), d_cbs_.ptr, s,
+                                fold_);
         kern::ivf_list_ynmax(d_rres_.as<float>(), d_list_off_.as<uint32_t>(),
                              d_list_len_.as<uint32_t>(), (int)nlist, d_rmax_.as<float>(), s);
         size_t mx = 0;
@@ -800,7 +805,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
                              dbg ? s_flags_.as<uint32_t>() : nullptr, distances, labels, &ktimes,
                              s, kern::ARENA_ALIGN, d_cbs_.ptr,
                              qready ? const_cast<void*>(qready) : s_q_.ptr, qready != nullptr,
-                             qdone_);
+                             qdone_, fold_);
     if (dbg) {
         uint32_t st[4];
         HIP_CHECK(hipMemcpyAsync(st, s_flags_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));

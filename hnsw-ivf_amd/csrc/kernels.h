@@ -262,6 +262,7 @@ constexpr int BDM_HOST = 128;  // bf3.h BDM: max padded dim of the MFMA paths
 inline int bf3_db_host(int d) { return (d + 31) / 32 * 32; }  // ordinal bits of the 32-bit keys
 double ivf_bf3_coef(int d);                // margin coefficient
 double ivf_bf2_coef(int d);
+double ivf_bf2f_coef(int d);  // bf16x2 with the norms folded into the MFMA (fold image)
 // |y - bf16(y)| per row (bf16x2 filter margins)
 void row_resnorm_bf16(const float* codes, int64_t rows, int d, int ldc, float* out,
                       hipStream_t s);
@@ -279,11 +280,18 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         float* D, int64_t* I, KernelTimes* kt, hipStream_t s,
                         int list_align = 16, const void* cbs = nullptr,
                         void* qscratch = nullptr,  // query_image_bytes(n, d) + 4 n bytes
-                        bool qready = false, unsigned long long* qdone = nullptr);      // qscratch already holds x's image
+                        bool qready = false,  // qscratch already holds x's image
+                        unsigned long long* qdone = nullptr,
+                        int fold = 0);  // cbs is the fold image (split_bf16_stream fold = 1)
 // stream image of the arena for the streamed filter: per row bf16(code) (DB
-// dims) + fp32 norm (+inf for padding rows) + 12 zero bytes = 2 DB + 16 bytes
+// dims) + a 16-byte tail = 2 DB + 16 bytes.  fold = 0: the tail is the fp32
+// norm (+inf for padding rows) + 12 zero bytes; fold = 1 (L2): the tail is the
+// row's bias A-fragment {bf16 split of -|y|^2/2 in three parts, 1, 1, 1, 0, 0}
+// (padding rows: -inf, 0, 0, 1, 1, 1, 0, 0), so one extra MFMA k-step adds
+// -(|x|^2 + |y|^2)/2 to <x, y> and the accumulator is -approx/2 directly.
 void split_bf16_stream(const float* codes, int64_t rows, int d, int ldc, int DB,
-                       const float* ynorm, const uint32_t* row_list, void* out, hipStream_t s);
+                       const float* ynorm, const uint32_t* row_list, void* out, hipStream_t s,
+                       int fold = 0);
 // ---------------- IVF-PQ ----------------
 // term[v] = sum_m (||c_{m,code}||^2 + 2 <yC_m, c_{m,code}>) for every arena row
 void ivfpq_terms(const uint8_t* codes, const uint32_t* row_list, int64_t nrows,

@@ -345,7 +345,13 @@ __device__ __forceinline__ void wait_lgkmcnt0() {  // s_waitcnt lgkmcnt(0) alone
     __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
 }
 
-template <bool L2, int KT, int NS, bool PIPE>
+// FOLD (L2, fold image): the row and query norms enter the MFMA as a ninth
+// k-step (A = the row's tail {-|y|^2/2 in three bf16 parts, 1, 1, 1, 0, 0},
+// B = {1, 1, 1, -|x|^2/2 in three parts, 0, 0}; lanes lh = 1 multiply code
+// bytes by zero), so the accumulator is -approx/2 and a candidate's key is
+// min + bfi instead of add + fma + max + bfi, with no norm reads from LDS
+// (fold_key_bits; margin coefficient ivf_bf2f_coef).
+template <bool L2, int KT, int NS, bool PIPE, bool FOLD = false>
 __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
         const float* __restrict__ x, int ldx, int d, const uint8_t* __restrict__ cbs,
         const float* __restrict__ ynmax, const float* __restrict__ rmax, int nprobe, float coef,
@@ -366,6 +372,7 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
     constexpr int G3 = NG / 4;
     constexpr int NB = 2;
     static_assert(FQ * 4 * 4 <= TB, "bounds fit in a tile buffer");
+    static_assert(!(FOLD && (PIPE || !L2)), "fold: L2, sequential form");
     // all LDS in one array (a second __shared__ object can make hipcc wait
     // vmcnt(0) before the tile reads): 2 tiles; after the loop tile buffer 0
     // holds the bounds [FQ][4].
@@ -433,6 +440,21 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
             load_query_image<NS>(qimg, qxn, qr, lh, bh, bl, xn);
         else
             load_query_frags<NS>(x, ldx, d, qr, lh, bh, bl, xn);
+    }
+    // FOLD: the bias B fragment {1, 1, 1, -|x|^2/2 in three parts, 0, 0} (lh = 0)
+    bf16x8 bq;
+    if constexpr (FOLD) {
+        __bf16 h, m, lo;
+        split3_bf16(-0.5f * xn, h, m, lo);
+        const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
+        bq[0] = lh ? zero : one;
+        bq[1] = lh ? zero : one;
+        bq[2] = lh ? zero : one;
+        bq[3] = lh ? zero : h;
+        bq[4] = lh ? zero : m;
+        bq[5] = lh ? zero : lo;
+        bq[6] = zero;
+        bq[7] = zero;
     }
 
     ThreadQueue32<KT> tq[2];
@@ -539,6 +561,17 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
                         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
                         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
                     }
+                    if constexpr (FOLD) {
+                        // the row's bias fragment (lh = 1: its code bytes, times 0)
+                        const bf16x8 ab = *(const bf16x8*)(T + (32 * bi + li) * SR + (lh ? 0 : 2 * DB));
+                        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, bq, acc, 0, 0, 0);
+                        mfma_read_guard();  // key_insert reads acc (inline asm)
+#pragma unroll
+                        for (int r = 0; r < 16; r++)
+                            tq[bi].push(key_insert(fold_key_bits(acc[r]), lowmask, ordbase | (uint32_t)r));
+                        __builtin_amdgcn_sched_barrier(0);
+                        continue;
+                    }
                     // this lane's 16 rows: 32 bi + 4 lh + 8 g + c (norm at byte 2 DB)
                     const uint8_t* nrow = T + (32 * bi + 4 * lh) * SR + 2 * DB;
 #pragma unroll
@@ -569,7 +602,7 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
             const uint32_t ord = last & lowmask;
             const int r = (int)(ord & 15u);
             const int row = (int)((ord >> 4) * BV) + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
-            if (row < len) bnd = key_decode_lo<L2>(last, lowmask);
+            if (row < len) bnd = FOLD ? fold_decode_lo(last, lowmask) : key_decode_lo<L2>(last, lowmask);
         }
         bnd_s[qloc * 4 + 2 * bi + lh] = bnd;
     }
@@ -622,7 +655,8 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
 // the fp32 norm (+inf for padding rows, row_list == ~0) and 12 zero bytes
 __global__ void k_split_stream(const float* __restrict__ codes, int64_t rows, int d, int ldc,
                                int DB, const float* __restrict__ ynorm,
-                               const uint32_t* __restrict__ row_list, uint8_t* __restrict__ out) {
+                               const uint32_t* __restrict__ row_list, uint8_t* __restrict__ out,
+                               int fold) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int per = DB + 8;  // bf16 slots per row (the last 8 = the 16-B tail)
     if (i >= rows * per) return;
@@ -632,6 +666,18 @@ __global__ void k_split_stream(const float* __restrict__ codes, int64_t rows, in
     if (j < DB) {
         const float v = j < d ? codes[r * ldc + j] : 0.f;
         ((__bf16*)row)[j] = (__bf16)v;
+    } else if (fold) {
+        // bias A-fragment {-|y|^2/2 in three bf16 parts, 1, 1, 1, 0, 0}
+        const int t = j - DB;
+        __bf16 v = (__bf16)0.f;
+        if (t < 3) {
+            __bf16 h = (__bf16)(-WS_INF), m = (__bf16)0.f, lo = (__bf16)0.f;
+            if (row_list[r] != 0xffffffffu) split3_bf16(-0.5f * ynorm[r], h, m, lo);
+            v = t == 0 ? h : t == 1 ? m : lo;
+        } else if (t < 6) {
+            v = (__bf16)1.f;
+        }
+        ((__bf16*)row)[j] = v;
     } else if (j == DB) {
         *(float*)(row + 2 * DB) = row_list[r] == 0xffffffffu ? WS_INF : ynorm[r];
     } else if (j > DB + 1) {
@@ -639,11 +685,12 @@ __global__ void k_split_stream(const float* __restrict__ codes, int64_t rows, in
     }
 }
 void split_bf16_stream(const float* codes, int64_t rows, int d, int ldc, int DB,
-                       const float* ynorm, const uint32_t* row_list, void* out, hipStream_t s) {
+                       const float* ynorm, const uint32_t* row_list, void* out, hipStream_t s,
+                       int fold) {
     if (rows <= 0) return;
     const int64_t tot = rows * (DB + 8);
     k_split_stream<<<dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, s>>>(
-            codes, rows, d, ldc, DB, ynorm, row_list, (uint8_t*)out);
+            codes, rows, d, ldc, DB, ynorm, row_list, (uint8_t*)out, fold);
     HIP_LAUNCH_CHECK();
 }
 
@@ -831,6 +878,7 @@ struct RerankStream {
     float my_d0;              // PQ: lane r: probe r's coarse distance
     PQArgs pa;
     const uint8_t* sel;       // IDSelector mask of the arena rows (nullptr: all)
+    bool fold;                // folded filter keys (ivf_decode_lo)
 
     __device__ __forceinline__ void emit(bool ok, uint32_t grow, int r, float& k1,
                                          long long& k2) const {
@@ -875,7 +923,7 @@ struct RerankStream {
             uint32_t grow = 0;
             if (c < E && !((fl >> sl) & 1u)) {
                 const uint32_t key = keys[c];
-                ok = key != 0xffffffffu && key_decode_lo<L2>(key, lowmask) - mr <= U;
+                ok = key != 0xffffffffu && ivf_decode_lo<L2>(key, lowmask, fold) - mr <= U;
                 grow = orr + ivf_key_row(key, lowmask, sl);
             }
             if (__ballot(ok) == 0ull) continue;
@@ -910,15 +958,19 @@ struct RerankStream {
     }
 };
 
+#ifndef RR_WAVES
+#define RR_WAVES 4  // waves per SIMD the re-rank is compiled for (tuning)
+#endif
 template <bool L2, int V, int PQD = 0>
-__global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
+__global__ __launch_bounds__(64 * RR_W, RR_WAVES) void k_ivf_rerank(
         const uint32_t* __restrict__ keys, const ProbeRec* __restrict__ recs,
         const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
         const int64_t* __restrict__ ids, int d, int64_t n, int nprobe, int KT, int obits, int k,
         float* __restrict__ D, int64_t* __restrict__ I, uint32_t* __restrict__ stats,
         unsigned long long* __restrict__ trace, PQArgs pa, const uint8_t* __restrict__ sel,
-        unsigned long long* __restrict__ qdone) {
+        unsigned long long* __restrict__ qdone, int fold_keys) {
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const bool fold = PQD == 0 && fold_keys != 0;
     __shared__ uint32_t surv[RR_W][RR_CAP];
     __shared__ uint16_t sprobe[RR_W][RR_CAP];
     __shared__ __attribute__((aligned(16))) float xsh[RR_W][BDM];
@@ -977,7 +1029,7 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
     float lmin = WS_INF;
 #pragma unroll
     for (int i = 0; i < V; i++) {
-        ub[i] = kv[i] != 0xffffffffu ? key_decode_hi<L2>(kv[i], lowmask) + lm : WS_INF;
+        ub[i] = kv[i] != 0xffffffffu ? ivf_decode_hi<L2>(kv[i], lowmask, fold) + lm : WS_INF;
         lmin = fminf(lmin, ub[i]);
     }
     float U;
@@ -1024,7 +1076,7 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
         bool sv = false;
         uint32_t grow = 0;
         if (kv[i] != 0xffffffffu && !((lfail >> sl) & 1u)) {
-            sv = key_decode_lo<L2>(kv[i], lowmask) - lm <= U;
+            sv = ivf_decode_lo<L2>(kv[i], lowmask, fold) - lm <= U;
             grow = loff + ivf_key_row(kv[i], lowmask, sl);
         }
         const unsigned long long m = __ballot(sv);
@@ -1088,6 +1140,7 @@ __global__ __launch_bounds__(64 * RR_W, 4) void k_ivf_rerank(
     st.my_d0 = my_d0;
     st.pa = pa;
     st.sel = sel;
+    st.fold = fold;
     // ---- round trip 2: candidate rows and ids; up to 4 batches are ranked
     // directly, anything else goes through the general resolve
     bool done = false;
@@ -1202,6 +1255,15 @@ double ivf_bf2_coef(int d) {
     const double u = 1.0 / 16777216.0;
     return 1.02 / 65536.0 + (6.1 * d + 8.0) * u;
 }
+// bf16x2 with the norms folded into the MFMA accumulation (fold image): the
+// accumulator sums 2 dp exact products and 6 exact bias products, |sum| <=
+// 2 (1 + 2^-8) sum|x_i y_i| + (|x|^2 + |y|^2) / 2 <= 1.51 (|x|^2 + |y|^2), so
+// its rounding is <= 1.51 (2 d + 6) u (|x|^2 + |y|^2), doubled by approx =
+// -2 acc; plus the norms' own roundings and the exact side, as above.
+double ivf_bf2f_coef(int d) {
+    const double u = 1.0 / 16777216.0;
+    return 1.02 / 65536.0 + (9.1 * d + 24.0) * u;
+}
 
 // |y - bf16(y)| per row (rounded up), the bf16x2 residual norms
 __global__ void k_row_resnorm(const float* __restrict__ codes, int64_t rows, int d, int ldc,
@@ -1241,7 +1303,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         int64_t max_items, uint32_t* keys, ProbeRec* recs, uint32_t* stats,
                         float* D, int64_t* I, KernelTimes* kt, hipStream_t s, int list_align,
                         const void* cbs, void* qscratch, bool qready,
-                        unsigned long long* qdone) {
+                        unsigned long long* qdone, int fold) {
     if (n <= 0) return;
     const bool aligned_lists = list_align % BV == 0 && cbs != nullptr;
     const int KE = ivf_mfma_kq(k, d, nprobe);
@@ -1276,7 +1338,10 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         HIP_CHECK(hipMemsetAsync(ftrace_buf, 0, 64 * grid, s));
         ftrace = ftrace_buf;
     }
-    const float coef = (float)(y3 ? ivf_bf3_coef(d) : ivf_bf2_coef(d));
+    // fold: the stream image carries bias fragments (L2 only; the streamed
+    // sequential kernel is the only reader of the image)
+    const bool fk = fold != 0 && l2 && aligned_lists && !y3 && !b.sel && d <= BDM;
+    const float coef = (float)(y3 ? ivf_bf3_coef(d) : fk ? ivf_bf2f_coef(d) : ivf_bf2_coef(d));
     // streamed (glds) bf16x2 filter: the default; the register-staged kernel
     // serves bf16x3, IDSelectors and the per-item trace
     // (FAISS_AMD_IVF_FILTER=staged forces it)
@@ -1288,7 +1353,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     // groups per CU, MFMAs of one block interleaved with the previous block's
     // selection)
     const char* penv = getenv("FAISS_AMD_IVF_PIPE");
-    const bool spipe = penv && !strcmp(penv, "1");
+    const bool spipe = penv && !strcmp(penv, "1") && !fk;
     // the streamed filter reads prepared query fragments: one k_query_prep
     // launch instead of every work item splitting its queries' fp32 rows
     const uint8_t* qimg = nullptr;
@@ -1304,6 +1369,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     do {                                                                                      \
         if (stream_ok)                                                                        \
             (spipe ? k_ivf_bf2_stream<L2V, KTV, NSV, true>                                   \
+             : fk  ? k_ivf_bf2_stream<L2V, KTV, NSV, false, L2V>                              \
                    : k_ivf_bf2_stream<L2V, KTV, NSV, false>)<<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const uint8_t*)cbs, ynmax, rmax, nprobe, coef, obits,         \
                     b.item_off, b.item_desc, b.item_entries, (uint32_t)max_items, nlist,      \
@@ -1340,6 +1406,25 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         if (l2) DISPATCH(LAUNCH_A, true);
         else DISPATCH(LAUNCH_A, false);
         HIP_LAUNCH_CHECK();
+        // FAISS_AMD_IVF_DUMP=<file>: the raw filter keys [n][nprobe][KE] and
+        // probe records [n][nprobe] of this call (debugging)
+        if (const char* dmp = getenv("FAISS_AMD_IVF_DUMP")) {
+            std::vector<uint32_t> hk((size_t)n * nprobe * KE);
+            std::vector<ProbeRec> hr((size_t)n * nprobe);
+            HIP_CHECK(hipMemcpyAsync(hk.data(), keys, 4 * hk.size(), hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipMemcpyAsync(hr.data(), recs, sizeof(ProbeRec) * hr.size(),
+                                     hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            const int SRB = 2 * bf3_db(d) + 16;  // stream-image row bytes
+            std::vector<uint8_t> hi(cbs ? 4 * (size_t)SRB : 0);
+            if (cbs) HIP_CHECK(hipMemcpy(hi.data(), cbs, hi.size(), hipMemcpyDeviceToHost));
+            if (FILE* f = fopen(dmp, "wb")) {
+                fwrite(hk.data(), 4, hk.size(), f);
+                fwrite(hr.data(), sizeof(ProbeRec), hr.size(), f);
+                fwrite(hi.data(), 1, hi.size(), f);
+                fclose(f);
+            }
+        }
         if (ftrace) {
             std::vector<unsigned long long> h(8 * grid);
             HIP_CHECK(hipMemcpyAsync(h.data(), ftrace, 64 * grid, hipMemcpyDeviceToHost, s));
@@ -1370,7 +1455,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 #define LAUNCH_B(L2V, VV)                                                                      \
     k_ivf_rerank<L2V, VV><<<dim3((unsigned)cdiv(n, RR_W)), dim3(64 * RR_W), 0, s>>>(           \
             keys, recs, x, ldx, codes, ldc, ids, d, n, nprobe, KE / 4, obits, k, D, I, stats,   \
-            trace, PQArgs{}, b.sel, qdone)
+            trace, PQArgs{}, b.sel, qdone, fk ? 1 : 0)
 #define DISPATCH_V(L2V)                      \
     do {                                     \
         if (V == 2) LAUNCH_B(L2V, 2);        \
@@ -1413,7 +1498,7 @@ void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, in
 #define LAUNCH_P(VV, DS)                                                                        \
     k_ivf_rerank<true, VV, DS><<<dim3((unsigned)cdiv(n, RR_W)), dim3(64 * RR_W), 0, s>>>(       \
             keys, recs, x, ldx, nullptr, 0, ids, d, n, nprobe, KT, obits, k, D, I, stats,         \
-            nullptr, pa, sel, qdone)
+            nullptr, pa, sel, qdone, 0)
 #define DISPATCH_P(DS)                       \
     do {                                     \
         if (V == 2) LAUNCH_P(2, DS);         \

@@ -554,6 +554,7 @@ struct IndexIVFFlat : IndexIVF {
                               bool store_pairs, hipStream_t s) const override;
     mutable DeviceBuffer d_ynorm_, d_ynmax_, d_cbf_, d_cbs_, d_rres_, d_rmax_, s_part_, s_flags_;
     mutable int obits_ = 4;
+    mutable int fold_ = 0;  // stream image carries folded norm fragments (L2)
 };
 
 // faiss/impl/ProductQuantizer.h:29-186
