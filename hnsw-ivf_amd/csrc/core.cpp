@@ -187,8 +187,12 @@ void IndexFlat::sync_device() const {
             kern::row_resnorm_bf16(d_xb_.as<float>(), ntotal, d, l, s_tile_.as<float>(), s);
             kern::array_max(s_tile_.as<float>(), ntotal, d_cnmax_.as<float>() + 1, s);
             d_cst_.reserve(kern::coarse_stream_image_bytes(ntotal, d));
+            // L2: the norms enter the coarse filter's MFMA as a bias k-step
+            // (FAISS_AMD_COARSE_FOLD=0 keeps the fp32-norm tails)
+            const char* fenv = getenv("FAISS_AMD_COARSE_FOLD");
+            cfold_ = (metric_type == METRIC_L2 && !(fenv && !strcmp(fenv, "0"))) ? 1 : 0;
             kern::coarse_stream_image(d_xb_.as<float>(), ntotal, d, l, d_norms_.as<float>(),
-                                      d_cst_.ptr, s);
+                                      d_cst_.ptr, s, cfold_);
         }
     }
     HIP_CHECK(hipStreamSynchronize(s));
@@ -298,7 +302,7 @@ bool IndexFlat::knn_impl(idx_t n, const float* x, int ldx, int k, float* distanc
                                  d_cst_.ptr,
                                  qi ? (const uint8_t*)qimg + q0 * kern::query_image_bytes(1, d)
                                     : nullptr,
-                                 &ktimes);
+                                 &ktimes, cfold_);
         }
         return qi && qimg_out;
     }

@@ -52,7 +52,8 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
                     const float* cnmax, int nlist, int d, int k, int metric_l2, uint32_t* keys,
                     float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s,
                     const void* cst = nullptr, const void* qimg = nullptr,
-                    KernelTimes* kt = nullptr);
+                    KernelTimes* kt = nullptr,
+                    int fold = 0);  // cst is the fold image (L2)
 // Query preparation for the MFMA filters (one launch): the reference-order
 // norms ref_norms[i] = fvec_norm_L2sqr(x_i) (skipped when null) and the query
 // image of bf3.h load_query_image — qimg [n][64 NS] bytes (NS = bf3_db(d)/16)
@@ -63,9 +64,12 @@ inline size_t query_image_bytes(int64_t n, int d) {
     return (size_t)std::max<int64_t>(n, 1) * 4 * ((d + 31) / 32 * 32);
 }
 // the streamed coarse filter's image of the centroids: per row bf16 hi | lo
-// (bf3_db(d) dims each) | fp32 norm | 12 B, padded to 64 rows (+inf norms)
+// (bf3_db(d) dims each) | a 16-byte tail, padded to 64 rows.  fold = 0: the
+// tail is the fp32 norm (+inf for padding rows) + 12 zero bytes; fold = 1
+// (L2): the bias A-fragment {-|c|^2/2 in three bf16 parts, 1, 1, 1, 0, 0}
+// (padding rows -inf, 0, 0, 1, 1, 1, 0, 0), as split_bf16_stream's
 void coarse_stream_image(const float* codes, int64_t rows, int d, int ldc, const float* norms,
-                         void* out, hipStream_t s);
+                         void* out, hipStream_t s, int fold = 0);
 size_t coarse_stream_image_bytes(int64_t rows, int d);
 void array_max(const float* a, int64_t n, float* out, hipStream_t s);
 
@@ -263,6 +267,7 @@ inline int bf3_db_host(int d) { return (d + 31) / 32 * 32; }  // ordinal bits of
 double ivf_bf3_coef(int d);                // margin coefficient
 double ivf_bf2_coef(int d);
 double ivf_bf2f_coef(int d);  // bf16x2 with the norms folded into the MFMA (fold image)
+double ivf_bf3f_coef(int d);  // bf16x3, norms folded (coarse fold image)
 // |y - bf16(y)| per row (bf16x2 filter margins)
 void row_resnorm_bf16(const float* codes, int64_t rows, int d, int ldc, float* out,
                       hipStream_t s);

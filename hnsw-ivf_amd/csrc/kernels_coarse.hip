@@ -218,7 +218,12 @@ __device__ __forceinline__ void cwait_vmcnt() {  // s_waitcnt vmcnt(N) alone
 // three times in the LDS up to DB = 96 (d <= 96), twice at DB = 128; the
 // register budget follows (three waves per SIMD need <= 168 VGPRs, which
 // KT = 16 queues do not leave).
-template <bool L2, int KT, int NS>
+// FOLD (L2, fold image): the centroid and query norms enter the MFMA as one
+// more k-step (A = the row's tail {-|c|^2/2 in three bf16 parts, 1, 1, 1, 0,
+// 0}, B = {1, 1, 1, -|x|^2/2 in three parts, 0, 0}), the accumulator is
+// -approx/2 and a candidate's key is one v_bfi_b32 of its bits (bf3.h
+// fold_key_bits) instead of add + fma + max + bfi; no norm reads from LDS.
+template <bool L2, int KT, int NS, bool FOLD = false>
 __global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stream(
         const float* __restrict__ x, int ldx, int64_t n, int d, const uint8_t* __restrict__ cst,
         const float* __restrict__ xnorm, int nlist, int nsplit, int split_len, int nqb,
@@ -281,6 +286,22 @@ __global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stre
     }
     const float xn = (active && q < n) ? xnorm[q] : 0.f;  // the reference-order norm
     if (tr) tr[1] = __builtin_amdgcn_s_memtime();
+    static_assert(!FOLD || L2, "fold: L2 only");
+    // FOLD: the bias B fragment {1, 1, 1, -|x|^2/2 in three parts, 0, 0} (lh = 0)
+    bf16x8 bq;
+    if constexpr (FOLD) {
+        __bf16 h, m, lo;
+        split3_bf16(-0.5f * xn, h, m, lo);
+        const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
+        bq[0] = lh ? zero : one;
+        bq[1] = lh ? zero : one;
+        bq[2] = lh ? zero : one;
+        bq[3] = lh ? zero : h;
+        bq[4] = lh ? zero : m;
+        bq[5] = lh ? zero : lo;
+        bq[6] = zero;
+        bq[7] = zero;
+    }
 
     ThreadQueue32<KT> tq[2];
     tq[0].init();
@@ -293,6 +314,10 @@ __global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stre
         for (int r = 0; r < 16; r++) nv[r] = *(const float*)(nrow + (8 * (r >> 2) + (r & 3)) * SR);
     };
     auto push1 = [&](ThreadQueue32<KT>& pq, float accr, float yv0, uint32_t ord) {
+        if constexpr (FOLD) {  // accr = -approx/2 already (read guarded by the caller)
+            pq.push(key_insert(fold_key_bits(accr), lowmask, ord));
+            return;
+        }
         const float yv = L2 ? yv0 : (yv0 < WS_INF ? 0.f : WS_INF);  // IP: padding +inf
         // L2: clamped at 0 inside key_bits, as the reference clamps
         const float a = L2 ? fmaf(-2.f, accr, xn + yv) : yv - accr;
@@ -318,11 +343,19 @@ __global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stre
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s2], bh[s2], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s2], bl[s2], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s2], bh[s2], acc, 0, 0, 0);
+            // FOLD: the inline-asm key insert reads pacc (an MFMA result)
+            if (FOLD && s2 == 0) mfma_read_guard();
 #pragma unroll
             for (int r = 16 * s2 / NS; r < 16 * (s2 + 1) / NS; r++)
                 push1(pq, pacc[r],
-                      pnT ? *(const float*)(pnT + (8 * (r >> 2) + (r & 3)) * SR) : pn[r],
+                      FOLD ? 0.f
+                           : pnT ? *(const float*)(pnT + (8 * (r >> 2) + (r & 3)) * SR) : pn[r],
                       pord | (uint32_t)r);
+        }
+        if constexpr (FOLD) {
+            // the row's bias fragment (lh = 1: its hi bytes, times 0)
+            const bf16x8 ab = *(const bf16x8*)(T + (32 * bi + li) * SR + (lh ? 0 : 4 * DB));
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, bq, acc, 0, 0, 0);
         }
         return acc;
     };
@@ -337,6 +370,10 @@ __global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stre
     if (ntile > 1) issue(1, 1);
     if (active) {
         acc0 = bf3_block<NS>(tiles + (0 * SR) + li * SR + 16 * lh, bh, bl);
+        if constexpr (FOLD) {
+            const bf16x8 ab = *(const bf16x8*)(tiles + li * SR + (lh ? 0 : 4 * DB));
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, bq, acc0, 0, 0, 0);
+        }
     }
     int b = 0;
     for (int j = 0; j < ntile; j++) {
@@ -345,7 +382,7 @@ __global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stre
         if (active) {
             // (block 0's norms straight from LDS: tile j stays until the barrier)
             acc1 = mfma_push(T, 1, acc0, n1, T + 4 * lh * SR + 4 * DB, ordbase, tq[0]);
-            norms(T, 1, n1);
+            if constexpr (!FOLD) norms(T, 1, n1);
         }
         if (j + 1 < ntile) {
             if (tr && j < 78) tr[2 + 2 * j] = __builtin_amdgcn_s_memtime();
@@ -359,8 +396,10 @@ __global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stre
                 acc0 = mfma_push(T1, 0, acc1, n1, nullptr, ordbase, tq[1]);
             }
         } else if (active) {
+            if constexpr (FOLD) mfma_read_guard();
 #pragma unroll
-            for (int r = 0; r < 16; r++) push1(tq[1], acc1[r], n1[r], ordbase | (uint32_t)r);
+            for (int r = 0; r < 16; r++)
+                push1(tq[1], acc1[r], FOLD ? 0.f : n1[r], ordbase | (uint32_t)r);
         }
         b ^= 1;
     }
@@ -380,7 +419,7 @@ __global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stre
             const uint32_t last = tq[bi].q[KT - 1];
             float bnd = WS_INF;
             if (last != 0xffffffffu && ivf_key_row(last, lowmask, slot) < (uint32_t)len)
-                bnd = key_decode_lo<L2>(last, lowmask);
+                bnd = FOLD ? fold_decode_lo(last, lowmask) : key_decode_lo<L2>(last, lowmask);
             pbs[(q * nsplit + sp) * 4 + slot] = bnd < WS_INF ? bnd - M : WS_INF;
         }
     }
@@ -391,7 +430,7 @@ __global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stre
 // the 64-row padding) are zero with a +inf norm
 __global__ void k_coarse_image(const float* __restrict__ codes, int64_t rows, int64_t rows_pad,
                                int d, int ldc, int DB, const float* __restrict__ norms,
-                               uint8_t* __restrict__ out) {
+                               uint8_t* __restrict__ out, int fold) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int per = DB + 4;  // slots per row: DB (hi, lo) pairs, norm, 3 pad words
     if (i >= rows_pad * per) return;
@@ -403,18 +442,29 @@ __global__ void k_coarse_image(const float* __restrict__ codes, int64_t rows, in
         const __bf16 h = (__bf16)v;
         ((__bf16*)row)[j] = h;
         ((__bf16*)row)[DB + j] = (__bf16)(v - (float)h);
+    } else if (fold) {
+        // bias A-fragment {-|c|^2/2 in three bf16 parts, 1, 1, 1, 0, 0}
+        // (padding rows: -inf, 0, 0, 1, 1, 1, 0, 0): two bf16 per slot
+        __bf16 h = (__bf16)(-WS_INF), m = (__bf16)0.f, lo = (__bf16)0.f;
+        if (r < rows) split3_bf16(-0.5f * norms[r], h, m, lo);
+        const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
+        const int t = j - DB;  // bf16 pair t of the 16-byte tail
+        __bf16* tail = (__bf16*)(row + 4 * DB);
+        const __bf16 v[8] = {h, m, lo, one, one, one, zero, zero};
+        tail[2 * t] = v[2 * t];
+        tail[2 * t + 1] = v[2 * t + 1];
     } else {
         float* tail = (float*)(row + 4 * DB);
         tail[j - DB] = j == DB ? (r < rows ? norms[r] : WS_INF) : 0.f;
     }
 }
 void coarse_stream_image(const float* codes, int64_t rows, int d, int ldc, const float* norms,
-                         void* out, hipStream_t s) {
+                         void* out, hipStream_t s, int fold) {
     const int DB = bf3_db(d);
     const int64_t rows_pad = (int64_t)roundup((size_t)std::max<int64_t>(rows, 1), BV);
     const int64_t tot = rows_pad * (DB + 4);
     k_coarse_image<<<dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, s>>>(
-            codes, rows, rows_pad, d, ldc, DB, norms, (uint8_t*)out);
+            codes, rows, rows_pad, d, ldc, DB, norms, (uint8_t*)out, fold);
     HIP_LAUNCH_CHECK();
 }
 size_t coarse_stream_image_bytes(int64_t rows, int d) {
@@ -489,6 +539,7 @@ struct CoarseStream {
     int ldc, d, nlist, nsplit, split_len, E, KT, lane, nsv;
     uint32_t lowmask;
     bool overflow;
+    bool fold;                 // folded filter keys (ivf_decode_lo)
     unsigned long long fmask;  // failing streams: bit 4 * split + slot
 
     __device__ __forceinline__ void emit(bool ok, int j, float& k1, long long& k2) const {
@@ -516,7 +567,7 @@ struct CoarseStream {
             int j = 0;
             if (c < E && !((fmask >> st) & 1ull)) {
                 const uint32_t key = keys[c];
-                ok = key != 0xffffffffu && key_decode_lo<L2>(key, lowmask) - M <= U;
+                ok = key != 0xffffffffu && ivf_decode_lo<L2>(key, lowmask, fold) - M <= U;
                 j = (st >> 2) * split_len + (int)ivf_key_row(key, lowmask, st & 3);
             }
             if (__ballot(ok) == 0ull) continue;
@@ -561,7 +612,8 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
         const float* __restrict__ cnmax_p, float coef, int y3, int64_t n, int d, int nlist,
         int nsplit, int split_len, int KT, int obits, int k, float* __restrict__ D,
         OutIdx* __restrict__ I, uint32_t* __restrict__ stats,
-        unsigned long long* __restrict__ trace) {
+        unsigned long long* __restrict__ trace, int fold_keys) {
+    const bool fold = L2 && fold_keys != 0;
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ uint32_t surv[CR_CAP];
     __shared__ float ck1[256];      // compaction scratch of the small-batch select
@@ -589,7 +641,7 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
     float ub[V];
 #pragma unroll
     for (int i = 0; i < V; i++)
-        ub[i] = kv[i] != 0xffffffffu ? key_decode_hi<L2>(kv[i], lowmask) + M : WS_INF;
+        ub[i] = kv[i] != 0xffffffffu ? ivf_decode_hi<L2>(kv[i], lowmask, fold) + M : WS_INF;
     float U = wave_kth_smallest<V>(ub, k);
     const unsigned long long t_u = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (!(U <= WS_INF)) U = WS_INF;
@@ -603,7 +655,7 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
         bool sv = false;
         uint32_t j = 0;
         if (kv[i] != 0xffffffffu && !lfail) {
-            sv = key_decode_lo<L2>(kv[i], lowmask) - M <= U;
+            sv = ivf_decode_lo<L2>(kv[i], lowmask, fold) - M <= U;
             j = (uint32_t)((lst >> 2) * split_len) + ivf_key_row(kv[i], lowmask, lst & 3);
         }
         const unsigned long long m = __ballot(sv);
@@ -651,6 +703,7 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
     st.nsv = ns;
     st.lowmask = lowmask;
     st.overflow = ns > CR_CAP;
+    st.fold = fold;
     st.fmask = fmask;
     bool done = false;
     unsigned long long t_e = 0ull;
@@ -805,7 +858,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
                     const float* cent, int ldc, const void* cbf, const float* cnorm,
                     const float* cnmax, int nlist, int d, int k, int metric_l2, uint32_t* keys,
                     float* pbs, float* D, int32_t* I32, int64_t* I64, hipStream_t s,
-                    const void* cst, const void* qimg, KernelTimes* kt) {
+                    const void* cst, const void* qimg, KernelTimes* kt, int fold) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(p.ok);
     static uint32_t* stats = nullptr;  // FAISS_AMD_IVF_STATS debug counters
@@ -821,11 +874,14 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     // per step) the streams overflow and fail; kept for clustered data
     const char* prec = getenv("FAISS_AMD_COARSE_PREC");
     const bool y3 = !(prec && !strcmp(prec, "bf16x2"));
-    const float coef = (float)(y3 ? ivf_bf3_coef(d) : ivf_bf2_coef(d));
     // streamed bf16x3 kernel (default when the image exists;
     // FAISS_AMD_COARSE=staged: the register-staged one)
     const char* cenv = getenv("FAISS_AMD_COARSE");
     const bool stream = cst && y3 && !(cenv && !strcmp(cenv, "staged"));
+    // fold: the image's tails are bias fragments (only the streamed L2 kernel
+    // reads the image)
+    const bool fk = stream && fold != 0 && metric_l2;
+    const float coef = (float)(fk ? ivf_bf3f_coef(d) : y3 ? ivf_bf3_coef(d) : ivf_bf2_coef(d));
     static unsigned long long* ctrace_buf = nullptr;
     static int64_t ctrace_n = 0;
     const char* ctr = getenv("FAISS_AMD_COARSE_TRACE");
@@ -845,7 +901,8 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
 #define LAUNCH_NS(L2V, KTV, NSV)                                                              \
     do {                                                                                      \
         if (stream)                                                                           \
-            k_coarse_stream<L2V, KTV, NSV><<<dim3((unsigned)grid), dim3(256), 0, s>>>(        \
+            (fk ? k_coarse_stream<L2V, KTV, NSV, L2V> : k_coarse_stream<L2V, KTV, NSV, false>) \
+                    <<<dim3((unsigned)grid), dim3(256), 0, s>>>(                              \
                     x, ldx, n, d, (const uint8_t*)cst, xnorm, nlist, p.nsplit, p.split_len,   \
                     (int)nqb, coef, cnmax, p.obits, keys, pbs, ctrace,                        \
                     (const uint8_t*)qimg);                                                    \
@@ -896,7 +953,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     k_coarse_rerank<L2V, OT, VV><<<dim3((unsigned)n), dim3(64), 0, s>>>(                       \
             keys, pbs, x, ldx, xnorm, cent, ldc, cnorm, cnmax, coef, y3 ? 1 : 0, n, d, nlist,  \
             p.nsplit,                                                                           \
-            p.split_len, p.kt, p.obits, k, D, OUT, st_ptr, crtrace)
+            p.split_len, p.kt, p.obits, k, D, OUT, st_ptr, crtrace, fk ? 1 : 0)
 #define LAUNCH_RV(L2V, OT, OUT)                  \
     do {                                         \
         if (V == 1) LAUNCH_R(L2V, OT, OUT, 1);   \

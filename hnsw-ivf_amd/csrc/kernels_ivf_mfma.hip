@@ -1251,6 +1251,14 @@ double ivf_bf3_coef(int d) {
 // bounded by |x| |y - yh| (Cauchy-Schwarz, |y - yh| stored per row), the
 // second by 2^-16 (1 + 2^-8) |x||y|; plus the f32 accumulation, norm and
 // exact-side roundings.  This is the (x^2 + y^2) coefficient of that bound.
+// bf16x3 with the norms folded into the MFMA accumulation (coarse fold image):
+// 3 dp exact products and 6 exact bias products, |sum| <= 1.51 (|x|^2 +
+// |y|^2); as ivf_bf2f_coef, twice the bound
+double ivf_bf3f_coef(int d) {
+    const double u = 1.0 / 16777216.0;
+    return 2.0 * (3.1 / 65536.0 + (9.1 * d + 24.0) * u);
+}
+
 double ivf_bf2_coef(int d) {
     const double u = 1.0 / 16777216.0;
     return 1.02 / 65536.0 + (6.1 * d + 8.0) * u;

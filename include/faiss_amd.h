@@ -252,6 +252,7 @@ struct IndexFlat : Index {
                   hipStream_t stream, void* qimg_out, bool direct) const;
     mutable StreamOrder order_;
     mutable DeviceBuffer d_xb_, d_norms_, d_cbf_, d_cnmax_, d_cst_;
+    mutable int cfold_ = 0;  // d_cst_ carries folded norm fragments (L2)
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
     mutable DeviceBuffer s_xn_, s_tile_, s_cand_d_, s_cand_i_, s_qimg_;
