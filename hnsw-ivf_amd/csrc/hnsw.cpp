@@ -260,6 +260,11 @@ IndexHNSW::IndexHNSW(IndexFlat* st, int M)
     if (st) device = st->device;
 }
 IndexHNSW::~IndexHNSW() {
+    if (side_) (void)hipStreamSynchronize(side_);
+    if (ev_split_) (void)hipEventDestroy(ev_split_);
+    if (ev_exact_) (void)hipEventDestroy(ev_exact_);
+    if (side_) (void)hipStreamDestroy(side_);
+    if (h_fcnt_) (void)hipHostFree(h_fcnt_);
     if (own_fields) delete storage;
 }
 IndexHNSWFlat::IndexHNSWFlat(int d_, int M, MetricType metric)
@@ -378,8 +383,8 @@ void IndexHNSW::sync_device() const {
 
 template <class OutIdx>
 void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* distances,
-                            OutIdx* labels, const SearchParameters* params,
-                            hipStream_t s) const {
+                            OutIdx* labels, const SearchParameters* params, hipStream_t s,
+                            bool defer) const {
     // faiss/IndexHNSW.cpp:246-343 (hnsw_search)
     FAISS_THROW_IF_NOT(k > 0);
     int efSearch = hnsw.efSearch;
@@ -407,6 +412,7 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
     gd.ntotal = (int)ntotal;
     const int64_t vwords = (int64_t)cdiv(std::max<idx_t>(ntotal, 1), 32);
     constexpr bool i32 = sizeof(OutIdx) == 4;
+    split_.active = false;
     if (!d_stats_.ptr) {
         d_stats_.reserve(4 * sizeof(unsigned long long));
         HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, 4 * sizeof(unsigned long long), s));
@@ -422,14 +428,86 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
                              : n;
     if (scratch) s_visited_.reserve(sizeof(uint32_t) * vwords * qc);
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(qc, 1));
+    // defer (split_begin): one chunk, batched kernel eligible
+    defer = defer && !scratch && i32 && ef <= 128 && k <= 64;
     for (idx_t q0 = 0; q0 < n; q0 += qc) {
         const idx_t nq = std::min(qc, n - q0);
         kern::hnsw_search(gd, x + q0 * ldx, ldx, nq, k, efSearch, distances + q0 * k,
                           i32 ? nullptr : (int64_t*)labels + q0 * k,
                           i32 ? (int32_t*)labels + q0 * k : nullptr, s_visited_.as<uint32_t>(),
                           vwords, d_stats_.as<unsigned long long>(), s_flags_.as<uint32_t>(), s,
-                          &ktimes);
+                          &ktimes, defer);
     }
+    if (!defer) return;
+    // the flagged queries -> compact list, count read back (pinned)
+    if (!h_fcnt_) HIP_CHECK(hipHostMalloc((void**)&h_fcnt_, sizeof(uint32_t), hipHostMallocDefault));
+    if (!ev_split_) HIP_CHECK(hipEventCreateWithFlags(&ev_split_, hipEventDisableTiming));
+    s_fidx_.reserve(sizeof(uint32_t) * std::max<idx_t>(n, 1));
+    s_fcnt_.reserve(sizeof(uint32_t));
+    kern::hnsw_flag_compact(s_flags_.as<uint32_t>(), n, s_fidx_.as<uint32_t>(),
+                            s_fcnt_.as<uint32_t>(), s);
+    HIP_CHECK(hipMemcpyAsync(h_fcnt_, s_fcnt_.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipEventRecord(ev_split_, s));
+    split_.active = true;
+    split_.n = n;
+    split_.x = x;
+    split_.ldx = ldx;
+    split_.k = k;
+    split_.efSearch = efSearch;
+    split_.s = s;
+}
+
+bool IndexHNSW::split_begin(idx_t n, const float* x, int ldx, int k, float* distances,
+                            int32_t* labels, const SearchParameters* params,
+                            hipStream_t s) const {
+    DevGuard2 dg(device);
+    hnsw_device<int32_t>(n, x, ldx, k, distances, labels, params, s, true);
+    return split_.active;
+}
+
+IndexHNSW::Split IndexHNSW::split_finish() const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    FAISS_THROW_IF_NOT_MSG(split_.active, "split_finish without split_begin");
+    DevGuard2 dg(device);
+    split_.active = false;
+    HIP_CHECK(hipEventSynchronize(ev_split_));
+    Split r;
+    r.nf = (idx_t)*h_fcnt_;
+    if (r.nf == 0) return r;
+    if (!side_) HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    if (!ev_exact_) HIP_CHECK(hipEventCreateWithFlags(&ev_exact_, hipEventDisableTiming));
+    const int k = split_.k;
+    s_fD_.reserve(sizeof(float) * r.nf * k);
+    s_fI_.reserve(sizeof(int32_t) * r.nf * k);
+    kern::HNSWDevice gd;
+    gd.storage = storage->device_vectors();
+    gd.norms = nullptr;
+    gd.ld = ld();
+    gd.d = d;
+    gd.levels = d_levels_.as<int32_t>();
+    gd.offsets = d_offsets_.as<uint64_t>();
+    gd.neighbors = d_neighbors_.as<int32_t>();
+    gd.cum_nb = d_cum_.as<int32_t>();
+    gd.nb0 = nb0_stride_ > 0 ? d_nb0_.as<int32_t>() : nullptr;
+    gd.nb0_stride = nb0_stride_;
+    gd.nlevels_cum = (int)hnsw.cum_nneighbor_per_level.size();
+    gd.entry_point = ntotal > 0 ? hnsw.entry_point : -1;
+    gd.max_level = hnsw.max_level;
+    gd.ntotal = (int)ntotal;
+    const int64_t vwords = (int64_t)cdiv(std::max<idx_t>(ntotal, 1), 32);
+    HIP_CHECK(hipStreamWaitEvent(side_, ev_split_, 0));
+    {
+        ScopedKernelTimer tm(&ktimes, "hnsw_exact", 0.0, side_);
+        kern::hnsw_exact_listed(gd, split_.x, split_.ldx, s_fidx_.as<uint32_t>(), r.nf, k,
+                                split_.efSearch, s_fD_.as<float>(), s_fI_.as<int32_t>(),
+                                nullptr, vwords, d_stats_.as<unsigned long long>(), side_);
+    }
+    HIP_CHECK(hipEventRecord(ev_exact_, side_));
+    r.idx = s_fidx_.as<uint32_t>();
+    r.D = s_fD_.as<float>();
+    r.I = s_fI_.as<int32_t>();
+    r.done = ev_exact_;
+    return r;
 }
 
 // HNSWStats counted by the kernel -> the host global (faiss::hnsw_stats)

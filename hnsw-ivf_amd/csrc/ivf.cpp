@@ -385,6 +385,11 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
             if (qf->assign_device_qimg(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
                                        s_ci_.as<int32_t>(), s_q_.ptr, s))
                 shared_qimg_ = s_q_.ptr;
+        } else if (mc == 0 && !selm &&
+                   scan_hnsw_split(nq, x + q0 * ldx, ldx, k, (int)np, distances + q0 * k,
+                                   labels + q0 * k,
+                                   params ? params->quantizer_params : nullptr, s)) {
+            continue;
         } else {
             quantize_device(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
                             s_ci_.as<int32_t>(), params ? params->quantizer_params : nullptr, s);
@@ -395,6 +400,47 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
                                   distances + q0 * k, labels + q0 * k, s, lim, selm);
     }
     order_.leave(s);
+}
+
+// An HNSW quantizer re-runs the queries whose batched search met an exact
+// distance tie with the reference's sequential algorithm (~0.6 % of c4's
+// queries, one wave each for ~1.5 ms).  Here the batched assignment of all
+// queries is scanned at once while that re-run proceeds on the quantizer's
+// side stream; the re-run queries are then scanned again with their exact
+// assignment and their rows replaced (results identical to scanning after
+// the full assignment; their first scan is wasted work).  FAISS_AMD_HNSW_DEFER=0
+// restores the sequential order.
+bool IndexIVF::scan_hnsw_split(idx_t nq, const float* x, int ldx, idx_t k, int np,
+                               float* distances, idx_t* labels, const SearchParameters* qparams,
+                               hipStream_t s) const {
+    const auto* qh = dynamic_cast<const IndexHNSW*>(quantizer);
+    const char* env = getenv("FAISS_AMD_HNSW_DEFER");
+    if (!qh || qdone_ || (env && !strcmp(env, "0"))) return false;
+    if (!qh->split_begin(nq, x, ldx, np, s_cd_.as<float>(), s_ci_.as<int32_t>(), qparams, s)) {
+        // not offered: split_begin ran the plain assignment
+        search_preassigned_device(nq, x, ldx, k, np, s_ci_.as<int32_t>(), s_cd_.as<float>(),
+                                  distances, labels, s, nullptr, nullptr);
+        return true;
+    }
+    search_preassigned_device(nq, x, ldx, k, np, s_ci_.as<int32_t>(), s_cd_.as<float>(),
+                              distances, labels, s, nullptr, nullptr);
+    const IndexHNSW::Split sp = qh->split_finish();
+    if (sp.nf == 0) return true;
+    HIP_CHECK(hipStreamWaitEvent(s, sp.done, 0));
+    const int l = (int)roundup((size_t)d, 4);
+    s_fx_.reserve(sizeof(float) * sp.nf * l);
+    s_fDo_.reserve(sizeof(float) * sp.nf * k);
+    s_fIo_.reserve(sizeof(idx_t) * sp.nf * k);
+    if (l != d) HIP_CHECK(hipMemsetAsync(s_fx_.ptr, 0, sizeof(float) * sp.nf * l, s));
+    kern::gather_rows(x, ldx, sp.idx, sp.nf, d, s_fx_.as<float>(), l, s);
+    search_preassigned_device(sp.nf, s_fx_.as<float>(), l, k, np, sp.I, sp.D, s_fDo_.as<float>(),
+                              s_fIo_.as<idx_t>(), s, nullptr, nullptr);
+    kern::scatter_rows(s_fDo_.ptr, (int)k, sp.idx, sp.nf, distances, s);
+    kern::scatter_rows(s_fIo_.ptr, 2 * (int)k, sp.idx, sp.nf, labels, s);
+    // the exact assignment in the coarse buffers too (their later readers)
+    kern::scatter_rows(sp.I, np, sp.idx, sp.nf, s_ci_.ptr, s);
+    kern::scatter_rows(sp.D, np, sp.idx, sp.nf, s_cd_.ptr, s);
+    return true;
 }
 
 void IndexIVF::search_preassigned_device_ordered(idx_t n, const float* x, int ldx, idx_t k,

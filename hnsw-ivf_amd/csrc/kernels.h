@@ -337,7 +337,23 @@ struct HNSWDevice {
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
-                 hipStream_t s, KernelTimes* kt = nullptr);
+                 hipStream_t s, KernelTimes* kt = nullptr,
+                 bool defer = false);  // leave the flagged queries to the caller
+// flagged queries (flags[q] != 0) -> idx[0 .. *count) (count zeroed first)
+void hnsw_flag_compact(const uint32_t* flags, int64_t n, uint32_t* idx, uint32_t* count,
+                       hipStream_t s);
+// the reference-exact sequential search of the listed queries x[qidx[i]],
+// results in compact rows i of D / I32
+void hnsw_exact_listed(const HNSWDevice& g, const float* x, int ldx, const uint32_t* qidx,
+                       int64_t nf, int k, int efSearch, float* D, int32_t* I32,
+                       uint32_t* visited_scratch, int64_t vwords, unsigned long long* stats,
+                       hipStream_t s);
+// rows: out[i] = in[idx[i]] (d floats, strides ldi / ldo); scatter of
+// packed rows of row_words 32-bit words: dst row idx[i] = src row i
+void gather_rows(const float* in, int ldi, const uint32_t* idx, int64_t n, int d, float* out,
+                 int ldo, hipStream_t s);
+void scatter_rows(const void* src, int row_words, const uint32_t* idx, int64_t n, void* dst,
+                  hipStream_t s);
 
 // IVF-Flat range search (kernels_range.hip): one wave per (query, probe).
 // offsets == nullptr: counts[q*np+p] = hits (dis < radius for L2, > for IP,

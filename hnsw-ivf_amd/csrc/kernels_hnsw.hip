@@ -443,8 +443,12 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
                                                    uint32_t* __restrict__ vis_global,
                                                    int64_t vwords,
                                                    unsigned long long* __restrict__ stats,
-                                                   const uint32_t* __restrict__ only) {
-    const int64_t q = blockIdx.x;
+                                                   const uint32_t* __restrict__ only,
+        const uint32_t* __restrict__ qidx) {
+    // qidx: compact launch over listed queries (input row qidx[b], output
+    // row b); else query b, output row b
+    const int64_t q = qidx ? (int64_t)qidx[blockIdx.x] : (int64_t)blockIdx.x;
+    const int64_t qo = blockIdx.x;
     if (only && only[q] == 0u) return;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* qs = sm;                              // [ld]
@@ -646,9 +650,9 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
     }
     __syncthreads();
     for (int j = lane; j < k; j += 64) {
-        if (D) D[q * k + j] = rdis[j];
-        if (I) I[q * k + j] = rid[j];
-        if (I32) I32[q * k + j] = rid[j];
+        if (D) D[qo * k + j] = rdis[j];
+        if (I) I[qo * k + j] = rid[j];
+        if (I32) I32[qo * k + j] = rid[j];
     }
 }
 
@@ -731,8 +735,12 @@ __global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float
                                                        uint32_t* __restrict__ vis_global,
                                                        int64_t vwords,
                                                        unsigned long long* __restrict__ stats,
-                                                       const uint32_t* __restrict__ only) {
-    const int64_t q = blockIdx.x;
+                                                       const uint32_t* __restrict__ only,
+        const uint32_t* __restrict__ qidx) {
+    // qidx: compact launch over listed queries (input row qidx[b], output
+    // row b); else query b, output row b
+    const int64_t q = qidx ? (int64_t)qidx[blockIdx.x] : (int64_t)blockIdx.x;
+    const int64_t qo = blockIdx.x;
     if (only && only[q] == 0u) return;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* qs = sm;  // [ld]
@@ -894,16 +902,79 @@ __global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float
     if (lane < k) {
         const float dv = lane < ii ? ov : FLT_MAX;
         const int32_t iv = lane < ii ? oi : -1;
-        if (D) D[q * k + lane] = dv;
-        if (I) I[q * k + lane] = iv;
-        if (I32) I32[q * k + lane] = iv;
+        if (D) D[qo * k + lane] = dv;
+        if (I) I[qo * k + lane] = iv;
+        if (I32) I32[qo * k + lane] = iv;
     }
+}
+
+// the sequential kernel over n queries (qidx: the listed ones, compact
+// outputs), register heaps for ef, k <= 64
+static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
+                              int efSearch, float* D, int64_t* I, int32_t* I32,
+                              uint32_t* visited_scratch, int64_t vwords,
+                              unsigned long long* stats, const uint32_t* only,
+                              const uint32_t* qidx, hipStream_t s) {
+    const int ef = efSearch > k ? efSearch : k;
+    const size_t lds_q = sizeof(float) * g.ld;
+    const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
+    const bool x_lds_vis = lds_x + vwords * 4 <= 64 * 1024;
+    const bool lds_vis = vwords * 4 <= 64 * 1024;
+    if (ef <= 64 && k <= 64) {  // register heaps
+        if (lds_vis)
+            k_hnsw_exact_reg<true><<<dim3((unsigned)n), dim3(64), lds_q + vwords * 4, s>>>(
+                    g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx);
+        else
+            k_hnsw_exact_reg<false><<<dim3((unsigned)n), dim3(64), lds_q, s>>>(
+                    g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
+                    only, qidx);
+        HIP_LAUNCH_CHECK();
+        return;
+    }
+    if (x_lds_vis)
+        k_hnsw_exact<true><<<dim3((unsigned)n), dim3(64), lds_x + vwords * 4, s>>>(
+                g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx);
+    else
+        k_hnsw_exact<false><<<dim3((unsigned)n), dim3(64), lds_x, s>>>(
+                g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats, only,
+                qidx);
+    HIP_LAUNCH_CHECK();
+}
+
+// flagged queries -> compact list (any order: the queries are independent)
+__global__ void k_flag_compact(const uint32_t* __restrict__ flags, int64_t n,
+                               uint32_t* __restrict__ idx, uint32_t* __restrict__ count) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool f = q < n && flags[q] != 0u;
+    const unsigned long long m = __ballot(f);
+    const int lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (m && lane == __ffsll((long long)m) - 1) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (f) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)q;
+}
+
+void hnsw_flag_compact(const uint32_t* flags, int64_t n, uint32_t* idx, uint32_t* count,
+                       hipStream_t s) {
+    HIP_CHECK(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
+    if (n <= 0) return;
+    k_flag_compact<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s>>>(flags, n, idx, count);
+    HIP_LAUNCH_CHECK();
+}
+
+void hnsw_exact_listed(const HNSWDevice& g, const float* x, int ldx, const uint32_t* qidx,
+                       int64_t nf, int k, int efSearch, float* D, int32_t* I32,
+                       uint32_t* visited_scratch, int64_t vwords, unsigned long long* stats,
+                       hipStream_t s) {
+    if (nf <= 0) return;
+    hnsw_exact_launch(g, x, ldx, nf, k, efSearch, D, nullptr, I32, visited_scratch, vwords,
+                      stats, nullptr, qidx, s);
 }
 
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
-                 hipStream_t s, KernelTimes* kt) {
+                 hipStream_t s, KernelTimes* kt, bool defer) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_FMT(k >= 1 && k <= kMaxKExact, "k = %d must be in [1, %d]", k,
                            kMaxKExact);
@@ -921,27 +992,11 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
         FAISS_THROW_IF_NOT(visited_scratch != nullptr);
         HIP_CHECK(hipMemsetAsync(visited_scratch, 0, sizeof(uint32_t) * vwords * n, s));
     }
+    (void)x_lds_vis;
     auto exact = [&](const uint32_t* only) {
         ScopedKernelTimer tm(kt, "hnsw_exact", 0.0, s);
-        if (ef <= 64 && k <= 64) {  // register heaps
-            if (lds_vis)
-                k_hnsw_exact_reg<true><<<dim3((unsigned)n), dim3(64), lds_q + vwords * 4, s>>>(
-                        g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only);
-            else
-                k_hnsw_exact_reg<false><<<dim3((unsigned)n), dim3(64), lds_q, s>>>(
-                        g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
-                        only);
-            HIP_LAUNCH_CHECK();
-            return;
-        }
-        if (x_lds_vis)
-            k_hnsw_exact<true><<<dim3((unsigned)n), dim3(64), lds_x + vwords * 4, s>>>(
-                    g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only);
-        else
-            k_hnsw_exact<false><<<dim3((unsigned)n), dim3(64), lds_x, s>>>(
-                    g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
-                    only);
-        HIP_LAUNCH_CHECK();
+        hnsw_exact_launch(g, x, ldx, n, k, efSearch, D, I, I32, visited_scratch, vwords, stats,
+                          only, nullptr, s);
     };
     // FAISS_AMD_HNSW_EXACT=1: every query through the sequential kernel (tests)
     const char* xenv = getenv("FAISS_AMD_HNSW_EXACT");
@@ -978,9 +1033,41 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
                     c, (long long)n, r[0], r[1], r[2], r[3]);
         }
         // the flagged queries again, sequentially; the visited scratch of a
-        // flagged query is reset by the kernel itself
-        exact(flags);
+        // flagged query is reset by the kernel itself.  defer: the caller
+        // re-runs them (hnsw_flag_compact + hnsw_exact_listed), overlapped
+        // with its own work
+        if (!defer) exact(flags);
     }
+}
+
+__global__ void k_gather_rows(const float* __restrict__ in, int ldi,
+                              const uint32_t* __restrict__ idx, int64_t n, int d,
+                              float* __restrict__ out, int ldo) {
+    const int64_t i = blockIdx.x;
+    if (i >= n) return;
+    const float* src = in + (int64_t)idx[i] * ldi;
+    for (int j = threadIdx.x; j < d; j += blockDim.x) out[i * ldo + j] = src[j];
+}
+void gather_rows(const float* in, int ldi, const uint32_t* idx, int64_t n, int d, float* out,
+                 int ldo, hipStream_t s) {
+    if (n <= 0) return;
+    k_gather_rows<<<dim3((unsigned)n), dim3(64), 0, s>>>(in, ldi, idx, n, d, out, ldo);
+    HIP_LAUNCH_CHECK();
+}
+__global__ void k_scatter_rows(const uint32_t* __restrict__ src, int words,
+                               const uint32_t* __restrict__ idx, int64_t n,
+                               uint32_t* __restrict__ dst) {
+    const int64_t i = blockIdx.x;
+    if (i >= n) return;
+    const int64_t q = idx[i];
+    for (int j = threadIdx.x; j < words; j += blockDim.x) dst[q * words + j] = src[i * words + j];
+}
+void scatter_rows(const void* src, int row_words, const uint32_t* idx, int64_t n, void* dst,
+                  hipStream_t s) {
+    if (n <= 0 || row_words <= 0) return;
+    k_scatter_rows<<<dim3((unsigned)n), dim3(64), 0, s>>>((const uint32_t*)src, row_words, idx,
+                                                         n, (uint32_t*)dst);
+    HIP_LAUNCH_CHECK();
 }
 
 }  // namespace kern

@@ -89,9 +89,12 @@ __global__ __launch_bounds__(1024) void k_bucket_count_lds(const int32_t* __rest
 }
 
 // single-workgroup exclusive scan of counts -> bucket_off, ceil(counts/QT)
-// -> item_off; per work item its list when asked.  Chunks of 4096 lists:
-// 4 consecutive counts per thread, shuffle scan per wave, 16 wave totals
-// through LDS; a running carry between chunks.
+// -> item_off; per work item its list when asked.  E consecutive counts per
+// thread (E = nlist / 1024 rounded up to a power of two, at most 64): every
+// count of a chunk of 1024 E lists is loaded at once (one round trip — c5's
+// 65536 lists in one chunk instead of sixteen), thread sums, shuffle scan per
+// wave, 16 wave totals through LDS; a running carry between chunks.
+template <int E>
 __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict__ counts,
                                                       int nlist, int QT,
                                                       uint32_t* __restrict__ bucket_off,
@@ -102,22 +105,11 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ perm) {
     __shared__ uint32_t wb[16], wi[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    uint32_t carry_b = 0, carry_i = 0;
-    for (int c0 = 0; c0 < nlist; c0 += 4096) {
-        const int l0 = c0 + 4 * t;
-        uint32_t c[4], n[4];
-        uint32_t sb = 0, si = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            c[j] = l0 + j < nlist ? counts[l0 + j] : 0u;
-            // zero_next == counts: each count is cleared once read (the fill
-            // takes the bucket sizes from bucket_off)
-            if (zero_next && l0 + j < nlist) zero_next[l0 + j] = 0u;
-            n[j] = (c[j] + QT - 1) / QT;
-            sb += c[j];
-            si += n[j];
-        }
-        // inclusive wave scan of the thread sums
+    constexpr int CH = 1024 * E;
+    // prefix of the thread sums (v[] per thread) over the work group: returns
+    // this thread's exclusive prefix and the chunk total
+    auto block_scan = [&](uint32_t sb, uint32_t si, uint32_t& pb, uint32_t& pi, uint32_t& tb,
+                          uint32_t& ti) {
         uint32_t ib = sb, ii = si;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -132,7 +124,10 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
             wi[w] = ii;
         }
         __syncthreads();
-        uint32_t pb = carry_b, pi = carry_i, tb = 0, ti = 0;
+        pb = 0;
+        pi = 0;
+        tb = 0;
+        ti = 0;
 #pragma unroll
         for (int v = 0; v < 16; v++) {
             pb += v < w ? wb[v] : 0u;
@@ -141,17 +136,44 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
             ti += wi[v];
         }
         __syncthreads();  // wb / wi are rewritten by the next chunk
-        uint32_t rb = pb + ib - sb, ri = pi + ii - si;  // exclusive prefix of this thread
+        pb += ib - sb;
+        pi += ii - si;
+    };
+    uint32_t carry_b = 0, carry_i = 0;
+    for (int c0 = 0; c0 < nlist; c0 += CH) {
+        const int l0 = c0 + E * t;
+        uint32_t c[E];
+        uint32_t sb = 0, si = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < E; j++) c[j] = l0 + j < nlist ? counts[l0 + j] : 0u;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+            // zero_next == counts: each count is cleared once read (the fill
+            // takes the bucket sizes from bucket_off)
+            if (zero_next && l0 + j < nlist) zero_next[l0 + j] = 0u;
+            sb += c[j];
+            si += (c[j] + QT - 1) / QT;
+        }
+        uint32_t pb, pi, tb, ti;
+        block_scan(sb, si, pb, pi, tb, ti);
+        uint32_t rb = carry_b + pb, ri = carry_i + pi;  // exclusive prefix of this thread
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+            const uint32_t nj = (c[j] + QT - 1) / QT;
             if (l0 + j < nlist) {
                 bucket_off[l0 + j] = rb;
                 item_off[l0 + j] = ri;
-                if (item_list)
-                    for (uint32_t i = 0; i < n[j]; i++) item_list[ri + i] = (uint32_t)(l0 + j);
             }
             rb += c[j];
-            ri += n[j];
+            ri += nj;
+        }
+        if (item_list) {  // rare (item_list users); a second walk keeps the first lean
+            ri = carry_i + pi;
+            for (int j = 0; j < E && l0 + j < nlist; j++) {
+                const uint32_t nj = (c[j] + QT - 1) / QT;
+                for (uint32_t i = 0; i < nj; i++) item_list[ri + i] = (uint32_t)(l0 + j);
+                ri += nj;
+            }
         }
         carry_b += tb;
         carry_i += ti;
@@ -163,43 +185,35 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
     }
     if (!perm) return;
     // items renumbered in perm order (bucket sizes from bucket_off: the counts
-    // are cleared)
+    // are cleared); the bucket_off stores above are this work group's own
+    __threadfence_block();
     __syncthreads();
     carry_i = 0;
-    for (int c0 = 0; c0 < nlist; c0 += 4096) {
-        const int i0 = c0 + 4 * t;
-        uint32_t n[4], si = 0;
-        int ls[4];
+    for (int c0 = 0; c0 < nlist; c0 += CH) {
+        const int i0 = c0 + E * t;
+        int ls[E];
+        uint32_t n[E], si = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            ls[j] = i0 + j < nlist ? (int)perm[i0 + j] : -1;
+        for (int j = 0; j < E; j++) ls[j] = i0 + j < nlist ? (int)perm[i0 + j] : -1;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
             n[j] = ls[j] >= 0 ? (bucket_off[ls[j] + 1] - bucket_off[ls[j]] + QT - 1) / QT : 0u;
             si += n[j];
         }
-        uint32_t ii = si;
+        uint32_t pb, pi, tb, ti;
+        block_scan(0u, si, pb, pi, tb, ti);
+        uint32_t ri = carry_i + pi;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t vi = __shfl_up(ii, off);
-            if (lane >= off) ii += vi;
-        }
-        if (lane == 63) wi[w] = ii;
-        __syncthreads();
-        uint32_t pi = carry_i, ti = 0;
-#pragma unroll
-        for (int v = 0; v < 16; v++) {
-            pi += v < w ? wi[v] : 0u;
-            ti += wi[v];
-        }
-        __syncthreads();
-        uint32_t ri = pi + ii - si;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (ls[j] >= 0) {
-                item_off[ls[j]] = ri;
-                if (item_list)
-                    for (uint32_t i = 0; i < n[j]; i++) item_list[ri + i] = (uint32_t)ls[j];
-            }
+        for (int j = 0; j < E; j++) {
+            if (ls[j] >= 0) item_off[ls[j]] = ri;
             ri += n[j];
+        }
+        if (item_list) {  // rare (item_list users); a second walk keeps the first lean
+            ri = carry_i + pi;
+            for (int j = 0; j < E; j++) {
+                for (uint32_t i = 0; i < n[j]; i++) item_list[ri + i] = (uint32_t)ls[j];
+                ri += n[j];
+            }
         }
         carry_i += ti;
     }
@@ -356,8 +370,14 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
         HIP_LAUNCH_CHECK();
         }
     }
-    k_bucket_scan<<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off, b.item_off,
-                                                 b.item_list, b.counts_next, b.item_ctr, b.perm);
+#define BSCAN(E)                                                                            \
+    k_bucket_scan<E><<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off,         \
+                                                    b.item_off, b.item_list, b.counts_next,    \
+                                                    b.item_ctr, b.perm)
+    if (nlist <= 4096) BSCAN(4);
+    else if (nlist <= 16384) BSCAN(16);
+    else BSCAN(16);
+#undef BSCAN
     HIP_LAUNCH_CHECK();
     if (total > 0) {
         k_bucket_fill<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(

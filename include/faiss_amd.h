@@ -310,12 +310,44 @@ struct IndexHNSW : Index {
                       const SearchParameters* params = nullptr,
                       QueryLatencyStats* per_query_stats = nullptr) const;
 
+    // Coarse assignment with the tie re-runs left to the caller, so it can
+    // overlap them with its own work (IndexIVF::search_device): split_begin
+    // queues the batched search of n queries (the flagged ones keep the
+    // batched result) and a read-back of the flagged count, and returns false
+    // when this form is not offered (visited bitmaps beyond LDS, ef > 128 or
+    // k > 64: the caller then uses assign_device).  split_finish waits for the
+    // count, queues the reference-exact sequential search of the flagged
+    // queries on a side stream into compact rows, and returns them; `done` is
+    // recorded after it (the caller waits on it before reading D / I).
+    struct Split {
+        idx_t nf = 0;                  // flagged queries
+        const uint32_t* idx = nullptr;  // their query numbers [nf]
+        const float* D = nullptr;       // [nf][k] exact coarse distances
+        const int32_t* I = nullptr;     // [nf][k] exact assignments
+        hipEvent_t done = nullptr;
+    };
+    bool split_begin(idx_t n, const float* x, int ldx, int k, float* distances, int32_t* labels,
+                     const SearchParameters* params, hipStream_t stream) const;
+    Split split_finish() const;
+
    private:
     template <class OutIdx>
     void hnsw_device(idx_t n, const float* x, int ldx, int k, float* distances, OutIdx* labels,
-                     const SearchParameters* params, hipStream_t stream) const;
+                     const SearchParameters* params, hipStream_t stream,
+                     bool defer = false) const;
     mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, d_nb0_, s_visited_, d_stats_,
-            s_flags_;
+            s_flags_, s_fidx_, s_fcnt_, s_fD_, s_fI_;
+    mutable uint32_t* h_fcnt_ = nullptr;  // pinned read-back of the flagged count
+    mutable hipEvent_t ev_split_ = nullptr, ev_exact_ = nullptr;
+    mutable hipStream_t side_ = nullptr;
+    struct SplitState {
+        bool active = false;
+        idx_t n = 0;
+        const float* x = nullptr;
+        int ldx = 0, k = 0, efSearch = 0;
+        hipStream_t s = nullptr;
+    };
+    mutable SplitState split_;
     mutable int nb0_stride_ = 0;  // level-0 table width (0: not built)
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
@@ -490,6 +522,11 @@ struct IndexIVF : Index {
     mutable DeviceBuffer s_ictr_;
     mutable DeviceBuffer s_x_, s_cd_, s_ci_, s_counts_, s_boff_, s_ioff_, s_cur_, s_ent_,
             s_pk1_, s_pk2_, s_q_;
+    // HNSW quantizer: quantize + scan with the tie re-runs overlapped
+    // (IndexHNSW::split_begin / split_finish); false = not applicable
+    bool scan_hnsw_split(idx_t nq, const float* x, int ldx, idx_t k, int np, float* distances,
+                         idx_t* labels, const SearchParameters* qparams, hipStream_t s) const;
+    mutable DeviceBuffer s_fx_, s_fDo_, s_fIo_;  // the re-run queries' rows and results
     // query image the flat quantizer prepared into s_q_ for the chunk
     // search() is scanning (IndexFlat::assign_device_qimg), null outside it
     mutable const void* shared_qimg_ = nullptr;

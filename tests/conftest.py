@@ -47,3 +47,30 @@ def assert_same_results(D, I, Dr, Ir, rtol=0.0):
         assert np.array_equal(D, Dr), f"max |dD| = {np.abs(D - Dr).max()}"
     else:
         np.testing.assert_allclose(D, Dr, rtol=rtol, atol=0)
+
+
+def device_search(idx, xq, k):
+    """Index::search_device (the device entry point bench.py times) on
+    hipMalloc'd copies of xq; returns host (D, I)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+
+    def dmalloc(nbytes):
+        p = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(max(nbytes, 4))) == 0
+        return p
+    xq = np.ascontiguousarray(xq, dtype=np.float32)
+    n = xq.shape[0]
+    px, pd, pi = dmalloc(xq.nbytes), dmalloc(n * k * 4), dmalloc(n * k * 8)
+    try:
+        hip.hipMemcpy(px, xq.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(xq.nbytes), 1)
+        idx.search_device(n, px.value, k, pd.value, pi.value)
+        assert hip.hipDeviceSynchronize() == 0
+        D = np.empty((n, k), np.float32)
+        I = np.empty((n, k), np.int64)
+        hip.hipMemcpy(D.ctypes.data_as(ctypes.c_void_p), pd, ctypes.c_size_t(D.nbytes), 2)
+        hip.hipMemcpy(I.ctypes.data_as(ctypes.c_void_p), pi, ctypes.c_size_t(I.nbytes), 2)
+    finally:
+        for p in (px, pd, pi):
+            hip.hipFree(p)
+    return D, I

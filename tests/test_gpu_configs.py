@@ -65,6 +65,22 @@ def c4_index(amd):
     return build(amd, "IVF16384_HNSW32,Flat", 128, 1_000_000, 638_976)
 
 
+@pytest.mark.parametrize("ef", [16, 64])
+def test_c4_device_entry_point(amd, orc, gpu, c4_index, ef):
+    """c4 through Index::search_device (bench.py's step), where the HNSW
+    quantizer's tie re-runs overlap the scan of the other queries."""
+    from conftest import device_search
+    d, nq = 128, 2000
+    idx = c4_index
+    idx.nprobe = 64
+    amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", ef)
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    D, I = device_search(idx, xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, 64, efSearch=ef, nslices=1)
+    check(D, I, Dr, Ir, f"c4 device efSearch {ef}")
+
+
 @pytest.mark.parametrize("ef", [16, 64, 128])
 def test_c4_hnsw32_ivf16384(amd, orc, gpu, c4_index, ef):
     d, nq = 128, 2000

@@ -156,6 +156,23 @@ def test_gpu_hnsw_ivf_equals_reference(amd, gpu, monkeypatch, ef, nprobe, path_)
     eq(D, I, f"hnswivf_ef{ef}_{nprobe}")
 
 
+@pytest.mark.parametrize("ef", [16, 64])
+@pytest.mark.parametrize("nprobe", [8, 100])
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_gpu_hnsw_ivf_device_equals_reference(amd, gpu, monkeypatch, ef, nprobe, defer):
+    """The device entry point (bench.py's step): the HNSW quantizer's tie
+    re-runs overlapped with the scan of the other queries (defer=1, the
+    default) or run before it (FAISS_AMD_HNSW_DEFER=0); both equal the
+    reference's IndexIVF::search."""
+    from conftest import device_search
+    monkeypatch.setenv("FAISS_AMD_HNSW_DEFER", defer)
+    idx = amd.read_index(path("hnswivf"))
+    idx.quantizer.efSearch = ef
+    idx.nprobe = nprobe
+    D, I = device_search(idx, FX["hnswivf_xq"], 10)
+    eq(D, I, f"hnswivf_ef{ef}_{nprobe}")
+
+
 @pytest.mark.parametrize("ef", [8, 32, 200])
 @pytest.mark.parametrize("k", [1, 10, 40])
 @pytest.mark.parametrize("path_", ["batched", "sequential"])
