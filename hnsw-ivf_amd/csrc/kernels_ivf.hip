@@ -106,6 +106,13 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
     __shared__ uint32_t wb[16], wi[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     constexpr int CH = 1024 * E;
+    static_assert(E % 4 == 0, "E counts per thread as uint4 groups");
+    // items of a bucket of c entries: ceil(c / QT), a shift when QT is a power
+    // of two (every caller's), else a division
+    const int qs = (QT & (QT - 1)) == 0 ? __builtin_ctz((unsigned)QT) : -1;
+    auto nitems = [&](uint32_t c) -> uint32_t {
+        return qs >= 0 ? (c + (uint32_t)QT - 1u) >> qs : (c + (uint32_t)QT - 1u) / (uint32_t)QT;
+    };
     // prefix of the thread sums (v[] per thread) over the work group: returns
     // this thread's exclusive prefix and the chunk total
     auto block_scan = [&](uint32_t sb, uint32_t si, uint32_t& pb, uint32_t& pi, uint32_t& tb,
@@ -144,33 +151,68 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
         const int l0 = c0 + E * t;
         uint32_t c[E];
         uint32_t sb = 0, si = 0;
+        const bool full = l0 + E <= nlist;  // this thread's E lists exist (uint4 access)
+        if (full) {
 #pragma unroll
-        for (int j = 0; j < E; j++) c[j] = l0 + j < nlist ? counts[l0 + j] : 0u;
+            for (int v = 0; v < E / 4; v++) {
+                const uint4 c4 = *(const uint4*)(counts + l0 + 4 * v);
+                c[4 * v] = c4.x;
+                c[4 * v + 1] = c4.y;
+                c[4 * v + 2] = c4.z;
+                c[4 * v + 3] = c4.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < E; j++) c[j] = l0 + j < nlist ? counts[l0 + j] : 0u;
+        }
+        // zero_next == counts: each count is cleared once read (the fill
+        // takes the bucket sizes from bucket_off)
+        if (zero_next) {
+            if (full) {
+#pragma unroll
+                for (int v = 0; v < E / 4; v++)
+                    *(uint4*)(zero_next + l0 + 4 * v) = make_uint4(0u, 0u, 0u, 0u);
+            } else {
+                for (int j = 0; j < E && l0 + j < nlist; j++) zero_next[l0 + j] = 0u;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < E; j++) {
-            // zero_next == counts: each count is cleared once read (the fill
-            // takes the bucket sizes from bucket_off)
-            if (zero_next && l0 + j < nlist) zero_next[l0 + j] = 0u;
             sb += c[j];
-            si += (c[j] + QT - 1) / QT;
+            si += nitems(c[j]);
         }
         uint32_t pb, pi, tb, ti;
         block_scan(sb, si, pb, pi, tb, ti);
         uint32_t rb = carry_b + pb, ri = carry_i + pi;  // exclusive prefix of this thread
+        uint32_t ob[E], oi[E];
 #pragma unroll
         for (int j = 0; j < E; j++) {
-            const uint32_t nj = (c[j] + QT - 1) / QT;
-            if (l0 + j < nlist) {
-                bucket_off[l0 + j] = rb;
-                item_off[l0 + j] = ri;
-            }
+            ob[j] = rb;
+            oi[j] = ri;
             rb += c[j];
-            ri += nj;
+            ri += nitems(c[j]);
+        }
+        if (full) {
+#pragma unroll
+            for (int v = 0; v < E / 4; v++) {
+                *(uint4*)(bucket_off + l0 + 4 * v) =
+                        make_uint4(ob[4 * v], ob[4 * v + 1], ob[4 * v + 2], ob[4 * v + 3]);
+                *(uint4*)(item_off + l0 + 4 * v) =
+                        make_uint4(oi[4 * v], oi[4 * v + 1], oi[4 * v + 2], oi[4 * v + 3]);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < E; j++) {
+                if (l0 + j < nlist) {
+                    bucket_off[l0 + j] = ob[j];
+                    item_off[l0 + j] = oi[j];
+                }
+            }
         }
         if (item_list) {  // rare (item_list users); a second walk keeps the first lean
             ri = carry_i + pi;
             for (int j = 0; j < E && l0 + j < nlist; j++) {
-                const uint32_t nj = (c[j] + QT - 1) / QT;
+                const uint32_t nj = nitems(c[j]);
                 for (uint32_t i = 0; i < nj; i++) item_list[ri + i] = (uint32_t)(l0 + j);
                 ri += nj;
             }
@@ -193,11 +235,22 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict
         const int i0 = c0 + E * t;
         int ls[E];
         uint32_t n[E], si = 0;
+        if (i0 + E <= nlist) {
 #pragma unroll
-        for (int j = 0; j < E; j++) ls[j] = i0 + j < nlist ? (int)perm[i0 + j] : -1;
+            for (int v = 0; v < E / 4; v++) {
+                const uint4 p4 = *(const uint4*)(perm + i0 + 4 * v);
+                ls[4 * v] = (int)p4.x;
+                ls[4 * v + 1] = (int)p4.y;
+                ls[4 * v + 2] = (int)p4.z;
+                ls[4 * v + 3] = (int)p4.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < E; j++) ls[j] = i0 + j < nlist ? (int)perm[i0 + j] : -1;
+        }
 #pragma unroll
         for (int j = 0; j < E; j++) {
-            n[j] = ls[j] >= 0 ? (bucket_off[ls[j] + 1] - bucket_off[ls[j]] + QT - 1) / QT : 0u;
+            n[j] = ls[j] >= 0 ? nitems(bucket_off[ls[j] + 1] - bucket_off[ls[j]]) : 0u;
             si += n[j];
         }
         uint32_t pb, pi, tb, ti;
@@ -374,9 +427,12 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
     k_bucket_scan<E><<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off,         \
                                                     b.item_off, b.item_list, b.counts_next,    \
                                                     b.item_ctr, b.perm)
-    if (nlist <= 4096) BSCAN(4);
-    else if (nlist <= 16384) BSCAN(16);
-    else BSCAN(16);
+    // counts per thread: 4 up to 4096 lists, else 16 (FAISS_AMD_SCAN_E: tuning)
+    const char* se = getenv("FAISS_AMD_SCAN_E");
+    const int E = se ? atoi(se) : nlist <= 4096 ? 4 : 16;
+    if (E >= 16) BSCAN(16);
+    else if (E >= 8) BSCAN(8);
+    else BSCAN(4);
 #undef BSCAN
     HIP_LAUNCH_CHECK();
     if (total > 0) {
