@@ -84,10 +84,16 @@ def pmc_traffic(config, kernel_sub):
         return None, None
     with open(files[-1]) as f:
         summ = json.load(f)
+    # several instantiations can match (e.g. the coarse filter of k-means
+    # assignment during the build): the search's is the one launched least
+    best = None
     for name, ent in summ.items():
         if kernel_sub in name and "hbm_bytes" in ent:
-            return ent["hbm_bytes"], os.path.relpath(files[-1], ROOT)
-    return None, None
+            if best is None or ent.get("launches", 0) < best.get("launches", 0):
+                best = ent
+    if best is None:
+        return None, None
+    return best["hbm_bytes"], os.path.relpath(files[-1], ROOT)
 
 
 def log(*a):
