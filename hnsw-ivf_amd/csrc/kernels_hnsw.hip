@@ -268,11 +268,27 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
                 fresh = (old & bit) == 0;
             }
             float dis = WS_INF;
-            if (fresh) dis = l2_row(qs, g.storage + (int64_t)v * g.ld, g.d);
             const unsigned long long fm = __ballot(fresh);
             st_ndis += (uint32_t)__popcll(fm);
             st_nhops += 1;  // nstep
             if (fm == 0ull) continue;
+            if (g.d <= 128) {
+                // the fresh neighbours compacted to lanes 0..nf-1 (a hop's
+                // neighbours are one batch: their lane order is immaterial)
+                // and evaluated 4 lanes per row, 16 rows per pass, in the
+                // reference order: a wave-instruction stream of ~16 rows'
+                // cost per pass instead of one full row per lane
+                const int nf = __popcll(fm);
+                const unsigned long long lt = (1ull << lane) - 1ull;
+                const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
+                v = __builtin_amdgcn_ds_permute(dst << 2, v);
+                fresh = lane < nf;
+                dis = ref_rows64_4lane<true, 16>(qs, qs, g.storage, g.ld, g.d,
+                                                 fresh ? (uint32_t)v : 0u, fresh, lane);
+                if (!fresh) dis = WS_INF;
+            } else if (fresh) {
+                dis = l2_row(qs, g.storage + (int64_t)v * g.ld, g.d);
+            }
             // Ties: the sequential heaps (strict admission, MinimaxHeap's
             // push / pop_min rules) and the batched union agree only for
             // distinct distances.  A fresh distance equal to the current k-th

@@ -92,5 +92,65 @@ struct RefAcc8 {
     }
 };
 
+// Exact reference-order distance of the row `grow` each lane names (valid
+// lanes only), 16 rows per pass, 4 lanes per row: lane j' of row g owns the
+// reference's partial sums c[2j'] and c[2j'+1] (dims 8m + 2j' + {0,1}) and
+// loads those float2 pairs straight from the arena — one load instruction
+// covers 16 rows x 32 contiguous bytes, the 4 lanes of a row complete its
+// cache lines.  x_j = c_j + c_{j+4}, then (x0 + x2) + (x1 + x3) (ref_arith.h
+// order), then the epilogue dims.  No LDS staging and no barriers.  XM = max dims / 8
+// (the query copy xr holds at least 8 XM floats).  Used by the IVF re-rank
+// (kernels_ivf_mfma.hip) and the HNSW hop (kernels_hnsw.hip).
+template <bool L2, int XM>
+__device__ __forceinline__ float ref_rows64_4lane(const float* xr /* LDS copy of the query */,
+                                                    const float* __restrict__ xq,
+                                                    const float* __restrict__ codes, int ldc,
+                                                    int d, uint32_t grow, bool valid, int lane) {
+    const int g = lane >> 2, jp = lane & 3;
+    const int n8 = d & ~7, nm = n8 >> 3;
+    const unsigned long long vm = __ballot(valid);
+    float out = 0.f;
+#pragma unroll 1
+    for (int p = 0; p < 4; p++) {
+        if (((vm >> (16 * p)) & 0xffffull) == 0ull) continue;  // wave-uniform
+        const uint32_t rg = __shfl(grow, 16 * p + g);
+        const bool rv = (vm >> (16 * p + g)) & 1ull;
+        const float* yr = codes + (int64_t)(rv ? rg : 0u) * ldc;
+        float2 yv[XM];
+#pragma unroll
+        for (int m = 0; m < XM; m++)
+            yv[m] = m < nm ? *(const float2*)(yr + 8 * m + 2 * jp) : make_float2(0.f, 0.f);
+        const float* xj = xr + 2 * jp;
+        float ca = 0.f, cb = 0.f;
+#pragma unroll
+        for (int m = 0; m < XM; m++) {
+            const float2 xv = *(const float2*)(xj + 8 * m);
+            const float ta = ref_term_fma<L2>(xv.x, yv[m].x, ca);
+            const float tb = ref_term_fma<L2>(xv.y, yv[m].y, cb);
+            ca = m < nm ? ta : ca;
+            cb = m < nm ? tb : cb;
+        }
+        ca += __shfl_xor(ca, 2);
+        cb += __shfl_xor(cb, 2);
+        ca += __shfl_xor(ca, 1);  // x0 + x2
+        cb += __shfl_xor(cb, 1);  // x1 + x3
+        float r = ca + cb;
+        if (n8 < d) {
+            int i = n8;
+            if (d - n8 >= 4) {
+                const float e0 = ref_term<L2>(xq[n8], yr[n8]), e1 = ref_term<L2>(xq[n8 + 1], yr[n8 + 1]);
+                const float e2 = ref_term<L2>(xq[n8 + 2], yr[n8 + 2]);
+                const float e3 = ref_term<L2>(xq[n8 + 3], yr[n8 + 3]);
+                r = r + ((e0 + e2) + (e1 + e3));
+                i += 4;
+            }
+            for (; i < d; i++) r = ref_term_fma<L2>(xq[i], yr[i], r);
+        }
+        const float got = __shfl(r, 4 * (lane & 15));
+        if ((lane >> 4) == p) out = got;
+    }
+    return out;
+}
+
 }  // namespace kern
 }  // namespace faiss_amd
