@@ -65,6 +65,7 @@ CONFIGS = {
 }
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector == fp32 MFMA peak
 PEAK_HBM_GBS = 8000.0
+PEAK_L2_GBS = 34500.0      # MI355X_MICROARCH.md: aggregate L2 (4 MiB per XCD), measured
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 # kernel stage (library timer name) -> device symbol substring of its kernel
 # in the committed rocprofv3 PMC summaries
@@ -216,10 +217,14 @@ def kernel_roofline(name, ms, work, config):
              "unit": "TFLOP/s", "mfma_dtype": "bf16", "algorithmic_flops_per_step": f,
              "flops_per_query_centroid": 6 * work["dpad16"]}
     elif name == "hnsw_search" and work.get("hnsw_ndis"):
-        # every distance reads one fp32 vector of the graph's storage
+        # every distance reads one fp32 vector of the graph's storage; the
+        # storage (c4: 16384 centroids, 8 MB) lives in the on-chip caches
+        # (4 MiB L2 per XCD, the 256 MiB Infinity Cache), so the bytes are
+        # priced against the aggregate L2 bandwidth, not HBM
         b = work["hnsw_ndis"] * 4.0 * work["d"]
-        r = {"bound": "hbm", "achieved": b / t / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-             "algorithmic_bytes_per_step": b, "hnsw_ndis_per_step": work["hnsw_ndis"]}
+        r = {"bound": "l2", "achieved": b / t / 1e9, "peak": PEAK_L2_GBS, "unit": "GB/s",
+             "algorithmic_bytes_per_step": b, "hnsw_ndis_per_step": work["hnsw_ndis"],
+             "hbm_frac_if_from_hbm": b / t / 1e9 / PEAK_HBM_GBS}
     if r is None:
         return None
     r["frac"] = r["achieved"] / r["peak"]
