@@ -102,10 +102,10 @@ struct DeviceBuffer {
     void release() {
         if (ptr) {
             int cur = 0;
-            hipGetDevice(&cur);
-            if (device >= 0 && device != cur) hipSetDevice(device);
-            hipFree(ptr);
-            if (device >= 0 && device != cur) hipSetDevice(cur);
+            (void)hipGetDevice(&cur);
+            if (device >= 0 && device != cur) (void)hipSetDevice(device);
+            (void)hipFree(ptr);
+            if (device >= 0 && device != cur) (void)hipSetDevice(cur);
             ptr = nullptr;
             bytes = 0;
         }

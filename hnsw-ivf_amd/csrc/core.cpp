@@ -146,6 +146,7 @@ void IndexFlat::add(idx_t n, const float* x) {
     FAISS_THROW_IF_NOT(n >= 0);
     xb.insert(xb.end(), x, x + (size_t)n * d);
     ntotal += n;
+    version_++;
     std::lock_guard<std::recursive_mutex> g(mu_);
     dirty_ = true;
 }
@@ -153,6 +154,7 @@ void IndexFlat::add(idx_t n, const float* x) {
 void IndexFlat::reset() {
     xb.clear();
     ntotal = 0;
+    version_++;
     std::lock_guard<std::recursive_mutex> g(mu_);
     dirty_ = true;
 }

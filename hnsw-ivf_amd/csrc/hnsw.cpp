@@ -317,6 +317,7 @@ void IndexHNSW::add(idx_t n, const float* x) {
         for (int j = i0; j < i1; j++) bld.add_point(order[j], hnsw.levels[order[j]] - 1);
         i1 = i0;
     }
+    version_++;
     std::lock_guard<std::recursive_mutex> g(mu_);
     dirty_ = true;
 }
@@ -325,6 +326,7 @@ void IndexHNSW::reset() {
     hnsw = HNSW((int)(hnsw.cum_nneighbor_per_level.size() > 1 ? hnsw.nb_neighbors(1) : 32));
     storage->reset();
     ntotal = 0;
+    version_++;
     std::lock_guard<std::recursive_mutex> g(mu_);
     dirty_ = true;
 }

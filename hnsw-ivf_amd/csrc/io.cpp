@@ -64,10 +64,12 @@ std::string fourcc_str(uint32_t h) {
 // an index back to the file it was mapped from (IO_FLAG_MMAP, or an ilod data
 // file) must not truncate the mapping it is reading the lists through (the
 // old inode stays alive while mapped).  Removed again when not committed.
-// Only an existing regular file is replaced this way (through a symlink, the
-// file it names, keeping its mode); a new name, a FIFO, a device such as
-// /dev/stdout, or a directory where no temporary can be created is written in
-// place, as fopen(path, "wb") would.
+// An existing regular file is replaced this way (through a symlink, the file
+// it names, keeping its mode), and so is a new name (mode 0666 & ~umask, as
+// fopen would create it), so a failed write never leaves a truncated file
+// under the final name.  A FIFO, a device such as /dev/stdout, or a directory
+// where no temporary can be created is written in place, as fopen(path, "wb")
+// would.
 struct AtomicFile {
     std::string target, tmp;
     FILE* f = nullptr;
@@ -75,12 +77,20 @@ struct AtomicFile {
     mode_t mode = 0;
     explicit AtomicFile(const std::string& path) : target(path) {
         struct stat st;
-        if (stat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode)) {
-            if (char* rp = realpath(path.c_str(), nullptr)) {
-                target = rp;
-                free(rp);
+        const bool exists = stat(path.c_str(), &st) == 0;
+        const bool fresh = !exists && errno == ENOENT;
+        if ((exists && S_ISREG(st.st_mode)) || fresh) {
+            if (exists) {
+                if (char* rp = realpath(path.c_str(), nullptr)) {
+                    target = rp;
+                    free(rp);
+                }
+                mode = st.st_mode & 07777;
+            } else {
+                const mode_t um = umask(0);
+                umask(um);
+                mode = 0666 & ~um;
             }
-            mode = st.st_mode & 07777;
             tmp = target + ".tmpXXXXXX";
             const int fd = mkstemp(&tmp[0]);
             if (fd >= 0) {

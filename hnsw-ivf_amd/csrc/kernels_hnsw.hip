@@ -22,6 +22,7 @@
 // are one sequential fma chain per lane, the same order as the CPU oracle.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cstdio>
 #include <cstdlib>
@@ -672,77 +673,343 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
     }
 }
 
-// The same sequential search for ef, k <= 64 with both heaps in registers:
-// slot s of a heap is lane s's register, and the reference's sift loops
-// (hx_push / hx_pop / hx_replace_top, index for index) run in scalar control
-// flow over v_readlane and a lane-select write — a few cycles per level instead of two
-// dependent LDS round trips, which is what paced the LDS form (a query is one
-// wave running ~100 hops of serial heap updates).
+// The same sequential search for ef, k <= 64 with both heaps in registers.
+// A heap entry is one 64-bit key: the distance's bits (>= 0: they order as
+// unsigned) over the id biased by 2^31, so faiss's cmp2 (dis, then id) is a
+// single unsigned compare.  The candidate MinimaxHeap keeps faiss's binary-
+// heap layout exactly (pop_min's tie rule and heap_pop's choice among equal
+// tops depend on it): heap position p (1-based, faiss/utils/Heap.h) lives in
+// lane p & 63 (position 64 in lane 0), so siblings 2f, 2f + 1 are a DPP lane
+// pair, and ballots rotated right by one put position p at bit p - 1.  Each
+// of heap_push / heap_pop is a few wave-wide steps with the serial loop's
+// exact outcome (tests/test_hnsw_wave_heap.py restates them lane by lane
+// against the serial loops, dead MinimaxHeap slots and ties included).
 namespace {
-struct LaneHeap {
-    float v;    // this lane's slot: distance
-    int32_t i;  // id
-    __device__ __forceinline__ float rv(int s) const {
-        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), s));
-    }
-    __device__ __forceinline__ int32_t ri(int s) const { return __builtin_amdgcn_readlane(i, s); }
-    __device__ __forceinline__ void w(int s, float val, int32_t id) {
-        const bool me = (int)threadIdx.x == s;  // one wave per block
-        v = me ? val : v;
-        i = me ? id : i;
-    }
-    // 1-based positions as in faiss/utils/Heap.h; position p is slot p - 1
-    __device__ void push(int k, float val, int32_t id) {  // hx_push
-        int p = k;
-        while (p > 1) {
-            const int f = p >> 1;
-            const float fv = rv(f - 1);
-            const int32_t fi = ri(f - 1);
-            if (!cmp2_gt(val, fv, id, fi)) break;
-            w(p - 1, fv, fi);
-            p = f;
-        }
-        w(p - 1, val, id);
-    }
-    __device__ int sift(int k, float val, int32_t id) {  // hx_pop / hx_replace_top loop
+__device__ __forceinline__ uint64_t hkey(float d, int32_t id) {
+    return ((uint64_t)(uint32_t)__float_as_int(d) << 32) | (uint32_t)(id ^ 0x80000000);
+}
+__device__ __forceinline__ float hkey_dis(uint64_t k) { return __int_as_float((int)(k >> 32)); }
+__device__ __forceinline__ int32_t hkey_id(uint64_t k) { return (int32_t)((uint32_t)k ^ 0x80000000u); }
+constexpr uint32_t HKEY_DEAD_LO = 0x7fffffffu;  // id -1
+__device__ __forceinline__ uint64_t rotr1(uint64_t m) { return (m >> 1) | (m << 63); }
+__device__ __forceinline__ uint64_t rotl1(uint64_t m) { return (m << 1) | (m >> 63); }
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, int src_lane) {
+    const uint32_t lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)v, CTRL, 0xf, 0xf, false);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(v >> 32), CTRL, 0xf, 0xf, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+struct KHeap {
+    uint64_t key;  // lane L: heap position L ? L : 64
+    __device__ __forceinline__ uint64_t at(int p) const { return rdlane64(key, p & 63); }
+    // heap_push(k, ...) (Heap.h): position k takes the new key and climbs
+    // while it beats its parent: the climb stops below the deepest ancestor
+    // it does not beat (one ballot), the path below moves down one level
+    __device__ __forceinline__ void push(int k, uint64_t nk, int lane) {
+        const int s = lane ? lane : 64;
+        const int dk = 31 - __builtin_clz((unsigned)k);
+        const int ds = 31 - __builtin_clz((unsigned)s);
+        const bool anc = s < k && (k >> (dk - ds)) == s;
+        const uint64_t nbt = rotr1(__ballot(anc && !(nk > key)));
         int p = 1;
-        for (;;) {
-            const int p1 = p << 1, p2 = p1 + 1;
-            if (p1 > k) break;
-            const float v1 = rv(p1 - 1);
-            const int32_t i1 = ri(p1 - 1);
-            if (p2 == k + 1) {
-                if (cmp2_gt(val, v1, id, i1)) break;
-                w(p - 1, v1, i1);
-                p = p1;
-                continue;
-            }
-            const float v2 = rv(p2 - 1);
-            const int32_t i2 = ri(p2 - 1);
-            if (cmp2_gt(v1, v2, i1, i2)) {
-                if (cmp2_gt(val, v1, id, i1)) break;
-                w(p - 1, v1, i1);
-                p = p1;
-            } else {
-                if (cmp2_gt(val, v2, id, i2)) break;
-                w(p - 1, v2, i2);
-                p = p2;
-            }
+        if (nbt) {
+            const int f = 64 - __builtin_clzll(nbt);  // deepest ancestor not beaten
+            p = k >> (dk - (31 - __builtin_clz((unsigned)f)) - 1);
         }
-        return p;
+        const uint64_t pk = bperm64(key, (s >> 1) & 63);
+        key = ((s == k || anc) && s > p) ? pk : (s == p ? nk : key);
     }
-    __device__ void pop(int k) {  // hx_pop: the top leaves, slot k - 1 is stale
-        const int p = sift(k, rv(k - 1), ri(k - 1));
-        w(p - 1, rv(k - 1), ri(k - 1));
+    // the sift of heap_pop / heap_replace_top over positions 1..k: the
+    // serial descent follows the larger child (siblings by DPP, the path by a
+    // scalar walk of one ballot), stops at the first path node nk beats; the
+    // nodes above it move up one level and nk takes the freed position
+    __device__ __forceinline__ void sift(int k, uint64_t nk, int lane) {
+        const int s = lane ? lane : 64;
+        const uint64_t sk = dpp64<0xB1>(key);  // quad_perm [1,0,3,2]: lane ^ 1
+        bool larger = (s & 1) ? !(sk > key) : (s == k || key > sk);
+        larger = larger && s >= 2 && s <= k;
+        const uint64_t lm = rotr1(__ballot(larger));
+        uint64_t path = 0;
+        for (int c = 1; 2 * c <= k;) {
+            c = ((lm >> ((2 * c - 1) & 63)) & 1ull) ? 2 * c : 2 * c + 1;
+            path |= 1ull << ((c - 1) & 63);
+        }
+        const uint64_t stop = rotr1(__ballot(((rotl1(path) >> lane) & 1ull) && nk > key));
+        const uint64_t moved = stop ? (path & ((stop & (~stop + 1ull)) - 1ull)) : path;
+        const int p = moved ? 64 - __builtin_clzll(moved) : 1;
+        const int c2 = 2 * s;
+        const bool m0 = c2 <= 64 && ((moved >> ((c2 - 1) & 63)) & 1ull);
+        const bool m1 = c2 < 64 && ((moved >> (c2 & 63)) & 1ull);
+        const uint64_t ck = bperm64(key, (m1 ? c2 + 1 : c2) & 63);
+        key = (m0 || m1) ? ck : (s == p ? nk : key);
     }
-    __device__ void replace_top(int k, float val, int32_t id) {
-        const int p = sift(k, val, id);
-        w(p - 1, val, id);
+    __device__ __forceinline__ void pop(int k, int lane) { sift(k, at(k), lane); }  // heap_pop
+};
+
+// minimum of a 32-bit unsigned key over the wave (every lane active): DPP
+// within quads, half-rows and rows, then the four row minima as scalars
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xf, 0xf, false));   // quad [1,0,3,2]
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xf, 0xf, false));   // quad [2,3,0,1]
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x141, 0xf, 0xf, false));  // half-row mirror
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x140, 0xf, 0xf, false));  // row mirror
+    const uint32_t a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
+    const uint32_t c = __builtin_amdgcn_readlane(x, 32), e = __builtin_amdgcn_readlane(x, 48);
+    return min(min(a, b), min(c, e));
+}
+// The result heap of search_from_candidates (HeapBlockResultHandler<CMax>,
+// faiss/impl/ResultHandler.h + heap_replace_top, faiss/utils/Heap.h:112-149)
+// as a sorted queue: lane j holds the j-th smallest key of the k kept.  Its
+// observable behaviour depends on the kept set only — admission is
+// `dis < top.dis`, replace_top evicts the top, the unique cmp2-largest key
+// (a valid heap: no slot is ever killed), heap_reorder emits the set in
+// ascending order — so the sorted set gives the reference's result exactly,
+// with an insert of one ballot and one DPP shift.
+struct SortedQ {
+    uint64_t key;
+    // nk whose dis is below the k-th kept dis: the largest leaves
+    __device__ __forceinline__ void insert(int k, uint64_t nk, int lane) {
+        const int pos = __popcll(__ballot(lane < k && key < nk));
+        const uint64_t up = dpp64<0x138>(key);  // wave_shr:1
+        key = lane > pos ? up : (lane == pos ? nk : key);
+    }
+};
+// The candidate MinimaxHeap (faiss/impl/HNSW.cpp:1096-1342) of the register
+// kernel, in two forms with one interface.
+//  * CandLayout keeps faiss's heap array (KHeap): exact in every case.
+//  * CandSet keeps the entries sorted by distance in lanes 0..hk-1 (one
+//    ballot + one DPP shift per update).  The MinimaxHeap's observable
+//    decisions depend on its entry set alone, except two that read the heap
+//    layout: pop_min among several alive entries of the smallest distance
+//    (the highest slot wins) and heap_pop of a full heap whose largest
+//    distance is shared (which of them is the top).  CandSet reports either
+//    case (returns false) and the query is searched again with CandLayout;
+//    otherwise it evolves exactly as the heap's set does.
+struct CandLayout {
+    KHeap h;
+    int hk;
+    __device__ __forceinline__ void init() {
+        h.key = hkey(FLT_MAX, -1);
+        hk = 0;
+    }
+    __device__ __forceinline__ void seed(uint64_t nk, int lane) { h.push(++hk, nk, lane); }
+    __device__ __forceinline__ float top_dis() const { return hkey_dis(h.at(1)); }
+    // pop_min + count_below(d0) (:1299-1342): the smallest alive distance,
+    // the highest position among equal ones (distances >= 0: their bits
+    // order as unsigned)
+    __device__ __forceinline__ bool pop_min(int lane, int32_t& v0, int& nb) {
+        const int spos = lane ? lane : 64;
+        const uint32_t chi = (uint32_t)(h.key >> 32);
+        const bool alive = spos <= hk && (uint32_t)h.key != HKEY_DEAD_LO;
+        const uint32_t kmin = wave_min_u32(alive ? chi : 0xffffffffu);
+        const uint64_t at = rotr1(__ballot(alive && chi == kmin));
+        const int bpos = 64 - __builtin_clzll(at);
+        v0 = hkey_id(h.at(bpos));
+        nb = __popcll(__ballot(spos <= hk && chi < kmin));
+        if (spos == bpos) h.key = (h.key & 0xffffffff00000000ull) | HKEY_DEAD_LO;
+        return true;
+    }
+    // MinimaxHeap::push (:1096-1107)
+    __device__ __forceinline__ bool push(int ef, uint64_t nk, float dis, int& nvalid, int lane) {
+        if (hk == ef) {
+            const uint64_t top = h.at(1);
+            if (dis >= hkey_dis(top)) return true;
+            if ((uint32_t)top != HKEY_DEAD_LO) --nvalid;
+            h.pop(hk--, lane);
+        }
+        h.push(++hk, nk, lane);
+        ++nvalid;
+        return true;
+    }
+};
+struct CandSet {
+    uint64_t key;  // lane j < hk: the j-th entry by distance
+    int hk;
+    __device__ __forceinline__ void init() {
+        key = hkey(FLT_MAX, -1);
+        hk = 0;
+    }
+    __device__ __forceinline__ void insert(int n, uint64_t nk, int lane) {
+        // into lanes 0..n (n entries kept sorted; lane n is free)
+        const int pos = __popcll(__ballot(lane < n && key < nk));
+        const uint64_t up = dpp64<0x138>(key);  // wave_shr:1
+        key = lane > pos ? up : (lane == pos ? nk : key);
+    }
+    __device__ __forceinline__ void seed(uint64_t nk, int lane) { insert(hk++, nk, lane); }
+    __device__ __forceinline__ float top_dis() const { return hkey_dis(rdlane64(key, hk - 1)); }
+    __device__ __forceinline__ bool pop_min(int lane, int32_t& v0, int& nb) {
+        const uint32_t chi = (uint32_t)(key >> 32);
+        const bool alive = lane < hk && (uint32_t)key != HKEY_DEAD_LO;
+        const unsigned long long am = __ballot(alive);
+        const int first = __builtin_ctzll(am);  // the sorted order: the smallest alive
+        const uint32_t kmin = __builtin_amdgcn_readlane(chi, first);
+        if (__popcll(__ballot(alive && chi == kmin)) > 1) return false;  // layout decides
+        v0 = hkey_id(rdlane64(key, first));
+        nb = __popcll(__ballot(lane < hk && chi < kmin));
+        if (lane == first) key = (key & 0xffffffff00000000ull) | HKEY_DEAD_LO;
+        return true;
+    }
+    __device__ __forceinline__ bool push(int ef, uint64_t nk, float dis, int& nvalid, int lane) {
+        if (hk == ef) {
+            const uint64_t top = rdlane64(key, hk - 1);
+            if (dis >= hkey_dis(top)) return true;
+            // the heap's top among several entries of the largest distance
+            // depends on its layout
+            if (hk >= 2 && (uint32_t)(rdlane64(key, hk - 2) >> 32) == (uint32_t)(top >> 32))
+                return false;
+            if ((uint32_t)top != HKEY_DEAD_LO) --nvalid;
+            insert(hk - 1, nk, lane);  // the top leaves, nk enters
+        } else {
+            insert(hk++, nk, lane);
+        }
+        ++nvalid;
+        return true;
     }
 };
 }  // namespace
 
-template <bool LDS_VISITED>
+// the register kernel's query copy: ld floats, at least 128 for ref_rows64_4lane
+__host__ __device__ inline int exact_reg_qpad(const HNSWDevice& g) {
+    return g.ld < 128 ? 128 : g.ld;
+}
+
+// passes of 16 rows whose loads the register kernel issues together
+#ifndef HNSW_PB
+#define HNSW_PB 2
+#endif
+// Trace of the register kernel (FAISS_AMD_HNSW_TRACE=<file>, profiling): per
+// query the core-clock cycles of each level-0 hop phase summed over its hops:
+// [0] pop_min + count_below, [1] neighbour ids, [2] visited test-and-set,
+// [3] distances, [4] heap updates, [5] hops, [6] fresh neighbours, [7] whole
+// query, [8] 1 if the query was searched again with the heap layout
+struct HopTrace {
+    unsigned long long t[16];
+    unsigned long long tc;
+    __device__ __forceinline__ void tick(int ph) {
+        const unsigned long long n = clock64();
+        t[ph] += n - tc;
+        tc = n;
+    }
+};
+
+// search_from_candidates at level 0 (faiss/impl/HNSW.cpp:605-741) from the
+// greedy descent's entry, with the candidate structure CQ; false when CQ
+// (CandSet) met a decision that depends on the heap layout (nothing written)
+template <class CQ, bool TRACE>
+__device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs, uint32_t* vis,
+                                            int k, int efSearch, int ef, int lane, int nearest,
+                                            float d_nearest, SortedQ& R, uint32_t& st_n2,
+                                            uint32_t& st_ndis, uint32_t& st_nhops, HopTrace& tr) {
+    CQ C;
+    C.init();
+    int nvalid = 1;
+    C.seed(hkey(d_nearest, nearest), lane);
+    // (:624-637): the seed enters the results
+    if (d_nearest < FLT_MAX) R.insert(k, hkey(d_nearest, nearest), lane);
+    float rmax = hkey_dis(rdlane64(R.key, k - 1));
+    if (lane == 0) vis[nearest >> 5] |= 1u << (nearest & 31);
+    __syncthreads();
+    if (TRACE) tr.tick(7);
+    for (;;) {
+        if (nvalid <= 0) {  // candidates.size() == 0
+            st_n2 = 1;
+            break;
+        }
+        int32_t v0;
+        int nb;
+        if (!C.pop_min(lane, v0, nb)) return false;
+        nvalid--;
+        if (nb >= efSearch) {
+            st_n2 = nvalid == 0 ? 1u : 0u;
+            break;
+        }
+        if (TRACE) tr.tick(0);
+        // neighbours of v0 in stored order, fresh ones compacted to lanes
+        // 0..nf-1 (their arrival order)
+        const int cnt = g.cum_nb[1] - g.cum_nb[0];
+        int32_t v1 = -1;
+        if (lane < cnt)
+            v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
+                       : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
+        const unsigned long long neg =
+                __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
+        const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
+        if (TRACE) tr.tick(1);
+        // visited test-and-set: the bits as they were before this hop decide;
+        // a node listed twice in this neighbour list (the atomic then finds the
+        // bit another lane of this hop set) is visited at its first position,
+        // so only then the lanes are compared pairwise
+        const uint32_t vbit = 1u << (v1 & 31);
+        bool fresh = lane < jmax && !(vis[v1 >> 5] & vbit);
+        uint32_t old = 0u;
+        if (fresh) old = atomicOr(&vis[v1 >> 5], vbit);
+        if (__ballot(fresh && (old & vbit)) != 0ull)
+            for (int i = 0; i < jmax; i++)
+                fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
+        const unsigned long long fm = __ballot(fresh);
+        const int nf = __popcll(fm);
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
+        const int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
+        if (TRACE) tr.tick(2);
+        // 4 lanes per row, 16 rows per pass, two passes' loads in flight
+        // (reference order)
+        float fdis = 0.f;
+        if (g.d <= 128)
+            fdis = ref_rows64_4lane_pb<true, 16, HNSW_PB>(qs, qs, g.storage, g.ld, g.d,
+                                                    lane < nf ? (uint32_t)fv : 0u, nf, lane);
+        else if (lane < nf)
+            fdis = l2_row(qs, g.storage + (int64_t)fv * g.ld, g.d);
+        st_ndis += (uint32_t)nf;
+        st_nhops += 1;
+        if (TRACE) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            tr.tick(3);
+            tr.t[5] += 1;
+            tr.t[6] += (unsigned long long)nf;
+        }
+        // add_to_heap (:678-689) for each fresh neighbour in arrival order.
+        // Only arrivals that can change a heap are visited: the result admits
+        // dis < rmax (rmax only falls during the hop); a full candidate heap
+        // admits dis < its top (which only falls while full); a heap not yet
+        // full takes every arrival.
+        const bool full0 = C.hk == ef;
+        const float ctop0 = full0 ? C.top_dis() : FLT_MAX;
+        unsigned long long todo = __ballot(lane < nf && (!full0 || fdis < rmax || fdis < ctop0));
+        while (todo) {
+            const int t = __builtin_ctzll(todo);
+            todo &= todo - 1ull;
+            const int32_t vt = __builtin_amdgcn_readlane(fv, t);
+            const float dis = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), t));
+            const uint64_t nk = hkey(dis, vt);
+            if (dis < rmax) {
+                R.insert(k, nk, lane);
+                rmax = hkey_dis(rdlane64(R.key, k - 1));
+            }
+            if (!C.push(ef, nk, dis, nvalid, lane)) return false;
+        }
+        if (TRACE) tr.tick(4);
+    }
+    return true;
+}
+
+// The reference's HNSW::search for ef, k <= 64, one wave per query: the
+// greedy descent, then level 0 with the CandSet form; a query whose search
+// meets a layout-dependent tie is searched again with CandLayout (layout = 1:
+// every query with CandLayout — tests).  Results are the reference's, bit for
+// bit, either way.
+template <bool LDS_VISITED, bool TRACE = false>
 __global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float* __restrict__ x,
                                                        int ldx, int64_t n, int k, int efSearch,
                                                        int ef, float* __restrict__ D,
@@ -752,23 +1019,29 @@ __global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float
                                                        int64_t vwords,
                                                        unsigned long long* __restrict__ stats,
                                                        const uint32_t* __restrict__ only,
-        const uint32_t* __restrict__ qidx) {
+                                                       const uint32_t* __restrict__ qidx, int layout,
+                                                       unsigned long long* __restrict__ trace) {
     // qidx: compact launch over listed queries (input row qidx[b], output
     // row b); else query b, output row b
     const int64_t q = qidx ? (int64_t)qidx[blockIdx.x] : (int64_t)blockIdx.x;
     const int64_t qo = blockIdx.x;
     if (only && only[q] == 0u) return;
+    HopTrace tr;
+    if (TRACE) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) tr.t[j] = 0;
+        tr.tc = clock64();
+    }
+    const unsigned long long tq = TRACE ? tr.tc : 0ull;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* qs = sm;  // [ld]
-    uint32_t* vis = LDS_VISITED ? (uint32_t*)(sm + g.ld) : vis_global + blockIdx.x * vwords;
+    const int qpad = exact_reg_qpad(g);
+    float* qs = sm;  // [qpad]
+    uint32_t* vis = LDS_VISITED ? (uint32_t*)(sm + qpad) : vis_global + blockIdx.x * vwords;
     const int lane = threadIdx.x;
-    for (int j = lane; j < g.ld; j += 64) qs[j] = j < g.d ? x[q * ldx + j] : 0.f;
+    for (int j = lane; j < qpad; j += 64) qs[j] = j < g.d ? x[q * ldx + j] : 0.f;
     for (int64_t w = lane; w < vwords; w += 64) vis[w] = 0u;
-    LaneHeap C, R;  // MinimaxHeap candidates (size hk <= ef), results (k, heapified)
-    C.v = FLT_MAX;
-    C.i = -1;
-    R.v = FLT_MAX;  // heap_heapify<CMax> (Heap.h:316-339)
-    R.i = -1;
+    SortedQ R;  // results: heap_heapify<CMax> (Heap.h:316-339) = k x (FLT_MAX, -1)
+    R.key = hkey(FLT_MAX, -1);
     __syncthreads();
     uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0;
     if (g.entry_point >= 0) {
@@ -807,96 +1080,29 @@ __global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float
                 }
             }
         }
-        // ---- level 0: MinimaxHeap candidates(ef) seeded with the entry
-        int hk = 0, nvalid = 1;
-        C.push(++hk, d_nearest, nearest);
-        {  // search_from_candidates (:624-637): the seeds enter the results
-            float threshold = R.rv(0);
-            for (int s = 0; s < hk; s++) {
-                const int32_t v1 = C.ri(s);
-                const float dd = C.rv(s);
-                if (dd < threshold && R.rv(0) > dd) {
-                    R.replace_top(k, dd, v1);
-                    threshold = R.rv(0);
-                }
-                if (lane == 0) vis[v1 >> 5] |= 1u << (v1 & 31);
-            }
-        }
-        __syncthreads();
-        for (;;) {
-            if (nvalid <= 0) {  // candidates.size() == 0
-                st_n2 = 1;
-                break;
-            }
-            // pop_min (:1299-1330): smallest alive dis, highest slot among ties
-            float bd = FLT_MAX;
-            int bp = -1;
-            if (lane < hk && C.i != -1) {
-                bd = C.v;
-                bp = lane;
-            }
-#pragma unroll
-            for (int m = 32; m > 0; m >>= 1) {
-                const float od = __shfl_xor(bd, m);
-                const int op = __shfl_xor(bp, m);
-                if (op >= 0 && (bp < 0 || od < bd || (od == bd && op > bp))) {
-                    bd = od;
-                    bp = op;
-                }
-            }
-            bp = __builtin_amdgcn_readfirstlane(bp);
-            const int32_t v0 = C.ri(bp);
-            const float d0 = bd;
-            // count_below(d0): every slot, dead ones included
-            const int nb = __popcll(__ballot(lane < hk && C.v < d0));
-            C.i = lane == bp ? -1 : C.i;
-            nvalid--;
-            if (nb >= efSearch) {
-                st_n2 = nvalid == 0 ? 1u : 0u;
-                break;
-            }
-            // neighbours of v0 in stored order (parallel test-and-set, as in
-            // k_hnsw_exact), fresh ones compacted to lanes 0..nf-1
-            const int cnt = g.cum_nb[1] - g.cum_nb[0];
-            int32_t v1 = -1;
-            if (lane < cnt)
-                v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
-                           : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
-            const unsigned long long neg =
-                    __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
-            const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
-            bool fresh = lane < jmax && !((vis[v1 >> 5] >> (v1 & 31)) & 1u);
-            for (int i = 0; i < jmax; i++)
-                fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
+        // ---- level 0
+        const uint32_t up_ndis = st_ndis, up_nhops = st_nhops;
+        bool done = false;
+        if (!layout)
+            done = hnsw_level0<CandSet, TRACE>(g, qs, vis, k, efSearch, ef, lane, nearest,
+                                               d_nearest, R, st_n2, st_ndis, st_nhops, tr);
+        if (!done) {
+            // again with the heap layout: fresh visited table, results, counters
             __syncthreads();
-            if (fresh) atomicOr(&vis[v1 >> 5], 1u << (v1 & 31));
-            const unsigned long long fm = __ballot(fresh);
-            const int nf = __popcll(fm);
-            const unsigned long long lt = (1ull << lane) - 1ull;
-            const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
-            const int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
-            const float fdis = lane < nf ? l2_row(qs, g.storage + (int64_t)fv * g.ld, g.d) : 0.f;
-            st_ndis += (uint32_t)nf;
-            st_nhops += 1;
-            float threshold = R.rv(0);
-            for (int t = 0; t < nf; t++) {
-                const int32_t vt = __builtin_amdgcn_readlane(fv, t);
-                const float dis = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), t));
-                // add_to_heap (:678-689)
-                if (dis < threshold && R.rv(0) > dis) {
-                    R.replace_top(k, dis, vt);
-                    threshold = R.rv(0);
-                }
-                // MinimaxHeap::push (:1096-1107)
-                if (hk == ef) {
-                    if (dis >= C.rv(0)) continue;
-                    if (C.ri(0) != -1) --nvalid;
-                    C.pop(hk--);
-                }
-                C.push(++hk, dis, vt);
-                ++nvalid;
-            }
+            for (int64_t w = lane; w < vwords; w += 64) vis[w] = 0u;
+            R.key = hkey(FLT_MAX, -1);
+            st_n2 = 0;
+            st_ndis = up_ndis;
+            st_nhops = up_nhops;
+            if (TRACE) tr.t[8] = 1;
+            __syncthreads();
+            hnsw_level0<CandLayout, TRACE>(g, qs, vis, k, efSearch, ef, lane, nearest, d_nearest,
+                                           R, st_n2, st_ndis, st_nhops, tr);
         }
+    }
+    if (TRACE && lane == 0) {
+        tr.t[7] = clock64() - tq;
+        for (int j = 0; j < 16; j++) trace[qo * 16 + j] = tr.t[j];
     }
     if (stats && lane == 0 && g.entry_point >= 0) {
         atomicAdd(&stats[0], 1ull);
@@ -904,23 +1110,14 @@ __global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float
         atomicAdd(&stats[2], (unsigned long long)st_ndis);
         atomicAdd(&stats[3], (unsigned long long)st_nhops);
     }
-    // heap_reorder<CMax> (Heap.h:421-450), then the memmove to the front
-    int ii = 0;
-    for (int s = 0; s < k; s++) {
-        const float val = R.rv(0);
-        const int32_t id = R.ri(0);
-        R.pop(k - s);
-        R.w(k - ii - 1, val, id);
-        if (id != -1) ii++;
-    }
-    const float ov = __shfl(R.v, min(k - ii + lane, 63));
-    const int32_t oi = __shfl(R.i, min(k - ii + lane, 63));
+    // heap_reorder<CMax> (Heap.h:421-450): the kept (dis, id) ascending, the
+    // placeholders (id -1) after them as (FLT_MAX, -1)
     if (lane < k) {
-        const float dv = lane < ii ? ov : FLT_MAX;
-        const int32_t iv = lane < ii ? oi : -1;
+        const int32_t id = hkey_id(R.key);
+        const float dv = id != -1 ? hkey_dis(R.key) : FLT_MAX;
         if (D) D[qo * k + lane] = dv;
-        if (I) I[qo * k + lane] = iv;
-        if (I32) I32[qo * k + lane] = iv;
+        if (I) I[qo * k + lane] = id;
+        if (I32) I32[qo * k + lane] = id;
     }
 }
 
@@ -935,15 +1132,40 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
     const size_t lds_q = sizeof(float) * g.ld;
     const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
     const bool x_lds_vis = lds_x + vwords * 4 <= 64 * 1024;
-    const bool lds_vis = vwords * 4 <= 64 * 1024;
     if (ef <= 64 && k <= 64) {  // register heaps
-        if (lds_vis)
-            k_hnsw_exact_reg<true><<<dim3((unsigned)n), dim3(64), lds_q + vwords * 4, s>>>(
-                    g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx);
+        const size_t lds_r = sizeof(float) * exact_reg_qpad(g);
+        const bool rvis = lds_r + vwords * 4 <= 64 * 1024;
+        // FAISS_AMD_HNSW_LAYOUT=1: every query with the heap-layout form (tests)
+        const char* lenv = getenv("FAISS_AMD_HNSW_LAYOUT");
+        const int layout = lenv && !strcmp(lenv, "1") ? 1 : 0;
+        // FAISS_AMD_HNSW_TRACE=<file>: per-query hop-phase cycles (profiling)
+        const char* tenv = getenv("FAISS_AMD_HNSW_TRACE");
+        if (tenv && rvis) {
+            unsigned long long* tb = nullptr;
+            HIP_CHECK(hipMalloc(&tb, 128 * std::max<int64_t>(n, 1)));
+            HIP_CHECK(hipMemsetAsync(tb, 0, 128 * std::max<int64_t>(n, 1), s));
+            k_hnsw_exact_reg<true, true><<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4, s>>>(
+                    g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
+                    layout, tb);
+            HIP_LAUNCH_CHECK();
+            std::vector<unsigned long long> h((size_t)n * 16);
+            HIP_CHECK(hipMemcpyAsync(h.data(), tb, 128 * n, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            HIP_CHECK(hipFree(tb));
+            if (FILE* f = fopen(tenv, "ab")) {
+                fwrite(h.data(), 128, n, f);
+                fclose(f);
+            }
+            return;
+        }
+        if (rvis)
+            k_hnsw_exact_reg<true><<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4, s>>>(
+                    g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
+                    layout, nullptr);
         else
-            k_hnsw_exact_reg<false><<<dim3((unsigned)n), dim3(64), lds_q, s>>>(
+            k_hnsw_exact_reg<false><<<dim3((unsigned)n), dim3(64), lds_r, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
-                    only, qidx);
+                    only, qidx, layout, nullptr);
         HIP_LAUNCH_CHECK();
         return;
     }

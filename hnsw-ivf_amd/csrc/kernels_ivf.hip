@@ -95,12 +95,12 @@ __global__ __launch_bounds__(1024) void k_bucket_count_lds(const int32_t* __rest
 // 65536 lists in one chunk instead of sixteen), thread sums, shuffle scan per
 // wave, 16 wave totals through LDS; a running carry between chunks.
 template <int E>
-__global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict__ counts,
+__global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* counts,
                                                       int nlist, int QT,
                                                       uint32_t* __restrict__ bucket_off,
                                                       uint32_t* __restrict__ item_off,
                                                       uint32_t* __restrict__ item_list,
-                                                      uint32_t* __restrict__ zero_next,
+                                                      uint32_t* zero_next,
                                                       uint32_t* __restrict__ item_ctr,
                                                       const uint32_t* __restrict__ perm) {
     __shared__ uint32_t wb[16], wi[16];

@@ -1295,16 +1295,17 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         HIP_CHECK(hipMemsetAsync(ftrace_buf, 0, 64 * grid, s));
         ftrace = ftrace_buf;
     }
-    // fold: the stream image carries bias fragments (L2 only; the streamed
-    // sequential kernel is the only reader of the image)
-    const bool fk = fold != 0 && l2 && aligned_lists && !y3 && !b.sel && d <= BDM;
-    const float coef = (float)(y3 ? ivf_bf3_coef(d) : fk ? ivf_bf2f_coef(d) : ivf_bf2_coef(d));
     // streamed (glds) bf16x2 filter: the default; the register-staged kernel
     // serves bf16x3, IDSelectors and the per-item trace
     // (FAISS_AMD_IVF_FILTER=staged forces it)
     const char* fenv = getenv("FAISS_AMD_IVF_FILTER");
     const bool stream_ok = aligned_lists && !y3 && !b.sel && d <= BDM &&
                            !(fenv && !strcmp(fenv, "staged"));
+    // fold: the stream image carries bias fragments (L2 only); only the
+    // streamed kernel reads the image, so folded keys exist only when it runs
+    // (the staged kernel writes plain distance keys)
+    const bool fk = fold != 0 && l2 && stream_ok;
+    const float coef = (float)(y3 ? ivf_bf3_coef(d) : fk ? ivf_bf2f_coef(d) : ivf_bf2_coef(d));
     // the sequential form (4 groups per CU) by default: measured faster on c2
     // (112 vs 117 us) than the block-pipelined one (FAISS_AMD_IVF_PIPE=1, 3
     // groups per CU, MFMAs of one block interleaved with the previous block's

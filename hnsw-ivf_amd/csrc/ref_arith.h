@@ -152,5 +152,87 @@ __device__ __forceinline__ float ref_rows64_4lane(const float* xr /* LDS copy of
     return out;
 }
 
+// ref_rows64_4lane for rows compacted to the low lanes (valid lanes 0..nv-1)
+// with the loads of PB passes issued together: one memory round trip per PB
+// passes instead of per pass (a hop of ~40 rows: 2 round trips at PB = 2
+// instead of 3), at PB x 2 XM VGPRs of row data.
+template <bool L2, int XM, int PB>
+__device__ __forceinline__ float ref_rows64_4lane_pb(const float* xr, const float* __restrict__ xq,
+                                                     const float* __restrict__ codes, int ldc,
+                                                     int d, uint32_t grow, int nv, int lane) {
+    const int g = lane >> 2, jp = lane & 3;
+    const int n8 = d & ~7, nm = n8 >> 3;
+    const int npass = (nv + 15) >> 4;
+    float out = 0.f;
+#pragma unroll 1
+    for (int p0 = 0; p0 < npass; p0 += PB) {
+        float2 yv[PB][XM];
+        const float* yr[PB];
+        // rows of a pass beyond the last one read row 0 (their results are
+        // never used): every load is unconditional, one base per row
+        const bool full = nm == XM;  // wave-uniform: no per-m selects
+#pragma unroll
+        for (int b = 0; b < PB; b++) {
+            const int p = p0 + b;
+            const uint32_t rg = __shfl(grow, (16 * p + g) & 63);
+            const bool rv = p < npass && 16 * p + g < nv;
+            yr[b] = codes + (int64_t)(rv ? rg : 0u) * ldc;
+            if (full) {
+#pragma unroll
+                for (int m = 0; m < XM; m++) yv[b][m] = *(const float2*)(yr[b] + 8 * m + 2 * jp);
+            } else {
+#pragma unroll
+                for (int m = 0; m < XM; m++)
+                    yv[b][m] = m < nm ? *(const float2*)(yr[b] + 8 * m + 2 * jp)
+                                      : make_float2(0.f, 0.f);
+            }
+        }
+        const float* xj = xr + 2 * jp;
+#pragma unroll
+        for (int b = 0; b < PB; b++) {
+            const int p = p0 + b;
+            if (p >= npass) break;  // wave-uniform
+            float ca = 0.f, cb = 0.f;
+            if (full) {
+#pragma unroll
+                for (int m = 0; m < XM; m++) {
+                    const float2 xv = *(const float2*)(xj + 8 * m);
+                    ca = ref_term_fma<L2>(xv.x, yv[b][m].x, ca);
+                    cb = ref_term_fma<L2>(xv.y, yv[b][m].y, cb);
+                }
+            } else {
+#pragma unroll
+                for (int m = 0; m < XM; m++) {
+                    const float2 xv = *(const float2*)(xj + 8 * m);
+                    const float ta = ref_term_fma<L2>(xv.x, yv[b][m].x, ca);
+                    const float tb = ref_term_fma<L2>(xv.y, yv[b][m].y, cb);
+                    ca = m < nm ? ta : ca;
+                    cb = m < nm ? tb : cb;
+                }
+            }
+            ca += __shfl_xor(ca, 2);
+            cb += __shfl_xor(cb, 2);
+            ca += __shfl_xor(ca, 1);
+            cb += __shfl_xor(cb, 1);
+            float r = ca + cb;
+            if (n8 < d) {
+                const float* y = yr[b];
+                int i = n8;
+                if (d - n8 >= 4) {
+                    const float e0 = ref_term<L2>(xq[n8], y[n8]), e1 = ref_term<L2>(xq[n8 + 1], y[n8 + 1]);
+                    const float e2 = ref_term<L2>(xq[n8 + 2], y[n8 + 2]);
+                    const float e3 = ref_term<L2>(xq[n8 + 3], y[n8 + 3]);
+                    r = r + ((e0 + e2) + (e1 + e3));
+                    i += 4;
+                }
+                for (; i < d; i++) r = ref_term_fma<L2>(xq[i], y[i], r);
+            }
+            const float got = __shfl(r, 4 * (lane & 15));
+            if ((lane >> 4) == p) out = got;
+        }
+    }
+    return out;
+}
+
 }  // namespace kern
 }  // namespace faiss_amd

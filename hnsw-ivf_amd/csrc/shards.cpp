@@ -392,7 +392,7 @@ struct IndexShardsIVF::MultiDev {
     std::vector<hipStream_t> own;  // ranks 1.. (rank 0 runs on the caller's stream)
     // ranks 1..: a copy of the common quantizer for the rank's query slice
     std::vector<std::unique_ptr<Index>> qrep;
-    idx_t q_ntotal = -1;
+    uint64_t q_version = 0;  // the quantizer's content_version() when copied
     // per rank: padded queries, coarse distances / lists of the whole batch,
     // the rank's slice of every shard's tables and the merged slice
     std::vector<DeviceBuffer> x, cd, ci, sd, si, md, mi;
@@ -453,7 +453,8 @@ void IndexShardsIVF::search_multi(idx_t n, const float* x, int ldx, idx_t k, flo
                                   hipStream_t s) const {
     const int home = quantizer->device;
     const int ns = (int)shards.size();
-    if (md_ && md_->q_ntotal != quantizer->ntotal) md_.reset();  // quantizer changed
+    // quantizer content changed since the copies were made: rebuild them
+    if (md_ && md_->q_version != quantizer->content_version()) md_.reset();
     if (!md_) {
         auto md = std::make_unique<MultiDev>();
         const char* per = getenv("FAISS_AMD_SHARDS_RANKS");
@@ -491,7 +492,7 @@ void IndexShardsIVF::search_multi(idx_t n, const float* x, int ldx, idx_t k, flo
             HIP_CHECK(hipStreamCreateWithFlags(&md->own[r], hipStreamNonBlocking));
             md->qrep[r].reset(clone_to_device(quantizer, md->devs[r]));
         }
-        md->q_ntotal = quantizer->ntotal;
+        md->q_version = quantizer->content_version();
         for (auto* v : {&md->x, &md->cd, &md->ci, &md->sd, &md->si, &md->md, &md->mi})
             v->resize(R);
         md->od.resize(ns);
@@ -499,6 +500,15 @@ void IndexShardsIVF::search_multi(idx_t n, const float* x, int ldx, idx_t k, flo
         md_ = std::move(md);
     }
     MultiDev& md = *md_;
+    // search-time fields of the quantizer follow the live one on every call
+    // (the C API sets efSearch between searches)
+    if (auto* hq = dynamic_cast<const IndexHNSW*>(quantizer))
+        for (auto& c : md.qrep)
+            if (auto* hc = dynamic_cast<IndexHNSW*>(c.get())) {
+                hc->hnsw.efSearch = hq->hnsw.efSearch;
+                hc->hnsw.check_relative_distance = hq->hnsw.check_relative_distance;
+                hc->hnsw.search_bounded_queue = hq->hnsw.search_bounded_queue;
+            }
     Exchange& xc = *md.xc;
     const int R = (int)md.devs.size();
     xc.streams = md.own;

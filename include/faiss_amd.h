@@ -199,6 +199,9 @@ struct Index {
     virtual void sync_device() const {}
     // fold device-side search counters (HNSWStats) into the host globals
     virtual void fold_device_stats() const {}
+    // bumped by every add / reset of the index's content (copies made of it,
+    // e.g. IndexShardsIVF's per-rank quantizers, are rebuilt when it moves)
+    virtual uint64_t content_version() const { return version_; }
 
     hipStream_t stream() const;
     int ld() const { return (int)roundup((size_t)d, 4); }
@@ -208,6 +211,7 @@ struct Index {
     // calls (one host call at a time per index)
     mutable std::mutex host_mu_;
     mutable DeviceBuffer h_x_, h_d_, h_i_;
+    uint64_t version_ = 0;
 };
 
 // ---------------------------------------------------------------- flat
@@ -304,6 +308,9 @@ struct IndexHNSW : Index {
     void reconstruct(idx_t key, float* recons) const override;
     void sync_device() const override;
     void fold_device_stats() const override;
+    uint64_t content_version() const override {
+        return version_ + (storage ? storage->content_version() : 0);
+    }
     // faiss/IndexHNSW.cpp:345-366: search with per-query latency statistics
     // (quantization_us = 0, list_scan_us = total_us, like the reference)
     void search_stats(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,

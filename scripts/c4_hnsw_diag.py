@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""c4's HNSW coarse quantizer in isolation (profiling aid, GPU box).
+
+Trains the c4 quantizer (IVF16384_HNSW32,Flat on the 638,976 training rows
+of the 10M float_rand set), then searches the 10k bench queries at k = 64
+(nprobe) for several efSearch values, printing per call the wall time, the
+tie-flag breakdown of the batched kernel (FAISS_AMD_HNSW_STATS) and, from
+FAISS_AMD_HNSW_TRACE, the sequential kernel's per-hop phase cycles.
+Also times every query through the sequential kernel (FAISS_AMD_HNSW_EXACT=1).
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+out = os.path.join(ROOT, "gpurun_out")
+os.makedirs(out, exist_ok=True)
+amd = ge.load_package()
+d, nb, nq = 128, 10_000_000, 10_000
+idx = amd.index_factory(d, "IVF16384_HNSW32,Flat")
+t0 = time.time()
+xt = amd.float_rand_rows(nb, d, 1234, 0, 1, 638_976)
+idx.train(xt)
+print(f"trained in {time.time() - t0:.1f}s", flush=True)
+q = idx.quantizer
+xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+efs = [int(e) for e in os.environ.get("EFS", "16,64,128").split(",")]
+for ef in efs:
+    q.efSearch = ef
+    q.search(xq, 64)  # warm-up
+    tf = os.path.join(out, f"htrace_ef{ef}.bin")
+    if os.path.exists(tf):
+        os.unlink(tf)
+    os.environ["FAISS_AMD_HNSW_STATS"] = "1"
+    os.environ["FAISS_AMD_HNSW_TRACE"] = tf
+    q.search(xq, 64)
+    del os.environ["FAISS_AMD_HNSW_STATS"], os.environ["FAISS_AMD_HNSW_TRACE"]
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        q.search(xq, 64)
+        ts.append(time.perf_counter() - t)
+    os.environ["FAISS_AMD_HNSW_EXACT"] = "1"
+    q.search(xq, 64)
+    tx = time.perf_counter()
+    q.search(xq, 64)
+    tx = time.perf_counter() - tx
+    os.environ["FAISS_AMD_HNSW_LAYOUT"] = "1"
+    q.search(xq, 64)
+    tl = time.perf_counter()
+    q.search(xq, 64)
+    tl = time.perf_counter() - tl
+    del os.environ["FAISS_AMD_HNSW_LAYOUT"]
+    ta = os.path.join(out, f"htrace_all_ef{ef}.bin")
+    if os.path.exists(ta):
+        os.unlink(ta)
+    os.environ["FAISS_AMD_HNSW_TRACE"] = ta
+    q.search(xq, 64)
+    del os.environ["FAISS_AMD_HNSW_TRACE"]
+    del os.environ["FAISS_AMD_HNSW_EXACT"]
+    print(f"ef {ef}: batched+reruns {min(ts) * 1e3:.3f} ms, all-sequential {tx * 1e3:.3f} ms "
+          f"(heap layout throughout: {tl * 1e3:.3f} ms)", flush=True)
+    for tf in (tf, ta):
+      if os.path.exists(tf):
+        tr = np.fromfile(tf, dtype=np.uint64).reshape(-1, 16).astype(np.float64)
+        tr = tr[tr[:, 7] > 0]
+        if len(tr):
+            hops = tr[:, 5].sum()
+            ph = ["pop", "nbr ids", "visited", "distances", "heaps"]
+            per = " ".join(f"{n} {tr[:, i].sum() / hops:.0f}" for i, n in enumerate(ph))
+            print(f"  {os.path.basename(tf)}: traced {len(tr)} queries: {tr[:, 5].mean():.1f} "
+                  f"hops, {tr[:, 6].sum() / hops:.1f} fresh/hop, cycles/hop: {per}, "
+                  f"query total {tr[:, 7].mean():.0f} cycles (max {tr[:, 7].max():.0f}), "
+                  f"{int(tr[:, 8].sum())} searched again with the heap layout",
+                  flush=True)
