@@ -503,15 +503,19 @@ class IndexIVF(Index):
         return out.reshape(n, self.code_size)
 
     def search_preassigned(self, x, k, assign, centroid_dis, store_pairs=False):
+        """centroid_dis may be None (NULL), as the reference allows where its
+        scanner does not read it."""
         x = _f32(x)
         n = x.shape[0]
         assign = np.ascontiguousarray(assign, dtype=np.int64)
-        centroid_dis = np.ascontiguousarray(centroid_dis, dtype=np.float32)
+        if centroid_dis is not None:
+            centroid_dis = np.ascontiguousarray(centroid_dis, dtype=np.float32)
         D = np.empty((n, k), dtype=np.float32)
         I = np.empty((n, k), dtype=np.int64)
-        _check(lib().faiss_IndexIVF_search_preassigned(self.h, n, _ptr(x), k, _ptr(assign),
-                                                       _ptr(centroid_dis), _ptr(D), _ptr(I),
-                                                       int(store_pairs)))
+        _check(lib().faiss_IndexIVF_search_preassigned(
+            self.h, n, _ptr(x), k, _ptr(assign),
+            _ptr(centroid_dis) if centroid_dis is not None else None, _ptr(D), _ptr(I),
+            int(store_pairs)))
         return D, I
 
     def range_search_preassigned(self, x, radius, assign, centroid_dis=None):

@@ -534,8 +534,9 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
                                sizeof(float) * d, n, hipMemcpyHostToDevice, s));
     HIP_CHECK(hipMemcpyAsync(ba.ptr, a32.data(), sizeof(int32_t) * n * np,
                              hipMemcpyHostToDevice, s));
-    HIP_CHECK(hipMemcpyAsync(bc.ptr, centroid_dis, sizeof(float) * n * np,
-                             hipMemcpyHostToDevice, s));
+    if (centroid_dis)
+        HIP_CHECK(hipMemcpyAsync(bc.ptr, centroid_dis, sizeof(float) * n * np,
+                                 hipMemcpyHostToDevice, s));
     std::lock_guard<std::recursive_mutex> g(mu_);
     s_stats_.reserve(2 * sizeof(unsigned long long));
     HIP_CHECK(hipMemsetAsync(s_stats_.ptr, 0, 2 * sizeof(unsigned long long), s));
@@ -562,6 +563,8 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
         ~ResetDup() { f = false; }
     } reset_dup{dup_probes_};
     dup_probes_ = dup;
+    if (!centroid_dis) HIP_CHECK(hipMemsetAsync(bc.ptr, 0, sizeof(float) * n * np, s));
+    own_coarse_dis(n, bx.as<float>(), ldx, (int)np, ba.as<int32_t>(), bc.as<float>(), s);
     search_preassigned_device(n, bx.as<float>(), ldx, k, (int)np, asg, bc.as<float>(),
                               bd.as<float>(), bi.as<idx_t>(), s, lim, selm, store_pairs);
     dup_probes_ = false;
@@ -1057,6 +1060,16 @@ void IndexIVFPQ::upload_extra() const {
         for (size_t li = 0; li < nlist; li++) mx = std::max(mx, invlists->list_size(li));
         pq_obits_ = kern::ivf_bf3_obits((uint32_t)std::min<size_t>(mx, 0xffffffffu));
         pq_mfma_ready_ = pq_obits_ <= 14;
+        // the streamed filter's image (by-residual terms in the bias tail)
+        pq_stream_ready_ = false;
+        if (pq_mfma_ready_ && kern::ivfpq_stream_eligible(d, (int)pq.M, 1, 1)) {
+            const int DB = kern::bf3_db_host(d);
+            d_pcbs_.reserve(rows * (2 * (size_t)DB + 16));
+            kern::pq_stream_image(d_codes_.as<uint8_t>(), device_code_stride(), (int64_t)rows, d,
+                                  (int)pq.dsub, d_pq_.as<float>(), d_terms_.as<float>(),
+                                  d_row_list_.as<uint32_t>(), DB, d_pcbs_.ptr, s);
+            pq_stream_ready_ = true;
+        }
         HIP_CHECK(hipStreamSynchronize(s));  // cn is a host temporary
     }
 }
@@ -1079,7 +1092,14 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
     if (!force_exact && !store_pairs && !dup_probes_ && pq_mfma_ready_ && metric_type == METRIC_L2 &&
         by_residual && kern::ivfpq_mfma_eligible(d, (int)pq.M, (int)k, np)) {
         std::lock_guard<std::recursive_mutex> g(mu_);
-        const int QT = 64;
+        // the streamed filter over the PQ stream image (default where
+        // eligible; FAISS_AMD_PQ_FILTER=decode keeps the in-loop decode filter
+        // k_ivfpq_filter_w, which also serves IDSelectors)
+        const char* fenv = getenv("FAISS_AMD_PQ_FILTER");
+        const bool stream = pq_stream_ready_ && !sel && !(fenv && !strcmp(fenv, "decode")) &&
+                            !(fenv && !strcmp(fenv, "wg")) &&
+                            kern::ivfpq_stream_eligible(d, (int)pq.M, (int)k, np);
+        const int QT = stream ? kern::IVF_FLAT_QT : 64;
         uint32_t* counts_next = nullptr;
         uint32_t* counts = bucket_counts(s, &counts_next);
         s_cur_.reserve(sizeof(uint32_t) * std::max<idx_t>(n * np, 1));
@@ -1128,11 +1148,18 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
                 qimg ? (const float*)((const uint8_t*)qimg + kern::query_image_bytes(n, d)) : nullptr;
         {
             ScopedKernelTimer tm(&ktimes, "ivfpq_filter", 0.0, s);
-            kern::ivfpq_filter(x, ldx, d, (int)pq.M, d_dec_.ptr, d_codes_.as<uint8_t>(),
-                               d_terms_.as<float>(), centroid_dis, d_cnorm_.as<float>(),
-                               d_lrmax_.as<float>(), d_lRmax_.as<float>(), (int)nlist, n, np,
-                               (int)k, pq_obits_, b, mi, s_pkeys_.as<uint32_t>(),
-                               s_precs_.as<kern::ProbeRec>(), &KT, s, qimg, qxn);
+            if (stream)
+                kern::ivfpq_stream_filter(x, ldx, d, (int)pq.M, d_pcbs_.ptr, centroid_dis,
+                                          d_cnorm_.as<float>(), d_lrmax_.as<float>(),
+                                          d_lRmax_.as<float>(), (int)nlist, n, np, (int)k,
+                                          pq_obits_, b, mi, s_pkeys_.as<uint32_t>(),
+                                          s_precs_.as<kern::ProbeRec>(), &KT, s, qimg, qxn);
+            else
+                kern::ivfpq_filter(x, ldx, d, (int)pq.M, d_dec_.ptr, d_codes_.as<uint8_t>(),
+                                   d_terms_.as<float>(), centroid_dis, d_cnorm_.as<float>(),
+                                   d_lrmax_.as<float>(), d_lRmax_.as<float>(), (int)nlist, n, np,
+                                   (int)k, pq_obits_, b, mi, s_pkeys_.as<uint32_t>(),
+                                   s_precs_.as<kern::ProbeRec>(), &KT, s, qimg, qxn);
         }
         {
             ScopedKernelTimer tm(&ktimes, "ivfpq_rerank", 0.0, s);
@@ -1148,7 +1175,8 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
             kern::ivfpq_rerank(s_pkeys_.as<uint32_t>(), s_precs_.as<kern::ProbeRec>(), x, ldx, d,
                                d_ids_.as<int64_t>(), pa, (int)pq.dsub, n, np, KT, pq_obits_,
                                (int)k, sel, distances, labels,
-                               dbg ? s_pflags_.as<uint32_t>() : nullptr, s, qdone_);
+                               dbg ? s_pflags_.as<uint32_t>() : nullptr, s, qdone_,
+                               stream ? 1 : 0);
         }
         if (dbg) {
             uint32_t st[4];
@@ -1163,6 +1191,15 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
     }
     exact_scan_device(n, x, ldx, k, np, assign, centroid_dis, distances, labels, s, lim, sel,
                       store_pairs);
+}
+
+void IndexIVFPQ::own_coarse_dis(idx_t n, const float* x, int ldx, int np,
+                                const int32_t* assign, float* cdis, hipStream_t s) const {
+    // table 0 (faiss/IndexIVFPQ.cpp:634-700) computes |r_m - c|^2 tables and
+    // never reads coarse_dis; the list filter's key coarse_dis + term - 2 <x,
+    // y_R> needs the true |x - y_C|^2
+    if (!(by_residual && metric_type == METRIC_L2 && use_precomputed_table != 1)) return;
+    kern::pair_l2(x, ldx, d_cent_.as<float>(), ld(), d, assign, n, np, cdis, s);
 }
 
 void IndexIVFPQ::exact_args(void* p) const {

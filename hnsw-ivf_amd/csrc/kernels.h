@@ -186,10 +186,30 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
                   const IVFBuckets& b, int64_t max_items, uint32_t* keys, ProbeRec* recs,
                   int* kt_out, hipStream_t s,
                   const void* qimg = nullptr, const float* qxn = nullptr);
+// |x_q - c_l|^2 in fvec_L2sqr order for the (query, probe) pairs of assign
+// (0 where l < 0): IVF-PQ table-0 filters key on the true coarse distance
+void pair_l2(const float* x, int ldx, const float* cent, int ldc, int d, const int32_t* assign,
+             int64_t n, int np, float* out, hipStream_t s);
+// fold: the keys are folded (ivfpq_stream_filter)
 void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx, int d,
                   const int64_t* ids, const PQArgs& pa, int dsub, int64_t n, int nprobe, int KT,
                   int obits, int k, const uint8_t* sel, float* D, int64_t* I, uint32_t* stats,
-                  hipStream_t s, unsigned long long* qdone = nullptr);
+                  hipStream_t s, unsigned long long* qdone = nullptr, int fold = 0);
+// PQ stream image (kernels_ivf_mfma.hip k_pq_stream_image): per arena row
+// 2 DB + 16 bytes, DB = bf3_db_host(d): bf16 of the decoded residual, then
+// the folded bias fragment of -term / 2
+void pq_stream_image(const uint8_t* codes, int cs, int64_t rows, int d, int dsub,
+                     const float* pq_cent, const float* terms, const uint32_t* row_list, int DB,
+                     void* out, hipStream_t s);
+bool ivfpq_stream_eligible(int d, int M, int k, int nprobe);
+double ivfpq_fold_coef(int d, int M);
+// the IVF-Flat streamed filter over the PQ stream image: keys + probe records
+// in the k_ivfpq_filter_w format (folded keys; the re-rank takes fold = 1)
+void ivfpq_stream_filter(const float* x, int ldx, int d, int M, const void* pcbs,
+                         const float* cdis, const float* cnorm, const float* lrmax,
+                         const float* lRmax, int nlist, int64_t n, int nprobe, int k, int obits,
+                         const IVFBuckets& b, int64_t max_items, uint32_t* keys, ProbeRec* recs,
+                         int* kt_out, hipStream_t s, const void* qimg, const float* qxn);
 // the device clock (s_memrealtime) into *out, in stream order
 void device_stamp(unsigned long long* out, hipStream_t s);
 

@@ -351,7 +351,14 @@ __device__ __forceinline__ void wait_lgkmcnt0() {  // s_waitcnt lgkmcnt(0) alone
 // bytes by zero), so the accumulator is -approx/2 and a candidate's key is
 // min + bfi instead of add + fma + max + bfi, with no norm reads from LDS
 // (fold_key_bits; margin coefficient ivf_bf2f_coef).
-template <bool L2, int KT, int NS, bool PIPE, bool FOLD = false>
+//
+// PQ (IVF-PQ by residual, L2, with FOLD): the image is the PQ stream image
+// (pq_stream_image: bf16 of each row's decoded residual y_R and the bias
+// fragment of -term/2, term = |y_R|^2 + 2 <y_C, y_R>), the query's bias part
+// is -coarse_dis(query, probe) / 2, so the accumulator is -approx / 2 of
+// coarse_dis + term - 2 <x, y_R> (the IVF-PQ filter's key); ynmax / rmax are
+// the lists' max |y_R| / |y_R - bf16(y_R)|, margins as k_ivfpq_filter_w.
+template <bool L2, int KT, int NS, bool PIPE, bool FOLD = false, bool PQ = false>
 __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
         const float* __restrict__ x, int ldx, int d, const uint8_t* __restrict__ cbs,
         const float* __restrict__ ynmax, const float* __restrict__ rmax, int nprobe, float coef,
@@ -359,7 +366,9 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
         const uint32_t* __restrict__ item_entries, uint32_t max_items, int nlist,
         const uint32_t* __restrict__ lim, uint32_t* __restrict__ keys,
         ProbeRec* __restrict__ recs, unsigned long long* __restrict__ ftrace,
-        const uint8_t* __restrict__ qimg, const float* __restrict__ qxn) {
+        const uint8_t* __restrict__ qimg, const float* __restrict__ qxn,
+        const float* __restrict__ pcdis = nullptr, const float* __restrict__ pcnorm = nullptr) {
+    static_assert(!PQ || (FOLD && L2 && !PIPE), "PQ: the folded L2 sequential form");
     const unsigned long long ft0 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     constexpr int DB = 16 * NS;          // bf16 per code row
     constexpr int SR = 2 * DB + 16;      // bytes per stream-image row
@@ -429,6 +438,8 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
     if (NB == 3 && ntile > 1) issue(1, 1);
     // epilogue operands, loaded now (their latency hides under the loop)
     const float rmax_l = rmax[l], ynmax_l = ynmax[l];
+    const float cnorm_l = PQ ? pcnorm[l] : 0.f;
+    const float cd_e = PQ ? pcdis[qvalid ? my_e : 0u] : 0.f;
     const uint32_t lim_e = (lim && qvalid) ? lim[my_e] : 0xffffffffu;
 
     // query fragments (B operand): registers for the whole work item
@@ -445,7 +456,7 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
     bf16x8 bq;
     if constexpr (FOLD) {
         __bf16 h, m, lo;
-        split3_bf16(-0.5f * xn, h, m, lo);
+        split3_bf16(-0.5f * (PQ ? cd_e : xn), h, m, lo);
         const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
         bq[0] = lh ? zero : one;
         bq[1] = lh ? zero : one;
@@ -623,8 +634,15 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
             }
         }
         if (lh == 0) {
-            const float mmax =
-                    2.f * (2.f * sqrtf(xn) * rmax_l + coef * (xn + ynmax_l)) + 1e-30f;
+            float mmax;
+            if constexpr (PQ) {
+                // 2 |x| r + coef (|x| + |y_C| + R)^2 (k_ivfpq_filter_w), doubled
+                const float xl = sqrtf(xn);
+                const float sr = xl + cnorm_l + ynmax_l;
+                mmax = 2.f * (2.f * xl * rmax_l + coef * sr * sr) + 1e-30f;
+            } else {
+                mmax = 2.f * (2.f * sqrtf(xn) * rmax_l + coef * (xn + ynmax_l)) + 1e-30f;
+            }
             ProbeRec pr;
 #pragma unroll
             for (int sl = 0; sl < 4; sl++) {
@@ -634,7 +652,7 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
             pr.mmax = mmax;
             pr.off = (uint32_t)row0;
             pr.len = elen;
-            pr.pad = 0u;
+            pr.pad = PQ ? (uint32_t)l : 0u;  // the PQ re-rank's list
             recs[e] = pr;
         }
     }
@@ -691,6 +709,104 @@ void split_bf16_stream(const float* codes, int64_t rows, int d, int ldc, int DB,
     const int64_t tot = rows * (DB + 8);
     k_split_stream<<<dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, s>>>(
             codes, rows, d, ldc, DB, ynorm, row_list, (uint8_t*)out, fold);
+    HIP_LAUNCH_CHECK();
+}
+
+// PQ stream image row r (k_ivf_bf2_stream<..., PQ>): bf16 of the row's
+// decoded residual y_R (dims < d; zero up to DB), then the bias A-fragment
+// {-term/2 in three bf16 parts, 1, 1, 1, 0, 0} (padding rows: -inf, 0, 0, 1,
+// 1, 1, 0, 0).  The decode is the reference's: y_R dims [m dsub, (m+1) dsub)
+// = pq centroid codes[m] of sub-quantizer m (faiss/impl/ProductQuantizer.cpp
+// decode).
+__global__ void k_pq_stream_image(const uint8_t* __restrict__ codes, int cs, int64_t rows, int d,
+                                  int dsub, const float* __restrict__ pq_cent,
+                                  const float* __restrict__ terms,
+                                  const uint32_t* __restrict__ row_list, int DB,
+                                  uint8_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int per = DB + 8;
+    if (i >= rows * per) return;
+    const int64_t r = i / per;
+    const int j = (int)(i - r * per);
+    __bf16* row = (__bf16*)(out + r * (int64_t)(2 * DB + 16));
+    const bool pad = row_list[r] == 0xffffffffu;
+    if (j < DB) {
+        float v = 0.f;
+        if (j < d && !pad) {
+            const int m = j / dsub;
+            const int c = codes[r * cs + m];
+            v = pq_cent[((int64_t)m * 256 + c) * dsub + (j - m * dsub)];
+        }
+        row[j] = (__bf16)v;
+    } else {
+        const int t = j - DB;
+        __bf16 v = (__bf16)0.f;
+        if (t < 3) {
+            __bf16 h = (__bf16)(-WS_INF), m = (__bf16)0.f, lo = (__bf16)0.f;
+            if (!pad) split3_bf16(-0.5f * terms[r], h, m, lo);
+            v = t == 0 ? h : t == 1 ? m : lo;
+        } else if (t < 6) {
+            v = (__bf16)1.f;
+        }
+        row[j] = v;
+    }
+}
+void pq_stream_image(const uint8_t* codes, int cs, int64_t rows, int d, int dsub,
+                     const float* pq_cent, const float* terms, const uint32_t* row_list, int DB,
+                     void* out, hipStream_t s) {
+    if (rows <= 0) return;
+    const int64_t tot = rows * (DB + 8);
+    k_pq_stream_image<<<dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, s>>>(
+            codes, cs, rows, d, dsub, pq_cent, terms, row_list, DB, (uint8_t*)out);
+    HIP_LAUNCH_CHECK();
+}
+
+// IVF-PQ filter + bound records over the PQ stream image (the IVF-Flat
+// streamed kernel in its PQ form): coarse_dis, |y_C| per list, list maxima of
+// |y_R| and |y_R - bf16(y_R)|
+bool ivfpq_stream_eligible(int d, int M, int k, int nprobe) {
+    if (d % M != 0 || d > BDM || k > 32 || nprobe > 64) return false;
+    const int NS = bf3_db_host(d) / 2 * 2 / 16;
+    return ivf_mfma_kq(k, d, nprobe) > 0 && (NS == 2 || NS == 4 || NS == 6 || NS == 8);
+}
+double ivfpq_fold_coef(int d, int M) {
+    // k_ivfpq_filter_w's coefficient, plus the folded bias: the accumulator
+    // sums 2 d exact products and 6 exact bias products of total magnitude
+    // <= 3.01 (|x| + |y_C| + R)^2, doubled by approx = -2 acc
+    const double u = 1.0 / 16777216.0;
+    return ivfpq_mfma_coef(d, M) + 6.02 * (2.0 * d + 6.0) * u;
+}
+void ivfpq_stream_filter(const float* x, int ldx, int d, int M, const void* pcbs,
+                         const float* cdis, const float* cnorm, const float* lrmax,
+                         const float* lRmax, int nlist, int64_t n, int nprobe, int k, int obits,
+                         const IVFBuckets& b, int64_t max_items, uint32_t* keys, ProbeRec* recs,
+                         int* kt_out, hipStream_t s, const void* qimg, const float* qxn) {
+    FAISS_THROW_IF_NOT(ivfpq_stream_eligible(d, M, k, nprobe));
+    FAISS_THROW_IF_NOT_MSG(qimg && qxn, "ivfpq_stream_filter needs the prepared query image");
+    FAISS_THROW_IF_NOT(!b.sel && obits >= 4 && obits <= 14);
+    const int KE = ivf_mfma_kq(k, d, nprobe);
+    *kt_out = KE / 4;
+    const int NS = bf3_db_host(d) / 2 * 2 / 16;
+    const int64_t grid = (int64_t)roundup((size_t)max_items, 32);
+    FAISS_THROW_IF_NOT(grid < (1ll << 31));
+    const float coef = (float)ivfpq_fold_coef(d, M);
+#define PQS(KTV, NSV)                                                                         \
+    k_ivf_bf2_stream<true, KTV, NSV, false, true, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+            x, ldx, d, (const uint8_t*)pcbs, lRmax, lrmax, nprobe, coef, obits, b.item_off,  \
+            b.item_desc, b.item_entries, (uint32_t)max_items, nlist, b.lim, keys, recs,      \
+            nullptr, (const uint8_t*)qimg, qxn, cdis, cnorm)
+#define PQS_NS(KTV)                 \
+    do {                            \
+        if (NS == 2) PQS(KTV, 2);   \
+        else if (NS == 4) PQS(KTV, 4); \
+        else if (NS == 6) PQS(KTV, 6); \
+        else PQS(KTV, 8);           \
+    } while (0)
+    if (KE == 8) PQS_NS(2);
+    else if (KE == 16) PQS_NS(4);
+    else PQS_NS(8);
+#undef PQS_NS
+#undef PQS
     HIP_LAUNCH_CHECK();
 }
 
@@ -919,7 +1035,7 @@ __global__ __launch_bounds__(64 * RR_W, RR_WAVES) void k_ivf_rerank(
         unsigned long long* __restrict__ trace, PQArgs pa, const uint8_t* __restrict__ sel,
         unsigned long long* __restrict__ qdone, int fold_keys) {
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    const bool fold = PQD == 0 && fold_keys != 0;
+    const bool fold = fold_keys != 0;
     __shared__ uint32_t surv[RR_W][RR_CAP];
     __shared__ uint16_t sprobe[RR_W][RR_CAP];
     __shared__ __attribute__((aligned(16))) float xsh[RR_W][BDM];
@@ -1331,7 +1447,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                    : k_ivf_bf2_stream<L2V, KTV, NSV, false>)<<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const uint8_t*)cbs, ynmax, rmax, nprobe, coef, obits,         \
                     b.item_off, b.item_desc, b.item_entries, (uint32_t)max_items, nlist,      \
-                    b.lim, keys, recs, ftrace, qimg, qxn);                                    \
+                    b.lim, keys, recs, ftrace, qimg, qxn, nullptr, nullptr);                  \
         else if (b.sel)                                                                       \
             k_ivf_bf3_filter<L2V, KTV, NSV, false, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
@@ -1447,7 +1563,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
 void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx, int d,
                   const int64_t* ids, const PQArgs& pa, int dsub, int64_t n, int nprobe, int KT,
                   int obits, int k, const uint8_t* sel, float* D, int64_t* I, uint32_t* stats,
-                  hipStream_t s, unsigned long long* qdone) {
+                  hipStream_t s, unsigned long long* qdone, int fold) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(d <= BDM && d % 4 == 0);
     const int KE = 4 * KT;
@@ -1456,7 +1572,7 @@ void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, in
 #define LAUNCH_P(VV, DS)                                                                        \
     k_ivf_rerank<true, VV, DS><<<dim3((unsigned)cdiv(n, RR_W)), dim3(64 * RR_W), 0, s>>>(       \
             keys, recs, x, ldx, nullptr, 0, ids, d, n, nprobe, KT, obits, k, D, I, stats,         \
-            nullptr, pa, sel, qdone, 0)
+            nullptr, pa, sel, qdone, fold)
 #define DISPATCH_P(DS)                       \
     do {                                     \
         if (V == 2) LAUNCH_P(2, DS);         \

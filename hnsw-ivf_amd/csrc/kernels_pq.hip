@@ -15,6 +15,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "ref_arith.h"
 #include "pq_ref.h"
 #include "wave_select.h"
 
@@ -131,6 +132,23 @@ __global__ __launch_bounds__(256) void k_pq_encode(const float* __restrict__ x, 
         }
     }
     codes[i * code_stride + m] = (uint8_t)bj;
+}
+
+// |x_q - c_l|^2 (fvec_L2sqr order) of every (query, probe) pair with l >= 0
+__global__ void k_pair_l2(const float* __restrict__ x, int ldx, const float* __restrict__ cent,
+                          int ldc, int d, const int32_t* __restrict__ assign, int64_t n, int np,
+                          float* __restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * np) return;
+    const int32_t l = assign[e];
+    out[e] = l >= 0 ? ref_l2(x + (e / np) * ldx, cent + (int64_t)l * ldc, d) : 0.f;
+}
+void pair_l2(const float* x, int ldx, const float* cent, int ldc, int d, const int32_t* assign,
+             int64_t n, int np, float* out, hipStream_t s) {
+    if (n <= 0 || np <= 0) return;
+    k_pair_l2<<<dim3((unsigned)cdiv(n * np, 256)), dim3(256), 0, s>>>(x, ldx, cent, ldc, d, assign,
+                                                                     n, np, out);
+    HIP_LAUNCH_CHECK();
 }
 
 void pq_encode(const float* x, int ldx, int64_t n, const int32_t* assign, const float* centroids,

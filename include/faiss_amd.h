@@ -508,6 +508,11 @@ struct IndexIVF : Index {
 
    protected:
     virtual void upload_extra() const {}
+    // search_preassigned with caller coarse distances (device copy cdis,
+    // [n][np]): an index whose scan must not trust them rewrites them (IVF-PQ
+    // table 0: the reference ignores them, its filter keys on them)
+    virtual void own_coarse_dis(idx_t n, const float* x, int ldx, int np, const int32_t* assign,
+                                float* cdis, hipStream_t s) const {}
     // general exact scan (kernels_exact.hip): any k <= 2048, any nprobe,
     // store_pairs; the reference's results bit for bit
     void exact_scan_device(idx_t n, const float* x, int ldx, idx_t k, int nprobe,
@@ -630,6 +635,8 @@ struct IndexIVFPQ : IndexIVF {
     void precompute_table();
 
    protected:
+    void own_coarse_dis(idx_t n, const float* x, int ldx, int np, const int32_t* assign,
+                        float* cdis, hipStream_t s) const override;
     void upload_extra() const override;
     void exact_args(void* args) const override;
     // one pass of the range scan (counts when offs == nullptr, else fill);
@@ -645,6 +652,11 @@ struct IndexIVFPQ : IndexIVF {
     mutable DeviceBuffer s_pkeys_, s_precs_, s_pflags_;
     mutable int pq_obits_ = 0;
     mutable bool pq_mfma_ready_ = false;
+    // PQ stream image (kern::pq_stream_image): the decoded residuals in bf16
+    // with the folded bias, what the streamed filter reads (4.3x the codes at
+    // M = d / 2: HBM spent to take the decode out of the filter's loop)
+    mutable DeviceBuffer d_pcbs_;
+    mutable bool pq_stream_ready_ = false;
 };
 
 // ---------------------------------------------------------------- shards

@@ -57,6 +57,28 @@ def test_gpu_preassigned_equals_reference(amd, gpu, tag):
         eq(D, I, key)
 
 
+@pytest.mark.parametrize("tag", ["pq_m32d128", "pq_m48d96", "pq_m16d64"])
+@pytest.mark.parametrize("cdis", ["null", "garbage"])
+def test_gpu_preassigned_table0_ignores_centroid_dis(amd, gpu, tag, cdis):
+    """Precomputed table 0 never reads coarse_dis (faiss/IndexIVFPQ.cpp:634-700):
+    NULL or unrelated centroid_dis must give the reference's table-0 result
+    (the list filter keys on |x - y_C|^2 and computes it itself)."""
+    idx = amd.read_index(path(tag))
+    xq = FX[tag + "_xq"]
+    ran = 0
+    for key, table, nprobe, k in pre_cases(tag):
+        if table != 0:
+            continue
+        idx.use_precomputed_table = 0
+        idx.nprobe = nprobe
+        cd = FX[f"{tag}_q{nprobe}_D"]
+        cd = None if cdis == "null" else (np.random.default_rng(7).random(cd.shape) * 50.0 - 20.0)
+        D, I = idx.search_preassigned(xq, k, FX[f"{tag}_q{nprobe}_I"], cd)
+        eq(D, I, key)
+        ran += 1
+    assert ran > 0
+
+
 @pytest.mark.parametrize("tag", ["flat_l2", "flat_ip", "pq_m32d128", "pq_m48d96", "pq_m16d64",
                                  "pq_ip_m16d64"])
 def test_gpu_search_equals_reference(amd, gpu, tag):
