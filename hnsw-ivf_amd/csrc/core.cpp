@@ -216,8 +216,7 @@ const float* IndexFlat::device_norms() const {
 template <class OutIdx>
 bool IndexFlat::knn_device(idx_t n, const float* x, int ldx, int k, float* distances,
                            OutIdx* labels, hipStream_t s, void* qimg_out, idx_t batch_n) const {
-    FAISS_THROW_IF_NOT_FMT(k >= 1 && k <= kern::kMaxKExact, "k = %d must be in [1, %d]", k,
-                           kern::kMaxKExact);
+    FAISS_THROW_IF_NOT_FMT(k >= 1, "k = %d must be >= 1", k);
     sync_device();
     std::lock_guard<std::recursive_mutex> g(mu_);
     order_.enter(s);
@@ -258,7 +257,7 @@ bool IndexFlat::knn_impl(idx_t n, const float* x, int ldx, int k, float* distanc
                                          metric_l2, s_tile_.as<float>(), ntotal, s);
             kern::select_rows_exact<OutIdx>(s_tile_.as<float>(), nq, ntotal, ntotal, k,
                                             metric_l2, 0, distances + q0 * k, labels + q0 * k, k,
-                                            s);
+                                            s, &s_sel_);
         }
         return false;
     }

@@ -397,6 +397,7 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
     }
     sync_device();
     std::lock_guard<std::recursive_mutex> g(mu_);
+    order_.enter(s);
     kern::HNSWDevice gd;
     gd.storage = storage->device_vectors();
     gd.norms = nullptr;
@@ -420,27 +421,36 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
         HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, 4 * sizeof(unsigned long long), s));
     }
     // queries per launch: the per-query visited bitmaps that do not fit in
-    // LDS live in a scratch kept under 256 MiB (chunks of the batch)
+    // LDS, and heaps beyond it (max(efSearch, k) in the thousands), live in
+    // scratch kept under 256 MiB each (chunks of the batch)
     const int ef = std::max(efSearch, k);
-    const size_t lds_need = sizeof(float) * ld() + 8 * (size_t)ef + 8 * (size_t)k + 544 +
-                            (size_t)vwords * 4;
+    const size_t hw = kern::hnsw_heap_scratch_words(k, efSearch, ld());
+    const size_t lds_need = sizeof(float) * ld() + (hw ? 0 : 8 * (size_t)ef + 8 * (size_t)k) +
+                            544 + (size_t)vwords * 4;
     const bool scratch = lds_need > 64 * 1024;
-    const idx_t qc = scratch ? std::max<idx_t>(1, std::min<idx_t>(
-                                       n, (idx_t)(((size_t)256 << 20) / ((size_t)vwords * 4))))
-                             : n;
+    idx_t qc = n;
+    if (scratch)
+        qc = std::min<idx_t>(qc, std::max<idx_t>(1, (idx_t)(((size_t)256 << 20) /
+                                                            ((size_t)vwords * 4))));
+    if (hw) qc = std::min<idx_t>(qc, std::max<idx_t>(1, (idx_t)(((size_t)256 << 20) / (hw * 4))));
+    qc = std::max<idx_t>(qc, 1);
     if (scratch) s_visited_.reserve(sizeof(uint32_t) * vwords * qc);
+    if (hw) s_heaps_.reserve(sizeof(float) * hw * qc);
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(qc, 1));
-    // defer (split_begin): one chunk, batched kernel eligible
-    defer = defer && !scratch && i32 && ef <= 128 && k <= 64;
+    // defer (split_begin): one chunk, the batched kernel in use
+    defer = defer && !scratch && !hw && i32 && kern::hnsw_uses_batched(k, efSearch);
     for (idx_t q0 = 0; q0 < n; q0 += qc) {
         const idx_t nq = std::min(qc, n - q0);
         kern::hnsw_search(gd, x + q0 * ldx, ldx, nq, k, efSearch, distances + q0 * k,
                           i32 ? nullptr : (int64_t*)labels + q0 * k,
                           i32 ? (int32_t*)labels + q0 * k : nullptr, s_visited_.as<uint32_t>(),
                           vwords, d_stats_.as<unsigned long long>(), s_flags_.as<uint32_t>(), s,
-                          &ktimes, defer);
+                          &ktimes, defer, hw ? s_heaps_.as<float>() : nullptr);
     }
-    if (!defer) return;
+    if (!defer) {
+        order_.leave(s);
+        return;
+    }
     // the flagged queries -> compact list, count read back (pinned)
     if (!h_fcnt_) HIP_CHECK(hipHostMalloc((void**)&h_fcnt_, sizeof(uint32_t), hipHostMallocDefault));
     if (!ev_split_) HIP_CHECK(hipEventCreateWithFlags(&ev_split_, hipEventDisableTiming));
@@ -463,15 +473,30 @@ bool IndexHNSW::split_begin(idx_t n, const float* x, int ldx, int k, float* dist
                             int32_t* labels, const SearchParameters* params,
                             hipStream_t s) const {
     DevGuard2 dg(device);
-    hnsw_device<int32_t>(n, x, ldx, k, distances, labels, params, s, true);
+    mu_.lock();  // held until split_release when a split is returned
+    try {
+        hnsw_device<int32_t>(n, x, ldx, k, distances, labels, params, s, true);
+    } catch (...) {
+        split_.active = false;
+        mu_.unlock();
+        throw;
+    }
+    if (!split_.active) mu_.unlock();
     return split_.active;
+}
+
+void IndexHNSW::split_release() const {
+    // the caller's stream has joined the re-runs (split_finish's `done`) and
+    // queued its last read of the split scratch
+    order_.leave(split_.s);
+    split_.active = false;
+    mu_.unlock();
 }
 
 IndexHNSW::Split IndexHNSW::split_finish() const {
     std::lock_guard<std::recursive_mutex> g(mu_);
     FAISS_THROW_IF_NOT_MSG(split_.active, "split_finish without split_begin");
     DevGuard2 dg(device);
-    split_.active = false;
     HIP_CHECK(hipEventSynchronize(ev_split_));
     Split r;
     r.nf = (idx_t)*h_fcnt_;

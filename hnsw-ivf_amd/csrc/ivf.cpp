@@ -422,6 +422,7 @@ bool IndexIVF::scan_hnsw_split(idx_t nq, const float* x, int ldx, idx_t k, int n
                                   distances, labels, s, nullptr, nullptr);
         return true;
     }
+    IndexHNSW::SplitHold hold{qh};  // the quantizer stays locked to this caller
     search_preassigned_device(nq, x, ldx, k, np, s_ci_.as<int32_t>(), s_cd_.as<float>(),
                               distances, labels, s, nullptr, nullptr);
     const IndexHNSW::Split sp = qh->split_finish();

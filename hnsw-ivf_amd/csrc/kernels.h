@@ -254,10 +254,12 @@ void ivf_exact_search(const ExactScanArgs& a, uint32_t* eoff, uint32_t* total, u
 // a.x / a.assign / a.cdis / a.sel / a.ids / a.row_list / a.store_pairs used)
 void ivfpq_range_exact(const ExactScanArgs& a, float radius, uint32_t* counts,
                        const uint64_t* offsets, float* outD, int64_t* outI, hipStream_t s);
-// exact top-k (reference heap semantics, label = col0 + column) of dense rows
+// exact top-k (reference heap semantics, label = col0 + column) of dense rows;
+// k > kMaxKExact runs with global scratch (required then)
 template <class OutIdx>
 void select_rows_exact(const float* D, int64_t nx, int64_t ny, int64_t ldD, int k, int metric_l2,
-                       int64_t col0, float* out_d, OutIdx* out_i, int64_t ldo, hipStream_t s);
+                       int64_t col0, float* out_d, OutIdx* out_i, int64_t ldo, hipStream_t s,
+                       DeviceBuffer* scratch = nullptr);
 
 // IndexIVFStats counters of a batch (faiss/IndexIVF.cpp:1184-1198):
 // stats[0] += non-empty lists visited, stats[1] += codes scanned (device)
@@ -353,12 +355,21 @@ struct HNSWDevice {
 // :605-741 (search_from_candidates), :1096-1342 (MinimaxHeap)
 // flags: [n] scratch; queries where an exact distance tie makes the batched
 // form unsafe are redone by the sequential kernel (nullptr: no check).
-// max(efSearch, k) > 128 or k > 64: the sequential kernel for every query.
+// max(efSearch, k) <= 64: the register kernel (k_hnsw_exact_reg) for every
+// query (FAISS_AMD_HNSW=batched: the batched kernel + re-runs); max(efSearch,
+// k) > 128 or k > 64: the sequential LDS kernel, with its heaps in
+// heap_scratch (hnsw_heap_scratch_words per query) when they exceed the LDS.
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
                  hipStream_t s, KernelTimes* kt = nullptr,
-                 bool defer = false);  // leave the flagged queries to the caller
+                 bool defer = false, float* heap_scratch = nullptr);
+// 32-bit words of global heap scratch per query (0: the heaps fit the LDS)
+size_t hnsw_heap_scratch_words(int k, int efSearch, int ld);
+// the register kernel serves max(efSearch, k) <= 64
+bool hnsw_register_eligible(int k, int efSearch);
+// the batched kernel (and its tie re-runs) runs for these parameters
+bool hnsw_uses_batched(int k, int efSearch);  // leave the flagged queries to the caller
 // flagged queries (flags[q] != 0) -> idx[0 .. *count) (count zeroed first)
 void hnsw_flag_compact(const uint32_t* flags, int64_t n, uint32_t* idx, uint32_t* count,
                        hipStream_t s);

@@ -282,15 +282,20 @@ struct SrcDense {
     __device__ void done(int64_t) const {}
 };
 
-template <class Src, class OutIdx>
+// GS: the collection arrays in global scratch (gs_words 64-bit words per
+// query) instead of LDS — k beyond what one work group's LDS holds
+template <class Src, class OutIdx, bool GS = false>
 __global__ __launch_bounds__(256) void k_ex_select(Src src, int k, int l2, float* __restrict__ D,
-                                                   OutIdx* __restrict__ I, int64_t ldo) {
+                                                   OutIdx* __restrict__ I, int64_t ldo,
+                                                   unsigned long long* __restrict__ gs = nullptr,
+                                                   int64_t gs_words = 0) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t wsum[4];
     __shared__ uint32_t sh_b, sh_kk, sh_all, nlt, neq;
     extern __shared__ unsigned long long smem[];
     const int KS = k <= 1 ? 1 : 1 << (32 - __clz(k - 1));  // pow2 >= k
-    int64_t* oid = (int64_t*)smem;                          // [KS]
+    unsigned long long* arr = GS ? gs + (int64_t)blockIdx.x * gs_words : smem;
+    int64_t* oid = (int64_t*)arr;                           // [KS]
     int64_t* eqid = oid + KS;                               // [k]
     uint32_t* okey = (uint32_t*)(eqid + k);                 // [KS]
     const int64_t q = blockIdx.x;
@@ -575,19 +580,38 @@ void merge_rows_general(const float* cand_d, const int64_t* cand_i, int64_t n, i
 
 template <class OutIdx>
 void select_rows_exact(const float* Dt, int64_t nx, int64_t ny, int64_t ldD, int k, int metric_l2,
-                       int64_t col0, float* out_d, OutIdx* out_i, int64_t ldo, hipStream_t s) {
+                       int64_t col0, float* out_d, OutIdx* out_i, int64_t ldo, hipStream_t s,
+                       DeviceBuffer* scratch) {
     if (nx <= 0) return;
-    FAISS_THROW_IF_NOT_FMT(k >= 1 && k <= kMaxKExact, "k = %d must be in [1, %d]", k,
-                           kMaxKExact);
-    SrcDense src{Dt, ldD, ny, col0, metric_l2};
-    k_ex_select<SrcDense, OutIdx><<<dim3((unsigned)nx), dim3(256), select_lds(k), s>>>(
-            src, k, metric_l2, out_d, out_i, ldo);
-    HIP_LAUNCH_CHECK();
+    FAISS_THROW_IF_NOT_FMT(k >= 1, "k = %d must be >= 1", k);
+    if (k <= kMaxKExact) {
+        SrcDense src{Dt, ldD, ny, col0, metric_l2};
+        k_ex_select<SrcDense, OutIdx><<<dim3((unsigned)nx), dim3(256), select_lds(k), s>>>(
+                src, k, metric_l2, out_d, out_i, ldo);
+        HIP_LAUNCH_CHECK();
+        return;
+    }
+    // k > kMaxKExact (e.g. nprobe in the thousands): the same select with its
+    // arrays in global scratch, queries in chunks of a 256 MiB scratch
+    FAISS_THROW_IF_NOT_MSG(scratch, "select_rows_exact: k > 2048 needs a scratch buffer");
+    const int64_t words = (int64_t)cdiv(select_lds(k), sizeof(unsigned long long));
+    const int64_t qc = std::max<int64_t>(1, std::min<int64_t>(nx, ((int64_t)256 << 20) / (8 * words)));
+    scratch->reserve((size_t)qc * words * 8);
+    for (int64_t q0 = 0; q0 < nx; q0 += qc) {
+        const int64_t nq = std::min(qc, nx - q0);
+        SrcDense src{Dt + q0 * ldD, ldD, ny, col0, metric_l2};
+        k_ex_select<SrcDense, OutIdx, true><<<dim3((unsigned)nq), dim3(256), 0, s>>>(
+                src, k, metric_l2, out_d + q0 * ldo, out_i + q0 * ldo, ldo,
+                scratch->as<unsigned long long>(), words);
+        HIP_LAUNCH_CHECK();
+    }
 }
 template void select_rows_exact<int32_t>(const float*, int64_t, int64_t, int64_t, int, int,
-                                         int64_t, float*, int32_t*, int64_t, hipStream_t);
+                                         int64_t, float*, int32_t*, int64_t, hipStream_t,
+                                         DeviceBuffer*);
 template void select_rows_exact<int64_t>(const float*, int64_t, int64_t, int64_t, int, int,
-                                         int64_t, float*, int64_t*, int64_t, hipStream_t);
+                                         int64_t, float*, int64_t*, int64_t, hipStream_t,
+                                         DeviceBuffer*);
 
 }  // namespace kern
 }  // namespace faiss_amd

@@ -451,7 +451,10 @@ __device__ void hx_replace_top(int k, float* bv, int32_t* bi, float val, int32_t
 }
 }  // namespace
 
-template <bool LDS_VISITED>
+// GH: the two heaps in global scratch (gheap: 2 ef + 2 k words per block) —
+// max(efSearch, k) beyond what the work group's LDS holds (the reference's
+// harness sweeps efSearch up to 3 nprobe, nprobe into the thousands)
+template <bool LDS_VISITED, bool GH = false>
 __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __restrict__ x,
                                                    int ldx, int64_t n, int k, int efSearch,
                                                    int ef, float* __restrict__ D,
@@ -461,7 +464,7 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
                                                    int64_t vwords,
                                                    unsigned long long* __restrict__ stats,
                                                    const uint32_t* __restrict__ only,
-        const uint32_t* __restrict__ qidx) {
+        const uint32_t* __restrict__ qidx, float* __restrict__ gheap = nullptr) {
     // qidx: compact launch over listed queries (input row qidx[b], output
     // row b); else query b, output row b
     const int64_t q = qidx ? (int64_t)qidx[blockIdx.x] : (int64_t)blockIdx.x;
@@ -469,11 +472,12 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
     if (only && only[q] == 0u) return;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* qs = sm;                              // [ld]
-    float* cdis = qs + g.ld;                     // [ef] MinimaxHeap dis
+    float* hp = GH ? gheap + (int64_t)blockIdx.x * (2 * (int64_t)ef + 2 * k) : qs + g.ld;
+    float* cdis = hp;                            // [ef] MinimaxHeap dis
     int32_t* cid = (int32_t*)(cdis + ef);        // [ef] MinimaxHeap ids
     float* rdis = (float*)(cid + ef);            // [k] result heap
     int32_t* rid = (int32_t*)(rdis + k);         // [k]
-    float* fd = (float*)(rid + k);               // [64] fresh neighbours of a hop
+    float* fd = GH ? qs + g.ld : (float*)(rid + k);  // [64] fresh neighbours of a hop
     int32_t* fi = (int32_t*)(fd + 64);           // [64]
     int32_t* sh = fi + 64;                       // [8] scalars: hk, nvalid, nfresh, ...
     uint32_t* vis = LDS_VISITED ? (uint32_t*)(sh + 8) : vis_global + blockIdx.x * vwords;
@@ -1127,11 +1131,27 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
                               int efSearch, float* D, int64_t* I, int32_t* I32,
                               uint32_t* visited_scratch, int64_t vwords,
                               unsigned long long* stats, const uint32_t* only,
-                              const uint32_t* qidx, hipStream_t s) {
+                              const uint32_t* qidx, hipStream_t s, float* gheap = nullptr) {
     const int ef = efSearch > k ? efSearch : k;
     const size_t lds_q = sizeof(float) * g.ld;
     const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
     const bool x_lds_vis = lds_x + vwords * 4 <= 64 * 1024;
+    if (lds_x > 64 * 1024) {
+        // heaps in global scratch; the LDS keeps the query, the hop's fresh
+        // neighbours and (when it fits) the visited bitmap
+        FAISS_THROW_IF_NOT(gheap != nullptr);
+        const size_t lds_g = lds_q + 8 * 64 + 4 * 8;
+        if (lds_g + vwords * 4 <= 64 * 1024)
+            k_hnsw_exact<true, true><<<dim3((unsigned)n), dim3(64), lds_g + vwords * 4, s>>>(
+                    g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
+                    gheap);
+        else
+            k_hnsw_exact<false, true><<<dim3((unsigned)n), dim3(64), lds_g, s>>>(
+                    g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats, only,
+                    qidx, gheap);
+        HIP_LAUNCH_CHECK();
+        return;
+    }
     if (ef <= 64 && k <= 64) {  // register heaps
         const size_t lds_r = sizeof(float) * exact_reg_qpad(g);
         const bool rvis = lds_r + vwords * 4 <= 64 * 1024;
@@ -1209,32 +1229,48 @@ void hnsw_exact_listed(const HNSWDevice& g, const float* x, int ldx, const uint3
                       stats, nullptr, qidx, s);
 }
 
+size_t hnsw_heap_scratch_words(int k, int efSearch, int ld) {
+    const int ef = efSearch > k ? efSearch : k;
+    const size_t lds_x = sizeof(float) * (size_t)ld + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 32;
+    return lds_x > 64 * 1024 ? 2 * (size_t)ef + 2 * (size_t)k : 0;
+}
+bool hnsw_register_eligible(int k, int efSearch) {
+    const int ef = efSearch > k ? efSearch : k;
+    return ef <= 64 && k <= 64;
+}
+bool hnsw_uses_batched(int k, int efSearch) {
+    const int ef = efSearch > k ? efSearch : k;
+    const char* menv = getenv("FAISS_AMD_HNSW");
+    const bool prefer_batched = menv && !strcmp(menv, "batched");
+    return ef <= 128 && k <= kMaxK && (prefer_batched || !hnsw_register_eligible(k, efSearch));
+}
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
-                 hipStream_t s, KernelTimes* kt, bool defer) {
+                 hipStream_t s, KernelTimes* kt, bool defer, float* heap_scratch) {
     if (n <= 0) return;
-    FAISS_THROW_IF_NOT_FMT(k >= 1 && k <= kMaxKExact, "k = %d must be in [1, %d]", k,
-                           kMaxKExact);
+    FAISS_THROW_IF_NOT_FMT(k >= 1, "k = %d must be >= 1", k);
     const int ef = efSearch > k ? efSearch : k;
     FAISS_THROW_IF_NOT(g.ld % 4 == 0);
     const int64_t vwords = visited_words_per_query;
     const size_t lds_q = sizeof(float) * g.ld;
-    const bool batched = ef <= 128 && k <= kMaxK;
+    // FAISS_AMD_HNSW=batched: the batched kernel (+ sequential re-runs of
+    // tied queries) also where the register kernel serves every query
+    const bool batched = hnsw_uses_batched(k, efSearch);
     // sequential kernel: query | ef heap | k heap | 64 fresh | 8 scalars | visited
+    // (heaps in global scratch when they do not fit)
     const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
-    const bool x_lds_vis = lds_x + vwords * 4 <= 64 * 1024;
-    FAISS_THROW_IF_NOT_FMT(lds_x <= 64 * 1024, "max(efSearch, k) = %d too large for LDS", ef);
+    const size_t lds_xg = lds_x > 64 * 1024 ? lds_q + 8 * 64 + 4 * 8 : lds_x;
+    const bool x_lds_vis = lds_xg + vwords * 4 <= 64 * 1024;
     const bool lds_vis = vwords * 4 <= 64 * 1024;
     if (!lds_vis || !x_lds_vis) {
         FAISS_THROW_IF_NOT(visited_scratch != nullptr);
         HIP_CHECK(hipMemsetAsync(visited_scratch, 0, sizeof(uint32_t) * vwords * n, s));
     }
-    (void)x_lds_vis;
     auto exact = [&](const uint32_t* only) {
         ScopedKernelTimer tm(kt, "hnsw_exact", 0.0, s);
         hnsw_exact_launch(g, x, ldx, n, k, efSearch, D, I, I32, visited_scratch, vwords, stats,
-                          only, nullptr, s);
+                          only, nullptr, s, heap_scratch);
     };
     // FAISS_AMD_HNSW_EXACT=1: every query through the sequential kernel (tests)
     const char* xenv = getenv("FAISS_AMD_HNSW_EXACT");

@@ -259,7 +259,7 @@ struct IndexFlat : Index {
     mutable int cfold_ = 0;  // d_cst_ carries folded norm fragments (L2)
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
-    mutable DeviceBuffer s_xn_, s_tile_, s_cand_d_, s_cand_i_, s_qimg_;
+    mutable DeviceBuffer s_xn_, s_tile_, s_cand_d_, s_cand_i_, s_qimg_, s_sel_;
 };
 struct IndexFlatL2 : IndexFlat {
     explicit IndexFlatL2(idx_t d = 0) : IndexFlat(d, METRIC_L2) {}
@@ -333,9 +333,20 @@ struct IndexHNSW : Index {
         const int32_t* I = nullptr;     // [nf][k] exact assignments
         hipEvent_t done = nullptr;
     };
+    // A split in progress holds this quantizer's lock from split_begin (when
+    // it returns true) until split_release, so searches of other callers
+    // sharing the quantizer wait instead of overwriting its split state;
+    // SplitHold releases it on scope exit.
     bool split_begin(idx_t n, const float* x, int ldx, int k, float* distances, int32_t* labels,
                      const SearchParameters* params, hipStream_t stream) const;
     Split split_finish() const;
+    void split_release() const;
+    struct SplitHold {
+        const IndexHNSW* q = nullptr;
+        ~SplitHold() {
+            if (q) q->split_release();
+        }
+    };
 
    private:
     template <class OutIdx>
@@ -343,7 +354,7 @@ struct IndexHNSW : Index {
                      const SearchParameters* params, hipStream_t stream,
                      bool defer = false) const;
     mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, d_nb0_, s_visited_, d_stats_,
-            s_flags_, s_fidx_, s_fcnt_, s_fD_, s_fI_;
+            s_flags_, s_fidx_, s_fcnt_, s_fD_, s_fI_, s_heaps_;
     mutable uint32_t* h_fcnt_ = nullptr;  // pinned read-back of the flagged count
     mutable hipEvent_t ev_split_ = nullptr, ev_exact_ = nullptr;
     mutable hipStream_t side_ = nullptr;
@@ -355,6 +366,9 @@ struct IndexHNSW : Index {
         hipStream_t s = nullptr;
     };
     mutable SplitState split_;
+    // device order of searches on different streams sharing this index's
+    // scratch (a split leaves it at split_release)
+    mutable StreamOrder order_;
     mutable int nb0_stride_ = 0;  // level-0 table width (0: not built)
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;

@@ -94,6 +94,40 @@ def test_c4_hnsw32_ivf16384(amd, orc, gpu, c4_index, ef):
     check(D, I, Dr, Ir, f"c4 efSearch {ef}")
 
 
+@pytest.mark.parametrize("nprobe,ef", [(256, 768), (2500, 2500), (6400, 19200)])
+def test_c4_harness_grid_corners(amd, orc, gpu, c4_index, nprobe, ef):
+    """The reference harness's (nprobe, efSearch) grid reaches nprobe 6400 and
+    efSearch 3 nprobe (tutorial/cpp/benchmark-hnsw-ivf/benchmark.config):
+    wide HNSW heaps (LDS, then global scratch past the LDS), nprobe past the
+    MFMA filters (the general exact scan)."""
+    d, nq = 128, 64
+    idx = c4_index
+    idx.nprobe = nprobe
+    amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", ef)
+    try:
+        xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+        D, I = idx.search(xq, 10)
+        ref = orc.IVFOracle.from_index(idx)
+        Dr, Ir, _, _ = ref.search(xq, 10, nprobe, efSearch=ef, nslices=1)
+        check(D, I, Dr, Ir, f"c4 nprobe {nprobe} efSearch {ef}")
+    finally:
+        idx.nprobe = 64
+        amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", 64)
+
+
+@pytest.mark.parametrize("nprobe", [2049, 4096])
+def test_flat_coarse_nprobe_beyond_2048(amd, orc, gpu, nprobe):
+    """A flat quantizer's top-nprobe beyond 2048 (the global-scratch select)."""
+    d, nq = 32, 40
+    idx = build(amd, "IVF4096,Flat", d, 200_000, 200_000)
+    idx.nprobe = nprobe
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    D, I = idx.search(xq, 10)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, nprobe, nslices=1)
+    check(D, I, Dr, Ir, f"IVF4096 nprobe {nprobe}")
+
+
 def test_c5_ivf65536_pq48_shard(amd, orc, gpu):
     d, nq = 96, 2000
     idx = build(amd, "IVF65536,PQ48", d, 2_000_000, 65536 * 16)
