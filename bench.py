@@ -67,34 +67,45 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector == fp32 MFMA peak
 PEAK_HBM_GBS = 8000.0
 PEAK_L2_GBS = 34500.0      # MI355X_MICROARCH.md: aggregate L2 (4 MiB per XCD), measured
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
-# kernel stage (library timer name) -> device symbol substring of its kernel
-# in the committed rocprofv3 PMC summaries
-PMC_SYMBOL = {"ivf_flat_scan": "k_ivf_bf2_stream", "ivfpq_filter": "k_ivfpq_filter",
-              "coarse_filter": "k_coarse_stream", "hnsw_search": "k_hnsw_search",
-              "ivf_rerank": "k_ivf_rerank", "coarse_rerank": "k_coarse_rerank"}
+# kernel stage (library timer name) -> regular expression of the demangled
+# symbol of the kernel that stage launches in this round's code, matched in
+# this round's committed rocprofv3 PMC summaries (a summary of an older kernel
+# or round is never used: traffic is null instead)
+ROUND = 4
+PMC_SYMBOL = {
+    "ivf_flat_scan": r"kern::k_ivf_bf2_stream<true, \d+, \d+, false, true, false>",
+    "ivfpq_filter": r"kern::k_ivf_bf2_stream<true, \d+, \d+, false, true, true>",
+    "coarse_filter": r"kern::k_coarse_stream<",
+    "hnsw_search": r"kern::k_hnsw_search<",
+    "hnsw_exact": r"kern::k_hnsw_exact_reg<",
+    "ivf_rerank": r"kern::k_ivf_rerank<true, \d+, 0>",
+    "ivfpq_rerank": r"kern::k_ivf_rerank<true, \d+, [1-9]\d*>",
+    "coarse_rerank": r"kern::k_coarse_rerank<",
+}
 
 
-def pmc_traffic(config, kernel_sub):
-    """HBM bytes per launch of a kernel from the newest committed rocprofv3
-    --pmc summary for this workload (profiles/rNN_<config>_pmc.json, written
-    by scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950 correction +
-    WRITE_SIZE, separate passes)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")))
-    if not files or not kernel_sub:
+def pmc_traffic(config, stage):
+    """HBM bytes per launch of a stage's kernel from this round's committed
+    rocprofv3 --pmc summary for the workload (profiles/rNN_<config>_pmc.json,
+    written by scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950 correction
+    + WRITE_SIZE, separate passes); (None, None) when there is none."""
+    import re
+    fn = os.path.join(ROOT, "profiles", f"r{ROUND:02d}_{config}_pmc.json")
+    pat = PMC_SYMBOL.get(stage)
+    if not pat or not os.path.exists(fn):
         return None, None
-    with open(files[-1]) as f:
+    with open(fn) as f:
         summ = json.load(f)
     # several instantiations can match (e.g. the coarse filter of k-means
     # assignment during the build): the search's is the one launched least
     best = None
     for name, ent in summ.items():
-        if kernel_sub in name and "hbm_bytes" in ent:
+        if re.search(pat, name) and "hbm_bytes" in ent:
             if best is None or ent.get("launches", 0) < best.get("launches", 0):
                 best = ent
     if best is None:
         return None, None
-    return best["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+    return best["hbm_bytes"], os.path.relpath(fn, ROOT)
 
 
 def log(*a):
@@ -201,22 +212,34 @@ def kernel_roofline(name, ms, work, config):
              "mfma_dtype": "bf16", "mfma_flops_per_step": work["flat_flops"],
              "mfma_tflops": work["flat_flops"] / t / 1e12,
              "mfma_frac": work["flat_flops"] / t / 1e12 / PEAK_BF16_TFLOPS}
-    elif name == "ivfpq_filter":
-        # codes decoded to bf16 and multiplied against the queries' hi + lo
-        # split: 2 products of 2 dpad flops per candidate
+    elif name == "ivfpq_filter" and os.environ.get("FAISS_AMD_PQ_FILTER") == "decode":
+        # codes decoded to bf16 in the loop and multiplied against the
+        # queries' hi + lo split: 2 products of 2 dpad flops per candidate
         f = work["cands"] * 4.0 * work["dpad16"]
         r = {"bound": "mfma", "achieved": f / t / 1e12, "peak": PEAK_BF16_TFLOPS,
              "unit": "TFLOP/s", "mfma_dtype": "bf16", "algorithmic_flops_per_step": f,
              "flops_per_candidate": 4 * work["dpad16"],
              "streamed_code_bytes_per_step": work["cands"] * work.get("M", 0),
              "streamed_code_gbs": work["cands"] * work.get("M", 0) / t / 1e9}
+    elif name == "ivfpq_filter":
+        # the streamed filter over the decoded residual image: one pass over
+        # the rows of every distinct probed list, bf16 of the residual (dims
+        # padded to 32) + its folded bias term: 2 dpad + 8 bytes per row (the
+        # IVF-Flat filter's model); the MFMA view beside it
+        b = work["flat_rows"] * work["flat_row_bytes"]
+        f = work["cands"] * 4.0 * work["dpad32"]
+        r = {"bound": "hbm", "achieved": b / t / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+             "algorithmic_bytes_per_step": b, "bytes_per_row": work["flat_row_bytes"],
+             "mfma_dtype": "bf16", "mfma_flops_per_step": f, "mfma_tflops": f / t / 1e12,
+             "mfma_frac": f / t / 1e12 / PEAK_BF16_TFLOPS,
+             "pq_code_bytes_per_step": work["flat_rows"] * work.get("M", 0)}
     elif name == "coarse_filter":
         # bf16x3 x.c of every (query, centroid): 3 products of 2 dpad flops
         f = work["nq_coarse"] * work["nlist"] * 6.0 * work["dpad16"]
         r = {"bound": "mfma", "achieved": f / t / 1e12, "peak": PEAK_BF16_TFLOPS,
              "unit": "TFLOP/s", "mfma_dtype": "bf16", "algorithmic_flops_per_step": f,
              "flops_per_query_centroid": 6 * work["dpad16"]}
-    elif name == "hnsw_search" and work.get("hnsw_ndis"):
+    elif name in ("hnsw_search", "hnsw_exact") and work.get("hnsw_ndis"):
         # every distance reads one fp32 vector of the graph's storage; the
         # storage (c4: 16384 centroids, 8 MB) lives in the on-chip caches
         # (4 MiB L2 per XCD, the 256 MiB Infinity Cache), so the bytes are
@@ -228,7 +251,7 @@ def kernel_roofline(name, ms, work, config):
     if r is None:
         return None
     r["frac"] = r["achieved"] / r["peak"]
-    traffic, src = pmc_traffic(config, PMC_SYMBOL.get(name))
+    traffic, src = pmc_traffic(config, name)
     r["traffic"] = traffic
     if traffic is not None:
         r["traffic_source"] = src
@@ -440,7 +463,8 @@ def main():
     dpad32 = -(-d // 32) * 32
     lists = np.unique(ci_np)
     lists = lists[lists >= 0]
-    work = {"cands": cand_per_q * scan_q, "dpad16": dpad16, "d": d, "nlist": cfg["nlist"],
+    work = {"cands": cand_per_q * scan_q, "dpad16": dpad16, "dpad32": dpad32, "d": d,
+            "nlist": cfg["nlist"],
             "nq_coarse": nq_loc,
             # distinct lists of this rank's own batch (the scan of a sharded
             # step sees every rank's: at least these)
