@@ -524,7 +524,9 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
     sync_device();
     hipStream_t s = stream();
     const int ldx = ld();
-    DeviceBuffer bx, ba, bc, bd, bi;
+    // the host entry points' device buffers, kept between calls
+    std::lock_guard<std::mutex> hg(host_mu_);
+    DeviceBuffer &bx = h_x_, &ba = s_as_, &bc = s_ad_, &bd = h_d_, &bi = h_i_;
     bx.reserve(sizeof(float) * n * ldx);
     ba.reserve(sizeof(int32_t) * n * np);
     bc.reserve(sizeof(float) * n * np);
