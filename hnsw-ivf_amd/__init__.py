@@ -203,6 +203,7 @@ def _declare(L):
         "faiss_amd_IndexIVF_quantize_device": (C.c_int, [_P, _I64, _P, C.c_int, _P, _P, _P]),
         "faiss_amd_merge_knn_results_device": (C.c_int, [C.c_size_t, C.c_size_t, C.c_int, _P, _P, _P, _P, C.c_int, _P]),
         "faiss_amd_set_kernel_timing": (C.c_int, [C.c_int]),
+        "faiss_amd_set_search_slices": (C.c_int, [C.c_int]),
         "faiss_amd_set_kernel_timing_filter": (C.c_int, [C.c_char_p]),
         "faiss_amd_Index_type": (C.c_char_p, [_P]),
         "faiss_amd_reset_kernel_times": (C.c_int, [_P]),
@@ -866,6 +867,13 @@ def device_count():
 
 def set_device(dev):
     _check(lib().faiss_amd_set_device(int(dev)))
+
+
+def set_search_slices(t):
+    """Emulate a reference IndexIVF::search on t OpenMP threads: the batch is
+    quantized in min(t, n) slices, each in the form its size selects
+    (faiss/IndexIVF.cpp:359-368); 1 (the default) = one slice."""
+    _check(lib().faiss_amd_set_search_slices(int(t)))
 
 
 def set_kernel_timing(enable=True, only=None):

@@ -712,6 +712,10 @@ int faiss_amd_merge_knn_results_device(size_t n, size_t k, int nshard, const flo
                      metric == ::METRIC_L2, d, l, (hipStream_t)stream);
     C_CATCH
 }
+int faiss_amd_set_search_slices(int t) {
+    C_TRY set_search_slices(t);
+    C_CATCH
+}
 int faiss_amd_set_kernel_timing(int enable) {
     C_TRY set_kernel_timing_enabled(enable != 0);
     C_CATCH

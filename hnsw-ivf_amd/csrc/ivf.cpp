@@ -4,6 +4,7 @@
 // (search_preassigned), :187-285 (add), faiss/IndexIVFFlat.cpp,
 // faiss/IndexIVFPQ.cpp, faiss/IndexShardsIVF.cpp:88-245.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -290,10 +291,40 @@ uint32_t* IndexIVF::bucket_counts(hipStream_t s, uint32_t** next) const {
     return base;
 }
 
+namespace {
+std::atomic<int> g_search_slices{1};
+// [i n / nt, (i + 1) n / nt): the reference's slice bounds (IndexIVF.cpp:367-368)
+bool slices_mixed(idx_t n, int nt) {
+    // slice sizes are floor(n / nt) or that + 1: one form unless they straddle 20
+    const idx_t lo = n / nt, hi = (n + nt - 1) / nt;
+    return lo < 20 && hi >= 20;
+}
+}  // namespace
+void set_search_slices(int t) {
+    FAISS_THROW_IF_NOT_MSG(t >= 1, "set_search_slices: t must be >= 1");
+    g_search_slices = t;
+}
+int get_search_slices() { return g_search_slices; }
+
 void IndexIVF::quantize_device(idx_t n, const float* x, int ldx, int np, float* coarse_dis,
                                int32_t* assign, const SearchParameters* qparams,
                                hipStream_t s) const {
-    quantizer->assign_device(n, x, ldx, np, coarse_dis, assign, qparams, s);
+    const int nt = (int)std::min<idx_t>(g_search_slices, std::max<idx_t>(n, 1));
+    if (nt <= 1) {
+        quantizer->assign_device(n, x, ldx, np, coarse_dis, assign, qparams, s);
+        return;
+    }
+    if (!slices_mixed(n, nt)) {
+        // every slice takes the form of its size: one call with that size
+        quantizer->assign_device_slice(n, x, ldx, np, coarse_dis, assign, qparams, s, n / nt);
+        return;
+    }
+    for (int i = 0; i < nt; i++) {
+        const idx_t a = (idx_t)i * n / nt, b = (idx_t)(i + 1) * n / nt;
+        if (b > a)
+            quantizer->assign_device_slice(b - a, x + a * ldx, ldx, np, coarse_dis + a * np,
+                                           assign + a * np, qparams, s, b - a);
+    }
 }
 
 // queries per chunk: bounds the partial-result scratch to ~1 GiB (the
@@ -381,10 +412,15 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
             const void*& p;
             ~Reset() { p = nullptr; }
         } reset{shared_qimg_};
-        if (qf && qf->d == d) {
+        const int nt = (int)std::min<idx_t>(get_search_slices(), std::max<idx_t>(nq, 1));
+        const bool one_form = nt <= 1 || (nq / nt >= 20);  // the whole batch's BLAS form
+        if (qf && qf->d == d && one_form) {
             if (qf->assign_device_qimg(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
                                        s_ci_.as<int32_t>(), s_q_.ptr, s))
                 shared_qimg_ = s_q_.ptr;
+        } else if (qf) {
+            quantize_device(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
+                            s_ci_.as<int32_t>(), params ? params->quantizer_params : nullptr, s);
         } else if (mc == 0 && !selm &&
                    scan_hnsw_split(nq, x + q0 * ldx, ldx, k, (int)np, distances + q0 * k,
                                    labels + q0 * k,

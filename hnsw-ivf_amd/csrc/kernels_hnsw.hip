@@ -824,6 +824,17 @@ struct CandLayout {
         if (spos == bpos) h.key = (h.key & 0xffffffff00000000ull) | HKEY_DEAD_LO;
         return true;
     }
+    // the alive entry pop_min would take now (prefetch hint; ~0 when none)
+    __device__ __forceinline__ uint64_t peek_min(int lane) const {
+        const int spos = lane ? lane : 64;
+        const uint32_t chi = (uint32_t)(h.key >> 32);
+        const bool alive = spos <= hk && (uint32_t)h.key != HKEY_DEAD_LO;
+        const unsigned long long am = __ballot(alive);
+        if (!am) return ~0ull;
+        const uint32_t kmin = wave_min_u32(alive ? chi : 0xffffffffu);
+        const uint64_t at = rotr1(__ballot(alive && chi == kmin));
+        return h.at(64 - __builtin_clzll(at));
+    }
     // MinimaxHeap::push (:1096-1107)
     __device__ __forceinline__ bool push(int ef, uint64_t nk, float dis, int& nvalid, int lane) {
         if (hk == ef) {
@@ -852,6 +863,10 @@ struct CandSet {
     }
     __device__ __forceinline__ void seed(uint64_t nk, int lane) { insert(hk++, nk, lane); }
     __device__ __forceinline__ float top_dis() const { return hkey_dis(rdlane64(key, hk - 1)); }
+    __device__ __forceinline__ uint64_t peek_min(int lane) const {
+        const unsigned long long am = __ballot(lane < hk && (uint32_t)key != HKEY_DEAD_LO);
+        return am ? rdlane64(key, __builtin_ctzll(am)) : ~0ull;
+    }
     __device__ __forceinline__ bool pop_min(int lane, int32_t& v0, int& nb) {
         const uint32_t chi = (uint32_t)(key >> 32);
         const bool alive = lane < hk && (uint32_t)key != HKEY_DEAD_LO;
@@ -925,6 +940,11 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
     if (lane == 0) vis[nearest >> 5] |= 1u << (nearest & 31);
     __syncthreads();
     if (TRACE) tr.tick(7);
+    const int cnt = g.cum_nb[1] - g.cum_nb[0];
+    // the next hop's neighbour ids, loaded during this hop's heap updates for
+    // the node pop_min is predicted to take (pf_v; a hint: a wrong guess only
+    // costs the load)
+    int32_t pf_v = -1, pf_nb = -1;
     for (;;) {
         if (nvalid <= 0) {  // candidates.size() == 0
             st_n2 = 1;
@@ -941,9 +961,10 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
         if (TRACE) tr.tick(0);
         // neighbours of v0 in stored order, fresh ones compacted to lanes
         // 0..nf-1 (their arrival order)
-        const int cnt = g.cum_nb[1] - g.cum_nb[0];
         int32_t v1 = -1;
-        if (lane < cnt)
+        if (v0 == pf_v)
+            v1 = pf_nb;
+        else if (lane < cnt)
             v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
                        : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
         const unsigned long long neg =
@@ -990,6 +1011,19 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
         // full takes every arrival.
         const bool full0 = C.hk == ef;
         const float ctop0 = full0 ? C.top_dis() : FLT_MAX;
+        if (g.nb0) {
+            // next pop: the closest arrival if it enters and beats the
+            // closest alive candidate, else that candidate
+            const uint32_t fb = lane < nf ? (uint32_t)__float_as_int(fdis) : 0xffffffffu;
+            const uint32_t amin = wave_min_u32(fb);
+            const uint64_t cmin = C.peek_min(lane);
+            int32_t pred = cmin != ~0ull ? hkey_id(cmin) : -1;
+            if (nf > 0 && (!full0 || __int_as_float((int)amin) < ctop0) &&
+                amin < (uint32_t)(cmin >> 32))
+                pred = __builtin_amdgcn_readlane(fv, __builtin_ctzll(__ballot(lane < nf && fb == amin)));
+            pf_v = pred;
+            if (pred >= 0 && lane < cnt) pf_nb = g.nb0[(int64_t)pred * g.nb0_stride + lane];
+        }
         unsigned long long todo = __ballot(lane < nf && (!full0 || fdis < rmax || fdis < ctop0));
         while (todo) {
             const int t = __builtin_ctzll(todo);

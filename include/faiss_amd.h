@@ -767,6 +767,16 @@ Index* read_index(FILE* f, int io_flags = 0);
 // faiss/index_factory.h (subset: Flat, IVFn[_HNSWm],Flat|PQm[xb][np], HNSWm)
 Index* index_factory(int d, const char* description, MetricType metric = METRIC_L2);
 
+// The reference's IndexIVF::search cuts a batch into min(omp threads, n)
+// slices and quantizes each with the form its size selects (the direct
+// fvec_L2sqr form below distance_compute_blas_threshold = 20 queries, else
+// the BLAS form; faiss/IndexIVF.cpp:359-368, faiss/utils/distances.cpp:
+// 807-823).  set_search_slices(t) makes the IVF searches emulate a reference
+// run on t OpenMP threads (default 1: the batch is one slice); results can
+// differ between t only by coarse near-ties.
+void set_search_slices(int t);
+int get_search_slices();
+
 // float_rand (faiss/utils/random.cpp:95-112), bit-exact restatement
 void float_rand(float* x, size_t n, int64_t seed);
 // selected rows (row0, row0 + step, ...) of float_rand(n_rows * d, seed)

@@ -510,6 +510,10 @@ int faiss_amd_merge_knn_results_device(
         idx_t* labels_dev,
         FaissMetricType metric,
         void* stream);
+/* extension: emulate a reference run on t OpenMP threads (IndexIVF::search
+ * quantizes min(t, n) slices, each in the form its size selects,
+ * faiss/IndexIVF.cpp:359-368); default 1 */
+int faiss_amd_set_search_slices(int t);
 /* timing of the dominant kernel in the last search on this index: number of
  * launches and summed milliseconds (HIP events, only when enabled) */
 int faiss_amd_set_kernel_timing(int enable);

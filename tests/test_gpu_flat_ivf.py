@@ -323,3 +323,26 @@ def test_preassigned_duplicate_probes(amd, orc, gpu, desc, k):
     ref = orc.IVFOracle.from_index(idx)
     Dr, Ir = ref.search_preassigned(xq, k, keys, cdis)
     assert_same_results(D, I, Dr, Ir)
+
+
+@pytest.mark.parametrize("nq,t", [(40, 3), (40, 2), (59, 3), (12, 4)])
+def test_search_slices_emulate_reference_threads(amd, orc, gpu, nq, t):
+    """set_search_slices(t) = a reference run on t OpenMP threads: slices of
+    fewer than 20 queries take the direct coarse form (faiss/IndexIVF.cpp:
+    359-368, faiss/utils/distances.cpp:807-823); the oracle slices the same."""
+    d = 32
+    xb = amd.float_rand(50_000 * d, 1234).reshape(-1, d)
+    idx = amd.index_factory(d, "IVF256,Flat")
+    idx.train(xb[:20_000])
+    idx.add(xb)
+    idx.nprobe = 8
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(xq, 10, 8, nslices=min(t, nq))
+    amd.set_search_slices(t)
+    try:
+        D, I = idx.search(xq, 10)
+    finally:
+        amd.set_search_slices(1)
+    np.testing.assert_array_equal(I, Ir)
+    np.testing.assert_array_equal(D, Dr)
