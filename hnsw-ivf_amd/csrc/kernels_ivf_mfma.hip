@@ -771,10 +771,13 @@ bool ivfpq_stream_eligible(int d, int M, int k, int nprobe) {
 }
 double ivfpq_fold_coef(int d, int M) {
     // k_ivfpq_filter_w's coefficient, plus the folded bias: the accumulator
-    // sums 2 d exact products and 6 exact bias products of total magnitude
-    // <= 3.01 (|x| + |y_C| + R)^2, doubled by approx = -2 acc
+    // sums 2 d exact products and 6 exact bias products whose magnitudes add
+    // to <= (1 + 2^-8) |x| R + |term| / 2 + coarse_dis / 2 <= 0.51 S^2
+    // (S = |x| + |y_C| + R; term = R^2 + 2 <y_C, y_R>, coarse_dis = |x -
+    // y_C|^2), so its rounding is <= 0.51 (2 d + 6) u S^2, doubled by
+    // approx = -2 acc
     const double u = 1.0 / 16777216.0;
-    return ivfpq_mfma_coef(d, M) + 6.02 * (2.0 * d + 6.0) * u;
+    return ivfpq_mfma_coef(d, M) + 1.02 * (2.0 * d + 6.0) * u;
 }
 void ivfpq_stream_filter(const float* x, int ldx, int d, int M, const void* pcbs,
                          const float* cdis, const float* cnorm, const float* lrmax,

@@ -57,15 +57,20 @@ for ef in efs:
     tl = time.perf_counter() - tl
     del os.environ["FAISS_AMD_HNSW_LAYOUT"]
     ta = os.path.join(out, f"htrace_all_ef{ef}.bin")
-    if os.path.exists(ta):
-        os.unlink(ta)
+    tl_ = os.path.join(out, f"htrace_layout_ef{ef}.bin")
+    for f_ in (ta, tl_):
+        if os.path.exists(f_):
+            os.unlink(f_)
     os.environ["FAISS_AMD_HNSW_TRACE"] = ta
     q.search(xq, 64)
-    del os.environ["FAISS_AMD_HNSW_TRACE"]
+    os.environ["FAISS_AMD_HNSW_TRACE"] = tl_
+    os.environ["FAISS_AMD_HNSW_LAYOUT"] = "1"
+    q.search(xq, 64)
+    del os.environ["FAISS_AMD_HNSW_TRACE"], os.environ["FAISS_AMD_HNSW_LAYOUT"]
     del os.environ["FAISS_AMD_HNSW_EXACT"]
     print(f"ef {ef}: batched+reruns {min(ts) * 1e3:.3f} ms, all-sequential {tx * 1e3:.3f} ms "
           f"(heap layout throughout: {tl * 1e3:.3f} ms)", flush=True)
-    for tf in (tf, ta):
+    for tf in (tf, ta, tl_):
       if os.path.exists(tf):
         tr = np.fromfile(tf, dtype=np.uint64).reshape(-1, 16).astype(np.float64)
         tr = tr[tr[:, 7] > 0]
