@@ -433,7 +433,15 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
         qc = std::min<idx_t>(qc, std::max<idx_t>(1, (idx_t)(((size_t)256 << 20) /
                                                             ((size_t)vwords * 4))));
     if (hw) qc = std::min<idx_t>(qc, std::max<idx_t>(1, (idx_t)(((size_t)256 << 20) / (hw * 4))));
+    // the register kernel's replay logs (kHnswReplayCap entries per query)
+    // (FAISS_AMD_HNSW_REPLAY=0: none; such queries search level 0 again — A/B)
+    const char* renv = getenv("FAISS_AMD_HNSW_REPLAY");
+    const bool rlog = kern::hnsw_register_eligible(k, efSearch) &&
+                      !kern::hnsw_uses_batched(k, efSearch) && !(renv && !strcmp(renv, "0"));
+    if (rlog)
+        qc = std::min<idx_t>(qc, (idx_t)(((size_t)256 << 20) / (8 * kern::kHnswReplayCap)));
     qc = std::max<idx_t>(qc, 1);
+    if (rlog) s_rlog_.reserve(8 * (size_t)kern::kHnswReplayCap * qc);
     if (scratch) s_visited_.reserve(sizeof(uint32_t) * vwords * qc);
     if (hw) s_heaps_.reserve(sizeof(float) * hw * qc);
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(qc, 1));
@@ -445,7 +453,8 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
                           i32 ? nullptr : (int64_t*)labels + q0 * k,
                           i32 ? (int32_t*)labels + q0 * k : nullptr, s_visited_.as<uint32_t>(),
                           vwords, d_stats_.as<unsigned long long>(), s_flags_.as<uint32_t>(), s,
-                          &ktimes, defer, hw ? s_heaps_.as<float>() : nullptr);
+                          &ktimes, defer, hw ? s_heaps_.as<float>() : nullptr,
+                          rlog ? s_rlog_.as<uint64_t>() : nullptr, rlog ? kern::kHnswReplayCap : 0);
     }
     if (!defer) {
         order_.leave(s);

@@ -84,6 +84,8 @@ IndexIVF::IndexIVF(Index* q, size_t d_, size_t nl, size_t cs, MetricType metric)
 }
 
 IndexIVF::~IndexIVF() {
+    for (hipEvent_t e : pipe_ev_) (void)hipEventDestroy(e);
+    if (pipe_s_) (void)hipStreamDestroy(pipe_s_);
     if (own_fields) delete quantizer;
 }
 
@@ -422,6 +424,11 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
             quantize_device(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
                             s_ci_.as<int32_t>(), params ? params->quantizer_params : nullptr, s);
         } else if (mc == 0 && !selm &&
+                   scan_hnsw_pipelined(nq, x + q0 * ldx, ldx, k, (int)np, distances + q0 * k,
+                                       labels + q0 * k,
+                                       params ? params->quantizer_params : nullptr, s)) {
+            continue;
+        } else if (mc == 0 && !selm &&
                    scan_hnsw_split(nq, x + q0 * ldx, ldx, k, (int)np, distances + q0 * k,
                                    labels + q0 * k,
                                    params ? params->quantizer_params : nullptr, s)) {
@@ -436,6 +443,47 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
                                   distances + q0 * k, labels + q0 * k, s, lim, selm);
     }
     order_.leave(s);
+}
+
+// An HNSW quantizer served by the register kernel (max(efSearch, k) <= 64):
+// that kernel is latency-bound with one wave per query, and its last waves
+// leave most of the GPU idle.  The batch is searched in chunks: chunk c's
+// quantizer search runs on pipe_s_ while the caller's stream scans chunk
+// c - 1, so the scan fills the idle slots.  Each chunk is an ordinary
+// assign + search_preassigned of its queries (results identical).
+// FAISS_AMD_HNSW_PIPE=<chunks> (1: off).
+bool IndexIVF::scan_hnsw_pipelined(idx_t nq, const float* x, int ldx, idx_t k, int np,
+                                   float* distances, idx_t* labels,
+                                   const SearchParameters* qparams, hipStream_t s) const {
+    const auto* qh = dynamic_cast<const IndexHNSW*>(quantizer);
+    if (!qh || qdone_ || get_search_slices() > 1) return false;
+    int ef = qh->hnsw.efSearch;
+    if (const auto* hp = dynamic_cast<const SearchParametersHNSW*>(qparams)) ef = hp->efSearch;
+    if (!kern::hnsw_register_eligible(np, ef) || kern::hnsw_uses_batched(np, ef)) return false;
+    const char* env = getenv("FAISS_AMD_HNSW_PIPE");
+    const int P = env ? atoi(env) : 2;
+    if (P <= 1 || nq < (idx_t)P * 1024) return false;
+    if (!pipe_s_) HIP_CHECK(hipStreamCreateWithFlags(&pipe_s_, hipStreamNonBlocking));
+    while ((int)pipe_ev_.size() < P + 1) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        pipe_ev_.push_back(e);
+    }
+    // the chunks' quantizer searches follow the caller's prior work (x, and
+    // the previous readers of the coarse buffers)
+    HIP_CHECK(hipEventRecord(pipe_ev_[P], s));
+    HIP_CHECK(hipStreamWaitEvent(pipe_s_, pipe_ev_[P], 0));
+    for (int c = 0; c < P; c++) {
+        const idx_t a = nq * c / P, b = nq * (c + 1) / P;
+        float* cd = s_cd_.as<float>() + a * np;
+        int32_t* ci = s_ci_.as<int32_t>() + a * np;
+        quantizer->assign_device(b - a, x + a * ldx, ldx, np, cd, ci, qparams, pipe_s_);
+        HIP_CHECK(hipEventRecord(pipe_ev_[c], pipe_s_));
+        HIP_CHECK(hipStreamWaitEvent(s, pipe_ev_[c], 0));
+        search_preassigned_device(b - a, x + a * ldx, ldx, k, np, ci, cd, distances + a * k,
+                                  labels + a * k, s, nullptr, nullptr);
+    }
+    return true;
 }
 
 // An HNSW quantizer re-runs the queries whose batched search met an exact

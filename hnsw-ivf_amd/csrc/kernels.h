@@ -363,7 +363,13 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
                  hipStream_t s, KernelTimes* kt = nullptr,
-                 bool defer = false, float* heap_scratch = nullptr);
+                 bool defer = false, float* heap_scratch = nullptr,
+                 uint64_t* replay_log = nullptr, int64_t replay_cap = 0);
+// the register kernel's CandSet update log (64-bit entries per query in
+// replay_log): a query whose candidate set meets a layout-dependent decision
+// continues from a replayed heap instead of searching level 0 again; a query
+// whose log would exceed it searches again
+constexpr int64_t kHnswReplayCap = 4096;
 // 32-bit words of global heap scratch per query (0: the heaps fit the LDS)
 size_t hnsw_heap_scratch_words(int k, int efSearch, int ld);
 // the register kernel serves max(efSearch, k) <= 64

@@ -801,6 +801,7 @@ struct SortedQ {
 //    case (returns false) and the query is searched again with CandLayout;
 //    otherwise it evolves exactly as the heap's set does.
 struct CandLayout {
+    static constexpr bool kMerge = false;
     KHeap h;
     int hk;
     __device__ __forceinline__ void init() {
@@ -849,6 +850,7 @@ struct CandLayout {
     }
 };
 struct CandSet {
+    static constexpr bool kMerge = true;
     uint64_t key;  // lane j < hk: the j-th entry by distance
     int hk;
     __device__ __forceinline__ void init() {
@@ -896,6 +898,63 @@ struct CandSet {
         return true;
     }
 };
+// One hop's add_to_heap calls for the arrivals `todo` (lanes, arrival order)
+// as one merge, for CandSet: when no two of the distances involved are equal
+// (the arrivals' among themselves and with the kept entries of C and R), the
+// sequential updates leave each structure holding the smallest of its old
+// entries and the arrivals (C: ef of them; R: k) — an arrival a heap rejects
+// has that many entries below it, and an eviction takes the largest — so each
+// arrival's place is its rank among C (R) plus its rank among the arrivals,
+// and the kept entries fill the other places in order.  False (nothing
+// changed) on any equality, or on a tie inside C when the merge evicts:
+// then the hop runs the sequential updates.
+__device__ __forceinline__ bool hop_merge(CandSet& C, SortedQ& R, int k, int ef,
+                                          unsigned long long todo, float fdis, int32_t fv,
+                                          int lane, int& nvalid, float& rmax) {
+    const uint32_t cd = (uint32_t)(C.key >> 32), rd = (uint32_t)(R.key >> 32);
+    const uint32_t fd = (uint32_t)__float_as_int(fdis);
+    const int hk = C.hk, m = __popcll(todo);
+    const uint64_t cm = hk >= 64 ? ~0ull : ((1ull << hk) - 1ull);
+    const uint64_t rm = k >= 64 ? ~0ull : ((1ull << k) - 1ull);
+    if (hk + m > ef) {
+        const uint32_t cprev = __builtin_amdgcn_update_dpp(0u, cd, 0x138, 0xf, 0xf, false);
+        if (__ballot(lane >= 1 && lane < hk && cprev == cd)) return false;
+    }
+    int arr = 0;  // lane r: the lane of the arrival of rank r
+    uint64_t da = 0, dr = 0, tie = 0;
+    for (unsigned long long t = todo; t; t &= t - 1ull) {
+        const int j = __builtin_ctzll(t);
+        const uint32_t a = __builtin_amdgcn_readlane(fd, j);
+        const int ra = __popcll(__ballot(fd < a) & todo);
+        const int pc = __popcll(__ballot(cd < a) & cm) + ra;
+        const int pr = __popcll(__ballot(rd < a) & rm) + ra;
+        tie |= (__ballot(cd == a) & cm) | (__ballot(rd == a) & rm) |
+               (__ballot(fd == a) & todo & ~(1ull << j));
+        if (pc < 64) da |= 1ull << pc;
+        if (pr < 64) dr |= 1ull << pr;
+        arr = lane == ra ? j : arr;
+    }
+    if (tie) return false;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint64_t ak = hkey(fdis, fv);
+    const int nh = min(ef, hk + m);
+    {
+        const int na = __popcll(da & lt);
+        const int al = __builtin_amdgcn_ds_bpermute(na << 2, arr);
+        const uint64_t fa = bperm64(ak, al), fc = bperm64(C.key, (lane - na) & 63);
+        C.key = ((da >> lane) & 1ull) ? fa : fc;
+        C.hk = nh;
+    }
+    {
+        const int na = __popcll(dr & lt);
+        const int al = __builtin_amdgcn_ds_bpermute(na << 2, arr);
+        const uint64_t fa = bperm64(ak, al), fr = bperm64(R.key, (lane - na) & 63);
+        R.key = ((dr >> lane) & 1ull) ? fa : fr;
+    }
+    nvalid = __popcll(__ballot(lane < nh && (uint32_t)C.key != HKEY_DEAD_LO));
+    rmax = hkey_dis(rdlane64(R.key, k - 1));
+    return true;
+}
 }  // namespace
 
 // the register kernel's query copy: ld floats, at least 128 for ref_rows64_4lane
@@ -906,6 +965,10 @@ __host__ __device__ inline int exact_reg_qpad(const HNSWDevice& g) {
 // passes of 16 rows whose loads the register kernel issues together
 #ifndef HNSW_PB
 #define HNSW_PB 2
+#endif
+// the register kernel's waves per SIMD (its VGPR budget: 512 / HNSW_WPE)
+#ifndef HNSW_WPE
+#define HNSW_WPE 4
 #endif
 // Trace of the register kernel (FAISS_AMD_HNSW_TRACE=<file>, profiling): per
 // query the core-clock cycles of each level-0 hop phase summed over its hops:
@@ -922,23 +985,57 @@ struct HopTrace {
     }
 };
 
-// search_from_candidates at level 0 (faiss/impl/HNSW.cpp:605-741) from the
-// greedy descent's entry, with the candidate structure CQ; false when CQ
-// (CandSet) met a decision that depends on the heap layout (nothing written)
-template <class CQ, bool TRACE>
-__device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs, uint32_t* vis,
-                                            int k, int efSearch, int ef, int lane, int nearest,
-                                            float d_nearest, SortedQ& R, uint32_t& st_n2,
-                                            uint32_t& st_ndis, uint32_t& st_nhops, HopTrace& tr) {
-    CQ C;
+// The level-0 loop's state between a CandSet run that stopped at a
+// layout-dependent decision and its continuation with CandLayout.  The CandSet
+// run logs, per hop, a pop marker and the hop's arrivals in arrival order
+// (the heap updates the layout depends on); replaying that log into a
+// CandLayout rebuilds the reference's heap array at the stopping point, and
+// the search goes on from there: the results, the visited table and every
+// distance computed so far depend on the entry set alone and are kept.
+constexpr uint64_t RLOG_POP = ~0ull;  // the marker (dis bits 0xffffffff: no distance)
+struct L0Run {
+    int nvalid;
+    float rmax;
+    unsigned long long todo;  // the stopped hop's arrivals not yet applied (0: at pop_min)
+    float fdis;               // that hop's arrivals (lanes)
+    int32_t fv;
+    int64_t logpos;           // log entries written (> logcap: overflowed)
+    int64_t stop;             // log entries the replay applies
+};
+
+// the seed (:624-637): the entry point enters the candidates and the results
+template <class CQ>
+__device__ __forceinline__ void level0_seed(CQ& C, SortedQ& R, L0Run& S, uint32_t* vis, int k,
+                                            int lane, int nearest, float d_nearest) {
     C.init();
-    int nvalid = 1;
     C.seed(hkey(d_nearest, nearest), lane);
-    // (:624-637): the seed enters the results
     if (d_nearest < FLT_MAX) R.insert(k, hkey(d_nearest, nearest), lane);
-    float rmax = hkey_dis(rdlane64(R.key, k - 1));
+    S.nvalid = 1;
+    S.rmax = hkey_dis(rdlane64(R.key, k - 1));
+    S.todo = 0ull;
+    S.logpos = 0;
     if (lane == 0) vis[nearest >> 5] |= 1u << (nearest & 31);
     __syncthreads();
+}
+
+// search_from_candidates at level 0 (faiss/impl/HNSW.cpp:605-741) from state
+// S with the candidate structure CQ (S.todo != 0: first the stopped hop's
+// remaining arrivals); false when CQ (CandSet) met a decision that depends on
+// the heap layout, with S describing where (rlog: CandSet's update log, or
+// nullptr)
+template <class CQ, bool TRACE>
+__device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs, uint32_t* vis,
+                                            int k, int efSearch, int ef, int lane, CQ& C,
+                                            L0Run& S, SortedQ& R, uint32_t& st_n2,
+                                            uint32_t& st_ndis, uint32_t& st_nhops, HopTrace& tr,
+                                            uint64_t* __restrict__ rlog, int64_t logcap) {
+    int nvalid = S.nvalid;
+    float rmax = S.rmax;
+    unsigned long long todo = S.todo, hop_todo = S.todo;
+    float fdis = S.fdis;
+    int32_t fv = S.fv;
+    int64_t hp = 0;  // this hop's log position
+    bool resume = todo != 0ull;
     if (TRACE) tr.tick(7);
     const int cnt = g.cum_nb[1] - g.cum_nb[0];
     // the next hop's neighbour ids, loaded during this hop's heap updates for
@@ -946,100 +1043,159 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
     // costs the load)
     int32_t pf_v = -1, pf_nb = -1;
     for (;;) {
-        if (nvalid <= 0) {  // candidates.size() == 0
-            st_n2 = 1;
-            break;
+        if (!resume) {
+            if (nvalid <= 0) {  // candidates.size() == 0
+                st_n2 = 1;
+                break;
+            }
+            int32_t v0;
+            int nb;
+            if (!C.pop_min(lane, v0, nb)) {
+                S.nvalid = nvalid;
+                S.rmax = rmax;
+                S.todo = 0ull;
+                S.stop = S.logpos;
+                return false;
+            }
+            nvalid--;
+            if (nb >= efSearch) {
+                st_n2 = nvalid == 0 ? 1u : 0u;
+                break;
+            }
+            if (TRACE) tr.tick(0);
+            // neighbours of v0 in stored order, fresh ones compacted to lanes
+            // 0..nf-1 (their arrival order)
+            int32_t v1 = -1;
+            if (v0 == pf_v)
+                v1 = pf_nb;
+            else if (lane < cnt)
+                v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
+                           : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
+            const unsigned long long neg =
+                    __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
+            const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
+            if (TRACE) tr.tick(1);
+            // visited test-and-set: the bits as they were before this hop
+            // decide; a node listed twice in this neighbour list (the atomic
+            // then finds the bit another lane of this hop set) is visited at
+            // its first position, so only then the lanes are compared pairwise
+            const uint32_t vbit = 1u << (v1 & 31);
+            bool fresh = lane < jmax && !(vis[v1 >> 5] & vbit);
+            uint32_t old = 0u;
+            if (fresh) old = atomicOr(&vis[v1 >> 5], vbit);
+            if (__ballot(fresh && (old & vbit)) != 0ull)
+                for (int i = 0; i < jmax; i++)
+                    fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
+            const unsigned long long fm = __ballot(fresh);
+            const int nf = __popcll(fm);
+            const unsigned long long lt = (1ull << lane) - 1ull;
+            const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
+            fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
+            if (TRACE) tr.tick(2);
+            // 4 lanes per row, 16 rows per pass, two passes' loads in flight
+            // (reference order)
+            fdis = 0.f;
+            if (g.d <= 128)
+                fdis = ref_rows64_4lane_pb<true, 16, HNSW_PB>(qs, qs, g.storage, g.ld, g.d,
+                                                        lane < nf ? (uint32_t)fv : 0u, nf, lane);
+            else if (lane < nf)
+                fdis = l2_row(qs, g.storage + (int64_t)fv * g.ld, g.d);
+            st_ndis += (uint32_t)nf;
+            st_nhops += 1;
+            if (TRACE) {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                tr.tick(3);
+                tr.t[5] += 1;
+                tr.t[6] += (unsigned long long)nf;
+            }
+            // add_to_heap (:678-689) for each fresh neighbour in arrival
+            // order.  Only arrivals that can change a heap are visited: the
+            // result admits dis < rmax (rmax only falls during the hop); a full
+            // candidate heap admits dis < its top (which only falls while
+            // full); a heap not yet full takes every arrival.
+            const bool full0 = C.hk == ef;
+            const float ctop0 = full0 ? C.top_dis() : FLT_MAX;
+            if (g.nb0) {
+                // next pop: the closest arrival if it enters and beats the
+                // closest alive candidate, else that candidate
+                const uint32_t fb = lane < nf ? (uint32_t)__float_as_int(fdis) : 0xffffffffu;
+                const uint32_t amin = wave_min_u32(fb);
+                const uint64_t cmin = C.peek_min(lane);
+                int32_t pred = cmin != ~0ull ? hkey_id(cmin) : -1;
+                if (nf > 0 && (!full0 || __int_as_float((int)amin) < ctop0) &&
+                    amin < (uint32_t)(cmin >> 32))
+                    pred = __builtin_amdgcn_readlane(
+                            fv, __builtin_ctzll(__ballot(lane < nf && fb == amin)));
+                pf_v = pred;
+                if (pred >= 0 && lane < cnt) pf_nb = g.nb0[(int64_t)pred * g.nb0_stride + lane];
+            }
+            todo = __ballot(lane < nf && (!full0 || fdis < rmax || fdis < ctop0));
+            hop_todo = todo;
+            if constexpr (CQ::kMerge) {
+                // the replay log: this hop's pop, then its arrivals in order
+                if (rlog) {
+                    hp = S.logpos;
+                    const int m = __popcll(todo);
+                    if (hp + 1 + m <= logcap) {
+                        if (lane == 0) rlog[hp] = RLOG_POP;
+                        if ((todo >> lane) & 1ull)
+                            rlog[hp + 1 + __popcll(todo & lt)] = hkey(fdis, fv);
+                    }
+                    S.logpos = hp + 1 + m;
+                }
+                if (todo && hop_merge(C, R, k, ef, todo, fdis, fv, lane, nvalid, rmax))
+                    todo = 0ull;
+            }
         }
-        int32_t v0;
-        int nb;
-        if (!C.pop_min(lane, v0, nb)) return false;
-        nvalid--;
-        if (nb >= efSearch) {
-            st_n2 = nvalid == 0 ? 1u : 0u;
-            break;
-        }
-        if (TRACE) tr.tick(0);
-        // neighbours of v0 in stored order, fresh ones compacted to lanes
-        // 0..nf-1 (their arrival order)
-        int32_t v1 = -1;
-        if (v0 == pf_v)
-            v1 = pf_nb;
-        else if (lane < cnt)
-            v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
-                       : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
-        const unsigned long long neg =
-                __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
-        const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
-        if (TRACE) tr.tick(1);
-        // visited test-and-set: the bits as they were before this hop decide;
-        // a node listed twice in this neighbour list (the atomic then finds the
-        // bit another lane of this hop set) is visited at its first position,
-        // so only then the lanes are compared pairwise
-        const uint32_t vbit = 1u << (v1 & 31);
-        bool fresh = lane < jmax && !(vis[v1 >> 5] & vbit);
-        uint32_t old = 0u;
-        if (fresh) old = atomicOr(&vis[v1 >> 5], vbit);
-        if (__ballot(fresh && (old & vbit)) != 0ull)
-            for (int i = 0; i < jmax; i++)
-                fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
-        const unsigned long long fm = __ballot(fresh);
-        const int nf = __popcll(fm);
-        const unsigned long long lt = (1ull << lane) - 1ull;
-        const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
-        const int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
-        if (TRACE) tr.tick(2);
-        // 4 lanes per row, 16 rows per pass, two passes' loads in flight
-        // (reference order)
-        float fdis = 0.f;
-        if (g.d <= 128)
-            fdis = ref_rows64_4lane_pb<true, 16, HNSW_PB>(qs, qs, g.storage, g.ld, g.d,
-                                                    lane < nf ? (uint32_t)fv : 0u, nf, lane);
-        else if (lane < nf)
-            fdis = l2_row(qs, g.storage + (int64_t)fv * g.ld, g.d);
-        st_ndis += (uint32_t)nf;
-        st_nhops += 1;
-        if (TRACE) {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            tr.tick(3);
-            tr.t[5] += 1;
-            tr.t[6] += (unsigned long long)nf;
-        }
-        // add_to_heap (:678-689) for each fresh neighbour in arrival order.
-        // Only arrivals that can change a heap are visited: the result admits
-        // dis < rmax (rmax only falls during the hop); a full candidate heap
-        // admits dis < its top (which only falls while full); a heap not yet
-        // full takes every arrival.
-        const bool full0 = C.hk == ef;
-        const float ctop0 = full0 ? C.top_dis() : FLT_MAX;
-        if (g.nb0) {
-            // next pop: the closest arrival if it enters and beats the
-            // closest alive candidate, else that candidate
-            const uint32_t fb = lane < nf ? (uint32_t)__float_as_int(fdis) : 0xffffffffu;
-            const uint32_t amin = wave_min_u32(fb);
-            const uint64_t cmin = C.peek_min(lane);
-            int32_t pred = cmin != ~0ull ? hkey_id(cmin) : -1;
-            if (nf > 0 && (!full0 || __int_as_float((int)amin) < ctop0) &&
-                amin < (uint32_t)(cmin >> 32))
-                pred = __builtin_amdgcn_readlane(fv, __builtin_ctzll(__ballot(lane < nf && fb == amin)));
-            pf_v = pred;
-            if (pred >= 0 && lane < cnt) pf_nb = g.nb0[(int64_t)pred * g.nb0_stride + lane];
-        }
-        unsigned long long todo = __ballot(lane < nf && (!full0 || fdis < rmax || fdis < ctop0));
+        resume = false;
         while (todo) {
             const int t = __builtin_ctzll(todo);
-            todo &= todo - 1ull;
             const int32_t vt = __builtin_amdgcn_readlane(fv, t);
             const float dis = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), t));
             const uint64_t nk = hkey(dis, vt);
+            if (!C.push(ef, nk, dis, nvalid, lane)) {
+                S.nvalid = nvalid;
+                S.rmax = rmax;
+                S.todo = todo;
+                S.fdis = fdis;
+                S.fv = fv;
+                S.stop = hp + 1 + __popcll(hop_todo & ((1ull << t) - 1ull));
+                return false;
+            }
+            todo &= todo - 1ull;
             if (dis < rmax) {
                 R.insert(k, nk, lane);
                 rmax = hkey_dis(rdlane64(R.key, k - 1));
             }
-            if (!C.push(ef, nk, dis, nvalid, lane)) return false;
         }
         if (TRACE) tr.tick(4);
     }
     return true;
+}
+
+// CandSet's log up to S.stop into a fresh CandLayout seeded like it: the
+// heap array the reference holds at that point (the pops before the stop
+// took a unique minimum, the evictions a unique top)
+__device__ __forceinline__ void level0_replay(CandLayout& C, const uint64_t* __restrict__ rlog,
+                                              int64_t stop, int ef, int lane, int nearest,
+                                              float d_nearest) {
+    C.init();
+    C.seed(hkey(d_nearest, nearest), lane);
+    int dummy = 0;
+    for (int64_t base = 0; base < stop; base += 64) {
+        const uint64_t e = base + lane < stop ? rlog[base + lane] : RLOG_POP;
+        const int cnt = stop - base < 64 ? (int)(stop - base) : 64;
+        for (int i = 0; i < cnt; i++) {
+            const uint64_t v = rdlane64(e, i);
+            if (v == RLOG_POP) {
+                int32_t v0;
+                int nb;
+                C.pop_min(lane, v0, nb);
+            } else {
+                C.push(ef, v, hkey_dis(v), dummy, lane);
+            }
+        }
+    }
 }
 
 // The reference's HNSW::search for ef, k <= 64, one wave per query: the
@@ -1048,7 +1204,7 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
 // every query with CandLayout — tests).  Results are the reference's, bit for
 // bit, either way.
 template <bool LDS_VISITED, bool TRACE = false>
-__global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float* __restrict__ x,
+__global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, const float* __restrict__ x,
                                                        int ldx, int64_t n, int k, int efSearch,
                                                        int ef, float* __restrict__ D,
                                                        int64_t* __restrict__ I,
@@ -1058,7 +1214,8 @@ __global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float
                                                        unsigned long long* __restrict__ stats,
                                                        const uint32_t* __restrict__ only,
                                                        const uint32_t* __restrict__ qidx, int layout,
-                                                       unsigned long long* __restrict__ trace) {
+                                                       unsigned long long* __restrict__ trace,
+                                                       uint64_t* __restrict__ rlog, int64_t logcap) {
     // qidx: compact launch over listed queries (input row qidx[b], output
     // row b); else query b, output row b
     const int64_t q = qidx ? (int64_t)qidx[blockIdx.x] : (int64_t)blockIdx.x;
@@ -1120,22 +1277,35 @@ __global__ __launch_bounds__(64) void k_hnsw_exact_reg(HNSWDevice g, const float
         }
         // ---- level 0
         const uint32_t up_ndis = st_ndis, up_nhops = st_nhops;
+        uint64_t* qlog = rlog ? rlog + (int64_t)blockIdx.x * logcap : nullptr;
+        L0Run S;
         bool done = false;
-        if (!layout)
-            done = hnsw_level0<CandSet, TRACE>(g, qs, vis, k, efSearch, ef, lane, nearest,
-                                               d_nearest, R, st_n2, st_ndis, st_nhops, tr);
+        if (!layout) {
+            CandSet C;
+            level0_seed(C, R, S, vis, k, lane, nearest, d_nearest);
+            done = hnsw_level0<CandSet, TRACE>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
+                                               st_ndis, st_nhops, tr, qlog, logcap);
+        }
         if (!done) {
-            // again with the heap layout: fresh visited table, results, counters
-            __syncthreads();
-            for (int64_t w = lane; w < vwords; w += 64) vis[w] = 0u;
-            R.key = hkey(FLT_MAX, -1);
-            st_n2 = 0;
-            st_ndis = up_ndis;
-            st_nhops = up_nhops;
+            CandLayout C;
             if (TRACE) tr.t[8] = 1;
-            __syncthreads();
-            hnsw_level0<CandLayout, TRACE>(g, qs, vis, k, efSearch, ef, lane, nearest, d_nearest,
-                                           R, st_n2, st_ndis, st_nhops, tr);
+            if (!layout && qlog && S.logpos <= logcap) {
+                // continue from the stopping point with the replayed heap
+                level0_replay(C, qlog, S.stop, ef, lane, nearest, d_nearest);
+                if (TRACE) tr.t[9] = (unsigned long long)S.stop;
+            } else {
+                // again from the start: fresh visited table, results, counters
+                __syncthreads();
+                for (int64_t w = lane; w < vwords; w += 64) vis[w] = 0u;
+                R.key = hkey(FLT_MAX, -1);
+                st_n2 = 0;
+                st_ndis = up_ndis;
+                st_nhops = up_nhops;
+                __syncthreads();
+                level0_seed(C, R, S, vis, k, lane, nearest, d_nearest);
+            }
+            hnsw_level0<CandLayout, TRACE>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
+                                           st_ndis, st_nhops, tr, nullptr, 0);
         }
     }
     if (TRACE && lane == 0) {
@@ -1165,7 +1335,8 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
                               int efSearch, float* D, int64_t* I, int32_t* I32,
                               uint32_t* visited_scratch, int64_t vwords,
                               unsigned long long* stats, const uint32_t* only,
-                              const uint32_t* qidx, hipStream_t s, float* gheap = nullptr) {
+                              const uint32_t* qidx, hipStream_t s, float* gheap = nullptr,
+                              uint64_t* rlog = nullptr, int64_t logcap = 0) {
     const int ef = efSearch > k ? efSearch : k;
     const size_t lds_q = sizeof(float) * g.ld;
     const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
@@ -1200,7 +1371,7 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
             HIP_CHECK(hipMemsetAsync(tb, 0, 128 * std::max<int64_t>(n, 1), s));
             k_hnsw_exact_reg<true, true><<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
-                    layout, tb);
+                    layout, tb, rlog, logcap);
             HIP_LAUNCH_CHECK();
             std::vector<unsigned long long> h((size_t)n * 16);
             HIP_CHECK(hipMemcpyAsync(h.data(), tb, 128 * n, hipMemcpyDeviceToHost, s));
@@ -1215,11 +1386,11 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
         if (rvis)
             k_hnsw_exact_reg<true><<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
-                    layout, nullptr);
+                    layout, nullptr, rlog, logcap);
         else
             k_hnsw_exact_reg<false><<<dim3((unsigned)n), dim3(64), lds_r, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
-                    only, qidx, layout, nullptr);
+                    only, qidx, layout, nullptr, rlog, logcap);
         HIP_LAUNCH_CHECK();
         return;
     }
@@ -1281,7 +1452,8 @@ bool hnsw_uses_batched(int k, int efSearch) {
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
-                 hipStream_t s, KernelTimes* kt, bool defer, float* heap_scratch) {
+                 hipStream_t s, KernelTimes* kt, bool defer, float* heap_scratch,
+                 uint64_t* replay_log, int64_t replay_cap) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_FMT(k >= 1, "k = %d must be >= 1", k);
     const int ef = efSearch > k ? efSearch : k;
@@ -1304,7 +1476,7 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
     auto exact = [&](const uint32_t* only) {
         ScopedKernelTimer tm(kt, "hnsw_exact", 0.0, s);
         hnsw_exact_launch(g, x, ldx, n, k, efSearch, D, I, I32, visited_scratch, vwords, stats,
-                          only, nullptr, s, heap_scratch);
+                          only, nullptr, s, heap_scratch, replay_log, replay_cap);
     };
     // FAISS_AMD_HNSW_EXACT=1: every query through the sequential kernel (tests)
     const char* xenv = getenv("FAISS_AMD_HNSW_EXACT");

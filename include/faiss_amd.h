@@ -354,7 +354,7 @@ struct IndexHNSW : Index {
                      const SearchParameters* params, hipStream_t stream,
                      bool defer = false) const;
     mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, d_nb0_, s_visited_, d_stats_,
-            s_flags_, s_fidx_, s_fcnt_, s_fD_, s_fI_, s_heaps_;
+            s_flags_, s_fidx_, s_fcnt_, s_fD_, s_fI_, s_heaps_, s_rlog_;
     mutable uint32_t* h_fcnt_ = nullptr;  // pinned read-back of the flagged count
     mutable hipEvent_t ev_split_ = nullptr, ev_exact_ = nullptr;
     mutable hipStream_t side_ = nullptr;
@@ -553,6 +553,14 @@ struct IndexIVF : Index {
     bool scan_hnsw_split(idx_t nq, const float* x, int ldx, idx_t k, int np, float* distances,
                          idx_t* labels, const SearchParameters* qparams, hipStream_t s) const;
     mutable DeviceBuffer s_fx_, s_fDo_, s_fIo_;  // the re-run queries' rows and results
+    // HNSW quantizer (register kernel): the batch in chunks, each chunk's
+    // quantizer search on pipe_s_ overlapping the previous chunk's scan on the
+    // caller's stream; false = not applicable
+    bool scan_hnsw_pipelined(idx_t nq, const float* x, int ldx, idx_t k, int np,
+                             float* distances, idx_t* labels, const SearchParameters* qparams,
+                             hipStream_t s) const;
+    mutable hipStream_t pipe_s_ = nullptr;
+    mutable std::vector<hipEvent_t> pipe_ev_;
     // query image the flat quantizer prepared into s_q_ for the chunk
     // search() is scanning (IndexFlat::assign_device_qimg), null outside it
     mutable const void* shared_qimg_ = nullptr;

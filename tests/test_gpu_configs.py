@@ -81,6 +81,28 @@ def test_c4_device_entry_point(amd, orc, gpu, c4_index, ef):
     check(D, I, Dr, Ir, f"c4 device efSearch {ef}")
 
 
+def test_c4_pipelined_chunks(amd, orc, gpu, c4_index, monkeypatch):
+    """IndexIVF::scan_hnsw_pipelined: the batch in 1 / 2 / 3 chunks (each
+    chunk's quantizer search on a side stream overlapping the previous chunk's
+    scan) gives one result, the reference's."""
+    from conftest import device_search
+    d, nq = 128, 4099
+    idx = c4_index
+    idx.nprobe = 64
+    amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", 64)
+    xq = amd.float_rand(nq * d, 777).reshape(nq, d)
+    out = {}
+    for p in ("1", "2", "3"):
+        monkeypatch.setenv("FAISS_AMD_HNSW_PIPE", p)
+        out[p] = device_search(idx, xq, 10)
+    for p in ("2", "3"):
+        check(out[p][0], out[p][1], out["1"][0], out["1"][1], f"c4 pipelined {p} chunks")
+    rows = np.arange(0, nq, 41)
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(np.ascontiguousarray(xq[rows]), 10, 64, efSearch=64, nslices=1)
+    check_subset(out["3"][0], out["3"][1], Dr, Ir, rows, "c4 pipelined vs oracle")
+
+
 @pytest.mark.parametrize("ef", [16, 64, 128])
 def test_c4_hnsw32_ivf16384(amd, orc, gpu, c4_index, ef):
     d, nq = 128, 2000
