@@ -369,7 +369,7 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
 // replay_log): a query whose candidate set meets a layout-dependent decision
 // continues from a replayed heap instead of searching level 0 again; a query
 // whose log would exceed it searches again
-constexpr int64_t kHnswReplayCap = 4096;
+constexpr int64_t kHnswReplayCap = 1024;
 // 32-bit words of global heap scratch per query (0: the heaps fit the LDS)
 size_t hnsw_heap_scratch_words(int k, int efSearch, int ld);
 // the register kernel serves max(efSearch, k) <= 64

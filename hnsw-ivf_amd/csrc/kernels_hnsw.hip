@@ -993,14 +993,15 @@ struct HopTrace {
 // the search goes on from there: the results, the visited table and every
 // distance computed so far depend on the entry set alone and are kept.
 constexpr uint64_t RLOG_POP = ~0ull;  // the marker (dis bits 0xffffffff: no distance)
+constexpr int RLOG_CAP = (int)kHnswReplayCap;  // entries per query
 struct L0Run {
     int nvalid;
     float rmax;
     unsigned long long todo;  // the stopped hop's arrivals not yet applied (0: at pop_min)
     float fdis;               // that hop's arrivals (lanes)
     int32_t fv;
-    int64_t logpos;           // log entries written (> logcap: overflowed)
-    int64_t stop;             // log entries the replay applies
+    int logpos;               // log entries written (> RLOG_CAP: overflowed)
+    int stop;                 // log entries the replay applies
 };
 
 // the seed (:624-637): the entry point enters the candidates and the results
@@ -1023,19 +1024,42 @@ __device__ __forceinline__ void level0_seed(CQ& C, SortedQ& R, L0Run& S, uint32_
 // remaining arrivals); false when CQ (CandSet) met a decision that depends on
 // the heap layout, with S describing where (rlog: CandSet's update log, or
 // nullptr)
-template <class CQ, bool TRACE>
+template <class CQ, bool TRACE, bool NB0>
 __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs, uint32_t* vis,
                                             int k, int efSearch, int ef, int lane, CQ& C,
                                             L0Run& S, SortedQ& R, uint32_t& st_n2,
                                             uint32_t& st_ndis, uint32_t& st_nhops, HopTrace& tr,
-                                            uint64_t* __restrict__ rlog, int64_t logcap) {
+                                            uint64_t* __restrict__ rlog) {
     int nvalid = S.nvalid;
     float rmax = S.rmax;
-    unsigned long long todo = S.todo, hop_todo = S.todo;
-    float fdis = S.fdis;
-    int32_t fv = S.fv;
-    int64_t hp = 0;  // this hop's log position
-    bool resume = todo != 0ull;
+    // the sequential add_to_heap calls (:678-689) for the arrivals `todo`
+    // (lanes fdis, fv) of the hop whose log entries start at hp; false when C
+    // stops (S then says where)
+    auto apply = [&](unsigned long long todo, unsigned long long hop_todo, float fdis, int32_t fv,
+                     int hp) -> bool {
+        while (todo) {
+            const int t = __builtin_ctzll(todo);
+            const int32_t vt = __builtin_amdgcn_readlane(fv, t);
+            const float dis = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), t));
+            const uint64_t nk = hkey(dis, vt);
+            if (!C.push(ef, nk, dis, nvalid, lane)) {
+                S.nvalid = nvalid;
+                S.rmax = rmax;
+                S.todo = todo;
+                S.fdis = fdis;
+                S.fv = fv;
+                S.stop = hp + 1 + __popcll(hop_todo & ((1ull << t) - 1ull));
+                return false;
+            }
+            todo &= todo - 1ull;
+            if (dis < rmax) {
+                R.insert(k, nk, lane);
+                rmax = hkey_dis(rdlane64(R.key, k - 1));
+            }
+        }
+        return true;
+    };
+    if (S.todo && !apply(S.todo, S.todo, S.fdis, S.fv, 0)) return false;
     if (TRACE) tr.tick(7);
     const int cnt = g.cum_nb[1] - g.cum_nb[0];
     // the next hop's neighbour ids, loaded during this hop's heap updates for
@@ -1043,7 +1067,7 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
     // costs the load)
     int32_t pf_v = -1, pf_nb = -1;
     for (;;) {
-        if (!resume) {
+        {
             if (nvalid <= 0) {  // candidates.size() == 0
                 st_n2 = 1;
                 break;
@@ -1069,8 +1093,8 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
             if (v0 == pf_v)
                 v1 = pf_nb;
             else if (lane < cnt)
-                v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
-                           : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
+                v1 = NB0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
+                         : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
             const unsigned long long neg =
                     __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
             const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
@@ -1090,11 +1114,11 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
             const int nf = __popcll(fm);
             const unsigned long long lt = (1ull << lane) - 1ull;
             const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
-            fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
+            const int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
             if (TRACE) tr.tick(2);
             // 4 lanes per row, 16 rows per pass, two passes' loads in flight
             // (reference order)
-            fdis = 0.f;
+            float fdis = 0.f;
             if (g.d <= 128)
                 fdis = ref_rows64_4lane_pb<true, 16, HNSW_PB>(qs, qs, g.storage, g.ld, g.d,
                                                         lane < nf ? (uint32_t)fv : 0u, nf, lane);
@@ -1115,7 +1139,7 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
             // full); a heap not yet full takes every arrival.
             const bool full0 = C.hk == ef;
             const float ctop0 = full0 ? C.top_dis() : FLT_MAX;
-            if (g.nb0) {
+            if (NB0) {
                 // next pop: the closest arrival if it enters and beats the
                 // closest alive candidate, else that candidate
                 const uint32_t fb = lane < nf ? (uint32_t)__float_as_int(fdis) : 0xffffffffu;
@@ -1129,44 +1153,28 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                 pf_v = pred;
                 if (pred >= 0 && lane < cnt) pf_nb = g.nb0[(int64_t)pred * g.nb0_stride + lane];
             }
-            todo = __ballot(lane < nf && (!full0 || fdis < rmax || fdis < ctop0));
-            hop_todo = todo;
+            unsigned long long todo = __ballot(lane < nf && (!full0 || fdis < rmax || fdis < ctop0));
+            const unsigned long long hop_todo = todo;
+            int hp = 0;  // this hop's log position
             if constexpr (CQ::kMerge) {
                 // the replay log: this hop's pop, then its arrivals in order
                 if (rlog) {
                     hp = S.logpos;
                     const int m = __popcll(todo);
-                    if (hp + 1 + m <= logcap) {
-                        if (lane == 0) rlog[hp] = RLOG_POP;
+                    if (hp + 1 + m <= RLOG_CAP) {
+                        // streaming stores: the log is read back only
+                        // after a tie (~1.5 % of c4's queries)
+                        if (lane == 0) __builtin_nontemporal_store(RLOG_POP, rlog + hp);
                         if ((todo >> lane) & 1ull)
-                            rlog[hp + 1 + __popcll(todo & lt)] = hkey(fdis, fv);
+                            __builtin_nontemporal_store(hkey(fdis, fv),
+                                                        rlog + hp + 1 + __popcll(todo & lt));
                     }
                     S.logpos = hp + 1 + m;
                 }
                 if (todo && hop_merge(C, R, k, ef, todo, fdis, fv, lane, nvalid, rmax))
                     todo = 0ull;
             }
-        }
-        resume = false;
-        while (todo) {
-            const int t = __builtin_ctzll(todo);
-            const int32_t vt = __builtin_amdgcn_readlane(fv, t);
-            const float dis = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), t));
-            const uint64_t nk = hkey(dis, vt);
-            if (!C.push(ef, nk, dis, nvalid, lane)) {
-                S.nvalid = nvalid;
-                S.rmax = rmax;
-                S.todo = todo;
-                S.fdis = fdis;
-                S.fv = fv;
-                S.stop = hp + 1 + __popcll(hop_todo & ((1ull << t) - 1ull));
-                return false;
-            }
-            todo &= todo - 1ull;
-            if (dis < rmax) {
-                R.insert(k, nk, lane);
-                rmax = hkey_dis(rdlane64(R.key, k - 1));
-            }
+            if (todo && !apply(todo, hop_todo, fdis, fv, hp)) return false;
         }
         if (TRACE) tr.tick(4);
     }
@@ -1177,12 +1185,12 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
 // heap array the reference holds at that point (the pops before the stop
 // took a unique minimum, the evictions a unique top)
 __device__ __forceinline__ void level0_replay(CandLayout& C, const uint64_t* __restrict__ rlog,
-                                              int64_t stop, int ef, int lane, int nearest,
-                                              float d_nearest) {
+                                              int stop, int ef, int ntotal, int lane,
+                                              int nearest, float d_nearest) {
     C.init();
     C.seed(hkey(d_nearest, nearest), lane);
     int dummy = 0;
-    for (int64_t base = 0; base < stop; base += 64) {
+    for (int base = 0; base < stop; base += 64) {
         const uint64_t e = base + lane < stop ? rlog[base + lane] : RLOG_POP;
         const int cnt = stop - base < 64 ? (int)(stop - base) : 64;
         for (int i = 0; i < cnt; i++) {
@@ -1191,7 +1199,7 @@ __device__ __forceinline__ void level0_replay(CandLayout& C, const uint64_t* __r
                 int32_t v0;
                 int nb;
                 C.pop_min(lane, v0, nb);
-            } else {
+            } else if ((uint32_t)hkey_id(v) < (uint32_t)ntotal) {  // (a key names a node)
                 C.push(ef, v, hkey_dis(v), dummy, lane);
             }
         }
@@ -1203,7 +1211,7 @@ __device__ __forceinline__ void level0_replay(CandLayout& C, const uint64_t* __r
 // meets a layout-dependent tie is searched again with CandLayout (layout = 1:
 // every query with CandLayout — tests).  Results are the reference's, bit for
 // bit, either way.
-template <bool LDS_VISITED, bool TRACE = false>
+template <bool LDS_VISITED, bool TRACE, bool NB0>
 __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, const float* __restrict__ x,
                                                        int ldx, int64_t n, int k, int efSearch,
                                                        int ef, float* __restrict__ D,
@@ -1215,7 +1223,7 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
                                                        const uint32_t* __restrict__ only,
                                                        const uint32_t* __restrict__ qidx, int layout,
                                                        unsigned long long* __restrict__ trace,
-                                                       uint64_t* __restrict__ rlog, int64_t logcap) {
+                                                       uint64_t* __restrict__ rlog) {
     // qidx: compact launch over listed queries (input row qidx[b], output
     // row b); else query b, output row b
     const int64_t q = qidx ? (int64_t)qidx[blockIdx.x] : (int64_t)blockIdx.x;
@@ -1277,21 +1285,21 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
         }
         // ---- level 0
         const uint32_t up_ndis = st_ndis, up_nhops = st_nhops;
-        uint64_t* qlog = rlog ? rlog + (int64_t)blockIdx.x * logcap : nullptr;
+        uint64_t* qlog = rlog ? rlog + (int64_t)blockIdx.x * RLOG_CAP : nullptr;
         L0Run S;
         bool done = false;
         if (!layout) {
             CandSet C;
             level0_seed(C, R, S, vis, k, lane, nearest, d_nearest);
-            done = hnsw_level0<CandSet, TRACE>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
-                                               st_ndis, st_nhops, tr, qlog, logcap);
+            done = hnsw_level0<CandSet, TRACE, NB0>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
+                                               st_ndis, st_nhops, tr, qlog);
         }
         if (!done) {
             CandLayout C;
             if (TRACE) tr.t[8] = 1;
-            if (!layout && qlog && S.logpos <= logcap) {
+            if (!layout && qlog && S.logpos <= RLOG_CAP) {
                 // continue from the stopping point with the replayed heap
-                level0_replay(C, qlog, S.stop, ef, lane, nearest, d_nearest);
+                level0_replay(C, qlog, S.stop, ef, g.ntotal, lane, nearest, d_nearest);
                 if (TRACE) tr.t[9] = (unsigned long long)S.stop;
             } else {
                 // again from the start: fresh visited table, results, counters
@@ -1304,8 +1312,8 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
                 __syncthreads();
                 level0_seed(C, R, S, vis, k, lane, nearest, d_nearest);
             }
-            hnsw_level0<CandLayout, TRACE>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
-                                           st_ndis, st_nhops, tr, nullptr, 0);
+            hnsw_level0<CandLayout, TRACE, NB0>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
+                                                st_ndis, st_nhops, tr, nullptr);
         }
     }
     if (TRACE && lane == 0) {
@@ -1336,7 +1344,7 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
                               uint32_t* visited_scratch, int64_t vwords,
                               unsigned long long* stats, const uint32_t* only,
                               const uint32_t* qidx, hipStream_t s, float* gheap = nullptr,
-                              uint64_t* rlog = nullptr, int64_t logcap = 0) {
+                              uint64_t* rlog = nullptr) {
     const int ef = efSearch > k ? efSearch : k;
     const size_t lds_q = sizeof(float) * g.ld;
     const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
@@ -1369,9 +1377,10 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
             unsigned long long* tb = nullptr;
             HIP_CHECK(hipMalloc(&tb, 128 * std::max<int64_t>(n, 1)));
             HIP_CHECK(hipMemsetAsync(tb, 0, 128 * std::max<int64_t>(n, 1), s));
-            k_hnsw_exact_reg<true, true><<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4, s>>>(
+            auto kt = g.nb0 ? k_hnsw_exact_reg<true, true, true> : k_hnsw_exact_reg<true, true, false>;
+            kt<<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
-                    layout, tb, rlog, logcap);
+                    layout, tb, rlog);
             HIP_LAUNCH_CHECK();
             std::vector<unsigned long long> h((size_t)n * 16);
             HIP_CHECK(hipMemcpyAsync(h.data(), tb, 128 * n, hipMemcpyDeviceToHost, s));
@@ -1383,14 +1392,13 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
             }
             return;
         }
-        if (rvis)
-            k_hnsw_exact_reg<true><<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4, s>>>(
-                    g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
-                    layout, nullptr, rlog, logcap);
-        else
-            k_hnsw_exact_reg<false><<<dim3((unsigned)n), dim3(64), lds_r, s>>>(
-                    g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
-                    only, qidx, layout, nullptr, rlog, logcap);
+        auto kr = rvis ? (g.nb0 ? k_hnsw_exact_reg<true, false, true>
+                                : k_hnsw_exact_reg<true, false, false>)
+                       : (g.nb0 ? k_hnsw_exact_reg<false, false, true>
+                                : k_hnsw_exact_reg<false, false, false>);
+        kr<<<dim3((unsigned)n), dim3(64), rvis ? lds_r + vwords * 4 : lds_r, s>>>(
+                g, x, ldx, n, k, efSearch, ef, D, I, I32, rvis ? nullptr : visited_scratch, vwords,
+                stats, only, qidx, layout, nullptr, rlog);
         HIP_LAUNCH_CHECK();
         return;
     }
@@ -1476,7 +1484,7 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
     auto exact = [&](const uint32_t* only) {
         ScopedKernelTimer tm(kt, "hnsw_exact", 0.0, s);
         hnsw_exact_launch(g, x, ldx, n, k, efSearch, D, I, I32, visited_scratch, vwords, stats,
-                          only, nullptr, s, heap_scratch, replay_log, replay_cap);
+                          only, nullptr, s, heap_scratch, replay_cap == kHnswReplayCap ? replay_log : nullptr);
     };
     // FAISS_AMD_HNSW_EXACT=1: every query through the sequential kernel (tests)
     const char* xenv = getenv("FAISS_AMD_HNSW_EXACT");
