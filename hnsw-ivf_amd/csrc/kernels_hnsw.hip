@@ -964,11 +964,11 @@ __host__ __device__ inline int exact_reg_qpad(const HNSWDevice& g) {
 
 // passes of 16 rows whose loads the register kernel issues together
 #ifndef HNSW_PB
-#define HNSW_PB 2
+#define HNSW_PB 1
 #endif
 // the register kernel's waves per SIMD (its VGPR budget: 512 / HNSW_WPE)
 #ifndef HNSW_WPE
-#define HNSW_WPE 4
+#define HNSW_WPE 5
 #endif
 // Trace of the register kernel (FAISS_AMD_HNSW_TRACE=<file>, profiling): per
 // query the core-clock cycles of each level-0 hop phase summed over its hops:
@@ -1116,7 +1116,7 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
             const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
             const int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
             if (TRACE) tr.tick(2);
-            // 4 lanes per row, 16 rows per pass, two passes' loads in flight
+            // 4 lanes per row, 16 rows per pass, HNSW_PB passes' loads in flight
             // (reference order)
             float fdis = 0.f;
             if (g.d <= 128)
@@ -1155,6 +1155,10 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
             }
             unsigned long long todo = __ballot(lane < nf && (!full0 || fdis < rmax || fdis < ctop0));
             const unsigned long long hop_todo = todo;
+            if (TRACE) {
+                tr.t[10] += (unsigned long long)__popcll(todo);
+                tr.t[11] += full0 ? 0ull : 1ull;
+            }
             int hp = 0;  // this hop's log position
             if constexpr (CQ::kMerge) {
                 // the replay log: this hop's pop, then its arrivals in order

@@ -88,5 +88,7 @@ for ef in efs:
                   f"hops, {tr[:, 6].sum() / hops:.1f} fresh/hop, cycles/hop: {per}, "
                   f"query total {tr[:, 7].mean():.0f} cycles (max {tr[:, 7].max():.0f}), "
                   f"{int(tr[:, 8].sum())} continued with the heap layout "
-                  f"(replayed log entries: {int(tr[:, 9].sum())})",
+                  f"(replayed log entries: {int(tr[:, 9].sum())}); arrivals that can enter a "
+                  f"heap {tr[:, 10].sum() / hops:.1f}/hop, hops before the candidates fill "
+                  f"{tr[:, 11].mean():.1f}",
                   flush=True)

@@ -10,7 +10,8 @@ tests/test_ref_fixtures.py).
       12.5M of an 8-GPU shard, nq = 2000)
 and at their real sizes (the bench's batches searched whole on the GPU, a
 subset of the queries re-derived by the oracle):
-  c4  10M vectors, the 10k-query batch, efSearch 64 (400 queries checked)
+  c4  10M vectors, the 10k-query batch, efSearch 64 through search() and
+      16 / 64 / 128 through search_device() (400 queries checked)
   c5  one 12.5M-vector shard of the 100M set (ids == 0 mod 8, as bench.py
       --shard-of 8), the 100k-query batch (400 queries checked): ~190 rows
       per list, the PQ filter's long-list work items at full length
@@ -166,8 +167,9 @@ def check_subset(D, I, Dr, Ir, rows, what):
     check(D[rows], I[rows], Dr, Ir, what)
 
 
-def test_c4_full_10m(amd, orc, gpu):
-    d, nb, nq = 128, 10_000_000, 10_000
+@pytest.fixture(scope="module")
+def c4_10m(amd):
+    d, nb = 128, 10_000_000
     idx = amd.index_factory(d, "IVF16384_HNSW32,Flat")
     xt = amd.float_rand_rows(nb, d, 1234, 0, 1, 638_976)
     idx.train(xt)
@@ -175,6 +177,12 @@ def test_c4_full_10m(amd, orc, gpu):
     for c0 in range(0, nb, 2_000_000):
         idx.add(amd.float_rand_rows(nb, d, 1234, c0, 1, 2_000_000))
     idx.nprobe = 64
+    return idx
+
+
+def test_c4_full_10m(amd, orc, gpu, c4_10m):
+    d, nq = 128, 10_000
+    idx = c4_10m
     amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", 64)
     xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
     D, I = idx.search(xq, 10)
@@ -182,6 +190,28 @@ def test_c4_full_10m(amd, orc, gpu):
     ref = orc.IVFOracle.from_index(idx)
     Dr, Ir, _, _ = ref.search(np.ascontiguousarray(xq[rows]), 10, 64, efSearch=64, nslices=1)
     check_subset(D, I, Dr, Ir, rows, "c4 10M efSearch 64")
+
+
+def test_c4_full_10m_device(amd, orc, gpu, c4_10m):
+    """The bench's step: the 10k-query batch through Index::search_device on
+    the 10M index (register HNSW kernel at efSearch 16 / 64, the batched
+    kernel with the overlapped tie re-runs at 128), a 400-query oracle
+    subset bit-exact."""
+    from conftest import device_search
+    d, nq = 128, 10_000
+    idx = c4_10m
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    rows = np.arange(0, nq, nq // 400)
+    ref = orc.IVFOracle.from_index(idx)
+    try:
+        for ef in (16, 64, 128):
+            amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", ef)
+            D, I = device_search(idx, xq, 10)
+            Dr, Ir, _, _ = ref.search(np.ascontiguousarray(xq[rows]), 10, 64, efSearch=ef,
+                                      nslices=1)
+            check_subset(D, I, Dr, Ir, rows, f"c4 10M device efSearch {ef}")
+    finally:
+        amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", 64)
 
 
 def test_c5_full_shard(amd, orc, gpu):
