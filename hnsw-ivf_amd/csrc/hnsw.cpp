@@ -379,6 +379,61 @@ void IndexHNSW::sync_device() const {
                                  hipMemcpyHostToDevice, s));
         nb0_stride_ = (int)c0;
     }
+    // int8 row image for the register kernel's level-0 prefilter: per row
+    // y, o = min y, s = (max y - min y) / 255, q = round((y - o) / s), and
+    // with yq = s q + o (exact real): ey >= |y - yq|, B2 = |yq|^2, Q1 = sum q.
+    // A fresh neighbour whose certified lower bound on its distance
+    // (kernels_hnsw.hip q8_filter) reaches both heaps' bounds cannot enter
+    // either, so only the others' fp32 rows are read.  FAISS_AMD_HNSW_Q8=0: off.
+    std::vector<uint8_t> q8;
+    std::vector<float> q8p, q8q1;
+    const char* q8env = getenv("FAISS_AMD_HNSW_Q8");
+    q8_ = metric_type == METRIC_L2 && d <= 128 && nb0_stride_ > 0 && ntotal > 0 &&
+          !(q8env && !strcmp(q8env, "0"));
+    if (q8_) {
+        const size_t nn = (size_t)ntotal;
+        q8.assign(nn * 128, 0);
+        q8p.assign(nn * 4, 0.f);
+        q8q1.assign(nn, 0.f);
+        const float* xb = storage->xb.data();
+        for (size_t v = 0; v < nn; v++) {
+            const float* y = xb + v * d;
+            float mn = y[0], mx = y[0];
+            for (int i = 1; i < d; i++) {
+                mn = std::min(mn, y[i]);
+                mx = std::max(mx, y[i]);
+            }
+            float sc = (float)(((double)mx - (double)mn) / 255.0);
+            if (!(sc > 0.f) || !std::isfinite(sc)) sc = 1.f;
+            double e2 = 0, b2 = 0, q1 = 0;
+            for (int i = 0; i < d; i++) {
+                const double t = std::nearbyint(((double)y[i] - (double)mn) / (double)sc);
+                const int q = (int)std::min(255.0, std::max(0.0, t));
+                const double yq = (double)sc * q + (double)mn;
+                e2 += ((double)y[i] - yq) * ((double)y[i] - yq);
+                b2 += yq * yq;
+                q1 += q;
+                q8[v * 128 + i] = (uint8_t)q;
+            }
+            // ey rounded up (fp32 above the double value)
+            const double ey = std::sqrt(e2) * (1.0 + 1e-9) + 1e-12 * std::sqrt(b2) + 1e-30;
+            float eyf = (float)ey;
+            if ((double)eyf < ey) eyf = std::nextafter(eyf, INFINITY);
+            q8p[v * 4 + 0] = mn;
+            q8p[v * 4 + 1] = sc;
+            q8p[v * 4 + 2] = eyf;
+            q8p[v * 4 + 3] = (float)b2;
+            q8q1[v] = (float)q1;
+        }
+        d_q8_.reserve(q8.size());
+        d_q8p_.reserve(sizeof(float) * q8p.size());
+        d_q8q1_.reserve(sizeof(float) * q8q1.size());
+        HIP_CHECK(hipMemcpyAsync(d_q8_.ptr, q8.data(), q8.size(), hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(d_q8p_.ptr, q8p.data(), sizeof(float) * q8p.size(),
+                                 hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(d_q8q1_.ptr, q8q1.data(), sizeof(float) * q8q1.size(),
+                                 hipMemcpyHostToDevice, s));
+    }
     HIP_CHECK(hipStreamSynchronize(s));
     dirty_ = false;
 }
@@ -409,6 +464,9 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
     gd.cum_nb = d_cum_.as<int32_t>();
     gd.nb0 = nb0_stride_ > 0 ? d_nb0_.as<int32_t>() : nullptr;
     gd.nb0_stride = nb0_stride_;
+    gd.q8 = q8_ ? d_q8_.as<uint8_t>() : nullptr;
+    gd.q8p = q8_ ? d_q8p_.as<float>() : nullptr;
+    gd.q8q1 = q8_ ? d_q8q1_.as<float>() : nullptr;
     gd.nlevels_cum = (int)hnsw.cum_nneighbor_per_level.size();
     gd.entry_point = ntotal > 0 ? hnsw.entry_point : -1;
     gd.max_level = hnsw.max_level;
@@ -526,6 +584,9 @@ IndexHNSW::Split IndexHNSW::split_finish() const {
     gd.cum_nb = d_cum_.as<int32_t>();
     gd.nb0 = nb0_stride_ > 0 ? d_nb0_.as<int32_t>() : nullptr;
     gd.nb0_stride = nb0_stride_;
+    gd.q8 = q8_ ? d_q8_.as<uint8_t>() : nullptr;
+    gd.q8p = q8_ ? d_q8p_.as<float>() : nullptr;
+    gd.q8q1 = q8_ ? d_q8q1_.as<float>() : nullptr;
     gd.nlevels_cum = (int)hnsw.cum_nneighbor_per_level.size();
     gd.entry_point = ntotal > 0 ? hnsw.entry_point : -1;
     gd.max_level = hnsw.max_level;

@@ -346,6 +346,12 @@ struct HNSWDevice {
     // load); null: read them through offsets
     const int32_t* nb0;
     int nb0_stride;
+    // int8 image of the rows for the level-0 prefilter (L2, d <= 128; null:
+    // none): q8 [ntotal][128] codes, q8p [ntotal] {o, s, ey, B2}, q8q1
+    // [ntotal] sum of the codes (IndexHNSW::sync_device, kernels_hnsw.hip)
+    const uint8_t* q8;
+    const float* q8p;
+    const float* q8q1;
     int nlevels_cum;
     int entry_point;
     int max_level;

@@ -613,7 +613,6 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
             }
             __syncthreads();
             if (lane < nf) fd[lane] = l2_row(qs, g.storage + (int64_t)fi[lane] * g.ld, g.d);
-            st_ndis += (uint32_t)nf;
             st_nhops += 1;
             __syncthreads();
             if (lane == 0) {
@@ -961,6 +960,143 @@ __device__ __forceinline__ bool hop_merge(CandSet& C, SortedQ& R, int k, int ef,
 __host__ __device__ inline int exact_reg_qpad(const HNSWDevice& g) {
     return g.ld < 128 ? 128 : g.ld;
 }
+// LDS before the visited bitmap: the query copy, its int8 image (128 B) and
+// the image's scalars (6 doubles)
+__host__ __device__ inline int exact_reg_head(const HNSWDevice& g) {
+    return 4 * exact_reg_qpad(g) + 128 + 48;
+}
+
+namespace {
+// The int8 prefilter of a hop's fresh neighbours (the rows' image:
+// IndexHNSW::sync_device).  The query gets the same kind of image:
+// xq = round((x - ox) / sx) with ox = min x, sx = (max x - min x) / 255, and
+// with xh = sx xq + ox (exact real), ex >= |x - xh|.  For a row image
+// yq = s q + o (ey >= |y - yq|):
+//   |xh - yq|^2 = A2 + B2 - 2 (s (sx P + ox Q1) + o SA),
+// A2 = |xh|^2, SA = sum xh, B2 = |yq|^2, Q1 = sum q, P = sum xq q (exact
+// integers, v_dot4_u32_u8), and |x - y| >= |xh - yq| - ex - ey.  Evaluated in
+// double with margins for B2's fp32 rounding and the double rounding, and the
+// bound scaled by 1 - (2d + 16) 2^-24 so that it stays below the reference's
+// own fp32 evaluation of the distance (ref_arith.h order).
+__device__ __forceinline__ void q8_query_prep(const float* qs, int d, uint8_t* q8x, double* qd,
+                                              int lane) {
+    const float x0 = qs[lane], x1 = qs[lane + 64];
+    const bool v0 = lane < d, v1 = lane + 64 < d;
+    float mn = fminf(v0 ? x0 : INFINITY, v1 ? x1 : INFINITY);
+    float mx = fmaxf(v0 ? x0 : -INFINITY, v1 ? x1 : -INFINITY);
+#pragma unroll
+    for (int m = 32; m; m >>= 1) {
+        mn = fminf(mn, __shfl_xor(mn, m));
+        mx = fmaxf(mx, __shfl_xor(mx, m));
+    }
+    const double ox = (double)mn;
+    double sx = ((double)mx - (double)mn) / 255.0;
+    if (!(sx > 0.0)) sx = 1.0;
+    double e2 = 0.0, a2 = 0.0, sa = 0.0;
+    uint32_t q[2] = {0u, 0u};
+    const float xv[2] = {x0, x1};
+    const bool vv[2] = {v0, v1};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        if (!vv[h]) continue;
+        const double t = rint(((double)xv[h] - ox) / sx);
+        q[h] = (uint32_t)fmin(255.0, fmax(0.0, t));
+        const double xh = sx * (double)q[h] + ox;
+        const double e = (double)xv[h] - xh;
+        e2 += e * e;
+        a2 += xh * xh;
+        sa += xh;
+    }
+    q8x[lane] = (uint8_t)q[0];
+    q8x[lane + 64] = (uint8_t)q[1];
+#pragma unroll
+    for (int m = 32; m; m >>= 1) {
+        e2 += __shfl_xor(e2, m);
+        a2 += __shfl_xor(a2, m);
+        sa += __shfl_xor(sa, m);
+    }
+    if (lane == 0) {
+        qd[0] = sx;
+        qd[1] = ox;
+        qd[2] = a2;
+        qd[3] = sa;
+        qd[4] = sqrt(e2) * (1.0 + 1e-12) + 1e-12 * sqrt(a2) + 1e-300;
+        qd[5] = 1.0 - (2.0 * d + 16.0) * 0x1p-24;
+    }
+}
+
+// Lanes < nf hold the hop's fresh ids (arrival order).  Rows whose lower
+// bound reaches thr (neither heap can take them) are dropped; the others
+// are compacted to the low lanes in arrival order (sv); returns their count.
+#ifndef HNSW_Q8PB
+#define HNSW_Q8PB 2
+#endif
+__device__ __forceinline__ int q8_filter(const HNSWDevice& g, const uint8_t* q8x, const double* qd,
+                                         int32_t fv, int nf, float thr, int lane, int32_t& sv) {
+    const int gq = lane >> 2, jp = lane & 3;
+    const int npass = (nf + 15) >> 4;
+    const uint4 x0 = *(const uint4*)(q8x + 32 * jp), x1 = *(const uint4*)(q8x + 32 * jp + 16);
+    const double sx = qd[0], ox = qd[1], a2 = qd[2], sa = qd[3], ex = qd[4], mref = qd[5];
+    const double thr_d = (double)thr;
+    bool keep = false;
+    // HNSW_Q8PB passes of 16 rows with their loads in flight together
+#pragma unroll 1
+    for (int p0 = 0; p0 < npass; p0 += HNSW_Q8PB) {
+        uint4 c0[HNSW_Q8PB], c1[HNSW_Q8PB];
+        float pp[HNSW_Q8PB], q1[HNSW_Q8PB];
+#pragma unroll
+        for (int b = 0; b < HNSW_Q8PB; b++) {
+            const int r = 16 * (p0 + b) + gq;
+            const int32_t rg = __shfl(fv, r & 63);
+            const uint32_t row = r < nf ? (uint32_t)rg : 0u;
+            const uint4* cp = (const uint4*)(g.q8 + (size_t)row * 128 + 32 * jp);
+            c0[b] = cp[0];
+            c1[b] = cp[1];
+            pp[b] = g.q8p[(size_t)row * 4 + jp];
+            q1[b] = g.q8q1[row];
+        }
+#pragma unroll
+        for (int b = 0; b < HNSW_Q8PB; b++) {
+            const int p = p0 + b;
+            if (p >= npass) break;  // wave-uniform
+            uint32_t P = __builtin_amdgcn_udot4(x0.x, c0[b].x, 0u, false);
+            P = __builtin_amdgcn_udot4(x0.y, c0[b].y, P, false);
+            P = __builtin_amdgcn_udot4(x0.z, c0[b].z, P, false);
+            P = __builtin_amdgcn_udot4(x0.w, c0[b].w, P, false);
+            P = __builtin_amdgcn_udot4(x1.x, c1[b].x, P, false);
+            P = __builtin_amdgcn_udot4(x1.y, c1[b].y, P, false);
+            P = __builtin_amdgcn_udot4(x1.z, c1[b].z, P, false);
+            P = __builtin_amdgcn_udot4(x1.w, c1[b].w, P, false);
+            P += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P, 0xB1, 0xf, 0xf, false);  // quad ^1
+            P += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P, 0x4E, 0xf, 0xf, false);  // quad ^2
+            const int pb = __float_as_int(pp[b]);
+            const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, pb, 0x00, 0xf, 0xf, false));
+            const float sc = __int_as_float(__builtin_amdgcn_update_dpp(0, pb, 0x55, 0xf, 0xf, false));
+            const float ey = __int_as_float(__builtin_amdgcn_update_dpp(0, pb, 0xAA, 0xf, 0xf, false));
+            const float b2 = __int_as_float(__builtin_amdgcn_update_dpp(0, pb, 0xFF, 0xf, 0xf, false));
+            const double sab = (double)sc * (sx * (double)P + ox * (double)q1[b]) + (double)o * sa;
+            const double d2 = a2 + (double)b2 - 2.0 * sab;
+            const double mag = a2 + (double)b2 + 2.0 * fabs(sab);
+            const double d2lo = d2 - 1e-7 * mag;
+            bool rej = false;
+            if (d2lo > 0.0) {
+                const double t = sqrt(d2lo) * (1.0 - 1e-12) - ex - (double)ey;
+                rej = t > 0.0 && t * t * mref >= thr_d;
+            }
+            // row 16 p + gq -> lane 16 p + gq
+            const int got = __shfl((int)!rej, 4 * (lane & 15));
+            if ((lane >> 4) == p) keep = got != 0;
+        }
+    }
+    keep = keep && lane < nf;
+    const unsigned long long sm = __ballot(keep);
+    const int ns = __popcll(sm);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int dst = keep ? __popcll(sm & lt) : ns + __popcll(~sm & lt);
+    sv = __builtin_amdgcn_ds_permute(dst << 2, fv);
+    return ns;
+}
+}  // namespace
 
 // passes of 16 rows whose loads the register kernel issues together
 #ifndef HNSW_PB
@@ -974,7 +1110,10 @@ __host__ __device__ inline int exact_reg_qpad(const HNSWDevice& g) {
 // query the core-clock cycles of each level-0 hop phase summed over its hops:
 // [0] pop_min + count_below, [1] neighbour ids, [2] visited test-and-set,
 // [3] distances, [4] heap updates, [5] hops, [6] fresh neighbours, [7] whole
-// query, [8] 1 if the query was searched again with the heap layout
+// query, [8] 1 if the query was searched again with the heap layout, [9]
+// replayed log entries, [10] arrivals that can enter a heap, [11] hops before
+// the candidates fill, [12] fp32 rows after the int8 bound, [13] the
+// next-pop prediction, [14] the replay log (of [4])
 struct HopTrace {
     unsigned long long t[16];
     unsigned long long tc;
@@ -1029,7 +1168,8 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                                             int k, int efSearch, int ef, int lane, CQ& C,
                                             L0Run& S, SortedQ& R, uint32_t& st_n2,
                                             uint32_t& st_ndis, uint32_t& st_nhops, HopTrace& tr,
-                                            uint64_t* __restrict__ rlog) {
+                                            uint64_t* __restrict__ rlog, const uint8_t* q8x,
+                                            const double* q8d) {
     int nvalid = S.nvalid;
     float rmax = S.rmax;
     // the sequential add_to_heap calls (:678-689) for the arrivals `todo`
@@ -1111,11 +1251,25 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                 for (int i = 0; i < jmax; i++)
                     fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
             const unsigned long long fm = __ballot(fresh);
-            const int nf = __popcll(fm);
+            int nf = __popcll(fm);
             const unsigned long long lt = (1ull << lane) - 1ull;
             const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
-            const int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
+            int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
             if (TRACE) tr.tick(2);
+            st_ndis += (uint32_t)nf;  // (every fresh neighbour is a distance computation)
+            // the bounds every arrival of this hop must beat to enter a heap:
+            // the result's rmax and, once full, the candidates' top (both only
+            // fall during the hop)
+            const bool full0 = C.hk == ef;
+            const float ctop0 = full0 ? C.top_dis() : FLT_MAX;
+            if (NB0 && g.q8 && full0 && nf > 0) {
+                // int8 lower bounds first: only the rows that may enter a
+                // heap have their fp32 row read (c4: ~5 of ~42 per hop)
+                int32_t sv;
+                nf = q8_filter(g, q8x, q8d, fv, nf, fmaxf(rmax, ctop0), lane, sv);
+                fv = sv;
+                if (TRACE) tr.t[12] += (unsigned long long)nf;
+            }
             // 4 lanes per row, 16 rows per pass, HNSW_PB passes' loads in flight
             // (reference order)
             float fdis = 0.f;
@@ -1124,7 +1278,6 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                                                         lane < nf ? (uint32_t)fv : 0u, nf, lane);
             else if (lane < nf)
                 fdis = l2_row(qs, g.storage + (int64_t)fv * g.ld, g.d);
-            st_ndis += (uint32_t)nf;
             st_nhops += 1;
             if (TRACE) {
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1137,8 +1290,6 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
             // result admits dis < rmax (rmax only falls during the hop); a full
             // candidate heap admits dis < its top (which only falls while
             // full); a heap not yet full takes every arrival.
-            const bool full0 = C.hk == ef;
-            const float ctop0 = full0 ? C.top_dis() : FLT_MAX;
             if (NB0) {
                 // next pop: the closest arrival if it enters and beats the
                 // closest alive candidate, else that candidate
@@ -1153,6 +1304,7 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                 pf_v = pred;
                 if (pred >= 0 && lane < cnt) pf_nb = g.nb0[(int64_t)pred * g.nb0_stride + lane];
             }
+            if (TRACE) tr.tick(13);
             unsigned long long todo = __ballot(lane < nf && (!full0 || fdis < rmax || fdis < ctop0));
             const unsigned long long hop_todo = todo;
             if (TRACE) {
@@ -1175,6 +1327,7 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                     }
                     S.logpos = hp + 1 + m;
                 }
+                if (TRACE) tr.tick(14);
                 if (todo && hop_merge(C, R, k, ef, todo, fdis, fv, lane, nvalid, rmax))
                     todo = 0ull;
             }
@@ -1243,13 +1396,20 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int qpad = exact_reg_qpad(g);
     float* qs = sm;  // [qpad]
-    uint32_t* vis = LDS_VISITED ? (uint32_t*)(sm + qpad) : vis_global + blockIdx.x * vwords;
+    uint8_t* q8x = (uint8_t*)(sm + qpad);      // [128] the query's int8 image
+    double* q8d = (double*)(q8x + 128);        // [6] its scalars
+    uint32_t* vis = LDS_VISITED ? (uint32_t*)((char*)sm + exact_reg_head(g))
+                                : vis_global + blockIdx.x * vwords;
     const int lane = threadIdx.x;
     for (int j = lane; j < qpad; j += 64) qs[j] = j < g.d ? x[q * ldx + j] : 0.f;
     for (int64_t w = lane; w < vwords; w += 64) vis[w] = 0u;
     SortedQ R;  // results: heap_heapify<CMax> (Heap.h:316-339) = k x (FLT_MAX, -1)
     R.key = hkey(FLT_MAX, -1);
     __syncthreads();
+    if (NB0 && g.q8) {
+        q8_query_prep(qs, g.d, q8x, q8d, lane);
+        __syncthreads();
+    }
     uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0;
     if (g.entry_point >= 0) {
         // ---- greedy descent (HNSW.cpp:852-924), as in k_hnsw_search
@@ -1296,7 +1456,7 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
             CandSet C;
             level0_seed(C, R, S, vis, k, lane, nearest, d_nearest);
             done = hnsw_level0<CandSet, TRACE, NB0>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
-                                               st_ndis, st_nhops, tr, qlog);
+                                               st_ndis, st_nhops, tr, qlog, q8x, q8d);
         }
         if (!done) {
             CandLayout C;
@@ -1317,7 +1477,7 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
                 level0_seed(C, R, S, vis, k, lane, nearest, d_nearest);
             }
             hnsw_level0<CandLayout, TRACE, NB0>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
-                                                st_ndis, st_nhops, tr, nullptr);
+                                                st_ndis, st_nhops, tr, nullptr, q8x, q8d);
         }
     }
     if (TRACE && lane == 0) {
@@ -1370,7 +1530,7 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
         return;
     }
     if (ef <= 64 && k <= 64) {  // register heaps
-        const size_t lds_r = sizeof(float) * exact_reg_qpad(g);
+        const size_t lds_r = (size_t)exact_reg_head(g);
         const bool rvis = lds_r + vwords * 4 <= 64 * 1024;
         // FAISS_AMD_HNSW_LAYOUT=1: every query with the heap-layout form (tests)
         const char* lenv = getenv("FAISS_AMD_HNSW_LAYOUT");

@@ -90,5 +90,7 @@ for ef in efs:
                   f"{int(tr[:, 8].sum())} continued with the heap layout "
                   f"(replayed log entries: {int(tr[:, 9].sum())}); arrivals that can enter a "
                   f"heap {tr[:, 10].sum() / hops:.1f}/hop, hops before the candidates fill "
-                  f"{tr[:, 11].mean():.1f}",
+                  f"{tr[:, 11].mean():.1f}, fp32 rows after the int8 bound "
+                  f"{tr[:, 12].sum() / hops:.1f}/hop; of the heap phase: prediction "
+                  f"{tr[:, 13].sum() / hops:.0f}, log {tr[:, 14].sum() / hops:.0f} cycles/hop",
                   flush=True)
