@@ -803,7 +803,7 @@ struct CandLayout {
     static constexpr bool kMerge = false;
     KHeap h;
     int hk;
-    __device__ __forceinline__ void init() {
+    __device__ __forceinline__ void init(int) {
         h.key = hkey(FLT_MAX, -1);
         hk = 0;
     }
@@ -850,45 +850,62 @@ struct CandLayout {
 };
 struct CandSet {
     static constexpr bool kMerge = true;
-    uint64_t key;  // lane j < hk: the j-th entry by distance
+    uint64_t key;    // lane j < hk: the j-th entry by (distance, id)
+    uint64_t amask;  // the alive entries (popped ones stay, as in the heap)
     int hk;
-    __device__ __forceinline__ void init() {
+    int kres;        // k of the results: they are derived from this set (below)
+    __device__ __forceinline__ void init(int k) {
         key = hkey(FLT_MAX, -1);
+        amask = 0ull;
         hk = 0;
+        kres = k;
+    }
+    // the alive mask with a slot opened at pos (entries pos.. move up one lane)
+    __device__ __forceinline__ static uint64_t open_bit(uint64_t m, int pos) {
+        const uint64_t low = (1ull << pos) - 1ull;  // pos <= 63
+        return (m & low) | (1ull << pos) | ((m & ~low) << 1);
     }
     __device__ __forceinline__ void insert(int n, uint64_t nk, int lane) {
         // into lanes 0..n (n entries kept sorted; lane n is free)
         const int pos = __popcll(__ballot(lane < n && key < nk));
         const uint64_t up = dpp64<0x138>(key);  // wave_shr:1
         key = lane > pos ? up : (lane == pos ? nk : key);
+        amask = open_bit(amask, pos);
     }
     __device__ __forceinline__ void seed(uint64_t nk, int lane) { insert(hk++, nk, lane); }
     __device__ __forceinline__ float top_dis() const { return hkey_dis(rdlane64(key, hk - 1)); }
     __device__ __forceinline__ uint64_t peek_min(int lane) const {
-        const unsigned long long am = __ballot(lane < hk && (uint32_t)key != HKEY_DEAD_LO);
-        return am ? rdlane64(key, __builtin_ctzll(am)) : ~0ull;
+        return amask ? rdlane64(key, __builtin_ctzll(amask)) : ~0ull;
     }
     __device__ __forceinline__ bool pop_min(int lane, int32_t& v0, int& nb) {
         const uint32_t chi = (uint32_t)(key >> 32);
-        const bool alive = lane < hk && (uint32_t)key != HKEY_DEAD_LO;
-        const unsigned long long am = __ballot(alive);
-        const int first = __builtin_ctzll(am);  // the sorted order: the smallest alive
+        const int first = __builtin_ctzll(amask);  // the sorted order: the smallest alive
         const uint32_t kmin = __builtin_amdgcn_readlane(chi, first);
-        if (__popcll(__ballot(alive && chi == kmin)) > 1) return false;  // layout decides
+        if (__popcll(__ballot(chi == kmin) & amask) > 1) return false;  // layout decides
         v0 = hkey_id(rdlane64(key, first));
         nb = __popcll(__ballot(lane < hk && chi < kmin));
-        if (lane == first) key = (key & 0xffffffff00000000ull) | HKEY_DEAD_LO;
+        amask &= ~(1ull << first);
         return true;
     }
     __device__ __forceinline__ bool push(int ef, uint64_t nk, float dis, int& nvalid, int lane) {
         if (hk == ef) {
             const uint64_t top = rdlane64(key, hk - 1);
             if (dis >= hkey_dis(top)) return true;
+        }
+        // results smaller than the set (k < ef) keep, among equal distances,
+        // the earliest arrivals, not the smallest ids: an arrival equal to a
+        // kept entry ends this form
+        if (kres < ef &&
+            __ballot(lane < hk && (uint32_t)(key >> 32) == (uint32_t)__float_as_int(dis)))
+            return false;
+        if (hk == ef) {
             // the heap's top among several entries of the largest distance
             // depends on its layout
-            if (hk >= 2 && (uint32_t)(rdlane64(key, hk - 2) >> 32) == (uint32_t)(top >> 32))
+            if (hk >= 2 && (uint32_t)(rdlane64(key, hk - 2) >> 32) ==
+                                   (uint32_t)(rdlane64(key, hk - 1) >> 32))
                 return false;
-            if ((uint32_t)top != HKEY_DEAD_LO) --nvalid;
+            if ((amask >> (hk - 1)) & 1ull) --nvalid;
+            amask &= ~(1ull << (hk - 1));
             insert(hk - 1, nk, lane);  // the top leaves, nk enters
         } else {
             insert(hk++, nk, lane);
@@ -896,62 +913,58 @@ struct CandSet {
         ++nvalid;
         return true;
     }
+    // search_from_candidates' result heap (HeapBlockResultHandler, strict
+    // admission): every entry of this set below FLT_MAX that ranks < k — the
+    // set holds the ef >= k smallest arrivals, the results the k smallest
+    __device__ __forceinline__ void results(SortedQ& R, int k, int lane) const {
+        const bool v = lane < hk && lane < k && (uint32_t)(key >> 32) < 0x7f7fffffu;
+        R.key = v ? key : hkey(FLT_MAX, -1);
+    }
 };
 // One hop's add_to_heap calls for the arrivals `todo` (lanes, arrival order)
-// as one merge, for CandSet: when no two of the distances involved are equal
-// (the arrivals' among themselves and with the kept entries of C and R), the
-// sequential updates leave each structure holding the smallest of its old
-// entries and the arrivals (C: ef of them; R: k) — an arrival a heap rejects
-// has that many entries below it, and an eviction takes the largest — so each
-// arrival's place is its rank among C (R) plus its rank among the arrivals,
-// and the kept entries fill the other places in order.  False (nothing
-// changed) on any equality, or on a tie inside C when the merge evicts:
-// then the hop runs the sequential updates.
-__device__ __forceinline__ bool hop_merge(CandSet& C, SortedQ& R, int k, int ef,
-                                          unsigned long long todo, float fdis, int32_t fv,
-                                          int lane, int& nvalid, float& rmax) {
-    const uint32_t cd = (uint32_t)(C.key >> 32), rd = (uint32_t)(R.key >> 32);
+// as one merge into CandSet: when no two of the distances involved are equal
+// (the arrivals' among themselves and with the kept entries), the sequential
+// pushes leave the set holding the ef smallest of its old entries and the
+// arrivals — an arrival the set rejects has ef entries below it, and an
+// eviction takes the largest — so each arrival's place is its rank among the
+// set plus its rank among the arrivals, and the kept entries fill the other
+// places in order.  False (nothing changed) on any equality, or on a tie
+// inside the set when the merge evicts: then the hop runs the sequential
+// pushes.
+__device__ __forceinline__ bool hop_merge(CandSet& C, int ef, unsigned long long todo, float fdis,
+                                          int32_t fv, int lane, int& nvalid) {
+    const uint32_t cd = (uint32_t)(C.key >> 32);
     const uint32_t fd = (uint32_t)__float_as_int(fdis);
     const int hk = C.hk, m = __popcll(todo);
     const uint64_t cm = hk >= 64 ? ~0ull : ((1ull << hk) - 1ull);
-    const uint64_t rm = k >= 64 ? ~0ull : ((1ull << k) - 1ull);
     if (hk + m > ef) {
         const uint32_t cprev = __builtin_amdgcn_update_dpp(0u, cd, 0x138, 0xf, 0xf, false);
         if (__ballot(lane >= 1 && lane < hk && cprev == cd)) return false;
     }
     int arr = 0;  // lane r: the lane of the arrival of rank r
-    uint64_t da = 0, dr = 0, tie = 0;
+    uint64_t da = 0, tie = 0;
     for (unsigned long long t = todo; t; t &= t - 1ull) {
         const int j = __builtin_ctzll(t);
         const uint32_t a = __builtin_amdgcn_readlane(fd, j);
         const int ra = __popcll(__ballot(fd < a) & todo);
         const int pc = __popcll(__ballot(cd < a) & cm) + ra;
-        const int pr = __popcll(__ballot(rd < a) & rm) + ra;
-        tie |= (__ballot(cd == a) & cm) | (__ballot(rd == a) & rm) |
-               (__ballot(fd == a) & todo & ~(1ull << j));
+        tie |= (__ballot(cd == a) & cm) | (__ballot(fd == a) & todo & ~(1ull << j));
         if (pc < 64) da |= 1ull << pc;
-        if (pr < 64) dr |= 1ull << pr;
         arr = lane == ra ? j : arr;
     }
     if (tie) return false;
     const uint64_t lt = (1ull << lane) - 1ull;
-    const uint64_t ak = hkey(fdis, fv);
     const int nh = min(ef, hk + m);
-    {
-        const int na = __popcll(da & lt);
-        const int al = __builtin_amdgcn_ds_bpermute(na << 2, arr);
-        const uint64_t fa = bperm64(ak, al), fc = bperm64(C.key, (lane - na) & 63);
-        C.key = ((da >> lane) & 1ull) ? fa : fc;
-        C.hk = nh;
-    }
-    {
-        const int na = __popcll(dr & lt);
-        const int al = __builtin_amdgcn_ds_bpermute(na << 2, arr);
-        const uint64_t fa = bperm64(ak, al), fr = bperm64(R.key, (lane - na) & 63);
-        R.key = ((dr >> lane) & 1ull) ? fa : fr;
-    }
-    nvalid = __popcll(__ballot(lane < nh && (uint32_t)C.key != HKEY_DEAD_LO));
-    rmax = hkey_dis(rdlane64(R.key, k - 1));
+    const int na = __popcll(da & lt);
+    const bool isa = (da >> lane) & 1ull;
+    const int al = __builtin_amdgcn_ds_bpermute(na << 2, arr);
+    const uint64_t fa = bperm64(hkey(fdis, fv), al);
+    const int src = (lane - na) & 63;
+    const uint64_t fc = bperm64(C.key, src);
+    C.key = isa ? fa : fc;
+    C.amask = __ballot(lane < nh && (isa || ((C.amask >> src) & 1ull)));
+    C.hk = nh;
+    nvalid = __popcll(C.amask);
     return true;
 }
 }  // namespace
@@ -1147,7 +1160,7 @@ struct L0Run {
 template <class CQ>
 __device__ __forceinline__ void level0_seed(CQ& C, SortedQ& R, L0Run& S, uint32_t* vis, int k,
                                             int lane, int nearest, float d_nearest) {
-    C.init();
+    C.init(k);
     C.seed(hkey(d_nearest, nearest), lane);
     if (d_nearest < FLT_MAX) R.insert(k, hkey(d_nearest, nearest), lane);
     S.nvalid = 1;
@@ -1183,6 +1196,10 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
             const float dis = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), t));
             const uint64_t nk = hkey(dis, vt);
             if (!C.push(ef, nk, dis, nvalid, lane)) {
+                if constexpr (CQ::kMerge) {
+                    C.results(R, k, lane);
+                    rmax = hkey_dis(rdlane64(R.key, k - 1));
+                }
                 S.nvalid = nvalid;
                 S.rmax = rmax;
                 S.todo = todo;
@@ -1192,9 +1209,11 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                 return false;
             }
             todo &= todo - 1ull;
-            if (dis < rmax) {
-                R.insert(k, nk, lane);
-                rmax = hkey_dis(rdlane64(R.key, k - 1));
+            if constexpr (!CQ::kMerge) {  // (CandSet: the results are derived from it)
+                if (dis < rmax) {
+                    R.insert(k, nk, lane);
+                    rmax = hkey_dis(rdlane64(R.key, k - 1));
+                }
             }
         }
         return true;
@@ -1215,6 +1234,10 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
             int32_t v0;
             int nb;
             if (!C.pop_min(lane, v0, nb)) {
+                if constexpr (CQ::kMerge) {
+                    C.results(R, k, lane);
+                    rmax = hkey_dis(rdlane64(R.key, k - 1));
+                }
                 S.nvalid = nvalid;
                 S.rmax = rmax;
                 S.todo = 0ull;
@@ -1266,7 +1289,9 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                 // int8 lower bounds first: only the rows that may enter a
                 // heap have their fp32 row read (c4: ~5 of ~42 per hop)
                 int32_t sv;
-                nf = q8_filter(g, q8x, q8d, fv, nf, fmaxf(rmax, ctop0), lane, sv);
+                // (CandSet: the results' bound is one of its entries, <= ctop0)
+                nf = q8_filter(g, q8x, q8d, fv, nf, CQ::kMerge ? ctop0 : fmaxf(rmax, ctop0),
+                               lane, sv);
                 fv = sv;
                 if (TRACE) tr.t[12] += (unsigned long long)nf;
             }
@@ -1305,7 +1330,8 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                 if (pred >= 0 && lane < cnt) pf_nb = g.nb0[(int64_t)pred * g.nb0_stride + lane];
             }
             if (TRACE) tr.tick(13);
-            unsigned long long todo = __ballot(lane < nf && (!full0 || fdis < rmax || fdis < ctop0));
+            unsigned long long todo = __ballot(
+                    lane < nf && (!full0 || fdis < ctop0 || (!CQ::kMerge && fdis < rmax)));
             const unsigned long long hop_todo = todo;
             if (TRACE) {
                 tr.t[10] += (unsigned long long)__popcll(todo);
@@ -1328,13 +1354,13 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                     S.logpos = hp + 1 + m;
                 }
                 if (TRACE) tr.tick(14);
-                if (todo && hop_merge(C, R, k, ef, todo, fdis, fv, lane, nvalid, rmax))
-                    todo = 0ull;
+                if (todo && hop_merge(C, ef, todo, fdis, fv, lane, nvalid)) todo = 0ull;
             }
             if (todo && !apply(todo, hop_todo, fdis, fv, hp)) return false;
         }
         if (TRACE) tr.tick(4);
     }
+    if constexpr (CQ::kMerge) C.results(R, k, lane);
     return true;
 }
 
@@ -1344,7 +1370,7 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
 __device__ __forceinline__ void level0_replay(CandLayout& C, const uint64_t* __restrict__ rlog,
                                               int stop, int ef, int ntotal, int lane,
                                               int nearest, float d_nearest) {
-    C.init();
+    C.init(0);
     C.seed(hkey(d_nearest, nearest), lane);
     int dummy = 0;
     for (int base = 0; base < stop; base += 64) {
