@@ -240,14 +240,23 @@ def kernel_roofline(name, ms, work, config):
              "unit": "TFLOP/s", "mfma_dtype": "bf16", "algorithmic_flops_per_step": f,
              "flops_per_query_centroid": 6 * work["dpad16"]}
     elif name in ("hnsw_search", "hnsw_exact") and work.get("hnsw_ndis"):
-        # every distance reads one fp32 vector of the graph's storage; the
-        # storage (c4: 16384 centroids, 8 MB) lives in the on-chip caches
-        # (4 MiB L2 per XCD, the 256 MiB Infinity Cache), so the bytes are
-        # priced against the aggregate L2 bandwidth, not HBM
-        b = work["hnsw_ndis"] * 4.0 * work["d"]
+        # bytes the traversal must read: per hop the node's level-0 neighbour
+        # ids (64 x 4 B); per distance either one fp32 row of the graph's
+        # storage or, for the register kernel's prefiltered neighbours, the
+        # row's int8 image (128 B + 20 B of scale / bound terms) and the fp32
+        # row only when the bound lets it through (counted on the device:
+        # cvar.hnsw_row_stats).  The storage (c4: 16384 centroids, 8 MB fp32,
+        # 2.4 MB int8) lives in the on-chip caches (4 MiB L2 per XCD, the
+        # 256 MiB Infinity Cache), so the bytes are priced against the
+        # aggregate L2 bandwidth, not HBM
+        f32, q8 = work.get("hnsw_fp32_rows"), work.get("hnsw_q8_rows")
+        if f32 is None:
+            f32, q8 = work["hnsw_ndis"], 0.0
+        b = f32 * 4.0 * work["d"] + q8 * 148.0 + work.get("hnsw_nhops", 0.0) * 256.0
         r = {"bound": "l2", "achieved": b / t / 1e9, "peak": PEAK_L2_GBS, "unit": "GB/s",
              "algorithmic_bytes_per_step": b, "hnsw_ndis_per_step": work["hnsw_ndis"],
-             "hbm_frac_if_from_hbm": b / t / 1e9 / PEAK_HBM_GBS}
+             "hnsw_fp32_rows_per_step": f32, "hnsw_q8_rows_per_step": q8,
+             "hnsw_nhops_per_step": work.get("hnsw_nhops", 0.0)}
     if r is None:
         return None
     r["frac"] = r["achieved"] / r["peak"]
@@ -480,6 +489,9 @@ def main():
         torch.cuda.synchronize()
         index.fold_device_stats()
         work["hnsw_ndis"] = float(amd.cvar.hnsw_stats.ndis)
+        work["hnsw_nhops"] = float(amd.cvar.hnsw_stats.nhops)
+        f32, q8 = amd.cvar.hnsw_row_stats
+        work["hnsw_fp32_rows"], work["hnsw_q8_rows"] = float(f32), float(q8)
     kernels = []
     for nm, ms in sorted(brk.items(), key=lambda kv: -kv[1]):
         if ms < 0.1 * ms_per_step and nm != dom:

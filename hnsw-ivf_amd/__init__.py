@@ -87,6 +87,14 @@ class _CVar:
     def hnsw_stats(self):
         return lib().faiss_amd_get_hnsw_stats().contents
 
+    @property
+    def hnsw_row_stats(self):
+        """(fp32 rows, int8-image rows) the GPU HNSW kernels read (not in the
+        reference; reset with hnsw_stats)."""
+        a, b = C.c_uint64(), C.c_uint64()
+        lib().faiss_amd_get_hnsw_row_stats(C.byref(a), C.byref(b))
+        return a.value, b.value
+
 
 cvar = _CVar()
 
@@ -165,6 +173,7 @@ def _declare(L):
         "faiss_amd_IndexHNSW_search_stats": (C.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P]),
         "faiss_amd_get_hnsw_stats": (C.POINTER(HNSWStats), []),
         "faiss_amd_HNSWStats_reset": (None, []),
+        "faiss_amd_get_hnsw_row_stats": (None, [C.c_void_p, C.c_void_p]),
         "faiss_amd_fold_device_stats": (C.c_int, [_P]),
         "faiss_IndexIVFFlat_new_with": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t]),
         "faiss_IndexIVFFlat_new_with_metric": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t, C.c_int]),

@@ -447,7 +447,14 @@ int faiss_amd_IndexHNSW_search_stats(const FaissIndexHNSW* p, idx_t n, const flo
 FaissHNSWStats* faiss_amd_get_hnsw_stats(void) {
     return reinterpret_cast<FaissHNSWStats*>(&hnsw_stats);
 }
-void faiss_amd_HNSWStats_reset(void) { hnsw_stats.reset(); }
+void faiss_amd_HNSWStats_reset(void) {
+    hnsw_stats.reset();
+    hnsw_row_stats = HNSWRowStats();
+}
+void faiss_amd_get_hnsw_row_stats(uint64_t* fp32_rows, uint64_t* q8_rows) {
+    if (fp32_rows) *fp32_rows = hnsw_row_stats.fp32_rows;
+    if (q8_rows) *q8_rows = hnsw_row_stats.q8_rows;
+}
 int faiss_amd_fold_device_stats(const FaissIndex* index) {
     C_TRY auto ix = IX(index);
     ix->fold_device_stats();

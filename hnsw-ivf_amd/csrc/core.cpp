@@ -14,6 +14,7 @@ namespace faiss_amd {
 
 IndexIVFStats indexIVF_stats;
 HNSWStats hnsw_stats;
+HNSWRowStats hnsw_row_stats;
 
 // ---------------------------------------------------------------- devices
 namespace {

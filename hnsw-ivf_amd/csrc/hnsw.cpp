@@ -475,8 +475,8 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
     constexpr bool i32 = sizeof(OutIdx) == 4;
     split_.active = false;
     if (!d_stats_.ptr) {
-        d_stats_.reserve(4 * sizeof(unsigned long long));
-        HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, 4 * sizeof(unsigned long long), s));
+        d_stats_.reserve(6 * sizeof(unsigned long long));
+        HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, 6 * sizeof(unsigned long long), s));
     }
     // queries per launch: the per-query visited bitmaps that do not fit in
     // LDS, and heaps beyond it (max(efSearch, k) in the thousands), live in
@@ -613,7 +613,7 @@ void IndexHNSW::fold_device_stats() const {
     if (!d_stats_.ptr) return;
     DevGuard2 dg(device);
     hipStream_t s = stream();
-    unsigned long long st[4];
+    unsigned long long st[6];
     HIP_CHECK(hipMemcpyAsync(st, d_stats_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, sizeof(st), s));
     HIP_CHECK(hipStreamSynchronize(s));
@@ -623,6 +623,8 @@ void IndexHNSW::fold_device_stats() const {
     add.ndis = st[2];
     add.nhops = st[3];
     hnsw_stats.combine(add);
+    hnsw_row_stats.fp32_rows += st[4];
+    hnsw_row_stats.q8_rows += st[5];
 }
 
 void IndexHNSW::search_stats(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,

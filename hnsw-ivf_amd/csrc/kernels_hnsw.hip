@@ -363,6 +363,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
         atomicAdd(&stats[1], (unsigned long long)st_n2);
         atomicAdd(&stats[2], (unsigned long long)st_ndis);
         atomicAdd(&stats[3], (unsigned long long)st_nhops);
+        atomicAdd(&stats[4], (unsigned long long)st_ndis);
     }
     if (lane < k) {
         float dis;
@@ -646,6 +647,7 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
         atomicAdd(&stats[1], (unsigned long long)st_n2);
         atomicAdd(&stats[2], (unsigned long long)st_ndis);
         atomicAdd(&stats[3], (unsigned long long)st_nhops);
+        atomicAdd(&stats[4], (unsigned long long)st_ndis);
     }
     // heap_reorder<CMax> (Heap.h:421-450) by lane 0, then the lanes write out
     if (lane == 0) {
@@ -1182,7 +1184,8 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                                             L0Run& S, SortedQ& R, uint32_t& st_n2,
                                             uint32_t& st_ndis, uint32_t& st_nhops, HopTrace& tr,
                                             uint64_t* __restrict__ rlog, const uint8_t* q8x,
-                                            const double* q8d) {
+                                            const double* q8d, uint32_t& st_q8,
+                                            uint32_t& st_x32) {
     int nvalid = S.nvalid;
     float rmax = S.rmax;
     // the sequential add_to_heap calls (:678-689) for the arrivals `todo`
@@ -1289,9 +1292,11 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                 // int8 lower bounds first: only the rows that may enter a
                 // heap have their fp32 row read (c4: ~5 of ~42 per hop)
                 int32_t sv;
+                st_q8 += (uint32_t)nf;
                 // (CandSet: the results' bound is one of its entries, <= ctop0)
                 nf = q8_filter(g, q8x, q8d, fv, nf, CQ::kMerge ? ctop0 : fmaxf(rmax, ctop0),
                                lane, sv);
+                st_x32 += (uint32_t)nf;
                 fv = sv;
                 if (TRACE) tr.t[12] += (unsigned long long)nf;
             }
@@ -1437,6 +1442,7 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
         __syncthreads();
     }
     uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0;
+    uint32_t st_q8 = 0, st_x32 = 0;  // rows the int8 bound read / of them read in fp32
     if (g.entry_point >= 0) {
         // ---- greedy descent (HNSW.cpp:852-924), as in k_hnsw_search
         int nearest = g.entry_point;
@@ -1482,7 +1488,8 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
             CandSet C;
             level0_seed(C, R, S, vis, k, lane, nearest, d_nearest);
             done = hnsw_level0<CandSet, TRACE, NB0>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
-                                               st_ndis, st_nhops, tr, qlog, q8x, q8d);
+                                               st_ndis, st_nhops, tr, qlog, q8x, q8d, st_q8,
+                                               st_x32);
         }
         if (!done) {
             CandLayout C;
@@ -1499,11 +1506,13 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
                 st_n2 = 0;
                 st_ndis = up_ndis;
                 st_nhops = up_nhops;
+                st_q8 = st_x32 = 0;
                 __syncthreads();
                 level0_seed(C, R, S, vis, k, lane, nearest, d_nearest);
             }
             hnsw_level0<CandLayout, TRACE, NB0>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
-                                                st_ndis, st_nhops, tr, nullptr, q8x, q8d);
+                                                st_ndis, st_nhops, tr, nullptr, q8x, q8d, st_q8,
+                                                st_x32);
         }
     }
     if (TRACE && lane == 0) {
@@ -1515,6 +1524,8 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
         atomicAdd(&stats[1], (unsigned long long)st_n2);
         atomicAdd(&stats[2], (unsigned long long)st_ndis);
         atomicAdd(&stats[3], (unsigned long long)st_nhops);
+        atomicAdd(&stats[4], (unsigned long long)(st_ndis - st_q8 + st_x32));
+        atomicAdd(&stats[5], (unsigned long long)st_q8);
     }
     // heap_reorder<CMax> (Heap.h:421-450): the kept (dis, id) ascending, the
     // placeholders (id -1) after them as (FLT_MAX, -1)

@@ -140,6 +140,14 @@ struct HNSWStats {
     }
 };
 extern HNSWStats hnsw_stats;
+// Not in the reference: rows the GPU HNSW kernels read per distance, for the
+// bench's byte count — fp32 rows (every distance computed exactly) and rows
+// whose int8 image the register kernel's prefilter read (hnsw_stats.ndis
+// counts the distances as the reference does).  Reset with hnsw_stats.
+struct HNSWRowStats {
+    uint64_t fp32_rows = 0, q8_rows = 0;
+};
+extern HNSWRowStats hnsw_row_stats;
 
 // faiss/impl/AuxIndexStructures.h:30-60: results of query i are
 // labels/distances[lims[i], lims[i+1]), in the order the scan found them.

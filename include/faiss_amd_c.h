@@ -333,6 +333,10 @@ typedef struct FaissHNSWStats {
 } FaissHNSWStats;
 FaissHNSWStats* faiss_amd_get_hnsw_stats(void);
 void faiss_amd_HNSWStats_reset(void);
+/* Not in the reference (diagnostic, the bench's byte count): rows the GPU
+ * HNSW kernels read — fp32 rows, and int8-image rows of the register kernel's
+ * level-0 prefilter — since the last faiss_amd_HNSWStats_reset. */
+void faiss_amd_get_hnsw_row_stats(uint64_t* fp32_rows, uint64_t* q8_rows);
 int faiss_amd_fold_device_stats(const FaissIndex* index);
 /* graph export for tests: levels[ntotal], offsets[ntotal+1], neighbors[],
  * cum_nneighbor_per_level[]; pass NULL to query sizes only */
