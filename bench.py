@@ -96,12 +96,14 @@ def pmc_traffic(config, stage):
         return None, None
     with open(fn) as f:
         summ = json.load(f)
-    # several instantiations can match (e.g. the coarse filter of k-means
-    # assignment during the build): the search's is the one launched least
+    # several entries can match (the build's launches of the same kernel —
+    # k-means assignment, adds through an HNSW quantizer — are kept apart by
+    # grid size): the search's is the one that ran last (the timed steps end
+    # the profiled run)
     best = None
     for name, ent in summ.items():
         if re.search(pat, name) and "hbm_bytes" in ent:
-            if best is None or ent.get("launches", 0) < best.get("launches", 0):
+            if best is None or ent.get("last_dispatch", 0) > best.get("last_dispatch", 0):
                 best = ent
     if best is None:
         return None, None

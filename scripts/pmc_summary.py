@@ -14,11 +14,17 @@ import sys
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 json_out = sys.argv[2] if len(sys.argv) > 2 else None  # per-kernel HBM bytes / launch
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
+last = collections.defaultdict(int)
 for f in sorted(glob.glob(os.path.join(root, "pmc*", "**", "*counter_collection*.csv"),
                           recursive=True)):
     per = collections.defaultdict(float)
     for r in csv.DictReader(open(f)):
-        per[(r["Kernel_Name"], r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        # one entry per (kernel, grid): the launches of the build (k-means
+        # assignment, adds through an HNSW quantizer) stay apart from the
+        # search's; "last_dispatch" tells which ran last (the timed steps)
+        kn = f'{r["Kernel_Name"]} [grid {r.get("Grid_Size", "?")}]'
+        per[(kn, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        last[kn] = max(last[kn], int(r["Dispatch_Id"]))
     for (kn, _, cn), v in per.items():
         acc[kn][cn].append(v)
 summary = {}
@@ -33,7 +39,7 @@ for kn, cs in acc.items():
         if cn == "WRITE_SIZE":
             extra = f"   -> HBM write {v / 1e3:.1f} MB/launch"
         print(f"  {cn:28s} {v:16.1f}  (n={len(cs[cn])}){extra}")
-    ent = {"launches": max(len(v) for v in cs.values())}
+    ent = {"launches": max(len(v) for v in cs.values()), "last_dispatch": last[kn]}
     if "FETCH_SIZE" in vals:
         ent["hbm_read_bytes"] = 2 * vals["FETCH_SIZE"] * 1e3   # KB, x2 (gfx950)
     if "WRITE_SIZE" in vals:
