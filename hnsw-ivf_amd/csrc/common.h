@@ -5,6 +5,7 @@
 // (reference faiss/impl/FaissAssert.h, faiss/impl/FaissException.h) which the
 // C-ABI turns into return code -2 (reference c_api/macros_impl.h:22-56).
 #pragma once
+#include <atomic>
 
 #include <hip/hip_runtime.h>
 
@@ -82,6 +83,14 @@ inline size_t roundup(size_t a, size_t b) { return (a + b - 1) / b * b; }
 inline size_t cdiv(size_t a, size_t b) { return (a + b - 1) / b; }
 
 // Owning device buffer (hipMalloc'ed), bound to the device current at alloc.
+// bumped by every DeviceBuffer (re)allocation: a captured search graph
+// (IndexIVF::search_device) holds raw pointers and is replayed only while
+// this has not moved
+inline std::atomic<uint64_t>& devbuf_epoch() {
+    static std::atomic<uint64_t> e{0};
+    return e;
+}
+
 struct DeviceBuffer {
     void* ptr = nullptr;
     size_t bytes = 0;
@@ -113,6 +122,7 @@ struct DeviceBuffer {
     // grow-only reallocation (contents not preserved)
     void reserve(size_t nbytes) {
         if (nbytes <= bytes && ptr) return;
+        devbuf_epoch().fetch_add(1, std::memory_order_relaxed);  // (captured graphs go stale)
         release();
         size_t nb = nbytes ? nbytes : 16;
         HIP_CHECK(hipGetDevice(&device));
@@ -188,6 +198,7 @@ void set_kernel_timing_enabled(bool);
 // only the kernel stage of this name is timed (nullptr / "": all of them)
 void set_kernel_timing_filter(const char* name);
 bool kernel_timing_wants(const char* name);
+std::string kernel_timing_state();  // "off" / "on:<only>" (graph cache keys)
 
 // Brackets a launch with HIP events when timing is enabled.
 struct ScopedKernelTimer {

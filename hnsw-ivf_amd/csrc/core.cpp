@@ -64,6 +64,11 @@ void set_kernel_timing_filter(const char* name) {
     std::lock_guard<std::mutex> g(g_timing_mu);
     g_timing_only = name ? name : "";
 }
+std::string kernel_timing_state() {
+    if (!g_timing) return "off";
+    std::lock_guard<std::mutex> g(g_timing_mu);
+    return "on:" + g_timing_only;
+}
 bool kernel_timing_wants(const char* name) {
     if (!g_timing) return false;
     std::lock_guard<std::mutex> g(g_timing_mu);

@@ -570,6 +570,25 @@ struct IndexIVF : Index {
                              hipStream_t s) const;
     mutable hipStream_t pipe_s_ = nullptr;
     mutable std::vector<hipEvent_t> pipe_ev_;
+    // search_device replayed from a hipGraph captured on the second identical
+    // call (flat quantizer, no parameters); FAISS_AMD_GRAPH=0: off
+    void search_device_eager(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                             idx_t* labels, const SearchParameters* params,
+                             hipStream_t stream) const;
+    struct SearchGraph {
+        std::string key;
+        int seen = 0;
+        bool failed = false;
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        // the event-record nodes of the stages timed at capture (kernel
+        // timing): each replay records fresh events there
+        std::vector<std::string> tnames;
+        std::vector<double> tunits;
+        std::vector<std::pair<hipGraphNode_t, hipGraphNode_t>> tnodes;
+        void clear();
+    };
+    mutable SearchGraph graph_;
     // query image the flat quantizer prepared into s_q_ for the chunk
     // search() is scanning (IndexFlat::assign_device_qimg), null outside it
     mutable const void* shared_qimg_ = nullptr;

@@ -1,0 +1,100 @@
+"""IndexIVF::search_device replayed from a captured hipGraph (ivf.cpp): the
+second identical call captures, later ones replay.  Every replay must give
+the eager result; a change the graph cannot see (new vectors added, nprobe,
+k, another output buffer, FAISS_AMD_GRAPH=0) must retire it; kernel timing
+must keep one record per replay."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class Bufs:
+    def __init__(self, xq, k):
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.n, self.k = xq.shape[0], k
+        self.ptrs = []
+        self.px = self._alloc(xq.nbytes)
+        self.pd = self._alloc(self.n * k * 4)
+        self.pi = self._alloc(self.n * k * 8)
+        x = np.ascontiguousarray(xq, dtype=np.float32)
+        self.hip.hipMemcpy(self.px, x.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(x.nbytes), 1)
+
+    def _alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        assert self.hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(max(nbytes, 4))) == 0
+        self.ptrs.append(p)
+        return p
+
+    def search(self, idx, k=None):
+        k = k or self.k
+        idx.search_device(self.n, self.px.value, k, self.pd.value, self.pi.value)
+        assert self.hip.hipDeviceSynchronize() == 0
+        D = np.empty((self.n, k), np.float32)
+        I = np.empty((self.n, k), np.int64)
+        self.hip.hipMemcpy(D.ctypes.data_as(ctypes.c_void_p), self.pd, ctypes.c_size_t(D.nbytes), 2)
+        self.hip.hipMemcpy(I.ctypes.data_as(ctypes.c_void_p), self.pi, ctypes.c_size_t(I.nbytes), 2)
+        return D, I
+
+    def close(self):
+        for p in self.ptrs:
+            self.hip.hipFree(p)
+
+
+@pytest.mark.parametrize("desc", ["IVF256,Flat", "IVF256,PQ16"])
+def test_graph_replay_equals_eager(amd, gpu, monkeypatch, desc):
+    d, nb, nq, k = 64, 60_000, 3000, 10
+    xb = amd.float_rand(nb * d, 1234).reshape(nb, d)
+    idx = amd.index_factory(d, desc)
+    idx.train(xb[:30_000])
+    idx.add(xb[:40_000])
+    idx.nprobe = 16
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    b = Bufs(xq, k)
+    try:
+        monkeypatch.setenv("FAISS_AMD_GRAPH", "0")
+        ref = b.search(idx)
+        monkeypatch.delenv("FAISS_AMD_GRAPH")
+        for _ in range(5):  # eager, capture, replays
+            D, I = b.search(idx)
+            np.testing.assert_array_equal(I, ref[1])
+            np.testing.assert_array_equal(D, ref[0])
+        # kernel timing: the same records per call as the eager path (the
+        # replays record fresh events at the timed stages' nodes)
+        import collections
+        amd.set_kernel_timing(True)
+        counts = []
+        for genv in ("0", None):
+            if genv:
+                monkeypatch.setenv("FAISS_AMD_GRAPH", genv)
+            else:
+                monkeypatch.delenv("FAISS_AMD_GRAPH")
+            idx.reset_kernel_times()
+            for _ in range(4):
+                b.search(idx)
+            counts.append(collections.Counter(nm for nm, ms, _ in idx.kernel_times()
+                                              if ms > 0))
+        amd.set_kernel_timing(False)
+        assert counts[0] and counts[0] == counts[1], counts
+        # a change the host sees retires the graph
+        idx.nprobe = 8
+        monkeypatch.setenv("FAISS_AMD_GRAPH", "0")
+        ref8 = b.search(idx)
+        monkeypatch.delenv("FAISS_AMD_GRAPH")
+        for _ in range(3):
+            np.testing.assert_array_equal(b.search(idx)[1], ref8[1])
+        idx.add(xb[40_000:])
+        monkeypatch.setenv("FAISS_AMD_GRAPH", "0")
+        refa = b.search(idx)
+        monkeypatch.delenv("FAISS_AMD_GRAPH")
+        assert not np.array_equal(refa[1], ref8[1])
+        for _ in range(3):
+            D, I = b.search(idx)
+            np.testing.assert_array_equal(I, refa[1])
+            np.testing.assert_array_equal(D, refa[0])
+        Dk, Ik = b.search(idx, k=5)
+        np.testing.assert_array_equal(Ik, refa[1][:, :5])
+    finally:
+        b.close()
