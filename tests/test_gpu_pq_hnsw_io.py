@@ -200,3 +200,32 @@ def test_ivfpq_mfma_duplicate_codes_ties(amd, orc, gpu):
     ref = orc.IVFOracle.from_index(idx)
     Dr, Ir = ref.search_preassigned(xq, 10, Iq, Dq)
     assert_same_results(D, I, Dr, Ir)
+
+
+@pytest.mark.parametrize("d", [37, 128])
+def test_hnsw_register_kernel_forms_equal_reference(amd, orc, gpu, monkeypatch, d):
+    """The register kernel's int8 prefilter (d = 37: padded image dims) and
+    its replay continuation, each switched off in turn, on a graph with
+    duplicated points (distance ties in the candidate set and the results;
+    k < ef and k = ef): every form gives the reference's results."""
+    nb = 5000
+    xb = rand(orc, nb, d, 61)
+    xb[1000:1150] = xb[:150]
+    xb[3000:3040] = xb[:40]
+    xq = np.concatenate([rand(orc, 300, d, 62), xb[:60]])
+    cases = [(16, 10), (64, 64), (40, 5), (64, 1)]
+    out = {}
+    for q8, rp in (("1", "1"), ("0", "1"), ("1", "0")):
+        monkeypatch.setenv("FAISS_AMD_HNSW_Q8", q8)
+        monkeypatch.setenv("FAISS_AMD_HNSW_REPLAY", rp)
+        h = amd.IndexHNSWFlat(d, 16)
+        h.add(xb)
+        for ef, k in cases:
+            h.efSearch = ef
+            out[(q8, rp, ef, k)] = h.search(xq, k)
+    g = orc.HNSWGraph.from_index(h)
+    for ef, k in cases:
+        Dr, Ir = g.search(xq, k, ef)
+        for q8, rp in (("1", "1"), ("0", "1"), ("1", "0")):
+            D, I = out[(q8, rp, ef, k)]
+            assert_same_results(D, I, Dr, Ir)
