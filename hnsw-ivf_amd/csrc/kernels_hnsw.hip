@@ -1117,6 +1117,11 @@ __device__ __forceinline__ int q8_filter(const HNSWDevice& g, const uint8_t* q8x
 #ifndef HNSW_PB
 #define HNSW_PB 1
 #endif
+// fp32 rows 8 lanes per row, 8 per pass (half the registers of the 4-lane
+// form; measured slower, also at 6 waves per SIMD: off)
+#ifndef HNSW_FP32_8LANE
+#define HNSW_FP32_8LANE 0
+#endif
 // the register kernel's waves per SIMD (its VGPR budget: 512 / HNSW_WPE)
 #ifndef HNSW_WPE
 #define HNSW_WPE 5
@@ -1147,14 +1152,15 @@ struct HopTrace {
 // the search goes on from there: the results, the visited table and every
 // distance computed so far depend on the entry set alone and are kept.
 constexpr uint64_t RLOG_POP = ~0ull;  // the marker (dis bits 0xffffffff: no distance)
-constexpr int RLOG_CAP = (int)kHnswReplayCap;  // entries per query
+constexpr int RLOG_CAP = (int)kHnswReplayCap;  // entries per query (global memory)
+constexpr int RLOG_LDS = 640;  // entries per query when the log lives in the LDS
 struct L0Run {
     int nvalid;
     float rmax;
     unsigned long long todo;  // the stopped hop's arrivals not yet applied (0: at pop_min)
     float fdis;               // that hop's arrivals (lanes)
     int32_t fv;
-    int logpos;               // log entries written (> RLOG_CAP: overflowed)
+    int logpos;               // log entries written (> the log's capacity: overflowed)
     int stop;                 // log entries the replay applies
 };
 
@@ -1185,7 +1191,7 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                                             uint32_t& st_ndis, uint32_t& st_nhops, HopTrace& tr,
                                             uint64_t* __restrict__ rlog, const uint8_t* q8x,
                                             const double* q8d, uint32_t& st_q8,
-                                            uint32_t& st_x32) {
+                                            uint32_t& st_x32, int logcap) {
     int nvalid = S.nvalid;
     float rmax = S.rmax;
     // the sequential add_to_heap calls (:678-689) for the arrivals `todo`
@@ -1304,8 +1310,13 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
             // (reference order)
             float fdis = 0.f;
             if (g.d <= 128)
+#if HNSW_FP32_8LANE
+                fdis = ref_rows64_8lane<true, 16>(qs, qs, g.storage, g.ld, g.d,
+                                                  lane < nf ? (uint32_t)fv : 0u, nf, lane);
+#else
                 fdis = ref_rows64_4lane_pb<true, 16, HNSW_PB>(qs, qs, g.storage, g.ld, g.d,
                                                         lane < nf ? (uint32_t)fv : 0u, nf, lane);
+#endif
             else if (lane < nf)
                 fdis = l2_row(qs, g.storage + (int64_t)fv * g.ld, g.d);
             st_nhops += 1;
@@ -1348,7 +1359,7 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
                 if (rlog) {
                     hp = S.logpos;
                     const int m = __popcll(todo);
-                    if (hp + 1 + m <= RLOG_CAP) {
+                    if (hp + 1 + m <= logcap) {
                         // streaming stores: the log is read back only
                         // after a tie (~1.5 % of c4's queries)
                         if (lane == 0) __builtin_nontemporal_store(RLOG_POP, rlog + hp);
@@ -1399,7 +1410,7 @@ __device__ __forceinline__ void level0_replay(CandLayout& C, const uint64_t* __r
 // meets a layout-dependent tie is searched again with CandLayout (layout = 1:
 // every query with CandLayout — tests).  Results are the reference's, bit for
 // bit, either way.
-template <bool LDS_VISITED, bool TRACE, bool NB0>
+template <bool LDS_VISITED, bool TRACE, bool NB0, bool LOGLDS>
 __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, const float* __restrict__ x,
                                                        int ldx, int64_t n, int k, int efSearch,
                                                        int ef, float* __restrict__ D,
@@ -1481,7 +1492,12 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
         }
         // ---- level 0
         const uint32_t up_ndis = st_ndis, up_nhops = st_nhops;
-        uint64_t* qlog = rlog ? rlog + (int64_t)blockIdx.x * RLOG_CAP : nullptr;
+        // the replay log: in the LDS after the visited bitmap (LOGLDS), else
+        // this query's slice of rlog
+        const int logcap = LOGLDS ? RLOG_LDS : RLOG_CAP;
+        uint64_t* qlog = LOGLDS ? (uint64_t*)((char*)sm + exact_reg_head(g) +
+                                              ((4 * vwords + 7) & ~(int64_t)7))
+                                : (rlog ? rlog + (int64_t)blockIdx.x * RLOG_CAP : nullptr);
         L0Run S;
         bool done = false;
         if (!layout) {
@@ -1489,12 +1505,12 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
             level0_seed(C, R, S, vis, k, lane, nearest, d_nearest);
             done = hnsw_level0<CandSet, TRACE, NB0>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
                                                st_ndis, st_nhops, tr, qlog, q8x, q8d, st_q8,
-                                               st_x32);
+                                               st_x32, logcap);
         }
         if (!done) {
             CandLayout C;
             if (TRACE) tr.t[8] = 1;
-            if (!layout && qlog && S.logpos <= RLOG_CAP) {
+            if (!layout && qlog && S.logpos <= logcap) {
                 // continue from the stopping point with the replayed heap
                 level0_replay(C, qlog, S.stop, ef, g.ntotal, lane, nearest, d_nearest);
                 if (TRACE) tr.t[9] = (unsigned long long)S.stop;
@@ -1512,7 +1528,7 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
             }
             hnsw_level0<CandLayout, TRACE, NB0>(g, qs, vis, k, efSearch, ef, lane, C, S, R, st_n2,
                                                 st_ndis, st_nhops, tr, nullptr, q8x, q8d, st_q8,
-                                                st_x32);
+                                                st_x32, 0);
         }
     }
     if (TRACE && lane == 0) {
@@ -1572,14 +1588,26 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
         // FAISS_AMD_HNSW_LAYOUT=1: every query with the heap-layout form (tests)
         const char* lenv = getenv("FAISS_AMD_HNSW_LAYOUT");
         const int layout = lenv && !strcmp(lenv, "1") ? 1 : 0;
+        // FAISS_AMD_HNSW_LOG=lds: the replay log in the LDS when it fits
+        // beside the query and the visited bitmap within the 8 KB per work
+        // group that keeps 20 of them on a CU (c4: 2 KB of bitmap); measured
+        // no faster than the nontemporal stores to rlog (1.715 vs 1.692 ms,
+        // same box), so rlog is the default
+        const char* genv = getenv("FAISS_AMD_HNSW_LOG");
+        const size_t lds_logb = (size_t)RLOG_LDS * 8 + ((vwords * 4) & 7);
+        const bool lds_log = rlog && rvis && g.nb0 && genv && !strcmp(genv, "lds") &&
+                             lds_r + (size_t)vwords * 4 + lds_logb <= 8192;
+        const size_t lds_logx = lds_log ? lds_logb : 0;
         // FAISS_AMD_HNSW_TRACE=<file>: per-query hop-phase cycles (profiling)
         const char* tenv = getenv("FAISS_AMD_HNSW_TRACE");
         if (tenv && rvis) {
             unsigned long long* tb = nullptr;
             HIP_CHECK(hipMalloc(&tb, 128 * std::max<int64_t>(n, 1)));
             HIP_CHECK(hipMemsetAsync(tb, 0, 128 * std::max<int64_t>(n, 1), s));
-            auto kt = g.nb0 ? k_hnsw_exact_reg<true, true, true> : k_hnsw_exact_reg<true, true, false>;
-            kt<<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4, s>>>(
+            auto kt = lds_log ? k_hnsw_exact_reg<true, true, true, true>
+                              : (g.nb0 ? k_hnsw_exact_reg<true, true, true, false>
+                                       : k_hnsw_exact_reg<true, true, false, false>);
+            kt<<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4 + lds_logx, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
                     layout, tb, rlog);
             HIP_LAUNCH_CHECK();
@@ -1593,11 +1621,12 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
             }
             return;
         }
-        auto kr = rvis ? (g.nb0 ? k_hnsw_exact_reg<true, false, true>
-                                : k_hnsw_exact_reg<true, false, false>)
-                       : (g.nb0 ? k_hnsw_exact_reg<false, false, true>
-                                : k_hnsw_exact_reg<false, false, false>);
-        kr<<<dim3((unsigned)n), dim3(64), rvis ? lds_r + vwords * 4 : lds_r, s>>>(
+        auto kr = lds_log ? k_hnsw_exact_reg<true, false, true, true>
+                  : rvis  ? (g.nb0 ? k_hnsw_exact_reg<true, false, true, false>
+                                   : k_hnsw_exact_reg<true, false, false, false>)
+                          : (g.nb0 ? k_hnsw_exact_reg<false, false, true, false>
+                                   : k_hnsw_exact_reg<false, false, false, false>);
+        kr<<<dim3((unsigned)n), dim3(64), rvis ? lds_r + vwords * 4 + lds_logx : lds_r, s>>>(
                 g, x, ldx, n, k, efSearch, ef, D, I, I32, rvis ? nullptr : visited_scratch, vwords,
                 stats, only, qidx, layout, nullptr, rlog);
         HIP_LAUNCH_CHECK();

@@ -234,5 +234,52 @@ __device__ __forceinline__ float ref_rows64_4lane_pb(const float* xr, const floa
     return out;
 }
 
+// ref_rows64_4lane_pb with 8 lanes per row and 8 rows per pass: lane j of a
+// row owns the reference's partial sum c_j (dims 8m + j); x_j = c_j + c_{j+4}
+// by a lane swap, then (x0 + x2) + (x1 + x3) (ref_arith.h order), then the
+// epilogue dims.  XM row floats per lane and pass (half of the 4-lane form's
+// registers), one memory round trip per pass.
+template <bool L2, int XM>
+__device__ __forceinline__ float ref_rows64_8lane(const float* xr, const float* __restrict__ xq,
+                                                  const float* __restrict__ codes, int ldc, int d,
+                                                  uint32_t grow, int nv, int lane) {
+    const int g = lane >> 3, j = lane & 7;
+    const int n8 = d & ~7, nm = n8 >> 3;
+    const int npass = (nv + 7) >> 3;
+    float out = 0.f;
+#pragma unroll 1
+    for (int p = 0; p < npass; p++) {
+        const uint32_t rg = __shfl(grow, (8 * p + g) & 63);
+        const bool rv = 8 * p + g < nv;
+        const float* yr = codes + (int64_t)(rv ? rg : 0u) * ldc;
+        float yv[XM];
+#pragma unroll
+        for (int m = 0; m < XM; m++) yv[m] = m < nm ? yr[8 * m + j] : 0.f;
+        float c = 0.f;
+#pragma unroll
+        for (int m = 0; m < XM; m++) {
+            const float t = ref_term_fma<L2>(xr[8 * m + j], yv[m], c);
+            c = m < nm ? t : c;
+        }
+        const float x = c + __shfl_xor(c, 4);   // x_j = c_j + c_{j+4}
+        const float y = x + __shfl_xor(x, 2);   // x0 + x2, x1 + x3
+        float r = y + __shfl_xor(y, 1);         // (x0 + x2) + (x1 + x3)
+        if (n8 < d) {
+            int i = n8;
+            if (d - n8 >= 4) {
+                const float e0 = ref_term<L2>(xq[n8], yr[n8]), e1 = ref_term<L2>(xq[n8 + 1], yr[n8 + 1]);
+                const float e2 = ref_term<L2>(xq[n8 + 2], yr[n8 + 2]);
+                const float e3 = ref_term<L2>(xq[n8 + 3], yr[n8 + 3]);
+                r = r + ((e0 + e2) + (e1 + e3));
+                i += 4;
+            }
+            for (; i < d; i++) r = ref_term_fma<L2>(xq[i], yr[i], r);
+        }
+        const float got = __shfl(r, 8 * (lane & 7));
+        if ((lane >> 3) == p) out = got;
+    }
+    return out;
+}
+
 }  // namespace kern
 }  // namespace faiss_amd
