@@ -470,7 +470,12 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     // second identical call: capture it
     const size_t t0 = ktimes.e0.size();
     hipGraph_t gr = nullptr;
-    HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();  // (e.g. the legacy default stream)
+        graph_.failed = true;
+        search_device_eager(n, x, ldx, k, distances, labels, params_in, s);
+        return;
+    }
     bool ok = true;
     try {
         search_device_eager(n, x, ldx, k, distances, labels, params_in, s);
