@@ -286,6 +286,11 @@ def main():
                          "value (instead of one replica per GPU)")
     ap.add_argument("--no-shard-figure", action="store_true",
                     help="c1-c4 at N > 1: skip the rccl_shards figure beside the replicas")
+    ap.add_argument("--nprobe", type=int, default=0,
+                    help="override the config's nprobe (a point of the reference "
+                         "harness's grid; not a BASELINE line)")
+    ap.add_argument("--efsearch", type=int, default=0,
+                    help="override the config's quantizer efSearch (HNSW configs)")
     ap.add_argument("--weak", action="store_true",
                     help="c5: every rank brings nq queries (global batch N x nq)")
     args = ap.parse_args()
@@ -313,6 +318,10 @@ def main():
     amd.set_device(gpu)
     stream = torch.cuda.current_stream().cuda_stream
 
+    if args.nprobe:
+        cfg["nprobe"] = args.nprobe
+    if args.efsearch and "efSearch" in cfg:
+        cfg["efSearch"] = args.efsearch
     d, nb, nq, k, nprobe = cfg["d"], cfg["nb"], cfg["nq"], cfg["k"], cfg["nprobe"]
     # ---- queries: c5 (strong) splits the batch of nq over the ranks; the
     # other forms give every rank its own nq queries
@@ -606,7 +615,9 @@ def main():
                        "nprobe": nprobe, "k": k, "global_batch": nq_glob,
                        "parallelism": par, "recall_at_10": recall,
                        "recall_ground_truth": gt_note if nr else None,
-                       "candidates_per_query": cand_per_q},
+                       "candidates_per_query": cand_per_q,
+                       "efSearch": cfg.get("efSearch"),
+                       "grid_point": bool(args.nprobe or args.efsearch)},
             "roofline": roofline,
             "kernels": kernels,
             "cpu_baseline": cpu,
