@@ -1406,10 +1406,12 @@ __device__ __forceinline__ void level0_replay(CandLayout& C, const uint64_t* __r
 }
 
 // The reference's HNSW::search for ef, k <= 64, one wave per query: the
-// greedy descent, then level 0 with the CandSet form; a query whose search
-// meets a layout-dependent tie is searched again with CandLayout (layout = 1:
-// every query with CandLayout — tests).  Results are the reference's, bit for
-// bit, either way.
+// greedy descent, then level 0 with the CandSet form (int8 prefilter, one
+// merge per hop, results derived from the set); a query whose search meets a
+// layout-dependent decision continues with CandLayout from its replayed log
+// (rlog, or the LDS when LOGLDS), or searches level 0 again when the log
+// overflowed (layout = 1: every query with CandLayout — tests).  Results are
+// the reference's, bit for bit, either way.
 template <bool LDS_VISITED, bool TRACE, bool NB0, bool LOGLDS>
 __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, const float* __restrict__ x,
                                                        int ldx, int64_t n, int k, int efSearch,
