@@ -861,6 +861,13 @@ static_assert(RR_W == 1, "k_ivf_rerank assumes one wave per block");
 
 // Exact reference-order distance of the row `grow` each lane names: ref_arith.h
 // ref_rows64_4lane (4 lanes per row, 16 rows per pass, no LDS staging).
+// passes of 16 rows whose loads the Flat re-rank issues together when its
+// candidates fill a prefix of the lanes (one round trip per RR_PB passes).
+// 2 measured no faster: c4 re-rank 0.283 ms (1), 0.310 (2, spilling at 4
+// waves per SIMD), 0.282 (2 at 3 waves per SIMD)
+#ifndef RR_PB
+#define RR_PB 1
+#endif
 template <bool L2>
 __device__ __forceinline__ float eval_rows64_direct(const float* xr, const float* __restrict__ xq,
                                                     const float* __restrict__ codes, int ldc,
@@ -948,8 +955,10 @@ struct RerankStream {
     const uint8_t* sel;       // IDSelector mask of the arena rows (nullptr: all)
     bool fold;                // folded filter keys (ivf_decode_lo)
 
+    // nv >= 0: the valid lanes are exactly 0..nv-1 (their rows' loads then
+    // go out RR_PB passes at a time); nv < 0: any lanes
     __device__ __forceinline__ void emit(bool ok, uint32_t grow, int r, float& k1,
-                                         long long& k2) const {
+                                         long long& k2, int nv = -1) const {
         // the id load is issued before the rows', so both share one round trip
         const long long idv = ok ? (long long)ids[grow] : 0ll;
         float dis;
@@ -958,7 +967,10 @@ struct RerankStream {
             const float d0 = __shfl(my_d0, r);
             dis = ok ? pq_exact<PQD>(pa, xs, grow, l, d0) : 0.f;
         } else {
-            dis = eval_rows64_direct<L2>(xs, xq, codes, ldc, d, grow, ok, lane);
+            if (nv >= 0)
+                dis = ref_rows64_4lane_pb<L2, RR_XM, RR_PB>(xs, xq, codes, ldc, d, grow, nv, lane);
+            else
+                dis = eval_rows64_direct<L2>(xs, xq, codes, ldc, d, grow, ok, lane);
         }
         k1 = WS_INF;
         k2 = WS_NOID;
@@ -974,7 +986,7 @@ struct RerankStream {
                 const long long rank = ok ? (((long long)rp << 32) | grow) : 0;
                 float k1;
                 long long k2;
-                emit(ok, grow, rp, k1, k2);
+                emit(ok, grow, rp, k1, k2, min(64, nsv - s0));
                 f(ok && key_admissible(k1), k1, k2, rank);
             }
             return;
@@ -1221,7 +1233,7 @@ __global__ __launch_bounds__(64 * RR_W, RR_WAVES) void k_ivf_rerank(
         for (int b = 0; b < NB; b++) {
             const bool ok = 64 * b + lane < ns;
             st.emit(ok, ok ? surv[w][64 * b + lane] : 0u, ok ? (int)sprobe[w][64 * b + lane] : 0,
-                    k1[b], k2[b]);
+                    k1[b], k2[b], max(0, min(64, ns - 64 * b)));
             if (!(ok && key_admissible(k1[b]))) {
                 k1[b] = WS_INF;
                 k2[b] = WS_NOID;
