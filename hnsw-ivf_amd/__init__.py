@@ -95,6 +95,14 @@ class _CVar:
         lib().faiss_amd_get_hnsw_row_stats(C.byref(a), C.byref(b))
         return a.value, b.value
 
+    @property
+    def hnsw_replay_stats(self):
+        """(replayed, searched again, corrupt logs) of the register HNSW
+        kernel's layout-dependent continuations (not in the reference)."""
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        lib().faiss_amd_get_hnsw_replay_stats(C.byref(a), C.byref(b), C.byref(c))
+        return a.value, b.value, c.value
+
 
 cvar = _CVar()
 
@@ -174,6 +182,7 @@ def _declare(L):
         "faiss_amd_get_hnsw_stats": (C.POINTER(HNSWStats), []),
         "faiss_amd_HNSWStats_reset": (None, []),
         "faiss_amd_get_hnsw_row_stats": (None, [C.c_void_p, C.c_void_p]),
+        "faiss_amd_get_hnsw_replay_stats": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
         "faiss_amd_fold_device_stats": (C.c_int, [_P]),
         "faiss_IndexIVFFlat_new_with": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t]),
         "faiss_IndexIVFFlat_new_with_metric": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t, C.c_int]),

@@ -455,6 +455,12 @@ void faiss_amd_get_hnsw_row_stats(uint64_t* fp32_rows, uint64_t* q8_rows) {
     if (fp32_rows) *fp32_rows = hnsw_row_stats.fp32_rows;
     if (q8_rows) *q8_rows = hnsw_row_stats.q8_rows;
 }
+void faiss_amd_get_hnsw_replay_stats(uint64_t* replayed, uint64_t* searched_again,
+                                     uint64_t* replay_bad) {
+    if (replayed) *replayed = hnsw_row_stats.replayed;
+    if (searched_again) *searched_again = hnsw_row_stats.searched_again;
+    if (replay_bad) *replay_bad = hnsw_row_stats.replay_bad;
+}
 int faiss_amd_fold_device_stats(const FaissIndex* index) {
     C_TRY auto ix = IX(index);
     ix->fold_device_stats();

@@ -170,6 +170,15 @@ void IndexFlat::reconstruct(idx_t key, float* recons) const {
     memcpy(recons, xb.data() + (size_t)key * d, sizeof(float) * d);
 }
 
+void IndexFlat::stream_enter(hipStream_t s) const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    order_.enter(s);
+}
+void IndexFlat::stream_leave(hipStream_t s) const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    order_.leave(s);
+}
+
 void IndexFlat::sync_device() const {
     std::lock_guard<std::recursive_mutex> g(mu_);
     if (!dirty_) return;

@@ -475,17 +475,15 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
     constexpr bool i32 = sizeof(OutIdx) == 4;
     split_.active = false;
     if (!d_stats_.ptr) {
-        d_stats_.reserve(6 * sizeof(unsigned long long));
-        HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, 6 * sizeof(unsigned long long), s));
+        d_stats_.reserve(kern::kHnswStatsWords * sizeof(unsigned long long));
+        HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, kern::kHnswStatsWords * sizeof(unsigned long long),
+                                 s));
     }
     // queries per launch: the per-query visited bitmaps that do not fit in
     // LDS, and heaps beyond it (max(efSearch, k) in the thousands), live in
     // scratch kept under 256 MiB each (chunks of the batch)
-    const int ef = std::max(efSearch, k);
     const size_t hw = kern::hnsw_heap_scratch_words(k, efSearch, ld());
-    const size_t lds_need = sizeof(float) * ld() + (hw ? 0 : 8 * (size_t)ef + 8 * (size_t)k) +
-                            544 + (size_t)vwords * 4;
-    const bool scratch = lds_need > 64 * 1024;
+    const bool scratch = kern::hnsw_visited_scratch_needed(ld(), k, efSearch, vwords);
     idx_t qc = n;
     if (scratch)
         qc = std::min<idx_t>(qc, std::max<idx_t>(1, (idx_t)(((size_t)256 << 20) /
@@ -496,6 +494,11 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
     const char* renv = getenv("FAISS_AMD_HNSW_REPLAY");
     const bool rlog = kern::hnsw_register_eligible(k, efSearch) &&
                       !kern::hnsw_uses_batched(k, efSearch) && !(renv && !strcmp(renv, "0"));
+    // FAISS_AMD_HNSW_REPLAY_CAP=<entries>: a smaller log per query (tests: the
+    // overflow path)
+    int64_t rcap = kern::kHnswReplayCap;
+    if (const char* cenv = getenv("FAISS_AMD_HNSW_REPLAY_CAP"))
+        rcap = std::max<int64_t>(1, std::min<int64_t>(atoll(cenv), kern::kHnswReplayCap));
     if (rlog)
         qc = std::min<idx_t>(qc, (idx_t)(((size_t)256 << 20) / (8 * kern::kHnswReplayCap)));
     qc = std::max<idx_t>(qc, 1);
@@ -512,7 +515,7 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
                           i32 ? (int32_t*)labels + q0 * k : nullptr, s_visited_.as<uint32_t>(),
                           vwords, d_stats_.as<unsigned long long>(), s_flags_.as<uint32_t>(), s,
                           &ktimes, defer, hw ? s_heaps_.as<float>() : nullptr,
-                          rlog ? s_rlog_.as<uint64_t>() : nullptr, rlog ? kern::kHnswReplayCap : 0);
+                          rlog ? s_rlog_.as<uint64_t>() : nullptr, rlog ? rcap : 0);
     }
     if (!defer) {
         order_.leave(s);
@@ -613,7 +616,7 @@ void IndexHNSW::fold_device_stats() const {
     if (!d_stats_.ptr) return;
     DevGuard2 dg(device);
     hipStream_t s = stream();
-    unsigned long long st[6];
+    unsigned long long st[kern::kHnswStatsWords];
     HIP_CHECK(hipMemcpyAsync(st, d_stats_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemsetAsync(d_stats_.ptr, 0, sizeof(st), s));
     HIP_CHECK(hipStreamSynchronize(s));
@@ -625,6 +628,9 @@ void IndexHNSW::fold_device_stats() const {
     hnsw_stats.combine(add);
     hnsw_row_stats.fp32_rows += st[4];
     hnsw_row_stats.q8_rows += st[5];
+    hnsw_row_stats.replayed += st[6];
+    hnsw_row_stats.searched_again += st[7];
+    hnsw_row_stats.replay_bad += st[8];
 }
 
 void IndexHNSW::search_stats(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,

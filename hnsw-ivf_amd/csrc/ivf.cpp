@@ -269,6 +269,7 @@ void IndexIVF::sync_device() const {
     upload_extra();
     HIP_CHECK(hipStreamSynchronize(s));
     dirty_ = false;
+    version_++;  // (the content uploaded may differ from what a captured graph saw)
 }
 
 uint32_t* IndexIVF::bucket_counts(hipStream_t s, uint32_t** next) const {
@@ -424,10 +425,10 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
                              idx_t* labels, const SearchParameters* params_in,
                              hipStream_t s) const {
     const char* genv = getenv("FAISS_AMD_GRAPH");
-    const bool eligible = !(genv && !strcmp(genv, "0")) && params_in == nullptr && !qdone_ &&
-                          dynamic_cast<const IndexFlat*>(quantizer) != nullptr &&
-                          get_search_slices() <= 1 && n > 0 && !dirty_;
     std::lock_guard<std::recursive_mutex> g(mu_);
+    const auto* qflat = dynamic_cast<const IndexFlat*>(quantizer);
+    const bool eligible = !(genv && !strcmp(genv, "0")) && params_in == nullptr && !qdone_ &&
+                          qflat != nullptr && get_search_slices() <= 1 && n > 0 && !dirty_;
     if (!eligible) {
         graph_.clear();
         search_device_eager(n, x, ldx, k, distances, labels, params_in, s);
@@ -456,7 +457,13 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
             ktimes.e0.push_back(a);
             ktimes.e1.push_back(b);
         }
+        // the graph writes this index's and the quantizer's scratch: wait
+        // for their last users on other streams, as the eager path does
+        qflat->stream_enter(s);
+        order_.enter(s);
         HIP_CHECK(hipGraphLaunch(graph_.exec, s));
+        order_.leave(s);
+        qflat->stream_leave(s);
         return;
     }
     if (graph_.key != key) {
@@ -1336,8 +1343,11 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         // eligible; FAISS_AMD_PQ_FILTER=decode keeps the in-loop decode filter
         // k_ivfpq_filter_w, which also serves IDSelectors)
         const char* fenv = getenv("FAISS_AMD_PQ_FILTER");
+        // (the streamed filter needs the query image: the flat quantizer's,
+        // or one prepared below for 16-B aligned rows)
         const bool stream = pq_stream_ready_ && !sel && !(fenv && !strcmp(fenv, "decode")) &&
                             !(fenv && !strcmp(fenv, "wg")) &&
+                            (shared_qimg_ != nullptr || ldx % 4 == 0) &&
                             kern::ivfpq_stream_eligible(d, (int)pq.M, (int)k, np);
         const int QT = stream ? kern::IVF_FLAT_QT : 64;
         uint32_t* counts_next = nullptr;

@@ -374,10 +374,18 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
 // the register kernel's CandSet update log (64-bit entries per query in
 // replay_log): a query whose candidate set meets a layout-dependent decision
 // continues from a replayed heap instead of searching level 0 again; a query
-// whose log would exceed it searches again
+// whose log would exceed it searches again.  replay_cap (<= kHnswReplayCap,
+// the per-query stride of replay_log) bounds the entries a query may log.
+// stats[6..8] count the register kernel's continuations: replayed, searched
+// again (log overflowed or absent), log found corrupt (searched again; 0
+// unless a bug)
 constexpr int64_t kHnswReplayCap = 1024;
+constexpr int kHnswStatsWords = 9;
 // 32-bit words of global heap scratch per query (0: the heaps fit the LDS)
 size_t hnsw_heap_scratch_words(int k, int efSearch, int ld);
+// a per-query visited bitmap of vwords words lives in global scratch (for
+// some kernel this search may run) rather than the LDS
+bool hnsw_visited_scratch_needed(int ld, int k, int efSearch, int64_t vwords);
 // the register kernel serves max(efSearch, k) <= 64
 bool hnsw_register_eligible(int k, int efSearch);
 // the batched kernel (and its tie re-runs) runs for these parameters

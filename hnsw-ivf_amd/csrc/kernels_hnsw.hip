@@ -1383,26 +1383,38 @@ __device__ __forceinline__ bool hnsw_level0(const HNSWDevice& g, const float* qs
 // CandSet's log up to S.stop into a fresh CandLayout seeded like it: the
 // heap array the reference holds at that point (the pops before the stop
 // took a unique minimum, the evictions a unique top)
-__device__ __forceinline__ void level0_replay(CandLayout& C, const uint64_t* __restrict__ rlog,
-                                              int stop, int ef, int ntotal, int lane,
-                                              int nearest, float d_nearest) {
+// (took the heap).  Every entry below S.stop was written by this query's
+// CandSet run (a hop is logged only when all of it fits the capacity, and the
+// replay runs only when nothing overflowed), so an entry that names no node
+// means the log is corrupt: the replay stops there and returns the number of
+// such entries read (the caller then searches level 0 again and counts it in
+// the `replay_bad` statistic, which the tests assert to be 0).
+__device__ __forceinline__ int level0_replay(CandLayout& C, const uint64_t* __restrict__ rlog,
+                                             int stop, int ef, int ntotal, int lane,
+                                             int nearest, float d_nearest) {
     C.init(0);
     C.seed(hkey(d_nearest, nearest), lane);
     int dummy = 0;
     for (int base = 0; base < stop; base += 64) {
         const uint64_t e = base + lane < stop ? rlog[base + lane] : RLOG_POP;
         const int cnt = stop - base < 64 ? (int)(stop - base) : 64;
+        // an entry is a pop marker or a key naming a node of the graph
+        const bool bad = base + lane < stop && e != RLOG_POP &&
+                         (uint32_t)hkey_id(e) >= (uint32_t)ntotal;
+        const unsigned long long badm = __ballot(bad);
+        if (badm) return __popcll(badm);
         for (int i = 0; i < cnt; i++) {
             const uint64_t v = rdlane64(e, i);
             if (v == RLOG_POP) {
                 int32_t v0;
                 int nb;
                 C.pop_min(lane, v0, nb);
-            } else if ((uint32_t)hkey_id(v) < (uint32_t)ntotal) {  // (a key names a node)
+            } else {
                 C.push(ef, v, hkey_dis(v), dummy, lane);
             }
         }
     }
+    return 0;
 }
 
 // The reference's HNSW::search for ef, k <= 64, one wave per query: the
@@ -1424,9 +1436,11 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
                                                        const uint32_t* __restrict__ only,
                                                        const uint32_t* __restrict__ qidx, int layout,
                                                        unsigned long long* __restrict__ trace,
-                                                       uint64_t* __restrict__ rlog) {
+                                                       uint64_t* __restrict__ rlog, int rcap) {
     // qidx: compact launch over listed queries (input row qidx[b], output
-    // row b); else query b, output row b
+    // row b); else query b, output row b.  rcap: entries of the replay log a
+    // query may use (<= RLOG_CAP for rlog, <= RLOG_LDS in the LDS; smaller in
+    // tests, to force the overflow path)
     const int64_t q = qidx ? (int64_t)qidx[blockIdx.x] : (int64_t)blockIdx.x;
     const int64_t qo = blockIdx.x;
     if (only && only[q] == 0u) return;
@@ -1496,7 +1510,7 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
         const uint32_t up_ndis = st_ndis, up_nhops = st_nhops;
         // the replay log: in the LDS after the visited bitmap (LOGLDS), else
         // this query's slice of rlog
-        const int logcap = LOGLDS ? RLOG_LDS : RLOG_CAP;
+        const int logcap = LOGLDS ? min(rcap, RLOG_LDS) : min(rcap, RLOG_CAP);
         uint64_t* qlog = LOGLDS ? (uint64_t*)((char*)sm + exact_reg_head(g) +
                                               ((4 * vwords + 7) & ~(int64_t)7))
                                 : (rlog ? rlog + (int64_t)blockIdx.x * RLOG_CAP : nullptr);
@@ -1512,11 +1526,17 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
         if (!done) {
             CandLayout C;
             if (TRACE) tr.t[8] = 1;
+            int how = 1;  // 0: replayed, 1: log overflowed or absent, 2: log corrupt
             if (!layout && qlog && S.logpos <= logcap) {
                 // continue from the stopping point with the replayed heap
-                level0_replay(C, qlog, S.stop, ef, g.ntotal, lane, nearest, d_nearest);
+                how = level0_replay(C, qlog, S.stop, ef, g.ntotal, lane, nearest, d_nearest)
+                              ? 2
+                              : 0;
                 if (TRACE) tr.t[9] = (unsigned long long)S.stop;
-            } else {
+            }
+            if (stats && lane == 0 && !layout)
+                atomicAdd(&stats[6 + how], 1ull);
+            if (how != 0) {
                 // again from the start: fresh visited table, results, counters
                 __syncthreads();
                 for (int64_t w = lane; w < vwords; w += 64) vis[w] = 0u;
@@ -1563,7 +1583,7 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
                               uint32_t* visited_scratch, int64_t vwords,
                               unsigned long long* stats, const uint32_t* only,
                               const uint32_t* qidx, hipStream_t s, float* gheap = nullptr,
-                              uint64_t* rlog = nullptr) {
+                              uint64_t* rlog = nullptr, int rcap = 0) {
     const int ef = efSearch > k ? efSearch : k;
     const size_t lds_q = sizeof(float) * g.ld;
     const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
@@ -1611,7 +1631,7 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
                                        : k_hnsw_exact_reg<true, true, false, false>);
             kt<<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4 + lds_logx, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
-                    layout, tb, rlog);
+                    layout, tb, rlog, rcap);
             HIP_LAUNCH_CHECK();
             std::vector<unsigned long long> h((size_t)n * 16);
             HIP_CHECK(hipMemcpyAsync(h.data(), tb, 128 * n, hipMemcpyDeviceToHost, s));
@@ -1630,7 +1650,7 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
                                    : k_hnsw_exact_reg<false, false, false, false>);
         kr<<<dim3((unsigned)n), dim3(64), rvis ? lds_r + vwords * 4 + lds_logx : lds_r, s>>>(
                 g, x, ldx, n, k, efSearch, ef, D, I, I32, rvis ? nullptr : visited_scratch, vwords,
-                stats, only, qidx, layout, nullptr, rlog);
+                stats, only, qidx, layout, nullptr, rlog, rcap);
         HIP_LAUNCH_CHECK();
         return;
     }
@@ -1679,6 +1699,25 @@ size_t hnsw_heap_scratch_words(int k, int efSearch, int ld) {
     const size_t lds_x = sizeof(float) * (size_t)ld + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 32;
     return lds_x > 64 * 1024 ? 2 * (size_t)ef + 2 * (size_t)k : 0;
 }
+bool hnsw_visited_scratch_needed(int ld, int k, int efSearch, int64_t vwords) {
+    // mirrors the LDS choices of the three kernels: any query may reach the
+    // sequential kernel (ties of the batched one), the register kernel keeps
+    // its own head (exact_reg_head) before the bitmap
+    constexpr size_t kL = 64 * 1024;
+    const int ef = efSearch > k ? efSearch : k;
+    const size_t vb = 4 * (size_t)std::max<int64_t>(vwords, 0);
+    const size_t lds_q = sizeof(float) * (size_t)ld;
+    const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
+    const size_t lds_xg = lds_x > kL ? lds_q + 8 * 64 + 4 * 8 : lds_x;
+    bool need = lds_xg + vb > kL;
+    if (ef <= 64 && k <= 64 && lds_x <= kL) {
+        HNSWDevice g{};
+        g.ld = ld;
+        need = need || (size_t)exact_reg_head(g) + vb > kL;
+    }
+    if (hnsw_uses_batched(k, efSearch)) need = need || lds_q + vb > kL;
+    return need;
+}
 bool hnsw_register_eligible(int k, int efSearch) {
     const int ef = efSearch > k ? efSearch : k;
     return ef <= 64 && k <= 64;
@@ -1705,18 +1744,17 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
     const bool batched = hnsw_uses_batched(k, efSearch);
     // sequential kernel: query | ef heap | k heap | 64 fresh | 8 scalars | visited
     // (heaps in global scratch when they do not fit)
-    const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
-    const size_t lds_xg = lds_x > 64 * 1024 ? lds_q + 8 * 64 + 4 * 8 : lds_x;
-    const bool x_lds_vis = lds_xg + vwords * 4 <= 64 * 1024;
-    const bool lds_vis = vwords * 4 <= 64 * 1024;
-    if (!lds_vis || !x_lds_vis) {
+    // the batched kernel: query | visited in the LDS when both fit
+    const bool lds_vis = lds_q + (size_t)vwords * 4 <= 64 * 1024;
+    if (hnsw_visited_scratch_needed(g.ld, k, efSearch, vwords)) {
         FAISS_THROW_IF_NOT(visited_scratch != nullptr);
         HIP_CHECK(hipMemsetAsync(visited_scratch, 0, sizeof(uint32_t) * vwords * n, s));
     }
     auto exact = [&](const uint32_t* only) {
         ScopedKernelTimer tm(kt, "hnsw_exact", 0.0, s);
         hnsw_exact_launch(g, x, ldx, n, k, efSearch, D, I, I32, visited_scratch, vwords, stats,
-                          only, nullptr, s, heap_scratch, replay_cap == kHnswReplayCap ? replay_log : nullptr);
+                          only, nullptr, s, heap_scratch, replay_cap > 0 ? replay_log : nullptr,
+                          (int)std::min<int64_t>(replay_cap, kHnswReplayCap));
     };
     // FAISS_AMD_HNSW_EXACT=1: every query through the sequential kernel (tests)
     const char* xenv = getenv("FAISS_AMD_HNSW_EXACT");

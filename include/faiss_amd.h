@@ -146,6 +146,10 @@ extern HNSWStats hnsw_stats;
 // counts the distances as the reference does).  Reset with hnsw_stats.
 struct HNSWRowStats {
     uint64_t fp32_rows = 0, q8_rows = 0;
+    // the register kernel's queries that met a layout-dependent decision:
+    // continued from the replayed log / searched level 0 again (log
+    // overflowed) / log found corrupt and searched again (0 unless a bug)
+    uint64_t replayed = 0, searched_again = 0, replay_bad = 0;
 };
 extern HNSWRowStats hnsw_row_stats;
 
@@ -207,9 +211,11 @@ struct Index {
     virtual void sync_device() const {}
     // fold device-side search counters (HNSWStats) into the host globals
     virtual void fold_device_stats() const {}
-    // bumped by every add / reset of the index's content (copies made of it,
-    // e.g. IndexShardsIVF's per-rank quantizers, are rebuilt when it moves)
-    virtual uint64_t content_version() const { return version_; }
+    // bumped by every add / reset of the index's content and by every upload
+    // of changed content to HBM (copies made of it, e.g. IndexShardsIVF's
+    // per-rank quantizers, and captured search graphs are rebuilt when it
+    // moves); atomic: searches on other threads read it without the lock
+    virtual uint64_t content_version() const { return version_.load(); }
 
     hipStream_t stream() const;
     int ld() const { return (int)roundup((size_t)d, 4); }
@@ -219,7 +225,7 @@ struct Index {
     // calls (one host call at a time per index)
     mutable std::mutex host_mu_;
     mutable DeviceBuffer h_x_, h_d_, h_i_;
-    uint64_t version_ = 0;
+    mutable std::atomic<uint64_t> version_{0};
 };
 
 // ---------------------------------------------------------------- flat
@@ -254,6 +260,11 @@ struct IndexFlat : Index {
                              idx_t batch_n) const override;
     // bytes of the query image assign_device_qimg writes for n queries
     size_t query_image_size(idx_t n) const;
+    // device order of this quantizer's scratch for work queued on `stream`
+    // outside its own entry points (a replayed IVF search graph that writes
+    // the quantizer's scratch): enter before queuing, leave after
+    void stream_enter(hipStream_t stream) const;
+    void stream_leave(hipStream_t stream) const;
 
    private:
     template <class OutIdx>
@@ -317,7 +328,7 @@ struct IndexHNSW : Index {
     void sync_device() const override;
     void fold_device_stats() const override;
     uint64_t content_version() const override {
-        return version_ + (storage ? storage->content_version() : 0);
+        return version_.load() + (storage ? storage->content_version() : 0);
     }
     // faiss/IndexHNSW.cpp:345-366: search with per-query latency statistics
     // (quantization_us = 0, list_scan_us = total_us, like the reference)

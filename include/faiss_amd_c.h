@@ -337,6 +337,12 @@ void faiss_amd_HNSWStats_reset(void);
  * HNSW kernels read — fp32 rows, and int8-image rows of the register kernel's
  * level-0 prefilter — since the last faiss_amd_HNSWStats_reset. */
 void faiss_amd_get_hnsw_row_stats(uint64_t* fp32_rows, uint64_t* q8_rows);
+/* Not in the reference (diagnostic): queries of the register HNSW kernel that
+ * met a layout-dependent decision and continued from the replayed update log,
+ * that searched level 0 again because their log overflowed, and whose log was
+ * found corrupt (searched again; must stay 0) — since the last reset. */
+void faiss_amd_get_hnsw_replay_stats(uint64_t* replayed, uint64_t* searched_again,
+                                     uint64_t* replay_bad);
 int faiss_amd_fold_device_stats(const FaissIndex* index);
 /* graph export for tests: levels[ntotal], offsets[ntotal+1], neighbors[],
  * cum_nneighbor_per_level[]; pass NULL to query sizes only */

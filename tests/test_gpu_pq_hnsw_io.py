@@ -229,3 +229,45 @@ def test_hnsw_register_kernel_forms_equal_reference(amd, orc, gpu, monkeypatch, 
         for q8, rp in (("1", "1"), ("0", "1"), ("1", "0")):
             D, I = out[(q8, rp, ef, k)]
             assert_same_results(D, I, Dr, Ir)
+
+
+@pytest.mark.parametrize("d", [37, 128])
+def test_hnsw_replay_log_overflow_and_lds_log(amd, orc, gpu, monkeypatch, d):
+    """The register kernel's layout-dependent continuations on the
+    duplicate-heavy graph: the replay log in HBM (default), in the LDS
+    (FAISS_AMD_HNSW_LOG=lds) and both with a 16-entry capacity
+    (FAISS_AMD_HNSW_REPLAY_CAP=16), so queries overflow it and search level 0
+    again.  Every form gives the reference's results; the counters show each
+    continuation was taken, and no replayed log entry ever named a non-node
+    (replay_bad == 0: a corrupt log is counted, never silently skipped)."""
+    nb = 5000
+    xb = rand(orc, nb, d, 61)
+    xb[1000:1150] = xb[:150]
+    xb[3000:3040] = xb[:40]
+    xq = np.concatenate([rand(orc, 300, d, 62), xb[:60]])
+    cases = [(16, 10), (64, 64), (40, 5)]
+    h = amd.IndexHNSWFlat(d, 16)
+    h.add(xb)
+    g = orc.HNSWGraph.from_index(h)
+    forms = [(None, None), ("lds", None), (None, "16"), ("lds", "16")]
+    seen = {}
+    for log, cap in forms:
+        for var, val in (("FAISS_AMD_HNSW_LOG", log), ("FAISS_AMD_HNSW_REPLAY_CAP", cap)):
+            if val is None:
+                monkeypatch.delenv(var, raising=False)
+            else:
+                monkeypatch.setenv(var, val)
+        amd.cvar.hnsw_stats.reset()
+        for ef, k in cases:
+            h.efSearch = ef
+            D, I = h.search(xq, k)
+            Dr, Ir = g.search(xq, k, ef)
+            assert_same_results(D, I, Dr, Ir)
+        seen[(log, cap)] = amd.cvar.hnsw_replay_stats
+    for form, (replayed, again, bad) in seen.items():
+        assert bad == 0, (form, seen)
+    # the default log replays every continuation; a 16-entry log overflows
+    assert seen[(None, None)][0] > 0 and seen[(None, None)][1] == 0, seen
+    assert seen[(None, "16")][1] > 0, seen
+    assert seen[("lds", "16")][1] > 0, seen
+    assert sum(seen[(None, None)][:2]) == sum(seen[(None, "16")][:2]), seen

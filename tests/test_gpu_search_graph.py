@@ -98,3 +98,75 @@ def test_graph_replay_equals_eager(amd, gpu, monkeypatch, desc):
         np.testing.assert_array_equal(Ik, refa[1][:, :5])
     finally:
         b.close()
+
+
+def test_graph_replay_new_queries_same_buffer(amd, orc, gpu, monkeypatch):
+    """The serving loop the graph is for rewrites its input buffer between
+    calls: c2's geometry (IVF4096,Flat, 1M vectors, nprobe 32, 10k queries),
+    three different query sets written into the same device buffer, each
+    searched by a replay of the graph captured on the first set.  Every
+    replay equals the eager search of its own queries bit for bit, and a
+    subset of each set equals the oracle."""
+    d, nb, nq, k = 128, 1_000_000, 10_000, 10
+    xb = amd.float_rand(nb * d, 1234).reshape(nb, d)
+    idx = amd.index_factory(d, "IVF4096,Flat")
+    idx.train(xb[:200_000])
+    idx.add(xb)
+    idx.nprobe = 32
+    sets = [amd.float_rand(nq * d, seed).reshape(nq, d) for seed in (5678, 91, 4242)]
+    b = Bufs(sets[0], k)
+    ref = orc.IVFOracle.from_index(idx)
+    rows = np.arange(0, nq, 25)
+    try:
+        eager = []
+        monkeypatch.setenv("FAISS_AMD_GRAPH", "0")
+        for xq in sets:
+            b.hip.hipMemcpy(b.px, xq.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(xq.nbytes), 1)
+            eager.append(b.search(idx))
+        monkeypatch.delenv("FAISS_AMD_GRAPH")
+        for rnd in range(2):
+            for i, xq in enumerate(sets):
+                b.hip.hipMemcpy(b.px, xq.ctypes.data_as(ctypes.c_void_p),
+                                ctypes.c_size_t(xq.nbytes), 1)
+                D, I = b.search(idx)  # round 0, set 0: eager, set 1: capture, then replays
+                np.testing.assert_array_equal(I, eager[i][1])
+                np.testing.assert_array_equal(D, eager[i][0])
+        for i, xq in enumerate(sets):
+            Dr, Ir, _, _ = ref.search(np.ascontiguousarray(xq[rows]), k, 32, nslices=1)
+            np.testing.assert_array_equal(eager[i][1][rows], Ir)
+            np.testing.assert_array_equal(eager[i][0][rows], Dr)
+        assert not np.array_equal(eager[0][1], eager[1][1])
+    finally:
+        b.close()
+
+
+def test_graph_retired_by_same_size_content_change(amd, gpu, monkeypatch):
+    """A reset + add of the same number of different vectors, synchronised by
+    a host search(), leaves ntotal and the buffers unchanged; the next
+    search_device must still not replay the graph captured on the old
+    content (the upload bumps the index's content version)."""
+    d, nb, nq, k = 64, 20_000, 500, 10
+    xa = amd.float_rand(nb * d, 11).reshape(nb, d)
+    xb = amd.float_rand(nb * d, 12).reshape(nb, d)
+    idx = amd.index_factory(d, "IVF64,Flat")
+    idx.train(xa)
+    idx.add(xa)
+    idx.nprobe = 8
+    xq = amd.float_rand(nq * d, 13).reshape(nq, d)
+    b = Bufs(xq, k)
+    try:
+        for _ in range(3):  # eager, capture, replay
+            old = b.search(idx)
+        idx.reset()
+        idx.add(xb)
+        idx.search(xq[:50], k)  # host entry point: uploads, clears the dirty flag
+        monkeypatch.setenv("FAISS_AMD_GRAPH", "0")
+        ref = b.search(idx)
+        monkeypatch.delenv("FAISS_AMD_GRAPH")
+        assert not np.array_equal(ref[1], old[1])
+        for _ in range(3):
+            D, I = b.search(idx)
+            np.testing.assert_array_equal(I, ref[1])
+            np.testing.assert_array_equal(D, ref[0])
+    finally:
+        b.close()
