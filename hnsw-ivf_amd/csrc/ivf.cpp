@@ -1048,7 +1048,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     if (env && !strcmp(env, "exact")) mode = 1;
     if (env && !strcmp(env, "mfma")) mode = 0;
     const int KQ = obits_ <= 14 ? kern::ivf_mfma_kq((int)k, d, np) : 0;
-    if (mode != 0 || KQ <= 0 || np > kern::kMaxK || store_pairs || dup_probes_) {
+    if (mode != 0 || KQ <= 0 || np > kern::kMaxNprobeFilter || store_pairs || dup_probes_) {
         exact_scan_device(n, x, ldx, k, np, assign, cdis, distances, labels, s, lim, sel,
                           store_pairs);
         return;

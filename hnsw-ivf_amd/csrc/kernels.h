@@ -20,6 +20,9 @@ namespace faiss_amd {
 namespace kern {
 
 constexpr int kMaxK = 64;  // largest k / nprobe served by the wave queues
+// largest nprobe of the list-centric MFMA filters + certified re-rank (one
+// probe record per lane up to 64, k_ivf_rerank_wide's 64-probe chunks beyond)
+constexpr int kMaxNprobeFilter = 2048;
 constexpr int kMaxKExact = 2048;  // largest k of the general exact path (faiss GPU's limit,
                                   // faiss/gpu/utils/DeviceDefs.cuh:28)
 

@@ -765,7 +765,7 @@ void pq_stream_image(const uint8_t* codes, int cs, int64_t rows, int d, int dsub
 // streamed kernel in its PQ form): coarse_dis, |y_C| per list, list maxima of
 // |y_R| and |y_R - bf16(y_R)|
 bool ivfpq_stream_eligible(int d, int M, int k, int nprobe) {
-    if (d % M != 0 || d > BDM || k > 32 || nprobe > 64) return false;
+    if (d % M != 0 || d > BDM || k > 32 || nprobe > kMaxNprobeFilter) return false;
     const int NS = bf3_db_host(d) / 2 * 2 / 16;
     return ivf_mfma_kq(k, d, nprobe) > 0 && (NS == 2 || NS == 4 || NS == 6 || NS == 8);
 }
@@ -1294,6 +1294,351 @@ __global__ __launch_bounds__(64 * RR_W, RR_WAVES) void k_ivf_rerank(
     }
 }
 
+// ---------------------------------------------------------------- B, wide
+// The re-rank for nprobe > 64 (the reference harness's grid reaches nprobe
+// 2048: tutorial/cpp/benchmark-hnsw-ivf/benchmark.config nprobe_ratio up to
+// 0.128 of nlist).  One wave per query walks its probes in chunks of 64, lane
+// r holding probe 64 c + r with its KE keys, and certifies exactly as
+// k_ivf_rerank does:
+//   T = the k-th smallest probe minimum of ub' (a running k-smallest set
+//       merged chunk by chunk) — k probes hold a value <= T, so T >= U;
+//   U = the k-th smallest ub' among the values <= T (at most (k + ties) KE of
+//       them: only probes whose minimum is <= T hold any), or T when they do
+//       not fit the LDS;
+//   candidates = kept entries with lb' <= U of the streams whose dropped bound
+//       is > U, and every row of the streams whose dropped bound is <= U.
+// The exact top-k over the candidates (arrival order = probe rank, then
+// arena row) is the reference result.  Each stage re-reads the query's keys
+// and records (L2-resident: 16 + 32 B per probe at KE = 4).
+constexpr int RRW_CB = 1024;  // values <= T ranked exactly (LDS)
+
+template <bool L2, int KE, int PQD>
+struct WideStream {
+    const uint32_t* surv;    // candidates' arena rows (LDS)
+    const uint16_t* sprobe;  // their probe rank
+    int nsv;
+    bool overflow;           // the candidate list did not fit: re-walk the probes
+    const uint32_t* kq;      // this query's keys [nprobe][KE]
+    const ProbeRec* rq;      // its probe records [nprobe]
+    const float* cdq;        // PQ table 1: its coarse distances [nprobe]
+    const int64_t* ids;
+    const float* xq;
+    const float* codes;
+    const float* xs;
+    int ldc, d, lane, nprobe;
+    uint32_t lowmask;
+    float U;
+    PQArgs pa;
+    const uint8_t* sel;
+    bool fold;
+    static constexpr int KT = KE / 4;
+
+    __device__ __forceinline__ void emit(bool ok, uint32_t grow, int r, float& k1, long long& k2,
+                                         int nv = -1) const {
+        const long long idv = ok ? (long long)ids[grow] : 0ll;
+        float dis;
+        if constexpr (PQD > 0) {
+            const uint32_t l = ok ? rq[r].pad : 0u;
+            const float d0 = ok && pa.table1 ? cdq[r] : 0.f;
+            dis = ok ? pq_exact<PQD>(pa, xs, grow, l, d0) : 0.f;
+        } else {
+            if (nv >= 0)
+                dis = ref_rows64_4lane_pb<L2, RR_XM, RR_PB>(xs, xq, codes, ldc, d, grow, nv, lane);
+            else
+                dis = eval_rows64_direct<L2>(xs, xq, codes, ldc, d, grow, ok, lane);
+        }
+        k1 = WS_INF;
+        k2 = WS_NOID;
+        if (ok) to_key(L2 ? 1 : 0, dis, idv, k1, k2);
+    }
+    __device__ __forceinline__ void load_keys(int p, bool has, uint32_t (&kv)[KE]) const {
+#pragma unroll
+        for (int i = 0; i < KE; i += 4) {
+            const uint4 v4 = has ? *(const uint4*)(kq + (int64_t)p * KE + i)
+                                 : make_uint4(~0u, ~0u, ~0u, ~0u);
+            kv[i] = v4.x;
+            kv[i + 1] = v4.y;
+            kv[i + 2] = v4.z;
+            kv[i + 3] = v4.w;
+        }
+    }
+    __device__ __forceinline__ uint32_t fail_bits(const ProbeRec& pr) const {
+        uint32_t f = 0u;
+#pragma unroll
+        for (int sl = 0; sl < 4; sl++) f |= (pr.pb[sl] < WS_INF && pr.pb[sl] <= U) ? (1u << sl) : 0u;
+        return f;
+    }
+    template <class F>
+    __device__ __forceinline__ void for_each(F f) const {
+        if (!overflow) {
+            for (int s0 = 0; s0 < nsv; s0 += 64) {
+                const bool ok = s0 + lane < nsv;
+                const uint32_t grow = ok ? surv[s0 + lane] : 0u;
+                const int rp = ok ? (int)sprobe[s0 + lane] : 0;
+                const long long rank = ok ? (((long long)rp << 32) | grow) : 0;
+                float k1;
+                long long k2;
+                emit(ok, grow, rp, k1, k2, min(64, nsv - s0));
+                f(ok && key_admissible(k1), k1, k2, rank);
+            }
+            return;
+        }
+        for (int c0 = 0; c0 < nprobe; c0 += 64) {
+            const int p = c0 + lane;
+            const bool has = p < nprobe;
+            ProbeRec pr;
+            if (has) pr = rq[p];
+            uint32_t kv[KE];
+            load_keys(p, has, kv);
+            const uint32_t fl = has ? fail_bits(pr) : 0u;
+#pragma unroll
+            for (int i = 0; i < KE; i++) {
+                const int sl = i / KT;
+                bool ok = false;
+                uint32_t grow = 0u;
+                if (has && kv[i] != 0xffffffffu && !((fl >> sl) & 1u)) {
+                    ok = ivf_decode_lo<L2>(kv[i], lowmask, fold) - pr.mmax <= U;
+                    grow = pr.off + ivf_key_row(kv[i], lowmask, sl);
+                }
+                if (__ballot(ok) == 0ull) continue;
+                float k1;
+                long long k2;
+                emit(ok, grow, p, k1, k2);
+                f(ok && key_admissible(k1), k1, k2, ((long long)p << 32) | grow);
+            }
+            unsigned long long m = __ballot(fl != 0u);
+            while (m) {
+                const int r = __ffsll((long long)m) - 1;
+                m &= m - 1ull;
+                const uint32_t o = __shfl(has ? pr.off : 0u, r), len = __shfl(has ? pr.len : 0u, r);
+                const uint32_t flr = __shfl(fl, r);
+                const int ne = (int)cdiv_dev(len, BV) * 16;
+                for (int sl = 0; sl < 4; sl++) {
+                    if (!((flr >> sl) & 1u)) continue;
+                    for (int e0 = 0; e0 < ne; e0 += 64) {
+                        const int row = ivf_stream_row(e0 + lane, sl);
+                        const bool ok = e0 + lane < ne && row < (int)len && (!sel || sel[o + row]);
+                        const uint32_t grow = o + (uint32_t)(ok ? row : 0);
+                        float k1;
+                        long long k2;
+                        emit(ok, grow, c0 + r, k1, k2);
+                        f(ok && key_admissible(k1), k1, k2, ((long long)(c0 + r) << 32) | grow);
+                    }
+                }
+            }
+        }
+    }
+};
+
+template <bool L2, int KE, int PQD = 0>
+__global__ __launch_bounds__(64, RR_WAVES) void k_ivf_rerank_wide(
+        const uint32_t* __restrict__ keys, const ProbeRec* __restrict__ recs,
+        const float* __restrict__ x, int ldx, const float* __restrict__ codes, int ldc,
+        const int64_t* __restrict__ ids, int d, int64_t n, int nprobe, int obits, int k,
+        float* __restrict__ D, int64_t* __restrict__ I, uint32_t* __restrict__ stats, PQArgs pa,
+        const uint8_t* __restrict__ sel, unsigned long long* __restrict__ qdone, int fold_keys) {
+    constexpr int KT = KE / 4;
+    const bool fold = fold_keys != 0;
+    __shared__ uint32_t surv[RR_CAP];
+    __shared__ uint16_t sprobe[RR_CAP];
+    __shared__ __attribute__((aligned(16))) float xsh[BDM];
+    __shared__ __attribute__((aligned(16))) float stg[64 * 4 * 3];
+    __shared__ float cb[RRW_CB];
+    const int lane = threadIdx.x;
+    const int64_t q = blockIdx.x;
+    if (q >= n) return;  // (one wave per block: the whole block leaves)
+    const uint32_t lowmask = (1u << obits) - 1u;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    WideStream<L2, KE, PQD> st;
+    st.kq = keys + q * (int64_t)nprobe * KE;
+    st.rq = recs + q * (int64_t)nprobe;
+    st.cdq = pa.cdis ? pa.cdis + q * (int64_t)nprobe : nullptr;
+    st.ids = ids;
+    st.xq = x + q * ldx;
+    st.codes = codes;
+    st.xs = xsh;
+    st.ldc = ldc;
+    st.d = d;
+    st.lane = lane;
+    st.nprobe = nprobe;
+    st.lowmask = lowmask;
+    st.pa = pa;
+    st.sel = sel;
+    st.fold = fold;
+    st.U = WS_INF;
+    if (lane < BDM / 4 && 4 * lane < (d & ~3))
+        *(float4*)(&xsh[4 * lane]) = *(const float4*)(st.xq + 4 * lane);
+    // ---- T: running set of the k smallest probe minima (lanes < k)
+    float rv = WS_INF, T = WS_INF;
+    for (int c0 = 0; c0 < nprobe; c0 += 64) {
+        const int p = c0 + lane;
+        const bool has = p < nprobe;
+        const float mm = has ? st.rq[p].mmax : 0.f;
+        uint32_t kv[KE];
+        st.load_keys(p, has, kv);
+        float pm = WS_INF;
+#pragma unroll
+        for (int i = 0; i < KE; i++)
+            if (kv[i] != 0xffffffffu) pm = fminf(pm, ivf_decode_hi<L2>(kv[i], lowmask, fold) + mm);
+        const float mv[2] = {rv, pm};
+        const float t = wave_kth_smallest<2>(mv, k);
+        // the new set: the values < t (fewer than k), then t up to k
+        const bool a = rv < t, b = pm < t;
+        const unsigned long long ma = __ballot(a), mb = __ballot(b);
+        if (a) cb[__popcll(ma & lt)] = rv;
+        if (b) cb[__popcll(ma) + __popcll(mb & lt)] = pm;
+        __syncthreads();
+        const int cnt = __popcll(ma) + __popcll(mb);
+        rv = lane < cnt ? cb[lane] : (lane < k ? t : WS_INF);
+        __syncthreads();
+        T = t;
+    }
+    if (!(T <= WS_INF)) T = WS_INF;  // NaN guard
+    // ---- U: the k-th smallest ub' among the values <= T
+    float U = T;
+    if (T < WS_INF) {
+        int cnt = 0;
+        for (int c0 = 0; c0 < nprobe; c0 += 64) {
+            const int p = c0 + lane;
+            const bool has = p < nprobe;
+            const float mm = has ? st.rq[p].mmax : 0.f;
+            uint32_t kv[KE];
+            st.load_keys(p, has, kv);
+#pragma unroll
+            for (int i = 0; i < KE; i++) {
+                const float ub = kv[i] != 0xffffffffu ? ivf_decode_hi<L2>(kv[i], lowmask, fold) + mm
+                                                      : WS_INF;
+                const bool in = ub <= T;
+                const unsigned long long m = __ballot(in);
+                const int pos = cnt + __popcll(m & lt);
+                if (in && pos < RRW_CB) cb[pos] = ub;
+                cnt += __popcll(m);
+            }
+        }
+        __syncthreads();
+        if (cnt <= RRW_CB) {
+            float v[RRW_CB / 64];
+#pragma unroll
+            for (int i = 0; i < RRW_CB / 64; i++)
+                v[i] = 64 * i + lane < cnt ? cb[64 * i + lane] : WS_INF;
+            U = wave_kth_smallest<RRW_CB / 64>(v, k);
+        }
+        __syncthreads();
+    }
+    st.U = U;
+    // ---- candidates -> LDS: kept entries under U of the streams that did not
+    // fail, then every row of the failing streams
+    int ns = 0, nfail = 0, nkept = 0;
+    for (int c0 = 0; c0 < nprobe; c0 += 64) {
+        const int p = c0 + lane;
+        const bool has = p < nprobe;
+        ProbeRec pr;
+        if (has) pr = st.rq[p];
+        uint32_t kv[KE];
+        st.load_keys(p, has, kv);
+        const uint32_t fl = has ? st.fail_bits(pr) : 0u;
+#pragma unroll
+        for (int i = 0; i < KE; i++) {
+            const int sl = i / KT;
+            bool sv = false;
+            uint32_t grow = 0u;
+            if (has && kv[i] != 0xffffffffu && !((fl >> sl) & 1u)) {
+                sv = ivf_decode_lo<L2>(kv[i], lowmask, fold) - pr.mmax <= U;
+                grow = pr.off + ivf_key_row(kv[i], lowmask, sl);
+            }
+            const unsigned long long m = __ballot(sv);
+            const int pos = ns + __popcll(m & lt);
+            if (sv && pos < RR_CAP) {
+                surv[pos] = grow;
+                sprobe[pos] = (uint16_t)p;
+            }
+            ns += __popcll(m);
+        }
+        nkept = ns;
+        unsigned long long m = __ballot(fl != 0u);
+        nfail += __popcll(m);
+        while (m) {
+            const int r = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const uint32_t o = __shfl(has ? pr.off : 0u, r), len = __shfl(has ? pr.len : 0u, r);
+            const uint32_t flr = __shfl(fl, r);
+            const int ne = (int)cdiv_dev(len, BV) * 16;
+            for (int sl = 0; sl < 4; sl++) {
+                if (!((flr >> sl) & 1u)) continue;
+                for (int e0 = 0; e0 < ne; e0 += 64) {
+                    const int row = ivf_stream_row(e0 + lane, sl);
+                    const bool in = e0 + lane < ne && row < (int)len && (!sel || sel[o + row]);
+                    const unsigned long long bm = __ballot(in);
+                    const int pos = ns + __popcll(bm & lt);
+                    if (in && pos < RR_CAP) {
+                        surv[pos] = o + (uint32_t)row;
+                        sprobe[pos] = (uint16_t)(c0 + r);
+                    }
+                    ns += __popcll(bm);
+                }
+            }
+        }
+    }
+    __syncthreads();  // the LDS query copy and candidate list
+    st.surv = surv;
+    st.sprobe = sprobe;
+    st.nsv = ns;
+    st.overflow = ns > RR_CAP;
+    // ---- exact top-k: up to 4 batches ranked directly, else the general resolve
+    bool done = false;
+    auto small = [&](auto nbc) {
+        constexpr int NB = decltype(nbc)::value;
+        float k1[NB];
+        long long k2[NB];
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const bool ok = 64 * b + lane < ns;
+            st.emit(ok, ok ? surv[64 * b + lane] : 0u, ok ? (int)sprobe[64 * b + lane] : 0, k1[b],
+                    k2[b], max(0, min(64, ns - 64 * b)));
+            if (!(ok && key_admissible(k1[b]))) {
+                k1[b] = WS_INF;
+                k2[b] = WS_NOID;
+            }
+        }
+        if constexpr (NB > 1) {
+            float* ck1 = stg;
+            long long* ck2 = reinterpret_cast<long long*>(stg + 64 * NB);
+            int m = 0;
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                const bool in = 64 * b + lane < ns && k1[b] < WS_INF && k1[b] <= U;
+                const unsigned long long bm = __ballot(in);
+                const int pos = m + __popcll(bm & lt);
+                if (in) {
+                    ck1[pos] = k1[b];
+                    ck2[pos] = k2[b];
+                }
+                m += __popcll(bm);
+            }
+            if (m <= 64) {
+                __syncthreads();
+                float c1[1] = {lane < m ? ck1[lane] : WS_INF};
+                long long c2[1] = {lane < m ? ck2[lane] : WS_NOID};
+                __syncthreads();
+                return exact_topk_small<1>(c1, c2, m, k, L2 ? 1 : 0, lane, true, D + q * k,
+                                           I + q * k);
+            }
+        }
+        return exact_topk_small<NB>(k1, k2, ns, k, L2 ? 1 : 0, lane, true, D + q * k, I + q * k);
+    };
+    if (ns <= 64) done = small(std::integral_constant<int, 1>());
+    else if (ns <= 128) done = small(std::integral_constant<int, 2>());
+    else if (ns <= 256) done = small(std::integral_constant<int, 4>());
+    if (!done) exact_topk_resolve(st, k, L2 ? 1 : 0, lane, true, D + q * k, I + q * k);
+    if (stats && lane == 0) {
+        atomicAdd(&stats[0], (uint32_t)min(nkept, RR_CAP));
+        atomicAdd(&stats[1], (uint32_t)nfail);
+        atomicAdd(&stats[2], st.overflow ? 1u : 0u);
+        atomicAdd(&stats[3], done ? 0u : 1u);
+    }
+    if (qdone && lane == 0) qdone[q] = __builtin_amdgcn_s_memrealtime();
+}
+
 // ---------------------------------------------------------------- host
 void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* list_len,
                     int nlist, float* out, hipStream_t s) {
@@ -1397,7 +1742,7 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
     const int KE = ivf_mfma_kq(k, d, nprobe);
     FAISS_THROW_IF_NOT(KE > 0);
     FAISS_THROW_IF_NOT(ldc % 4 == 0);
-    FAISS_THROW_IF_NOT(nprobe <= 64);
+    FAISS_THROW_IF_NOT(nprobe <= kMaxNprobeFilter);
     FAISS_THROW_IF_NOT(obits >= 4 && obits <= 14);
     const int NS = bf3_db(d) / 16;
     const int64_t grid = (int64_t)roundup((size_t)max_items, 32);
@@ -1553,9 +1898,24 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         else if (V == 16) LAUNCH_B(L2V, 16); \
         else LAUNCH_B(L2V, 32);              \
     } while (0)
-        if (l2) DISPATCH_V(true);
+#define LAUNCH_W(L2V, KEV)                                                                     \
+    k_ivf_rerank_wide<L2V, KEV><<<dim3((unsigned)n), dim3(64), 0, s>>>(                          \
+            keys, recs, x, ldx, codes, ldc, ids, d, n, nprobe, obits, k, D, I, stats, PQArgs{},  \
+            b.sel, qdone, fk ? 1 : 0)
+#define DISPATCH_W(L2V)                      \
+    do {                                     \
+        if (KE == 8) LAUNCH_W(L2V, 8);       \
+        else if (KE == 16) LAUNCH_W(L2V, 16); \
+        else LAUNCH_W(L2V, 32);              \
+    } while (0)
+        if (nprobe > 64) {  // probes walked in chunks of 64 (k_ivf_rerank_wide)
+            if (l2) DISPATCH_W(true);
+            else DISPATCH_W(false);
+        } else if (l2) DISPATCH_V(true);
         else DISPATCH_V(false);
         HIP_LAUNCH_CHECK();
+#undef DISPATCH_W
+#undef LAUNCH_W
         if (trace) {
             std::vector<unsigned long long> h(8 * n);
             HIP_CHECK(hipMemcpyAsync(h.data(), trace, 64 * n, hipMemcpyDeviceToHost, s));
@@ -1596,11 +1956,29 @@ void ivfpq_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, in
         else if (V == 16) LAUNCH_P(16, DS);  \
         else LAUNCH_P(32, DS);               \
     } while (0)
-    if (dsub == 2) DISPATCH_P(2);
+#define LAUNCH_PW(KEV, DS)                                                                     \
+    k_ivf_rerank_wide<true, KEV, DS><<<dim3((unsigned)n), dim3(64), 0, s>>>(                     \
+            keys, recs, x, ldx, nullptr, 0, ids, d, n, nprobe, obits, k, D, I, stats, pa, sel,  \
+            qdone, fold)
+#define DISPATCH_PW(DS)                       \
+    do {                                      \
+        if (KE == 8) LAUNCH_PW(8, DS);        \
+        else if (KE == 16) LAUNCH_PW(16, DS); \
+        else LAUNCH_PW(32, DS);               \
+    } while (0)
+    FAISS_THROW_IF_NOT(nprobe <= kMaxNprobeFilter);
+    FAISS_THROW_IF_NOT_MSG(dsub == 2 || dsub == 4 || dsub == 8,
+                           "ivfpq_rerank: dsub must be 2, 4 or 8");
+    if (nprobe > 64) {  // probes walked in chunks of 64 (k_ivf_rerank_wide)
+        if (dsub == 2) DISPATCH_PW(2);
+        else if (dsub == 4) DISPATCH_PW(4);
+        else DISPATCH_PW(8);
+    } else if (dsub == 2) DISPATCH_P(2);
     else if (dsub == 4) DISPATCH_P(4);
-    else if (dsub == 8) DISPATCH_P(8);
-    else FAISS_THROW_MSG("ivfpq_rerank: dsub must be 2, 4 or 8");
+    else DISPATCH_P(8);
     HIP_LAUNCH_CHECK();
+#undef DISPATCH_PW
+#undef LAUNCH_PW
 #undef DISPATCH_P
 #undef LAUNCH_P
 }

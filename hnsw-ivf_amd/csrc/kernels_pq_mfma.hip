@@ -539,7 +539,7 @@ __global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
 }
 
 bool ivfpq_mfma_eligible(int d, int M, int k, int nprobe) {
-    if (d % 16 != 0 || M <= 0 || d % M != 0 || k > 32 || nprobe > 64) return false;
+    if (d % 16 != 0 || M <= 0 || d % M != 0 || k > 32 || nprobe > kMaxNprobeFilter) return false;
     const int dsub = d / M, NS = d / 16;
     if (dsub != 2 && dsub != 4 && dsub != 8) return false;
     return NS == 4 || NS == 6 || NS == 8;

@@ -109,7 +109,7 @@ def harness_recall(I, gt, k):
 def run_harness(name, work, config_text):
     exe = os.path.join(HDIR, name)
     assert os.access(exe, os.X_OK), f"{exe} missing: built by __graft_entry__.build()"
-    run = work / "run"
+    run = work / f"run_{name}"  # (a sibling of ../sift, as the harness expects)
     run.mkdir(exist_ok=True)
     cfg = run / "bench.config"
     cfg.write_text(config_text)
