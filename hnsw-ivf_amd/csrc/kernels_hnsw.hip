@@ -386,73 +386,112 @@ __global__ __launch_bounds__(64) void k_hnsw_search(HNSWDevice g, const float* _
 // equal minima; count_below: every slot, dead ones included).  Used for
 // max(efSearch, k) > 128, k > 64, and the queries the batched kernel flags.
 namespace {
-// binary heaps on (float, int32) with CMax cmp2 (faiss/utils/Heap.h:47-149)
-__device__ __forceinline__ bool cmp2_gt(float a1, float b1, int32_t a2, int32_t b2) {
-    return a1 > b1 || (a1 == b1 && a2 > b2);
+// The heaps as faiss lays them out (1-based binary heaps, faiss/utils/Heap.h),
+// one 64-bit key per slot: the distance's bits (>= 0: they order as unsigned)
+// over the id biased by 2^31, so CMax's cmp2 (dis, then id) is one unsigned
+// compare; a MinimaxHeap slot killed by pop_min keeps its distance with id -1,
+// as faiss's does.  The code runs wave-uniform (every lane computes the same
+// serial steps; lane 0 stores), so the lanes can load a push's ancestors and a
+// sift's next three levels at once.
+__device__ __forceinline__ uint64_t sx_key(float d, int32_t id) {
+    return ((uint64_t)(uint32_t)__float_as_int(d) << 32) | (uint32_t)(id ^ (int32_t)0x80000000);
 }
-__device__ void hx_pop(int k, float* bv, int32_t* bi) {
-    bv--;
-    bi--;
-    const float val = bv[k];
-    const int32_t id = bi[k];
+__device__ __forceinline__ float sx_dis(uint64_t k) { return __int_as_float((int)(k >> 32)); }
+__device__ __forceinline__ int32_t sx_id(uint64_t k) { return (int32_t)((uint32_t)k ^ 0x80000000u); }
+__host__ __device__ inline int seq_qpad(int ld) { return ld < 128 ? 128 : ld; }
+// slots of a heap of capacity c (1-based, index 0 unused, sibling pairs
+// (2i, 2i + 1) 16-byte aligned and always inside the array)
+__host__ __device__ inline size_t seq_slots(int c) { return (size_t)((c + 2) & ~1); }
+__host__ __device__ inline size_t seq_heap_bytes(int ef, int k) {
+    return 8 * (seq_slots(ef) + seq_slots(k));
+}
+// LDS of the sequential kernel: query | candidate heap | result heap | 64
+// fresh neighbours (id) | visited (when it fits)
+__host__ __device__ inline size_t seq_lds_bytes(int ld, int ef, int k) {
+    return 4 * (size_t)seq_qpad(ld) + seq_heap_bytes(ef, k) + 4 * 64;
+}
+__host__ __device__ inline size_t seq_lds_bytes_gheap(int ld) { return 4 * (size_t)seq_qpad(ld) + 4 * 64; }
+
+// heap_pop (val = b[n], n the size before the pop) / heap_replace_top (val
+// the new key, n the size) of faiss/utils/Heap.h:112-149, CMax: the sift from
+// the root, the serial loop's decisions exactly (i2 == n + 1 takes i1; an
+// equal child is followed), three levels per LDS round trip (the children
+// pair and the pairs of the 2 grandchildren / 4 great-grandchildren slots)
+__device__ __forceinline__ void sx_sift(uint64_t* b, int n, uint64_t val, int lane) {
     int i = 1;
     for (;;) {
-        const int i1 = i << 1, i2 = i1 + 1;
-        if (i1 > k) break;
-        if (i2 == k + 1 || cmp2_gt(bv[i1], bv[i2], bi[i1], bi[i2])) {
-            if (cmp2_gt(val, bv[i1], id, bi[i1])) break;
-            bv[i] = bv[i1];
-            bi[i] = bi[i1];
-            i = i1;
-        } else {
-            if (cmp2_gt(val, bv[i2], id, bi[i2])) break;
-            bv[i] = bv[i2];
-            bi[i] = bi[i2];
-            i = i2;
+        const int i1 = 2 * i;
+        if (i1 > n) break;
+        // lane 0: pair i1; lanes 1-2: pairs 2 i1 + {0, 2}; lanes 3-6: 4 i1 + {0, 2, 4, 6}
+        int pi = -1;
+        if (lane == 0) pi = i1;
+        else if (lane < 3) pi = 2 * i1 + 2 * (lane - 1);
+        else if (lane < 7) pi = 4 * i1 + 2 * (lane - 3);
+        uint4 pv = make_uint4(0u, 0u, 0u, 0u);
+        if (pi >= 0 && pi <= n) pv = *(const uint4*)(b + pi);
+        const uint64_t lo = ((uint64_t)pv.y << 32) | pv.x, hi = ((uint64_t)pv.w << 32) | pv.z;
+        bool stop = false;
+#pragma unroll
+        for (int lev = 0; lev < 3; lev++) {
+            const int c1 = 2 * i;
+            if (c1 > n) {
+                stop = true;
+                break;
+            }
+            // the lane holding pair c1 (relative to i1's subtree)
+            const int src = lev == 0 ? 0 : lev == 1 ? 1 + ((c1 - 2 * i1) >> 1) : 3 + ((c1 - 4 * i1) >> 1);
+            const uint64_t k1 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(lo >> 32), src) << 32) |
+                                __builtin_amdgcn_readlane((uint32_t)lo, src);
+            const uint64_t k2 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(hi >> 32), src) << 32) |
+                                __builtin_amdgcn_readlane((uint32_t)hi, src);
+            int j;
+            uint64_t kj;
+            if (c1 + 1 == n + 1 || k1 > k2) {
+                j = c1;
+                kj = k1;
+            } else {
+                j = c1 + 1;
+                kj = k2;
+            }
+            if (val > kj) {
+                stop = true;
+                break;
+            }
+            if (lane == 0) b[i] = kj;
+            i = j;
         }
+        if (stop) break;
     }
-    bv[i] = bv[k];
-    bi[i] = bi[k];
+    if (lane == 0) b[i] = val;
 }
-__device__ void hx_push(int k, float* bv, int32_t* bi, float val, int32_t id) {
-    bv--;
-    bi--;
-    int i = k;
-    while (i > 1) {
-        const int f = i >> 1;
-        if (!cmp2_gt(val, bv[f], id, bi[f])) break;
-        bv[i] = bv[f];
-        bi[i] = bi[f];
-        i = f;
-    }
-    bv[i] = val;
-    bi[i] = id;
-}
-__device__ void hx_replace_top(int k, float* bv, int32_t* bi, float val, int32_t id) {
-    bv--;
-    bi--;
-    int i = 1;
-    for (;;) {
-        const int i1 = i << 1, i2 = i1 + 1;
-        if (i1 > k) break;
-        if (i2 == k + 1 || cmp2_gt(bv[i1], bv[i2], bi[i1], bi[i2])) {
-            if (cmp2_gt(val, bv[i1], id, bi[i1])) break;
-            bv[i] = bv[i1];
-            bi[i] = bi[i1];
-            i = i1;
-        } else {
-            if (cmp2_gt(val, bv[i2], id, bi[i2])) break;
-            bv[i] = bv[i2];
-            bi[i] = bi[i2];
-            i = i2;
-        }
-    }
-    bv[i] = val;
-    bi[i] = id;
+
+// heap_push of faiss/utils/Heap.h:150-170, CMax, after the size became n:
+// the ancestors n >> j (j = 1 .. log2 n) are loaded at once, one per lane;
+// the serial loop moves them down while val > ancestor (the run of such
+// ancestors from the parent up) and stores val where it stopped
+__device__ __forceinline__ void sx_push(uint64_t* b, int n, uint64_t val, int lane) {
+    const int L = 31 - __clz(n);
+    const int j = lane + 1;
+    const bool in = j <= L;
+    const uint64_t a = in ? b[n >> j] : 0ull;
+    const unsigned long long gt = __ballot(in && val > a);
+    const int m = __builtin_ctzll(~gt);
+    if (j <= m) b[n >> (j - 1)] = a;
+    if (lane == 0) b[n >> m] = val;
 }
 }  // namespace
 
-// GH: the two heaps in global scratch (gheap: 2 ef + 2 k words per block) —
+// HNSW::search with the reference's own data structures, operation for
+// operation (faiss/impl/HNSW.cpp:605-741, :943-996; MinimaxHeap :1096-1342;
+// heap_push / heap_pop / heap_replace_top / heap_reorder, faiss/utils/Heap.h):
+// one wave per query, both heaps in LDS in faiss's layout (sx_* above), the
+// hop's fresh neighbours evaluated by the lanes (4 lanes per row in the
+// reference order) and applied in arrival order; pop_min / count_below are
+// wave scans with the reference's tie rules (pop_min: the highest slot among
+// equal minima; count_below: every slot, dead ones included).  Serves
+// max(efSearch, k) > 64 (beyond 128 always), k > 64, and the queries the
+// batched kernel flags.
+// GH: the two heaps in global scratch (gheap: seq_heap_bytes per block) —
 // max(efSearch, k) beyond what the work group's LDS holds (the reference's
 // harness sweeps efSearch up to 3 nprobe, nprobe into the thousands)
 template <bool LDS_VISITED, bool GH = false>
@@ -472,22 +511,17 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
     const int64_t qo = blockIdx.x;
     if (only && only[q] == 0u) return;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* qs = sm;                              // [ld]
-    float* hp = GH ? gheap + (int64_t)blockIdx.x * (2 * (int64_t)ef + 2 * k) : qs + g.ld;
-    float* cdis = hp;                            // [ef] MinimaxHeap dis
-    int32_t* cid = (int32_t*)(cdis + ef);        // [ef] MinimaxHeap ids
-    float* rdis = (float*)(cid + ef);            // [k] result heap
-    int32_t* rid = (int32_t*)(rdis + k);         // [k]
-    float* fd = GH ? qs + g.ld : (float*)(rid + k);  // [64] fresh neighbours of a hop
-    int32_t* fi = (int32_t*)(fd + 64);           // [64]
-    int32_t* sh = fi + 64;                       // [8] scalars: hk, nvalid, nfresh, ...
-    uint32_t* vis = LDS_VISITED ? (uint32_t*)(sh + 8) : vis_global + blockIdx.x * vwords;
+    const int qpad = seq_qpad(g.ld);
+    float* qs = sm;  // [qpad]
+    uint64_t* cb = GH ? (uint64_t*)((char*)gheap + (int64_t)blockIdx.x * seq_heap_bytes(ef, k))
+                      : (uint64_t*)(sm + qpad);         // MinimaxHeap [1 .. ef]
+    uint64_t* rb = cb + seq_slots(ef);                  // result heap [1 .. k]
+    int32_t* fi = GH ? (int32_t*)(sm + qpad) : (int32_t*)((char*)(sm + qpad) + seq_heap_bytes(ef, k));
+    uint32_t* vis = LDS_VISITED ? (uint32_t*)(fi + 64) : vis_global + blockIdx.x * vwords;
     const int lane = threadIdx.x;
-    for (int j = lane; j < g.ld; j += 64) qs[j] = j < g.d ? x[q * ldx + j] : 0.f;
-    for (int j = lane; j < k; j += 64) {
-        rdis[j] = FLT_MAX;  // heap_heapify<CMax> (Heap.h:316-339)
-        rid[j] = -1;
-    }
+    for (int j = lane; j < qpad; j += 64) qs[j] = j < g.d ? x[q * ldx + j] : 0.f;
+    const uint64_t rinit = sx_key(FLT_MAX, -1);  // heap_heapify<CMax> (Heap.h:316-339)
+    for (int j = lane; j < k; j += 64) rb[1 + j] = rinit;
     for (int64_t w = lane; w < vwords; w += 64) vis[w] = 0u;
     __syncthreads();
     uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0;
@@ -527,40 +561,37 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
                 }
             }
         }
-        // ---- level 0: MinimaxHeap candidates(ef) seeded with the entry
+        // ---- level 0: MinimaxHeap candidates(ef) seeded with the entry;
+        // search_from_candidates (:624-637): the seed enters the results
+        int hk = 1, nvalid = 1;
         if (lane == 0) {
-            int hk = 0;
-            hx_push(++hk, cdis, cid, d_nearest, nearest);  // MinimaxHeap::push on empty
-            sh[0] = hk;
-            sh[1] = 1;  // nvalid
-            // search_from_candidates (:624-637): the seeds enter the results
-            float threshold = rdis[0];
-            for (int i = 0; i < hk; i++) {
-                const int32_t v1 = cid[i];
-                const float dd = cdis[i];
-                if (dd < threshold && rdis[0] > dd) {
-                    hx_replace_top(k, rdis, rid, dd, v1);
-                    threshold = rdis[0];
-                }
-                vis[v1 >> 5] |= 1u << (v1 & 31);
-            }
+            cb[1] = sx_key(d_nearest, nearest);
+            vis[nearest >> 5] |= 1u << (nearest & 31);
         }
         __syncthreads();
+        float rthr = sx_dis(rb[1]);
+        if (d_nearest < rthr) {
+            sx_sift(rb, k, sx_key(d_nearest, nearest), lane);
+            rthr = sx_dis(rb[1]);
+        }
+        const int cnt = g.cum_nb[1] - g.cum_nb[0];
         for (;;) {
-            const int hk = sh[0];
-            if (sh[1] <= 0) {  // candidates.size() == 0
+            if (nvalid <= 0) {  // candidates.size() == 0
                 st_n2 = 1;
                 break;
             }
             // pop_min (:1299-1330): the smallest dis among alive slots, the
-            // highest slot index among equal minima
+            // highest slot among equal minima
             float bd = FLT_MAX;
             int bp = -1;
-            for (int i = lane; i < hk; i += 64)
-                if (cid[i] != -1 && (bp < 0 || cdis[i] < bd || (cdis[i] == bd && i > bp))) {
-                    bd = cdis[i];
+            for (int i = 1 + lane; i <= hk; i += 64) {
+                const uint64_t kv = cb[i];
+                const float dv = sx_dis(kv);
+                if (sx_id(kv) != -1 && (bp < 0 || dv < bd || (dv == bd && i > bp))) {
+                    bd = dv;
                     bp = i;
                 }
+            }
 #pragma unroll
             for (int m = 32; m > 0; m >>= 1) {
                 const float od = __shfl_xor(bd, m);
@@ -570,74 +601,71 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
                     bp = op;
                 }
             }
-            const int32_t v0 = cid[bp];
+            const int32_t v0 = sx_id(cb[bp]);
             const float d0 = bd;
             // count_below(d0): every slot, dead ones included
             int nb = 0;
-            for (int i = lane; i < hk; i += 64) nb += cdis[i] < d0;
+            for (int i = 1 + lane; i <= hk; i += 64) nb += sx_dis(cb[i]) < d0;
 #pragma unroll
             for (int m = 32; m > 0; m >>= 1) nb += __shfl_xor(nb, m);
-            __syncthreads();
-            if (lane == 0) {
-                cid[bp] = -1;
-                sh[1] -= 1;
-            }
-            __syncthreads();
+            if (lane == 0) cb[bp] = sx_key(d0, -1);
+            nvalid--;
             if (nb >= efSearch) {
-                st_n2 = sh[1] == 0 ? 1u : 0u;
+                st_n2 = nvalid == 0 ? 1u : 0u;
                 break;
             }
             // neighbours of v0 in stored order; visited test-and-set in order
-            // (the ids are loaded by all lanes at once; the stored-order
-            // test-and-set is restated in parallel: neighbour j is fresh when
-            // its bit was clear before this hop and no earlier neighbour of the
-            // list is the same node; the fresh ones keep their stored order)
-            const int cnt = g.cum_nb[1] - g.cum_nb[0];
-            int nf;
-            {
-                int32_t v1 = -1;
-                if (lane < cnt)
-                    v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
-                               : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
-                const unsigned long long neg =
-                        __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
-                const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
-                const bool live = lane < jmax;
-                bool fresh = live && !((vis[v1 >> 5] >> (v1 & 31)) & 1u);
-                for (int i = 0; i < jmax; i++)  // a node listed twice: the first is the visit
-                    fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
-                __syncthreads();  // every lane read the bits before any is set
-                if (fresh) atomicOr(&vis[v1 >> 5], 1u << (v1 & 31));
-                const unsigned long long fm = __ballot(fresh);
-                nf = __popcll(fm);
-                if (fresh) fi[__popcll(fm & ((1ull << lane) - 1ull))] = v1;
-            }
-            __syncthreads();
-            if (lane < nf) fd[lane] = l2_row(qs, g.storage + (int64_t)fi[lane] * g.ld, g.d);
+            // (neighbour j is fresh when its bit was clear before this hop and
+            // no earlier neighbour of the list is the same node; the fresh
+            // ones keep their stored order)
+            int32_t v1 = -1;
+            if (lane < cnt)
+                v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
+                           : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
+            const unsigned long long neg =
+                    __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
+            const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
+            const bool live = lane < jmax;
+            bool fresh = live && !((vis[v1 >> 5] >> (v1 & 31)) & 1u);
+            for (int i = 0; i < jmax; i++)  // a node listed twice: the first is the visit
+                fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
+            __syncthreads();  // every lane read the bits before any is set
+            if (fresh) atomicOr(&vis[v1 >> 5], 1u << (v1 & 31));
+            const unsigned long long fm = __ballot(fresh);
+            const int nf = __popcll(fm);
+            const unsigned long long lt = (1ull << lane) - 1ull;
+            const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
+            const int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
+            // the fresh rows, 4 lanes per row (reference order)
+            float fdis = 0.f;
+            if (g.d <= 128)
+                fdis = ref_rows64_4lane_pb<true, 16, 1>(qs, qs, g.storage, g.ld, g.d,
+                                                        lane < nf ? (uint32_t)fv : 0u, nf, lane);
+            else if (lane < nf)
+                fdis = l2_row(qs, g.storage + (int64_t)fv * g.ld, g.d);
+            st_ndis += (uint32_t)nf;
             st_nhops += 1;
-            __syncthreads();
-            if (lane == 0) {
-                int hk2 = sh[0], nvalid = sh[1];
-                float threshold = rdis[0];
-                for (int t = 0; t < nf; t++) {
-                    const int32_t v1 = fi[t];
-                    const float dis = fd[t];
-                    // add_to_heap (:678-689)
-                    if (dis < threshold && rdis[0] > dis) {
-                        hx_replace_top(k, rdis, rid, dis, v1);
-                        threshold = rdis[0];
-                    }
-                    // MinimaxHeap::push (:1096-1107)
-                    if (hk2 == ef) {
-                        if (dis >= cdis[0]) continue;
-                        if (cid[0] != -1) --nvalid;
-                        hx_pop(hk2--, cdis, cid);
-                    }
-                    hx_push(++hk2, cdis, cid, dis, v1);
-                    ++nvalid;
+            // add_to_heap (:678-689) in arrival order; an arrival that can
+            // enter neither heap (dis >= the result threshold, and >= the
+            // full candidate heap's top) changes nothing
+            for (int t = 0; t < nf; t++) {
+                const float dis = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), t));
+                const int32_t id = __builtin_amdgcn_readlane(fv, t);
+                const uint64_t key = sx_key(dis, id);
+                if (dis < rthr) {
+                    sx_sift(rb, k, key, lane);  // res.add_result: heap_replace_top
+                    rthr = sx_dis(rb[1]);
                 }
-                sh[0] = hk2;
-                sh[1] = nvalid;
+                // MinimaxHeap::push (:1096-1107)
+                if (hk == ef) {
+                    const uint64_t top = cb[1];
+                    if (dis >= sx_dis(top)) continue;
+                    if (sx_id(top) != -1) --nvalid;
+                    sx_sift(cb, hk, cb[hk], lane);  // heap_pop(k--)
+                    hk--;
+                }
+                sx_push(cb, ++hk, key, lane);
+                ++nvalid;
             }
             __syncthreads();
         }
@@ -649,32 +677,27 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
         atomicAdd(&stats[3], (unsigned long long)st_nhops);
         atomicAdd(&stats[4], (unsigned long long)st_ndis);
     }
-    // heap_reorder<CMax> (Heap.h:421-450) by lane 0, then the lanes write out
-    if (lane == 0) {
-        int ii = 0;
-        for (int i = 0; i < k; i++) {
-            const float val = rdis[0];
-            const int32_t id = rid[0];
-            hx_pop(k - i, rdis, rid);
-            rdis[k - ii - 1] = val;
-            rid[k - ii - 1] = id;
-            if (id != -1) ii++;
-        }
-        // memmove to the front, pad (FLT_MAX, -1)
-        for (int i = 0; i < ii; i++) {
-            rdis[i] = rdis[k - ii + i];
-            rid[i] = rid[k - ii + i];
-        }
-        for (int i = ii; i < k; i++) {
-            rdis[i] = FLT_MAX;
-            rid[i] = -1;
-        }
+    // heap_reorder<CMax> (Heap.h:421-450): pops into the vacated tail, then
+    // the kept ones to the front and (FLT_MAX, -1) padding
+    int ii = 0;
+    for (int i = 0; i < k; i++) {
+        const uint64_t top = rb[1];
+        sx_sift(rb, k - i, rb[k - i], lane);
+        if (lane == 0) rb[k - ii] = top;  // 0-based slot k - ii - 1
+        if (sx_id(top) != -1) ii++;
     }
     __syncthreads();
     for (int j = lane; j < k; j += 64) {
-        if (D) D[qo * k + j] = rdis[j];
-        if (I) I[qo * k + j] = rid[j];
-        if (I32) I32[qo * k + j] = rid[j];
+        float dv = FLT_MAX;
+        int32_t id = -1;
+        if (j < ii) {
+            const uint64_t kv = rb[1 + k - ii + j];
+            dv = sx_dis(kv);
+            id = sx_id(kv);
+        }
+        if (D) D[qo * k + j] = dv;
+        if (I) I[qo * k + j] = id;
+        if (I32) I32[qo * k + j] = id;
     }
 }
 
@@ -1585,14 +1608,13 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
                               const uint32_t* qidx, hipStream_t s, float* gheap = nullptr,
                               uint64_t* rlog = nullptr, int rcap = 0) {
     const int ef = efSearch > k ? efSearch : k;
-    const size_t lds_q = sizeof(float) * g.ld;
-    const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
+    const size_t lds_x = seq_lds_bytes(g.ld, ef, k);
     const bool x_lds_vis = lds_x + vwords * 4 <= 64 * 1024;
     if (lds_x > 64 * 1024) {
         // heaps in global scratch; the LDS keeps the query, the hop's fresh
         // neighbours and (when it fits) the visited bitmap
         FAISS_THROW_IF_NOT(gheap != nullptr);
-        const size_t lds_g = lds_q + 8 * 64 + 4 * 8;
+        const size_t lds_g = seq_lds_bytes_gheap(g.ld);
         if (lds_g + vwords * 4 <= 64 * 1024)
             k_hnsw_exact<true, true><<<dim3((unsigned)n), dim3(64), lds_g + vwords * 4, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
@@ -1696,8 +1718,7 @@ void hnsw_exact_listed(const HNSWDevice& g, const float* x, int ldx, const uint3
 
 size_t hnsw_heap_scratch_words(int k, int efSearch, int ld) {
     const int ef = efSearch > k ? efSearch : k;
-    const size_t lds_x = sizeof(float) * (size_t)ld + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 32;
-    return lds_x > 64 * 1024 ? 2 * (size_t)ef + 2 * (size_t)k : 0;
+    return seq_lds_bytes(ld, ef, k) > 64 * 1024 ? seq_heap_bytes(ef, k) / 4 : 0;
 }
 bool hnsw_visited_scratch_needed(int ld, int k, int efSearch, int64_t vwords) {
     // mirrors the LDS choices of the three kernels: any query may reach the
@@ -1707,8 +1728,8 @@ bool hnsw_visited_scratch_needed(int ld, int k, int efSearch, int64_t vwords) {
     const int ef = efSearch > k ? efSearch : k;
     const size_t vb = 4 * (size_t)std::max<int64_t>(vwords, 0);
     const size_t lds_q = sizeof(float) * (size_t)ld;
-    const size_t lds_x = lds_q + 8 * (size_t)ef + 8 * (size_t)k + 8 * 64 + 4 * 8;
-    const size_t lds_xg = lds_x > kL ? lds_q + 8 * 64 + 4 * 8 : lds_x;
+    const size_t lds_x = seq_lds_bytes(ld, ef, k);
+    const size_t lds_xg = lds_x > kL ? seq_lds_bytes_gheap(ld) : lds_x;
     bool need = lds_xg + vb > kL;
     if (ef <= 64 && k <= 64 && lds_x <= kL) {
         HNSWDevice g{};

@@ -271,3 +271,24 @@ def test_hnsw_replay_log_overflow_and_lds_log(amd, orc, gpu, monkeypatch, d):
     assert seen[(None, "16")][1] > 0, seen
     assert seen[("lds", "16")][1] > 0, seen
     assert sum(seen[(None, None)][:2]) == sum(seen[(None, "16")][:2]), seen
+
+
+@pytest.mark.parametrize("d", [37, 128])
+def test_hnsw_sequential_kernel_wide_ef(amd, orc, gpu, d):
+    """The sequential kernel (max(efSearch, k) > 64 or k > 64: faiss's heap
+    layout in the LDS, or in global scratch past it) on the duplicate-heavy
+    graph: heap pops / pushes / replace_top in the reference's layout, ties
+    included, for efSearch 100 .. 9000 and k up to 100."""
+    nb = 5000
+    xb = rand(orc, nb, d, 61)
+    xb[1000:1150] = xb[:150]
+    xb[3000:3040] = xb[:40]
+    xq = np.concatenate([rand(orc, 200, d, 63), xb[:40]])
+    h = amd.IndexHNSWFlat(d, 16)
+    h.add(xb)
+    g = orc.HNSWGraph.from_index(h)
+    for ef, k in [(100, 10), (257, 5), (768, 10), (500, 100), (2500, 1), (9000, 10)]:
+        h.efSearch = ef
+        D, I = h.search(xq, k)
+        Dr, Ir = g.search(xq, k, ef)
+        assert_same_results(D, I, Dr, Ir)
