@@ -440,10 +440,13 @@ __device__ __forceinline__ void sx_sift(uint64_t* b, int n, uint64_t val, int la
             }
             // the lane holding pair c1 (relative to i1's subtree)
             const int src = lev == 0 ? 0 : lev == 1 ? 1 + ((c1 - 2 * i1) >> 1) : 3 + ((c1 - 4 * i1) >> 1);
-            const uint64_t k1 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(lo >> 32), src) << 32) |
-                                __builtin_amdgcn_readlane((uint32_t)lo, src);
-            const uint64_t k2 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(hi >> 32), src) << 32) |
-                                __builtin_amdgcn_readlane((uint32_t)hi, src);
+            // (readlane returns int: through uint32_t, or the low word sign-extends)
+            const uint64_t k1 =
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(lo >> 32), src) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((uint32_t)lo, src);
+            const uint64_t k2 =
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(hi >> 32), src) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((uint32_t)hi, src);
             int j;
             uint64_t kj;
             if (c1 + 1 == n + 1 || k1 > k2) {
@@ -473,7 +476,7 @@ __device__ __forceinline__ void sx_push(uint64_t* b, int n, uint64_t val, int la
     const int L = 31 - __clz(n);
     const int j = lane + 1;
     const bool in = j <= L;
-    const uint64_t a = in ? b[n >> j] : 0ull;
+    const uint64_t a = in ? b[n >> (j & 31)] : 0ull;
     const unsigned long long gt = __ballot(in && val > a);
     const int m = __builtin_ctzll(~gt);
     if (j <= m) b[n >> (j - 1)] = a;
@@ -608,6 +611,12 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
             for (int i = 1 + lane; i <= hk; i += 64) nb += sx_dis(cb[i]) < d0;
 #pragma unroll
             for (int m = 32; m > 0; m >>= 1) nb += __shfl_xor(nb, m);
+#ifdef HNSW_SEQ_DEBUG
+            if (q == 0 && lane == 0 && st_nhops < 12)
+                printf("hop %u: bp %d v0 %d d0 %g nb %d hk %d nvalid %d rthr %g rb1 %llx cb1 %llx\n",
+                       st_nhops, bp, v0, d0, nb, hk, nvalid, rthr, (unsigned long long)rb[1],
+                       (unsigned long long)cb[1]);
+#endif
             if (lane == 0) cb[bp] = sx_key(d0, -1);
             nvalid--;
             if (nb >= efSearch) {
@@ -625,12 +634,17 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
             const unsigned long long neg =
                     __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
             const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
-            const bool live = lane < jmax;
-            bool fresh = live && !((vis[v1 >> 5] >> (v1 & 31)) & 1u);
-            for (int i = 0; i < jmax; i++)  // a node listed twice: the first is the visit
-                fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
-            __syncthreads();  // every lane read the bits before any is set
-            if (fresh) atomicOr(&vis[v1 >> 5], 1u << (v1 & 31));
+            // (the bits as they were before this hop decide; a node listed
+            // twice — the atomic then finds the bit another lane of this hop
+            // set — is visited at its first position, so only then the lanes
+            // are compared pairwise)
+            const uint32_t vbit = 1u << (v1 & 31);
+            bool fresh = lane < jmax && !(vis[v1 >> 5] & vbit);
+            uint32_t old = 0u;
+            if (fresh) old = atomicOr(&vis[v1 >> 5], vbit);
+            if (__ballot(fresh && (old & vbit)) != 0ull)
+                for (int i = 0; i < jmax; i++)
+                    fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
             const unsigned long long fm = __ballot(fresh);
             const int nf = __popcll(fm);
             const unsigned long long lt = (1ull << lane) - 1ull;
@@ -648,8 +662,11 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
             // add_to_heap (:678-689) in arrival order; an arrival that can
             // enter neither heap (dis >= the result threshold, and >= the
             // full candidate heap's top) changes nothing
+            uint64_t top = hk == ef ? cb[1] : 0ull;  // the full heap's top
             for (int t = 0; t < nf; t++) {
                 const float dis = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), t));
+                const bool cin = hk < ef || dis < sx_dis(top);
+                if (!(dis < rthr) && !cin) continue;
                 const int32_t id = __builtin_amdgcn_readlane(fv, t);
                 const uint64_t key = sx_key(dis, id);
                 if (dis < rthr) {
@@ -657,15 +674,15 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
                     rthr = sx_dis(rb[1]);
                 }
                 // MinimaxHeap::push (:1096-1107)
+                if (!cin) continue;
                 if (hk == ef) {
-                    const uint64_t top = cb[1];
-                    if (dis >= sx_dis(top)) continue;
                     if (sx_id(top) != -1) --nvalid;
                     sx_sift(cb, hk, cb[hk], lane);  // heap_pop(k--)
                     hk--;
                 }
                 sx_push(cb, ++hk, key, lane);
                 ++nvalid;
+                if (hk == ef) top = cb[1];
             }
             __syncthreads();
         }
