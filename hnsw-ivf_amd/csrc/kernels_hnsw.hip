@@ -415,55 +415,21 @@ __host__ __device__ inline size_t seq_lds_bytes_gheap(int ld) { return 4 * (size
 // heap_pop (val = b[n], n the size before the pop) / heap_replace_top (val
 // the new key, n the size) of faiss/utils/Heap.h:112-149, CMax: the sift from
 // the root, the serial loop's decisions exactly (i2 == n + 1 takes i1; an
-// equal child is followed), three levels per LDS round trip (the children
-// pair and the pairs of the 2 grandchildren / 4 great-grandchildren slots)
+// equal child is followed); one 16-byte LDS read of the children pair per
+// level.  (A three-level lookahead per LDS round trip measured slower: the
+// kernel is bound by instruction issue across its waves, not by latency.)
 __device__ __forceinline__ void sx_sift(uint64_t* b, int n, uint64_t val, int lane) {
     int i = 1;
     for (;;) {
         const int i1 = 2 * i;
         if (i1 > n) break;
-        // lane 0: pair i1; lanes 1-2: pairs 2 i1 + {0, 2}; lanes 3-6: 4 i1 + {0, 2, 4, 6}
-        int pi = -1;
-        if (lane == 0) pi = i1;
-        else if (lane < 3) pi = 2 * i1 + 2 * (lane - 1);
-        else if (lane < 7) pi = 4 * i1 + 2 * (lane - 3);
-        uint4 pv = make_uint4(0u, 0u, 0u, 0u);
-        if (pi >= 0 && pi <= n) pv = *(const uint4*)(b + pi);
-        const uint64_t lo = ((uint64_t)pv.y << 32) | pv.x, hi = ((uint64_t)pv.w << 32) | pv.z;
-        bool stop = false;
-#pragma unroll
-        for (int lev = 0; lev < 3; lev++) {
-            const int c1 = 2 * i;
-            if (c1 > n) {
-                stop = true;
-                break;
-            }
-            // the lane holding pair c1 (relative to i1's subtree)
-            const int src = lev == 0 ? 0 : lev == 1 ? 1 + ((c1 - 2 * i1) >> 1) : 3 + ((c1 - 4 * i1) >> 1);
-            // (readlane returns int: through uint32_t, or the low word sign-extends)
-            const uint64_t k1 =
-                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(lo >> 32), src) << 32) |
-                    (uint32_t)__builtin_amdgcn_readlane((uint32_t)lo, src);
-            const uint64_t k2 =
-                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(hi >> 32), src) << 32) |
-                    (uint32_t)__builtin_amdgcn_readlane((uint32_t)hi, src);
-            int j;
-            uint64_t kj;
-            if (c1 + 1 == n + 1 || k1 > k2) {
-                j = c1;
-                kj = k1;
-            } else {
-                j = c1 + 1;
-                kj = k2;
-            }
-            if (val > kj) {
-                stop = true;
-                break;
-            }
-            if (lane == 0) b[i] = kj;
-            i = j;
-        }
-        if (stop) break;
+        const uint4 pv = *(const uint4*)(b + i1);
+        const uint64_t k1 = ((uint64_t)pv.y << 32) | pv.x, k2 = ((uint64_t)pv.w << 32) | pv.z;
+        const bool first = i1 + 1 == n + 1 || k1 > k2;
+        const uint64_t kj = first ? k1 : k2;
+        if (val > kj) break;
+        if (lane == 0) b[i] = kj;
+        i = first ? i1 : i1 + 1;
     }
     if (lane == 0) b[i] = val;
 }
@@ -587,12 +553,34 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
             // highest slot among equal minima
             float bd = FLT_MAX;
             int bp = -1;
-            for (int i = 1 + lane; i <= hk; i += 64) {
-                const uint64_t kv = cb[i];
-                const float dv = sx_dis(kv);
-                if (sx_id(kv) != -1 && (bp < 0 || dv < bd || (dv == bd && i > bp))) {
-                    bd = dv;
-                    bp = i;
+            // (the slots' distances stay in registers for count_below when
+            // the heap has at most 64 SX_CACHE slots)
+            constexpr int SX_CACHE = 16;
+            float dc[SX_CACHE];
+            const bool cached = hk <= 64 * SX_CACHE;
+            if (cached) {
+#pragma unroll
+                for (int u = 0; u < SX_CACHE; u++) {
+                    const int i = 1 + lane + 64 * u;
+                    dc[u] = FLT_MAX;
+                    if (i <= hk) {
+                        const uint64_t kv = cb[i];
+                        const float dv = sx_dis(kv);
+                        dc[u] = dv;
+                        if (sx_id(kv) != -1 && (bp < 0 || dv < bd || (dv == bd && i > bp))) {
+                            bd = dv;
+                            bp = i;
+                        }
+                    }
+                }
+            } else {
+                for (int i = 1 + lane; i <= hk; i += 64) {
+                    const uint64_t kv = cb[i];
+                    const float dv = sx_dis(kv);
+                    if (sx_id(kv) != -1 && (bp < 0 || dv < bd || (dv == bd && i > bp))) {
+                        bd = dv;
+                        bp = i;
+                    }
                 }
             }
 #pragma unroll
@@ -608,7 +596,12 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
             const float d0 = bd;
             // count_below(d0): every slot, dead ones included
             int nb = 0;
-            for (int i = 1 + lane; i <= hk; i += 64) nb += sx_dis(cb[i]) < d0;
+            if (cached) {
+#pragma unroll
+                for (int u = 0; u < SX_CACHE; u++) nb += dc[u] < d0;  // (padding: FLT_MAX)
+            } else {
+                for (int i = 1 + lane; i <= hk; i += 64) nb += sx_dis(cb[i]) < d0;
+            }
 #pragma unroll
             for (int m = 32; m > 0; m >>= 1) nb += __shfl_xor(nb, m);
 #ifdef HNSW_SEQ_DEBUG
