@@ -1307,9 +1307,15 @@ void IndexIVFPQ::upload_extra() const {
         for (size_t li = 0; li < nlist; li++) mx = std::max(mx, invlists->list_size(li));
         pq_obits_ = kern::ivf_bf3_obits((uint32_t)std::min<size_t>(mx, 0xffffffffu));
         pq_mfma_ready_ = pq_obits_ <= 14;
-        // the streamed filter's image (by-residual terms in the bias tail)
+        // the streamed filter's image (by-residual terms in the bias tail):
+        // only on request (FAISS_AMD_PQ_FILTER=image at upload) — the default
+        // filter gathers the same bf16 values from the codes (4.3-8.5x less
+        // HBM per row than the image)
         pq_stream_ready_ = false;
-        if (pq_mfma_ready_ && kern::ivfpq_stream_eligible(d, (int)pq.M, 1, 1)) {
+        const char* ienv = getenv("FAISS_AMD_PQ_FILTER");
+        d_pcbs_.release();
+        if (pq_mfma_ready_ && ienv && !strcmp(ienv, "image") &&
+            kern::ivfpq_stream_eligible(d, (int)pq.M, 1, 1)) {
             const int DB = kern::bf3_db_host(d);
             d_pcbs_.reserve(rows * (2 * (size_t)DB + 16));
             kern::pq_stream_image(d_codes_.as<uint8_t>(), device_code_stride(), (int64_t)rows, d,
@@ -1318,6 +1324,10 @@ void IndexIVFPQ::upload_extra() const {
             pq_stream_ready_ = true;
         }
         HIP_CHECK(hipStreamSynchronize(s));  // cn is a host temporary
+        // the per-row norms only fed the list maxima: per row the index keeps
+        // its codes, id, term and list number (code_size + 16 bytes)
+        d_prn_.release();
+        d_prr_.release();
     }
 }
 
@@ -1343,13 +1353,21 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         // eligible; FAISS_AMD_PQ_FILTER=decode keeps the in-loop decode filter
         // k_ivfpq_filter_w, which also serves IDSelectors)
         const char* fenv = getenv("FAISS_AMD_PQ_FILTER");
-        // (the streamed filter needs the query image: the flat quantizer's,
-        // or one prepared below for 16-B aligned rows)
-        const bool stream = pq_stream_ready_ && !sel && !(fenv && !strcmp(fenv, "decode")) &&
-                            !(fenv && !strcmp(fenv, "wg")) &&
-                            (shared_qimg_ != nullptr || ldx % 4 == 0) &&
-                            kern::ivfpq_stream_eligible(d, (int)pq.M, (int)k, np);
-        const int QT = stream ? kern::IVF_FLAT_QT : 64;
+        // filters (all need the query image: the flat quantizer's, or one
+        // prepared below for 16-B aligned rows):
+        //  * codes (default): k_ivfpq_codes, the folded arithmetic gathered
+        //    from the codes through the LDS decode table;
+        //  * image (FAISS_AMD_PQ_FILTER=image when the index was uploaded):
+        //    the streamed Flat filter over the decoded bf16 image;
+        //  * decode / wg (FAISS_AMD_PQ_FILTER=decode|wg, and IDSelectors):
+        //    k_ivfpq_filter_w / k_ivfpq_filter (unfolded keys, 64-query items)
+        const bool qimg_ok = shared_qimg_ != nullptr || ldx % 4 == 0;
+        const bool stream = pq_stream_ready_ && !sel && fenv && !strcmp(fenv, "image") &&
+                            qimg_ok && kern::ivfpq_stream_eligible(d, (int)pq.M, (int)k, np);
+        const bool codesf = !stream && !sel && qimg_ok &&
+                            !(fenv && (!strcmp(fenv, "decode") || !strcmp(fenv, "wg"))) &&
+                            kern::ivfpq_codes_eligible(d, (int)pq.M, (int)k, np);
+        const int QT = stream || codesf ? kern::IVF_FLAT_QT : 64;
         uint32_t* counts_next = nullptr;
         uint32_t* counts = bucket_counts(s, &counts_next);
         s_cur_.reserve(sizeof(uint32_t) * std::max<idx_t>(n * np, 1));
@@ -1404,6 +1422,13 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
                                           d_lRmax_.as<float>(), (int)nlist, n, np, (int)k,
                                           pq_obits_, b, mi, s_pkeys_.as<uint32_t>(),
                                           s_precs_.as<kern::ProbeRec>(), &KT, s, qimg, qxn);
+            else if (codesf)
+                kern::ivfpq_codes_filter(d, (int)pq.M, d_dec_.ptr, d_codes_.as<uint8_t>(),
+                                         d_terms_.as<float>(), centroid_dis, d_cnorm_.as<float>(),
+                                         d_lrmax_.as<float>(), d_lRmax_.as<float>(), (int)nlist,
+                                         n, np, (int)k, pq_obits_, b, mi,
+                                         s_pkeys_.as<uint32_t>(), s_precs_.as<kern::ProbeRec>(),
+                                         &KT, s, qimg, qxn);
             else
                 kern::ivfpq_filter(x, ldx, d, (int)pq.M, d_dec_.ptr, d_codes_.as<uint8_t>(),
                                    d_terms_.as<float>(), centroid_dis, d_cnorm_.as<float>(),
@@ -1426,7 +1451,7 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
                                d_ids_.as<int64_t>(), pa, (int)pq.dsub, n, np, KT, pq_obits_,
                                (int)k, sel, distances, labels,
                                dbg ? s_pflags_.as<uint32_t>() : nullptr, s, qdone_,
-                               stream ? 1 : 0);
+                               stream || codesf ? 1 : 0);
         }
         if (dbg) {
             uint32_t st[4];

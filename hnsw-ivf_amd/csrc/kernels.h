@@ -205,6 +205,15 @@ void pq_stream_image(const uint8_t* codes, int cs, int64_t rows, int d, int dsub
                      const float* pq_cent, const float* terms, const uint32_t* row_list, int DB,
                      void* out, hipStream_t s);
 bool ivfpq_stream_eligible(int d, int M, int k, int nprobe);
+// the default IVF-PQ filter (kernels_pq_mfma.hip k_ivfpq_codes): the streamed
+// filter's folded arithmetic with each row's A fragments gathered from the
+// LDS decode table `dec` by its code bytes (no image); same keys / records
+bool ivfpq_codes_eligible(int d, int M, int k, int nprobe);
+void ivfpq_codes_filter(int d, int M, const void* dec, const uint8_t* codes, const float* terms,
+                        const float* cdis, const float* cnorm, const float* lrmax,
+                        const float* lRmax, int nlist, int64_t n, int nprobe, int k, int obits,
+                        const IVFBuckets& b, int64_t max_items, uint32_t* keys, ProbeRec* recs,
+                        int* kt_out, hipStream_t s, const void* qimg, const float* qxn);
 double ivfpq_fold_coef(int d, int M);
 // the IVF-Flat streamed filter over the PQ stream image: keys + probe records
 // in the k_ivfpq_filter_w format (folded keys; the re-rank takes fold = 1)
