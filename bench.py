@@ -71,10 +71,10 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 # symbol of the kernel that stage launches in this round's code, matched in
 # this round's committed rocprofv3 PMC summaries (a summary of an older kernel
 # or round is never used: traffic is null instead)
-ROUND = 4
+ROUND = 5
 PMC_SYMBOL = {
     "ivf_flat_scan": r"kern::k_ivf_bf2_stream<true, \d+, \d+, false, true, false>",
-    "ivfpq_filter": r"kern::k_ivf_bf2_stream<true, \d+, \d+, false, true, true>",
+    "ivfpq_filter": r"kern::k_ivfpq_filter_w<",
     "coarse_filter": r"kern::k_coarse_stream<",
     "hnsw_search": r"kern::k_hnsw_search<",
     "hnsw_exact": r"kern::k_hnsw_exact_reg<",
@@ -214,20 +214,10 @@ def kernel_roofline(name, ms, work, config):
              "mfma_dtype": "bf16", "mfma_flops_per_step": work["flat_flops"],
              "mfma_tflops": work["flat_flops"] / t / 1e12,
              "mfma_frac": work["flat_flops"] / t / 1e12 / PEAK_BF16_TFLOPS}
-    elif name == "ivfpq_filter" and os.environ.get("FAISS_AMD_PQ_FILTER") == "decode":
-        # codes decoded to bf16 in the loop and multiplied against the
-        # queries' hi + lo split: 2 products of 2 dpad flops per candidate
-        f = work["cands"] * 4.0 * work["dpad16"]
-        r = {"bound": "mfma", "achieved": f / t / 1e12, "peak": PEAK_BF16_TFLOPS,
-             "unit": "TFLOP/s", "mfma_dtype": "bf16", "algorithmic_flops_per_step": f,
-             "flops_per_candidate": 4 * work["dpad16"],
-             "streamed_code_bytes_per_step": work["cands"] * work.get("M", 0),
-             "streamed_code_gbs": work["cands"] * work.get("M", 0) / t / 1e9}
-    elif name == "ivfpq_filter":
-        # the streamed filter over the decoded residual image: one pass over
-        # the rows of every distinct probed list, bf16 of the residual (dims
-        # padded to 32) + its folded bias term: 2 dpad + 8 bytes per row (the
-        # IVF-Flat filter's model); the MFMA view beside it
+    elif name == "ivfpq_filter" and os.environ.get("FAISS_AMD_PQ_FILTER") == "image":
+        # (opt-in) the streamed filter over the decoded residual image: one
+        # pass over the rows of every distinct probed list at 2 dpad + 8 bytes
+        # per row (the IVF-Flat filter's model); the code bytes beside it
         b = work["flat_rows"] * work["flat_row_bytes"]
         f = work["cands"] * 4.0 * work["dpad32"]
         r = {"bound": "hbm", "achieved": b / t / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -235,6 +225,20 @@ def kernel_roofline(name, ms, work, config):
              "mfma_dtype": "bf16", "mfma_flops_per_step": f, "mfma_tflops": f / t / 1e12,
              "mfma_frac": f / t / 1e12 / PEAK_BF16_TFLOPS,
              "pq_code_bytes_per_step": work["flat_rows"] * work.get("M", 0)}
+    elif name == "ivfpq_filter":
+        # the default filter streams the code bytes (list x
+        # code_size, one pass over the rows of every distinct probed list)
+        # and decodes each row's bf16 residual through the LDS table, 2
+        # products of 2 dpad flops per (query, row) candidate on the bf16
+        # MFMA: priced on the MFMA (the code bytes are a small fraction of
+        # HBM: list reuse across the batch's queries)
+        b = work["flat_rows"] * work.get("M", 0)
+        f = work["cands"] * 4.0 * work["dpad16"]
+        r = {"bound": "mfma", "achieved": f / t / 1e12, "peak": PEAK_BF16_TFLOPS,
+             "unit": "TFLOP/s", "mfma_dtype": "bf16", "algorithmic_flops_per_step": f,
+             "flops_per_candidate": 4 * work["dpad16"],
+             "algorithmic_bytes_per_step": b, "bytes_per_row": work.get("M", 0),
+             "hbm_gbs": b / t / 1e9, "hbm_frac": b / t / 1e9 / PEAK_HBM_GBS}
     elif name == "coarse_filter":
         # bf16x3 x.c of every (query, centroid): 3 products of 2 dpad flops
         f = work["nq_coarse"] * work["nlist"] * 6.0 * work["dpad16"]

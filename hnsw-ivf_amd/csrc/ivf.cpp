@@ -1314,7 +1314,12 @@ void IndexIVFPQ::upload_extra() const {
         pq_stream_ready_ = false;
         const char* ienv = getenv("FAISS_AMD_PQ_FILTER");
         d_pcbs_.release();
+        // (at most 4 GiB of image: a 100M-row single-GPU index gave wrong
+        // filter keys through the image in a round-5 A/B, not root-caused;
+        // the 12.5M-row c5 shard, 2.6 GB, is bit-exact)
+        const int DBi = kern::bf3_db_host(d);
         if (pq_mfma_ready_ && ienv && !strcmp(ienv, "image") &&
+            rows * (2 * (size_t)DBi + 16) <= ((size_t)4 << 30) &&
             kern::ivfpq_stream_eligible(d, (int)pq.M, 1, 1)) {
             const int DB = kern::bf3_db_host(d);
             d_pcbs_.reserve(rows * (2 * (size_t)DB + 16));
@@ -1353,21 +1358,18 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         // eligible; FAISS_AMD_PQ_FILTER=decode keeps the in-loop decode filter
         // k_ivfpq_filter_w, which also serves IDSelectors)
         const char* fenv = getenv("FAISS_AMD_PQ_FILTER");
-        // filters (all need the query image: the flat quantizer's, or one
+        // filters (both need the query image: the flat quantizer's, or one
         // prepared below for 16-B aligned rows):
-        //  * codes (default): k_ivfpq_codes, the folded arithmetic gathered
-        //    from the codes through the LDS decode table;
-        //  * image (FAISS_AMD_PQ_FILTER=image when the index was uploaded):
-        //    the streamed Flat filter over the decoded bf16 image;
-        //  * decode / wg (FAISS_AMD_PQ_FILTER=decode|wg, and IDSelectors):
-        //    k_ivfpq_filter_w / k_ivfpq_filter (unfolded keys, 64-query items)
+        //  * default (and IDSelectors): k_ivfpq_filter_w, the codes streamed
+        //    from HBM and each row's A fragments gathered from the decode
+        //    table in the LDS (FAISS_AMD_PQ_FILTER=wg: its 4-wave group form);
+        //  * image (FAISS_AMD_PQ_FILTER=image both when the index is uploaded
+        //    and when it is searched): the streamed Flat filter over a decoded
+        //    bf16 image of the residuals (4.3-8.5x the codes' bytes)
         const bool qimg_ok = shared_qimg_ != nullptr || ldx % 4 == 0;
         const bool stream = pq_stream_ready_ && !sel && fenv && !strcmp(fenv, "image") &&
                             qimg_ok && kern::ivfpq_stream_eligible(d, (int)pq.M, (int)k, np);
-        const bool codesf = !stream && !sel && qimg_ok &&
-                            !(fenv && (!strcmp(fenv, "decode") || !strcmp(fenv, "wg"))) &&
-                            kern::ivfpq_codes_eligible(d, (int)pq.M, (int)k, np);
-        const int QT = stream || codesf ? kern::IVF_FLAT_QT : 64;
+        const int QT = stream ? kern::IVF_FLAT_QT : 64;
         uint32_t* counts_next = nullptr;
         uint32_t* counts = bucket_counts(s, &counts_next);
         s_cur_.reserve(sizeof(uint32_t) * std::max<idx_t>(n * np, 1));
@@ -1422,13 +1424,6 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
                                           d_lRmax_.as<float>(), (int)nlist, n, np, (int)k,
                                           pq_obits_, b, mi, s_pkeys_.as<uint32_t>(),
                                           s_precs_.as<kern::ProbeRec>(), &KT, s, qimg, qxn);
-            else if (codesf)
-                kern::ivfpq_codes_filter(d, (int)pq.M, d_dec_.ptr, d_codes_.as<uint8_t>(),
-                                         d_terms_.as<float>(), centroid_dis, d_cnorm_.as<float>(),
-                                         d_lrmax_.as<float>(), d_lRmax_.as<float>(), (int)nlist,
-                                         n, np, (int)k, pq_obits_, b, mi,
-                                         s_pkeys_.as<uint32_t>(), s_precs_.as<kern::ProbeRec>(),
-                                         &KT, s, qimg, qxn);
             else
                 kern::ivfpq_filter(x, ldx, d, (int)pq.M, d_dec_.ptr, d_codes_.as<uint8_t>(),
                                    d_terms_.as<float>(), centroid_dis, d_cnorm_.as<float>(),
@@ -1451,7 +1446,7 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
                                d_ids_.as<int64_t>(), pa, (int)pq.dsub, n, np, KT, pq_obits_,
                                (int)k, sel, distances, labels,
                                dbg ? s_pflags_.as<uint32_t>() : nullptr, s, qdone_,
-                               stream || codesf ? 1 : 0);
+                               stream ? 1 : 0);
         }
         if (dbg) {
             uint32_t st[4];

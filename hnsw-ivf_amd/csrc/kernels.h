@@ -164,6 +164,14 @@ void probe_limits(const int32_t* assign, int64_t n, int nprobe, const uint32_t* 
                   hipStream_t s);
 void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* list_len,
                 const uint32_t* list_off, int nlist, int QT, IVFBuckets b, hipStream_t s);
+// the certified exact re-rank of the IVF-Flat filter's keys / probe records
+// (kernels_ivf_rerank.hip; one wave per query, probes in chunks of 64 past
+// nprobe 64); ivf_flat_scan_mfma calls it after the filter
+void ivf_flat_rerank(const uint32_t* keys, const ProbeRec* recs, const float* x, int ldx,
+                     const float* codes, int ldc, const int64_t* ids, int d, int64_t n,
+                     int nprobe, int KE, int obits, int k, int metric_l2, const uint8_t* sel,
+                     uint32_t* stats, float* D, int64_t* I, KernelTimes* kt, hipStream_t s,
+                     unsigned long long* qdone, int fold);
 // IVF-PQ list-centric MFMA filter + exact re-rank (kernels_pq_mfma.hip)
 struct PQArgs {
     const float* pq_cent = nullptr;  // [M][256][dsub] fp32
@@ -205,15 +213,6 @@ void pq_stream_image(const uint8_t* codes, int cs, int64_t rows, int d, int dsub
                      const float* pq_cent, const float* terms, const uint32_t* row_list, int DB,
                      void* out, hipStream_t s);
 bool ivfpq_stream_eligible(int d, int M, int k, int nprobe);
-// the default IVF-PQ filter (kernels_pq_mfma.hip k_ivfpq_codes): the streamed
-// filter's folded arithmetic with each row's A fragments gathered from the
-// LDS decode table `dec` by its code bytes (no image); same keys / records
-bool ivfpq_codes_eligible(int d, int M, int k, int nprobe);
-void ivfpq_codes_filter(int d, int M, const void* dec, const uint8_t* codes, const float* terms,
-                        const float* cdis, const float* cnorm, const float* lrmax,
-                        const float* lRmax, int nlist, int64_t n, int nprobe, int k, int obits,
-                        const IVFBuckets& b, int64_t max_items, uint32_t* keys, ProbeRec* recs,
-                        int* kt_out, hipStream_t s, const void* qimg, const float* qxn);
 double ivfpq_fold_coef(int d, int M);
 // the IVF-Flat streamed filter over the PQ stream image: keys + probe records
 // in the k_ivfpq_filter_w format (folded keys; the re-rank takes fold = 1)

@@ -538,298 +538,6 @@ __global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
     }
 }
 
-// ---------------------------------------------------------------- codes, folded
-// The default IVF-PQ filter (round 5): the IVF-Flat streamed filter's
-// arithmetic (k_ivf_bf2_stream<..., FOLD, PQ>: bf16 y_R fragments, the row's
-// -term/2 and the query's -coarse_dis/2 as a ninth k-step, accumulator =
-// -approx/2, one v_bfi_b32 per key, margins ivfpq_fold_coef) computed from the
-// M code bytes of each row instead of a decoded image: a lane's A fragment of
-// k-step s is gathered from the decode table in the LDS ([M][256][dsub] bf16,
-// loaded once per work group) — the same bf16 values the image held, so the
-// keys and probe records are bit for bit the image filter's and
-// k_ivf_rerank<..., PQD> reads them unchanged.  HBM per row: the code bytes
-// and the fp32 term (c3: 36 B instead of the image's 272 B).
-// Workers as k_ivfpq_filter_w: every wave is its own worker on a task = (work
-// item of <= FQ = 128 queries, query quarter bj); it loads its rows' code words
-// and terms itself, one 64-row tile ahead, so no barrier follows the table
-// load.  Gathers: one v_bfe_u32 + one address op + one LDS read per table
-// entry (the subquantizer's table base is an immediate offset).
-template <int DSUB>
-__device__ __forceinline__ bf16x8 pq_gather_frag(uint32_t w, int lh, const uint8_t* __restrict__ dec,
-                                                 int s) {
-    constexpr int E = 8 / DSUB;     // table entries per fragment
-    constexpr int EB = 2 * DSUB;    // bytes per entry
-    union {
-        uint32_t u[4];
-        bf16x8 v;
-    } cv;
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-        // subquantizer m = (16 s + 8 lh) / DSUB + e; its code byte is byte
-        // (m & 3) of word w (the caller picked the word holding it)
-        const int mb = (16 * s) / DSUB + e;  // lh = 0 (compile time)
-        const uint32_t boff = DSUB == 4 ? 8u * (uint32_t)(e + 2 * lh)
-                                        : DSUB == 2 ? 8u * (uint32_t)e
-                                                    : 8u * (uint32_t)(((2 * s) & 3) + lh);
-        const uint32_t j = __builtin_amdgcn_ubfe(w, boff, 8);
-        const uint8_t* src = dec + (size_t)mb * 256 * EB + (uint32_t)lh * (E * 256 * EB) + j * EB;
-        if constexpr (DSUB == 2) {
-            cv.u[e] = *(const uint32_t*)src;
-        } else if constexpr (DSUB == 4) {
-            const uint2 v = *(const uint2*)src;
-            cv.u[2 * e] = v.x;
-            cv.u[2 * e + 1] = v.y;
-        } else {
-            const uint4 v = *(const uint4*)src;
-            cv.u[0] = v.x;
-            cv.u[1] = v.y;
-            cv.u[2] = v.z;
-            cv.u[3] = v.w;
-        }
-    }
-    return cv.v;
-}
-// the code word holding a lane's bytes of k-step s
-template <int DSUB, int NWC>
-__device__ __forceinline__ uint32_t pq_frag_word(const uint32_t (&cw)[NWC], int lh, int s) {
-    if constexpr (DSUB == 4) return cw[s];                     // bytes 4 s .. 4 s + 3
-    else if constexpr (DSUB == 2) return lh ? cw[2 * s + 1] : cw[2 * s];
-    else return cw[s >> 1];                                    // byte 2 s + lh
-}
-
-template <int DSUB, int NS, int KT>
-__global__ __launch_bounds__(384, 3) void k_ivfpq_codes(
-        const __bf16* __restrict__ dec_g, const uint8_t* __restrict__ codes,
-        const float* __restrict__ terms, const float* __restrict__ cdis,
-        const float* __restrict__ cnorm, const float* __restrict__ lrmax,
-        const float* __restrict__ lRmax, int d, int nlist, int nprobe, float coef, int obits,
-        const uint32_t* __restrict__ item_off, const ItemDesc* __restrict__ item_desc,
-        const uint32_t* __restrict__ item_entries, const uint32_t* __restrict__ lim,
-        uint32_t* __restrict__ keys, ProbeRec* __restrict__ recs,
-        const uint8_t* __restrict__ qimg, const float* __restrict__ qxn) {
-    constexpr int D = 16 * NS;  // padded dims (DB of the Flat filter)
-    constexpr int NWC = (D / DSUB + 3) / 4;  // code words covering the padded dims
-    extern __shared__ __attribute__((aligned(16))) uint8_t dec[];  // [M][256][DSUB] bf16
-    const int M = d / DSUB, CS = (M + 3) & ~3;
-    const int nthr = blockDim.x, wpb = nthr >> 6;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    {
-        const int n16 = M * 256 * DSUB * 2 / 16;
-        const uint4* src = (const uint4*)dec_g;
-        for (int i = t; i < n16; i += nthr) ((uint4*)dec)[i] = src[i];
-    }
-    __syncthreads();  // the decode table (the only barrier)
-    const int li = lane & 31, lh = lane >> 5;
-    const uint32_t lowmask = (1u << obits) - 1u;
-    const uint32_t nitems = item_off[nlist];
-    const uint32_t ntask = 4u * nitems;
-    const uint32_t nstatic = gridDim.x * (uint32_t)wpb;
-    const int nwc = CS / 4;  // code words per row (runtime: M may be < D / DSUB)
-    for (uint32_t task = blockIdx.x * (uint32_t)wpb + (uint32_t)w; task < ntask;) {
-        const uint32_t nxt = task + nstatic;
-        const uint32_t it = task >> 2;
-        const int bj = (int)(task & 3u);
-        const ItemDesc dsc = item_desc[it];
-        const int nQ = (int)dsc.nq;
-        if (32 * bj >= nQ) {  // wave-uniform: this quarter of the item is empty
-            task = nxt;
-            continue;
-        }
-        const int l = (int)dsc.l;
-        const int len = (int)dsc.len;
-        const int64_t row0 = dsc.off;
-        const int qloc = 32 * bj + li;
-        const bool qvalid = qloc < nQ;
-        const uint32_t my_e = item_entries[(size_t)it * FQ + qloc];
-        const float cn_l = cnorm[l], rmax_l = lrmax[l], Rmax_l = lRmax[l];
-        bf16x8 bh[NS], bl[NS];
-        float xn = 0.f;
-        load_query_image<NS>(qimg, qxn, qvalid ? (int32_t)(my_e / (uint32_t)nprobe) : -1, lh,
-                             bh, bl, xn);
-        const float cd_e = cdis[qvalid ? my_e : 0u];
-        const uint32_t elen = (lim && qvalid) ? min((uint32_t)len, lim[my_e]) : (uint32_t)len;
-        // the bias B fragment {1, 1, 1, -coarse_dis/2 in three parts, 0, 0} (lh = 0)
-        bf16x8 bq;
-        {
-            __bf16 h, m, lo;
-            split3_bf16(-0.5f * cd_e, h, m, lo);
-            const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
-            bq[0] = lh ? zero : one;
-            bq[1] = lh ? zero : one;
-            bq[2] = lh ? zero : one;
-            bq[3] = lh ? zero : h;
-            bq[4] = lh ? zero : m;
-            bq[5] = lh ? zero : lo;
-            bq[6] = zero;
-            bq[7] = zero;
-        }
-        // code words and term of this lane's two rows (li, 32 + li) of a tile
-        // (rows past the list end read the slot's zero padding codes; their
-        // bias is -inf, so their keys sort after every real candidate)
-        uint32_t cw[2][NWC];
-        float tv[2];
-        auto load_rows = [&](int bi, int v0n) {
-            const int r = v0n + 32 * bi + li;
-            const uint8_t* cp = codes + (row0 + r) * CS;
-            if (CS % 16 == 0) {
-#pragma unroll
-                for (int i = 0; i < NWC; i += 4) {
-                    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                    if (i < nwc) v = *(const uint4*)(cp + 4 * i);
-                    cw[bi][i] = v.x;
-                    if (i + 1 < NWC) cw[bi][i + 1] = v.y;
-                    if (i + 2 < NWC) cw[bi][i + 2] = v.z;
-                    if (i + 3 < NWC) cw[bi][i + 3] = v.w;
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < NWC; i++) cw[bi][i] = i < nwc ? *(const uint32_t*)(cp + 4 * i) : 0u;
-            }
-            tv[bi] = r < len ? terms[row0 + r] : WS_INF;
-        };
-        load_rows(0, 0);
-        load_rows(1, 0);
-        ThreadQueue32<KT> tq[2];
-        tq[0].init();
-        tq[1].init();
-        const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
-        for (int v0 = 0, tile = 0; v0 < len; v0 += BV, tile++) {
-            const bool more = v0 + BV < len;
-            const uint32_t ordbase = (uint32_t)tile << 4;
-#pragma unroll
-            for (int bi = 0; bi < 2; bi++) {
-                // the row's bias A fragment {-term/2 in three parts, 1, 1, 1, 0, 0}
-                // (lh = 1 lanes: zero; padding rows: -inf)
-                bf16x8 ab;
-                {
-                    __bf16 h = (__bf16)(-WS_INF), m = zero, lo = zero;
-                    if (tv[bi] < WS_INF) split3_bf16(-0.5f * tv[bi], h, m, lo);
-                    ab[0] = lh ? zero : h;
-                    ab[1] = lh ? zero : m;
-                    ab[2] = lh ? zero : lo;
-                    ab[3] = lh ? zero : one;
-                    ab[4] = lh ? zero : one;
-                    ab[5] = lh ? zero : one;
-                    ab[6] = zero;
-                    ab[7] = zero;
-                }
-                floatx16 acc;
-#pragma unroll
-                for (int r = 0; r < 16; r++) acc[r] = 0.f;
-#pragma unroll
-                for (int s = 0; s < NS; s++) {
-                    bf16x8 ah = pq_gather_frag<DSUB>(pq_frag_word<DSUB, NWC>(cw[bi], lh, s), lh,
-                                                     dec, s);
-                    if (16 * s + 8 * lh >= d) {  // dims past d (padded D): zero
-#pragma unroll
-                        for (int j = 0; j < 8; j++) ah[j] = zero;
-                    }
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
-                }
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, bq, acc, 0, 0, 0);
-                // block bi decoded: its next rows load under the pushes
-                if (more) load_rows(bi, v0 + BV);
-                mfma_read_guard();  // key_insert reads acc (inline asm)
-#pragma unroll
-                for (int r = 0; r < 16; r++)
-                    tq[bi].push(key_insert(fold_key_bits(acc[r]), lowmask, ordbase | (uint32_t)r));
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        // ---- outputs: this lane's two streams (slot 2 bi + lh) of query qloc
-        const float xl = sqrtf(xn);
-        const float sr = xl + cn_l + Rmax_l;
-        const float mmax = 2.f * (2.f * xl * rmax_l + coef * sr * sr) + 1e-30f;
-        float pb[2];
-#pragma unroll
-        for (int bi = 0; bi < 2; bi++) {
-            const int slot = 2 * bi + lh;
-            const uint32_t last = tq[bi].q[KT - 1];
-            float bnd = WS_INF;
-            if (last != 0xffffffffu && (int)ivf_key_row(last, lowmask, slot) < len)
-                bnd = fold_decode_lo(last, lowmask);
-            pb[bi] = bnd < WS_INF ? bnd - mmax : WS_INF;
-            if (qvalid) {
-                uint32_t* ko = keys + (int64_t)my_e * (4 * KT) + slot * KT;
-#pragma unroll
-                for (int i = 0; i < KT; i++) {
-                    const uint32_t key = tq[bi].q[i];
-                    const uint32_t row = ivf_key_row(key, lowmask, slot);
-                    ko[i] = (key != 0xffffffffu && row < elen) ? key : 0xffffffffu;
-                }
-            }
-        }
-        // slots 1 and 3 live in the other lane half of the column
-        const float pb1 = __shfl_xor(pb[0], 32), pb3 = __shfl_xor(pb[1], 32);
-        if (qvalid && lh == 0) {
-            ProbeRec pr;
-            pr.pb[0] = pb[0];
-            pr.pb[1] = pb1;
-            pr.pb[2] = pb[1];
-            pr.pb[3] = pb3;
-            pr.mmax = mmax;
-            pr.off = (uint32_t)row0;
-            pr.len = elen;
-            pr.pad = (uint32_t)l;
-            recs[my_e] = pr;
-        }
-        task = nxt;
-    }
-}
-
-bool ivfpq_codes_eligible(int d, int M, int k, int nprobe) {
-    if (M <= 0 || d % M != 0 || d > BDM || k > 32 || nprobe > kMaxNprobeFilter) return false;
-    const int dsub = d / M, NS = bf3_db(d) / 16;
-    if (dsub != 2 && dsub != 4 && dsub != 8) return false;
-    return ivf_mfma_kq(k, d, nprobe) > 0 && (NS == 2 || NS == 4 || NS == 6 || NS == 8);
-}
-
-void ivfpq_codes_filter(int d, int M, const void* dec, const uint8_t* codes, const float* terms,
-                        const float* cdis, const float* cnorm, const float* lrmax,
-                        const float* lRmax, int nlist, int64_t n, int nprobe, int k, int obits,
-                        const IVFBuckets& b, int64_t max_items, uint32_t* keys, ProbeRec* recs,
-                        int* kt_out, hipStream_t s, const void* qimg, const float* qxn) {
-    FAISS_THROW_IF_NOT(ivfpq_codes_eligible(d, M, k, nprobe));
-    FAISS_THROW_IF_NOT(b.item_desc && b.item_entries && !b.sel);
-    FAISS_THROW_IF_NOT_MSG(qimg && qxn, "ivfpq_codes_filter needs the prepared query image");
-    FAISS_THROW_IF_NOT(obits >= 4 && obits <= 14);
-    const int KE = ivf_mfma_kq(k, d, nprobe);
-    *kt_out = KE / 4;
-    const int dsub = d / M, NS = bf3_db(d) / 16;
-    const size_t tbl = (size_t)M * 256 * dsub * 2;
-    int dev = 0, ncu = 256;
-    HIP_CHECK(hipGetDevice(&dev));
-    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    // as many 6-wave groups per CU as the LDS holds tables (c3: 64 KB, 2 per
-    // CU; c5: 48 KB, 3), every wave its own worker
-    const int groups = std::max(1, std::min(3, (int)((160 * 1024) / (tbl + 1024))));
-    const int wpb = 6;
-    const int64_t ntask = 4 * max_items;
-    const int64_t grid =
-            std::max<int64_t>(1, std::min<int64_t>(cdiv(ntask, wpb), (int64_t)ncu * groups));
-    const float coef = (float)ivfpq_fold_coef(d, M);
-#define PQC(DS, NSV, KTV)                                                                      \
-    if (dsub == DS && NS == NSV && KE / 4 == KTV) {                                            \
-        auto kfn = k_ivfpq_codes<DS, NSV, KTV>;                                                \
-        HIP_CHECK(hipFuncSetAttribute((const void*)kfn,                                        \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)tbl));  \
-        kfn<<<dim3((unsigned)grid), dim3(64 * wpb), tbl, s>>>(                                 \
-                (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, d, nlist, nprobe, \
-                coef, obits, b.item_off, b.item_desc, b.item_entries, b.lim, keys, recs,       \
-                (const uint8_t*)qimg, qxn);                                                    \
-        HIP_LAUNCH_CHECK();                                                                    \
-        return;                                                                                \
-    }
-#define PQC_KT(DS, NSV) PQC(DS, NSV, 2) PQC(DS, NSV, 4) PQC(DS, NSV, 8)
-#define PQC_NS(DS) PQC_KT(DS, 2) PQC_KT(DS, 4) PQC_KT(DS, 6) PQC_KT(DS, 8)
-    PQC_NS(2) PQC_NS(4) PQC_NS(8)
-#undef PQC_NS
-#undef PQC_KT
-#undef PQC
-    FAISS_THROW_MSG("ivfpq_codes_filter: no kernel instance for this geometry");
-}
-
 bool ivfpq_mfma_eligible(int d, int M, int k, int nprobe) {
     if (d % 16 != 0 || M <= 0 || d % M != 0 || k > 32 || nprobe > kMaxNprobeFilter) return false;
     const int dsub = d / M, NS = d / 16;
