@@ -5,6 +5,7 @@
 // message in a thread-local slot read by faiss_get_last_error()
 // (reference c_api/macros_impl.h:22-56, c_api/error_impl.cpp:15-26).
 #include <cmath>
+#include <limits>
 #include <cstring>
 #include <string>
 
@@ -737,6 +738,24 @@ int faiss_amd_set_kernel_timing_filter(const char* name) {
     C_TRY set_kernel_timing_filter(name);
     C_CATCH
 }
+namespace {
+// KernelTimes::resolve, leaving no HIP error behind: a pair whose events
+// never completed a record (a failed launch) reads NaN, and the error its
+// query returned is cleared rather than left for the caller's next check
+void resolve_times(KernelTimes* t) {
+    for (; t->resolved < t->e0.size(); t->resolved++) {
+        float ms = 0;
+        hipError_t e = hipEventSynchronize(t->e1[t->resolved]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, t->e0[t->resolved], t->e1[t->resolved]);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            ms = std::numeric_limits<float>::quiet_NaN();
+        }
+        t->millis.push_back(ms);
+    }
+}
+}  // namespace
+
 int faiss_amd_last_kernel_times(const FaissIndex* index, int* n_kernels, char* names,
                                 double* millis, double* units) {
     C_TRY const Index* ix = IX(index);
@@ -748,7 +767,7 @@ int faiss_amd_last_kernel_times(const FaissIndex* index, int* n_kernels, char* n
     }
     int cnt = 0;
     for (auto t : all) {
-        t->resolve();
+        resolve_times(t);
         cnt += (int)t->names.size();
     }
     if (names && millis) {

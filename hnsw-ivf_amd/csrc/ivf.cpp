@@ -389,6 +389,7 @@ void IndexIVF::SearchGraph::clear() {
     if (graph) (void)hipGraphDestroy(graph);
     exec = nullptr;
     graph = nullptr;
+    tsinks.clear();
     tnames.clear();
     tunits.clear();
     tnodes.clear();
@@ -436,10 +437,10 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     }
     char buf[512];
     const auto* pq = dynamic_cast<const IndexIVFPQ*>(this);
-    snprintf(buf, sizeof(buf), "%lld|%p|%d|%lld|%p|%p|%p|%zu|%zu|%d|%d|%lld|%llu|%llu|%llu|%d|%d|%d",
+    snprintf(buf, sizeof(buf), "%lld|%p|%d|%lld|%p|%p|%p|%zu|%zu|%d|%d|%lld|%llu|%p|%llu|%llu|%d|%d|%d",
              (long long)n, (const void*)x, ldx, (long long)k, (void*)distances, (void*)labels,
              (void*)s, nprobe, max_codes, parallel_mode, (int)metric_type, (long long)ntotal,
-             (unsigned long long)content_version(),
+             (unsigned long long)content_version(), (const void*)quantizer,
              (unsigned long long)quantizer->content_version(),
              (unsigned long long)devbuf_epoch().load(), device, pq ? pq->use_precomputed_table : -1,
              (int)by_residual);
@@ -452,10 +453,11 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
             HIP_CHECK(hipEventCreate(&b));
             HIP_CHECK(hipGraphExecEventRecordNodeSetEvent(graph_.exec, graph_.tnodes[i].first, a));
             HIP_CHECK(hipGraphExecEventRecordNodeSetEvent(graph_.exec, graph_.tnodes[i].second, b));
-            ktimes.names.push_back(graph_.tnames[i]);
-            ktimes.units.push_back(graph_.tunits[i]);
-            ktimes.e0.push_back(a);
-            ktimes.e1.push_back(b);
+            KernelTimes* t = graph_.tsinks[i];
+            t->names.push_back(graph_.tnames[i]);
+            t->units.push_back(graph_.tunits[i]);
+            t->e0.push_back(a);
+            t->e1.push_back(b);
         }
         // the graph writes this index's and the quantizer's scratch: wait
         // for their last users on other streams, as the eager path does
@@ -474,8 +476,24 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
         search_device_eager(n, x, ldx, k, distances, labels, params_in, s);
         return;
     }
-    // second identical call: capture it
-    const size_t t0 = ktimes.e0.size();
+    // second identical call: capture it (the stages timed in it are this
+    // index's and the quantizer's: sinks[j] from its entry t0s[j] on)
+    KernelTimes* sinks[2] = {&ktimes, &quantizer->ktimes};
+    const size_t t0s[2] = {ktimes.e0.size(), quantizer->ktimes.e0.size()};
+    auto drop_captured = [&] {
+        for (int j = 0; j < 2; j++) {
+            KernelTimes& t = *sinks[j];
+            const size_t t0 = t0s[j];
+            t.names.resize(std::min(t.names.size(), t0));
+            t.units.resize(std::min(t.units.size(), t0));
+            for (size_t i = t0; i < t.e0.size(); i++) {
+                (void)hipEventDestroy(t.e0[i]);
+                (void)hipEventDestroy(t.e1[i]);
+            }
+            t.e0.resize(t0);
+            t.e1.resize(t0);
+        }
+    };
     hipGraph_t gr = nullptr;
     if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
         (void)hipGetLastError();  // (e.g. the legacy default stream)
@@ -493,7 +511,19 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     hipGraphExec_t ex = nullptr;
     if (ok && e == hipSuccess && gr) e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
     // the timed stages' record nodes, matched by the events captured into them
-    std::vector<std::pair<hipGraphNode_t, hipGraphNode_t>> tn(ktimes.e0.size() - t0);
+    std::vector<std::pair<hipGraphNode_t, hipGraphNode_t>> tn;
+    std::vector<KernelTimes*> tsk;
+    std::vector<std::string> tnm;
+    std::vector<double> tun;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+    for (int j = 0; j < 2; j++)
+        for (size_t i = t0s[j]; i < sinks[j]->e0.size(); i++) {
+            tn.emplace_back(nullptr, nullptr);
+            tsk.push_back(sinks[j]);
+            tnm.push_back(sinks[j]->names[i]);
+            tun.push_back(sinks[j]->units[i]);
+            tev.emplace_back(sinks[j]->e0[i], sinks[j]->e1[i]);
+        }
     if (ok && e == hipSuccess && ex) {
         size_t nn = 0;
         e = hipGraphGetNodes(gr, nullptr, &nn);
@@ -505,9 +535,9 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
                 continue;
             hipEvent_t ev = nullptr;
             if (hipGraphEventRecordNodeGetEvent(nodes[j], &ev) != hipSuccess) continue;
-            for (size_t i = t0; i < ktimes.e0.size(); i++) {
-                if (ktimes.e0[i] == ev) tn[i - t0].first = nodes[j];
-                if (ktimes.e1[i] == ev) tn[i - t0].second = nodes[j];
+            for (size_t i = 0; i < tev.size(); i++) {
+                if (tev[i].first == ev) tn[i].first = nodes[j];
+                if (tev[i].second == ev) tn[i].second = nodes[j];
             }
         }
         for (auto& p : tn)
@@ -518,14 +548,8 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
         (void)hipGetLastError();
         if (ex) (void)hipGraphExecDestroy(ex);
         if (gr) (void)hipGraphDestroy(gr);
-        ktimes.names.resize(std::min(ktimes.names.size(), t0));
-        ktimes.units.resize(std::min(ktimes.units.size(), t0));
-        for (size_t i = t0; i < ktimes.e0.size(); i++) {
-            (void)hipEventDestroy(ktimes.e0[i]);
-            (void)hipEventDestroy(ktimes.e1[i]);
-        }
-        ktimes.e0.resize(t0);
-        ktimes.e1.resize(t0);
+        drop_captured();
+        (void)hipGetLastError();
         graph_.failed = true;
         search_device_eager(n, x, ldx, k, distances, labels, params_in, s);
         return;
@@ -533,8 +557,25 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     graph_.graph = gr;
     graph_.exec = ex;
     graph_.tnodes = tn;
-    graph_.tnames.assign(ktimes.names.begin() + t0, ktimes.names.end());
-    graph_.tunits.assign(ktimes.units.begin() + t0, ktimes.units.end());
+    graph_.tsinks = tsk;
+    graph_.tnames = tnm;
+    graph_.tunits = tun;
+    // the events captured are not recorded by the graph's launches (its
+    // nodes hold them only as handles): drop them, and time this first
+    // launch through the replay path's fresh events
+    drop_captured();
+    for (size_t i = 0; i < graph_.tnodes.size(); i++) {
+        hipEvent_t a, b;
+        HIP_CHECK(hipEventCreate(&a));
+        HIP_CHECK(hipEventCreate(&b));
+        HIP_CHECK(hipGraphExecEventRecordNodeSetEvent(ex, graph_.tnodes[i].first, a));
+        HIP_CHECK(hipGraphExecEventRecordNodeSetEvent(ex, graph_.tnodes[i].second, b));
+        KernelTimes* t = graph_.tsinks[i];
+        t->names.push_back(graph_.tnames[i]);
+        t->units.push_back(graph_.tunits[i]);
+        t->e0.push_back(a);
+        t->e1.push_back(b);
+    }
     HIP_CHECK(hipGraphLaunch(ex, s));
 }
 

@@ -351,7 +351,7 @@ __global__ __launch_bounds__(256, 3) void k_ivfpq_filter(
 // workers as its registers allow instead of as many 4-wave groups as its LDS
 // holds tables; waves desynchronise and hide each other's load latency.
 template <int DSUB, int NS, int KT, bool HS>
-__global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
+__global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
         const __bf16* __restrict__ dec_g, const uint8_t* __restrict__ codes,
         const float* __restrict__ terms, const float* __restrict__ cdis,
         const float* __restrict__ cnorm, const float* __restrict__ lrmax,
@@ -360,7 +360,10 @@ __global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
         const uint32_t* __restrict__ item_entries, const uint32_t* __restrict__ lim,
         const uint8_t* __restrict__ sel, uint32_t* __restrict__ keys,
         ProbeRec* __restrict__ recs, const uint8_t* __restrict__ qimg,
-        const float* __restrict__ qxn, uint32_t* __restrict__ task_ctr) {
+        const float* __restrict__ qxn, uint32_t* __restrict__ task_ctr,
+        unsigned long long* __restrict__ trace, int snake) {
+    // FAISS_AMD_PQ_TRACE=<file>: per task [start, prologue done, end, info]
+    // (s_memrealtime; info = len | nQ << 16 | bj << 24 | worker << 32)
     constexpr int D = 16 * NS;
     constexpr int M = D / DSUB;
     constexpr int CS = (M + 3) & ~3;  // code stride (bytes)
@@ -380,16 +383,30 @@ __global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
     const uint32_t nitems = item_off[nlist];
     const uint32_t ntask = 2u * nitems;
     const uint32_t nstatic = gridDim.x * (uint32_t)wpb;
-    // (a work counter fetched one task ahead measured slower on c3: 204 vs
-    // 170 us, same-address atomics from every wave; tasks are strided)
-    for (uint32_t task = blockIdx.x * (uint32_t)wpb + (uint32_t)w; task < ntask;) {
-        const uint32_t nxt = task + nstatic;
+    // Static rounds of nstatic tasks over the items in longest-list-first
+    // order (IVFBuckets::perm), walked boustrophedon (snake): worker w takes
+    // task w of even rounds and nstatic - 1 - w of odd ones, so a worker given
+    // a long task in one round gets a short one in the next and the last,
+    // partial round's (shortest) tasks go to the workers the previous round
+    // loaded least.  (r05 per-task trace on c3: the plain stride left workers
+    // 4 or 5 tasks each — busy p50 81 us, max 126 us; a work counter claimed
+    // per task was slower still, 0.20 vs 0.13 ms: the same-address atomics of
+    // 3072 waves serialise, and each wave's later loads return behind its
+    // claim.)  !snake: the plain stride.
+    const uint32_t wid = blockIdx.x * (uint32_t)wpb + (uint32_t)w;
+    uint32_t round = 0u;
+    for (uint32_t task = wid; task < ntask;) {
         const uint32_t it = task >> 1;
         const int bj = (int)(task & 1u);
+        auto next_task = [&]() -> uint32_t {
+            round++;
+            return round * nstatic + ((snake && (round & 1u)) ? nstatic - 1u - wid : wid);
+        };
+        const unsigned long long t_s = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
         const ItemDesc dsc = item_desc[it];
         const int nQ = (int)dsc.nq;
         if (32 * bj >= nQ) {  // wave-uniform: an item of <= 32 queries
-            task = nxt;
+            task = next_task();
             continue;
         }
         const int l = (int)dsc.l;
@@ -461,6 +478,14 @@ __global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
         ThreadQueue32<KT> tq[2];
         tq[0].init();
         tq[1].init();
+        unsigned long long t_p = 0ull;
+        if (trace) {  // (waits for the prologue's loads: profiling only)
+            float acc0 = base + xn;
+#pragma unroll
+            for (int i = 0; i < NWC; i++) acc0 += (float)(cw[0][i] & 1u);
+            if (__builtin_amdgcn_readfirstlane(__float_as_uint(acc0)) == 0xffffffffu) t_p = 1ull;
+            t_p += __builtin_amdgcn_s_memrealtime();
+        }
         for (int v0 = 0, tile = 0; v0 < len; v0 += BV, tile++) {
             const int buf = tile & 1;
             const bool more = v0 + BV < len;
@@ -534,7 +559,16 @@ __global__ __launch_bounds__(384, 3) void k_ivfpq_filter_w(
             pr.pad = (uint32_t)l;
             recs[my_e] = pr;
         }
-        task = nxt;
+        if (trace && lane == 0) {
+            unsigned long long* tr = trace + 4ull * task;
+            tr[0] = t_s;
+            tr[1] = t_p;
+            tr[2] = __builtin_amdgcn_s_memrealtime();
+            tr[3] = (unsigned long long)(uint32_t)len | ((unsigned long long)(uint32_t)nQ << 16) |
+                    ((unsigned long long)bj << 24) |
+                    ((unsigned long long)(blockIdx.x * (uint32_t)wpb + (uint32_t)w) << 32);
+        }
+        task = next_task();
     }
 }
 
@@ -568,18 +602,50 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(max_items, (int64_t)ncu * per_cu));
     const float coef = (float)ivfpq_mfma_coef(d, M);
     // wave-independent kernel (default; FAISS_AMD_PQ_FILTER=wg: the 4-wave
-    // work-group form): WPB waves per group sharing one table, as many groups
-    // per CU as the LDS holds, enough waves to reach 12 per CU
+    // work-group form): one group of 12 waves per CU sharing one table — the
+    // 3 waves per SIMD its registers allow (<= 168 VGPRs), 3 on every SIMD.
+    // (r05: two 6-wave groups per CU did not co-reside: each group's waves
+    // land 2, 2, 1, 1 on the SIMDs and a second one would need 4 on two of
+    // them, so half the groups waited for the first half to finish — c3's
+    // per-task trace showed 256 groups starting at 0 us and 256 at ~60 us.)
     const char* fenv = getenv("FAISS_AMD_PQ_FILTER");
     if (!(fenv && !strcmp(fenv, "wg")) && b.item_ctr) {
         const size_t tbl = lds;
-        const int g_lds = std::max(1, (int)((160 * 1024) / (tbl + 8 * 2 * BV * 4 + 1024)));
-        const int wpb = std::min(6, std::max(4, (12 + g_lds - 1) / g_lds));  // waves per group
-        const int groups = std::min(g_lds, std::max(1, 12 / wpb));
+        const char* wenv = getenv("FAISS_AMD_PQ_WPB");  // (A/B: waves per group)
+        const int wpb = std::max(1, std::min(12, wenv ? atoi(wenv) : 12));
+        const int groups = std::max(1, 12 / wpb);
         const size_t ldsw = tbl + (size_t)wpb * 2 * BV * sizeof(float);
+        FAISS_THROW_IF_NOT(ldsw <= 160 * 1024);
+        const char* denv = getenv("FAISS_AMD_PQ_SCHED");  // "stride": the plain stride (A/B)
+        const int snake = (denv && !strcmp(denv, "stride")) ? 0 : 1;
         const int64_t ntask = 2 * max_items;
         const int64_t gridw = std::max<int64_t>(
                 1, std::min<int64_t>(cdiv(ntask, wpb), (int64_t)ncu * groups));
+        // FAISS_AMD_PQ_TRACE=<file>: per-task stamps (profiling; synchronises)
+        static unsigned long long* trace_buf = nullptr;
+        static int64_t trace_n = 0;
+        const char* trf = getenv("FAISS_AMD_PQ_TRACE");
+        unsigned long long* trace = nullptr;
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (trf && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+            if (trace_n < ntask) {
+                if (trace_buf) HIP_CHECK(hipFree(trace_buf));
+                HIP_CHECK(hipMalloc(&trace_buf, 32 * ntask));
+                trace_n = ntask;
+            }
+            HIP_CHECK(hipMemsetAsync(trace_buf, 0, 32 * ntask, s));
+            trace = trace_buf;
+        }
+        auto dump = [&] {
+            if (!trace) return;
+            std::vector<unsigned long long> h(4 * ntask);
+            HIP_CHECK(hipMemcpyAsync(h.data(), trace, 32 * ntask, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            if (FILE* f = fopen(trf, "wb")) {
+                fwrite(h.data(), 8, h.size(), f);
+                fclose(f);
+            }
+        };
 #define PQW(DS, NSV, KTV)                                                                      \
     if (dsub == DS && NS == NSV && KE / 4 == KTV) {                                            \
         auto kfn = b.sel ? k_ivfpq_filter_w<DS, NSV, KTV, true>                                \
@@ -589,8 +655,9 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
         kfn<<<dim3((unsigned)gridw), dim3(64 * wpb), ldsw, s>>>(                               \
                 (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, nlist, nprobe,    \
                 coef, obits, b.item_off, b.item_desc, b.item_entries, b.lim, b.sel, keys,      \
-                recs, (const uint8_t*)qimg, qxn, b.item_ctr);                                  \
+                recs, (const uint8_t*)qimg, qxn, b.item_ctr, trace, snake);                    \
         HIP_LAUNCH_CHECK();                                                                    \
+        dump();                                                                                \
         return;                                                                                \
     }
 #define PQW_KT(DS, NSV) PQW(DS, NSV, 2) PQW(DS, NSV, 4) PQW(DS, NSV, 8)

@@ -593,7 +593,9 @@ struct IndexIVF : Index {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
         // the event-record nodes of the stages timed at capture (kernel
-        // timing): each replay records fresh events there
+        // timing; this index's and the quantizer's): each replay records
+        // fresh events there, listed in the owner's times (tsinks)
+        std::vector<KernelTimes*> tsinks;
         std::vector<std::string> tnames;
         std::vector<double> tunits;
         std::vector<std::pair<hipGraphNode_t, hipGraphNode_t>> tnodes;

@@ -43,7 +43,7 @@ class Bufs:
             self.hip.hipFree(p)
 
 
-@pytest.mark.parametrize("desc", ["IVF256,Flat", "IVF256,PQ16"])
+@pytest.mark.parametrize("desc", ["IVF256,Flat", "IVF256,PQ16", "IVF2048,PQ16"])
 def test_graph_replay_equals_eager(amd, gpu, monkeypatch, desc):
     d, nb, nq, k = 64, 60_000, 3000, 10
     xb = amd.float_rand(nb * d, 1234).reshape(nb, d)
@@ -61,23 +61,33 @@ def test_graph_replay_equals_eager(amd, gpu, monkeypatch, desc):
             D, I = b.search(idx)
             np.testing.assert_array_equal(I, ref[1])
             np.testing.assert_array_equal(D, ref[0])
-        # kernel timing: the same records per call as the eager path (the
-        # replays record fresh events at the timed stages' nodes)
+        # kernel timing: the same records per call as the eager path, the
+        # quantizer's stages included (the capture and the replays record
+        # fresh events at the timed stages' nodes), every one a completed
+        # measurement, and no HIP error left behind by reading them (r05: the
+        # captured events read "invalid resource handle", picked up by the
+        # caller's next HIP check)
         import collections
-        amd.set_kernel_timing(True)
         counts = []
-        for genv in ("0", None):
-            if genv:
-                monkeypatch.setenv("FAISS_AMD_GRAPH", genv)
-            else:
-                monkeypatch.delenv("FAISS_AMD_GRAPH")
-            idx.reset_kernel_times()
-            for _ in range(4):
-                b.search(idx)
-            counts.append(collections.Counter(nm for nm, ms, _ in idx.kernel_times()
-                                              if ms > 0))
+        for only in (None, "coarse_filter"):
+            amd.set_kernel_timing(True, only=only)
+            for genv in ("0", None):
+                if genv:
+                    monkeypatch.setenv("FAISS_AMD_GRAPH", genv)
+                else:
+                    monkeypatch.delenv("FAISS_AMD_GRAPH")
+                idx.reset_kernel_times()
+                for _ in range(4):
+                    b.search(idx)
+                kt = idx.kernel_times()
+                assert b.hip.hipGetLastError() == 0
+                assert all(np.isfinite(ms) and ms > 0 for _, ms, _ in kt), kt
+                counts.append(collections.Counter(nm for nm, _, _ in kt))
         amd.set_kernel_timing(False)
         assert counts[0] and counts[0] == counts[1], counts
+        assert counts[2] == counts[3], counts
+        if "coarse_filter" in counts[0]:  # (the quantizer's MFMA path ran)
+            assert counts[2] == collections.Counter({"coarse_filter": 4}), counts
         # a change the host sees retires the graph
         idx.nprobe = 8
         monkeypatch.setenv("FAISS_AMD_GRAPH", "0")
