@@ -1411,6 +1411,9 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         const bool stream = pq_stream_ready_ && !sel && fenv && !strcmp(fenv, "image") &&
                             qimg_ok && kern::ivfpq_stream_eligible(d, (int)pq.M, (int)k, np);
         const int QT = stream ? kern::IVF_FLAT_QT : 64;
+        // folded-bias keys: the image filter and k_ivfpq_filter_w (not its
+        // 4-wave group form, FAISS_AMD_PQ_FILTER=wg)
+        const bool pq_fold = stream || !(fenv && !strcmp(fenv, "wg"));
         uint32_t* counts_next = nullptr;
         uint32_t* counts = bucket_counts(s, &counts_next);
         s_cur_.reserve(sizeof(uint32_t) * std::max<idx_t>(n * np, 1));
@@ -1487,7 +1490,7 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
                                d_ids_.as<int64_t>(), pa, (int)pq.dsub, n, np, KT, pq_obits_,
                                (int)k, sel, distances, labels,
                                dbg ? s_pflags_.as<uint32_t>() : nullptr, s, qdone_,
-                               stream ? 1 : 0);
+                               pq_fold ? 1 : 0);
         }
         if (dbg) {
             uint32_t st[4];

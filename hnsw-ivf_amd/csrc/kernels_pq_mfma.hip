@@ -361,7 +361,7 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
         const uint8_t* __restrict__ sel, uint32_t* __restrict__ keys,
         ProbeRec* __restrict__ recs, const uint8_t* __restrict__ qimg,
         const float* __restrict__ qxn, uint32_t* __restrict__ task_ctr,
-        unsigned long long* __restrict__ trace, int snake) {
+        unsigned long long* __restrict__ trace, int sched) {
     // FAISS_AMD_PQ_TRACE=<file>: per task [start, prologue done, end, info]
     // (s_memrealtime; info = len | nQ << 16 | bj << 24 | worker << 32)
     constexpr int D = 16 * NS;
@@ -370,43 +370,63 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
     constexpr int NWC = CS / 4;
     constexpr int TBL = M * 256 * DSUB * 2;  // decode table bytes
     extern __shared__ __attribute__((aligned(16))) uint8_t dec[];  // table | per-wave terms
+    __shared__ uint32_t grp_next;  // the group's next task position (sched & 2)
     const int nthr = blockDim.x, wpb = nthr >> 6;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     {
         const uint4* src = (const uint4*)dec_g;
         for (int i = t; i < TBL / 16; i += nthr) ((uint4*)dec)[i] = src[i];
     }
+    if (t == 0) grp_next = (uint32_t)wpb;
     __syncthreads();  // the decode table (the only barrier)
-    float* ynt = (float*)(dec + TBL) + w * 2 * BV;  // this wave's [2][BV] terms
     const int li = lane & 31, lh = lane >> 5;
     const uint32_t lowmask = (1u << obits) - 1u;
     const uint32_t nitems = item_off[nlist];
     const uint32_t ntask = 2u * nitems;
     const uint32_t nstatic = gridDim.x * (uint32_t)wpb;
-    // Static rounds of nstatic tasks over the items in longest-list-first
-    // order (IVFBuckets::perm), walked boustrophedon (snake): worker w takes
-    // task w of even rounds and nstatic - 1 - w of odd ones, so a worker given
-    // a long task in one round gets a short one in the next and the last,
-    // partial round's (shortest) tasks go to the workers the previous round
-    // loaded least.  (r05 per-task trace on c3: the plain stride left workers
-    // 4 or 5 tasks each — busy p50 81 us, max 126 us; a work counter claimed
-    // per task was slower still, 0.20 vs 0.13 ms: the same-address atomics of
-    // 3072 waves serialise, and each wave's later loads return behind its
-    // claim.)  !snake: the plain stride.
-    const uint32_t wid = blockIdx.x * (uint32_t)wpb + (uint32_t)w;
-    uint32_t round = 0u;
-    for (uint32_t task = wid; task < ntask;) {
+    // Work assignment.  Static rounds of nstatic tasks over the items in
+    // longest-list-first order (IVFBuckets::perm): position p of round r
+    // (worker p of the grid) is task r nstatic + p, walked boustrophedon
+    // (sched & 1: nstatic - 1 - p in odd rounds), so a position given a long
+    // task in one round gets a short one in the next.  sched & 2: the group's
+    // waves share its positions (blockIdx wpb + 0 .. wpb - 1 of every round)
+    // and take the next one from an LDS counter when they finish a task, so a
+    // CU's waves end together instead of a third of the span in the CU's own
+    // tail (r05 per-task traces: with fixed positions the first wave of a CU
+    // finished at 56 % (c3) / 77 % (c5) of the last one's end).  A global work
+    // counter measured slower (c3 0.20 vs 0.13 ms): the same-address atomics
+    // of 3072 waves serialise and each wave's later loads return behind its
+    // claim.
+    const uint32_t g0 = blockIdx.x * (uint32_t)wpb;
+    const bool share = (sched & 2) != 0;
+    const uint32_t cycle = share ? (uint32_t)wpb : 1u;  // positions per round per claimer
+    uint32_t j = share ? (uint32_t)w : 0u;               // position index (this group / wave)
+    auto task_of = [&](uint32_t jj) -> uint32_t {
+        const uint32_t r = jj / cycle;
+        const uint32_t p = share ? g0 + jj % cycle : g0 + (uint32_t)w;
+        return r * nstatic + (((sched & 1) && (r & 1u)) ? nstatic - 1u - p : p);
+    };
+    auto next_pos = [&]() -> uint32_t {
+        if (!share) return j + 1u;
+        uint32_t v = 0u;
+        if (lane == 0) v = atomicAdd(&grp_next, 1u);
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    };
+    // (a round whose first task is past the end ends the walk; within the
+    // last round a position past the end is skipped)
+    for (; (j / cycle) * nstatic < ntask;) {
+        const uint32_t task = task_of(j);
+        if (task >= ntask) {
+            j = next_pos();
+            continue;
+        }
         const uint32_t it = task >> 1;
         const int bj = (int)(task & 1u);
-        auto next_task = [&]() -> uint32_t {
-            round++;
-            return round * nstatic + ((snake && (round & 1u)) ? nstatic - 1u - wid : wid);
-        };
         const unsigned long long t_s = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
         const ItemDesc dsc = item_desc[it];
         const int nQ = (int)dsc.nq;
         if (32 * bj >= nQ) {  // wave-uniform: an item of <= 32 queries
-            task = next_task();
+            j = next_pos();
             continue;
         }
         const int l = (int)dsc.l;
@@ -423,8 +443,11 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
                              bh, bl, xn);
         const float base = cdis[qvalid ? my_e : 0u];
         const uint32_t elen = (lim && qvalid) ? min((uint32_t)len, lim[my_e]) : (uint32_t)len;
-        // code words of this lane's two rows (li, 32 + li) of a tile
+        // code words and term of this lane's two rows (li, 32 + li) of a tile
+        // (rows past the list, and IDSelector non-members, get term +inf: the
+        // padding key, sorted after every real one)
         uint32_t cw[2][NWC];
+        float tv[2];
         auto load_codes = [&](int bi, int v0n) {
             const int r = v0n + 32 * bi + li;
             const uint8_t* cp = codes + (row0 + (r < len ? r : 0)) * CS;
@@ -441,56 +464,61 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
 #pragma unroll
                 for (int i = 0; i < NWC; i++) cw[bi][i] = *(const uint32_t*)(cp + 4 * i);
             }
-        };
-        // the tile's 64 terms: lanes 0..15 load a float4 each, stored masked
-        float4 traw = make_float4(0.f, 0.f, 0.f, 0.f);
-        uchar4 mraw = make_uchar4(1, 1, 1, 1);
-        auto load_terms = [&](int v0n) {
-            const int r = 4 * lane;
-            if (lane < BV / 4 && r < len - v0n) {
-                traw = *(const float4*)(terms + row0 + v0n + r);
-                if constexpr (HS) mraw = *(const uchar4*)(sel + row0 + v0n + r);
-            }
-        };
-        auto store_terms = [&](int buf, int v0n) {
-            if (lane < BV / 4) {
-                const int r = 4 * lane;
-                const int nvn = min(BV, len - v0n);
-                float4 tn;
-                if constexpr (HS) {
-                    // non-members of an IDSelector are treated as padding rows
-                    tn.x = r + 0 < nvn && mraw.x ? traw.x : WS_INF;
-                    tn.y = r + 1 < nvn && mraw.y ? traw.y : WS_INF;
-                    tn.z = r + 2 < nvn && mraw.z ? traw.z : WS_INF;
-                    tn.w = r + 3 < nvn && mraw.w ? traw.w : WS_INF;
-                } else {
-                    tn.x = r + 0 < nvn ? traw.x : WS_INF;
-                    tn.y = r + 1 < nvn ? traw.y : WS_INF;
-                    tn.z = r + 2 < nvn ? traw.z : WS_INF;
-                    tn.w = r + 3 < nvn ? traw.w : WS_INF;
-                }
-                *(float4*)(&ynt[buf * BV + r]) = tn;
+            tv[bi] = r < len ? terms[row0 + r] : WS_INF;
+            if constexpr (HS) {
+                if (r < len && !sel[row0 + r]) tv[bi] = WS_INF;
             }
         };
         load_codes(0, 0);
         load_codes(1, 0);
-        load_terms(0);
+        // folded bias (as the Flat filter's fold images): one more k-step with
+        // A = {-term/2 in three bf16 parts, 1, 1, 1, 0, 0} (the row, lh = 0
+        // lanes; zeros for lh = 1) and B = {1, 1, 1, -coarse_dis/2 in three
+        // parts, 0, 0}, so the accumulator is -approx/2 of coarse_dis + term -
+        // 2 <x, y_R> and a key is one v_bfi_b32 of its bits (ivfpq_fold_coef
+        // covers the six bias products; r05: 7 VALU per candidate before)
+        bf16x8 bq;
+        {
+            __bf16 h, m, lo;
+            split3_bf16(-0.5f * base, h, m, lo);
+            const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
+            bq[0] = lh ? zero : one;
+            bq[1] = lh ? zero : one;
+            bq[2] = lh ? zero : one;
+            bq[3] = lh ? zero : h;
+            bq[4] = lh ? zero : m;
+            bq[5] = lh ? zero : lo;
+            bq[6] = zero;
+            bq[7] = zero;
+        }
+        auto bias_frag = [&](float term) {
+            __bf16 h, m, lo;
+            split3_bf16(-0.5f * term, h, m, lo);
+            const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
+            bf16x8 ab;
+            ab[0] = lh ? zero : h;
+            ab[1] = lh ? zero : m;
+            ab[2] = lh ? zero : lo;
+            ab[3] = lh ? zero : one;
+            ab[4] = lh ? zero : one;
+            ab[5] = lh ? zero : one;
+            ab[6] = zero;
+            ab[7] = zero;
+            return ab;
+        };
         ThreadQueue32<KT> tq[2];
         tq[0].init();
         tq[1].init();
         unsigned long long t_p = 0ull;
         if (trace) {  // (waits for the prologue's loads: profiling only)
-            float acc0 = base + xn;
+            float acc0 = base + xn + tv[0];
 #pragma unroll
             for (int i = 0; i < NWC; i++) acc0 += (float)(cw[0][i] & 1u);
             if (__builtin_amdgcn_readfirstlane(__float_as_uint(acc0)) == 0xffffffffu) t_p = 1ull;
             t_p += __builtin_amdgcn_s_memrealtime();
         }
         for (int v0 = 0, tile = 0; v0 < len; v0 += BV, tile++) {
-            const int buf = tile & 1;
             const bool more = v0 + BV < len;
-            store_terms(buf, v0);  // (wave-private: ordered by the wave's own lgkm waits)
-            if (more) load_terms(v0 + BV);
             const uint32_t ordbase = (uint32_t)tile << 4;
 #pragma unroll
             for (int bi = 0; bi < 2; bi++) {
@@ -503,19 +531,14 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
                 }
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bias_frag(tv[bi]), bq, acc, 0, 0, 0);
                 // block bi decoded: its next code words load under the pushes
                 if (more) load_codes(bi, v0 + BV);
+                mfma_read_guard();  // key_insert reads acc (inline asm)
 #pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const float4 yq = *(const float4*)(&ynt[buf * BV + 32 * bi + 4 * lh + 8 * g]);
-#pragma unroll
-                    for (int c = 0; c < 4; c++) {
-                        const int r = 4 * g + c;
-                        const float yv = c == 0 ? yq.x : c == 1 ? yq.y : c == 2 ? yq.z : yq.w;
-                        const float a = fmaf(-2.f, acc[r], base + yv);
-                        tq[bi].push(key_encode<true>(a, lowmask, ordbase | (uint32_t)r));
-                    }
-                }
+                for (int r = 0; r < 16; r++)
+                    tq[bi].push(key_insert(fold_key_bits(acc[r]), lowmask, ordbase | (uint32_t)r));
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
         // ---- outputs: this lane's two streams (slot 2 bi + lh) of query qloc
@@ -529,7 +552,7 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
             const uint32_t last = tq[bi].q[KT - 1];
             float bnd = WS_INF;
             if (last != 0xffffffffu && (int)ivf_key_row(last, lowmask, slot) < len)
-                bnd = key_decode_lo<true>(last, lowmask);
+                bnd = fold_decode_lo(last, lowmask);
             pb[bi] = bnd < WS_INF ? bnd - mmax : WS_INF;
             if (qvalid) {
                 uint32_t* ko = keys + (int64_t)my_e * (4 * KT) + slot * KT;
@@ -568,7 +591,7 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
                     ((unsigned long long)bj << 24) |
                     ((unsigned long long)(blockIdx.x * (uint32_t)wpb + (uint32_t)w) << 32);
         }
-        task = next_task();
+        j = next_pos();
     }
 }
 
@@ -614,10 +637,13 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
         const char* wenv = getenv("FAISS_AMD_PQ_WPB");  // (A/B: waves per group)
         const int wpb = std::max(1, std::min(12, wenv ? atoi(wenv) : 12));
         const int groups = std::max(1, 12 / wpb);
-        const size_t ldsw = tbl + (size_t)wpb * 2 * BV * sizeof(float);
+        const size_t ldsw = tbl;
         FAISS_THROW_IF_NOT(ldsw <= 160 * 1024);
-        const char* denv = getenv("FAISS_AMD_PQ_SCHED");  // "stride": the plain stride (A/B)
-        const int snake = (denv && !strcmp(denv, "stride")) ? 0 : 1;
+        const float coefw = (float)ivfpq_fold_coef(d, M);  // (folded bias keys)
+        // FAISS_AMD_PQ_SCHED (A/B): "stride" (fixed positions, plain stride),
+        // "snake" (fixed positions, boustrophedon); default: shared, snake
+        const char* denv = getenv("FAISS_AMD_PQ_SCHED");
+        const int sched = !denv ? 3 : !strcmp(denv, "stride") ? 0 : !strcmp(denv, "snake") ? 1 : 3;
         const int64_t ntask = 2 * max_items;
         const int64_t gridw = std::max<int64_t>(
                 1, std::min<int64_t>(cdiv(ntask, wpb), (int64_t)ncu * groups));
@@ -654,8 +680,8 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsw)); \
         kfn<<<dim3((unsigned)gridw), dim3(64 * wpb), ldsw, s>>>(                               \
                 (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, nlist, nprobe,    \
-                coef, obits, b.item_off, b.item_desc, b.item_entries, b.lim, b.sel, keys,      \
-                recs, (const uint8_t*)qimg, qxn, b.item_ctr, trace, snake);                    \
+                coefw, obits, b.item_off, b.item_desc, b.item_entries, b.lim, b.sel, keys,      \
+                recs, (const uint8_t*)qimg, qxn, b.item_ctr, trace, sched);                    \
         HIP_LAUNCH_CHECK();                                                                    \
         dump();                                                                                \
         return;                                                                                \

@@ -259,6 +259,32 @@ def test_coarse_bf3_equals_f32_tile_and_oracle(amd, orc, gpu, monkeypatch, metri
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("metric", [1, 0])
+@pytest.mark.parametrize("k,nsplit", [(64, 64), (40, 64), (64, 16), (10, 0)])
+def test_coarse_bf3_wide_splits(amd, orc, gpu, monkeypatch, metric, k, nsplit):
+    # 64 splits x 4 thread streams of KT = 4 (r05: c5's coarse plan): 256
+    # streams per query, dropped bounds of streams lane + 64 h in the
+    # re-rank.  A tight cluster inside the first split puts far more than KT
+    # of a nearby query's top-k in single streams (those streams fail and
+    # are re-scanned exactly); duplicated rows give ties at the k boundary.
+    d, ny = 64, 65536
+    y = rand(orc, ny, d, 43)
+    rng = np.random.default_rng(7)
+    y[:300] = y[0] + 1e-3 * rng.standard_normal((300, d)).astype(np.float32)
+    y[ny // 2: ny // 2 + 40] = y[1000:1040]
+    x = np.ascontiguousarray(np.concatenate([rand(orc, 150, d, 44), y[:10] + 1e-3, y[1000:1010]]))
+    idx = amd.IndexFlat(d, metric)
+    idx.add(y)
+    monkeypatch.setenv("FAISS_AMD_COARSE_WIDE", "1")
+    if nsplit:
+        monkeypatch.setenv("FAISS_AMD_COARSE_NSPLIT", str(nsplit))
+    monkeypatch.setenv("FAISS_AMD_COARSE", "bf3")
+    Db, Ib = idx.search(x, k)
+    Dr, Ir = orc.knn(x, y, k, metric=metric, blas_form=True)
+    assert_same_results(Db, Ib, Dr, Ir)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k", [1, 10, 32])
 def test_filter_precisions_identical(amd, orc, cfg1, monkeypatch, k):
     # bf16x2 / bf16x3 filters and the direct exact scan return the same result
