@@ -74,7 +74,8 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 ROUND = 5
 PMC_SYMBOL = {
     "ivf_flat_scan": r"kern::k_ivf_bf2_stream<true, \d+, \d+, false, true, false>",
-    "ivfpq_filter": r"kern::k_ivfpq_filter_w<",
+    # (rocprofv3 leaves this one mangled: its name holds a __bf16, "DF16b")
+    "ivfpq_filter": r"kern::k_ivfpq_filter_w<|k_ivfpq_filter_wILi",
     "coarse_filter": r"kern::k_coarse_stream<",
     "hnsw_search": r"kern::k_hnsw_search<",
     "hnsw_exact": r"kern::k_hnsw_exact_reg<",
