@@ -78,7 +78,7 @@ PMC_SYMBOL = {
     "ivfpq_filter": r"kern::k_ivfpq_filter_w<|k_ivfpq_filter_wILi",
     "coarse_filter": r"kern::k_coarse_stream<",
     "hnsw_search": r"kern::k_hnsw_search<",
-    "hnsw_exact": r"kern::k_hnsw_exact_reg<",
+    "hnsw_exact": r"kern::k_hnsw_exact(_reg)?[<(]",
     "ivf_rerank": r"kern::k_ivf_rerank<true, \d+, 0>",
     "ivfpq_rerank": r"kern::k_ivf_rerank<true, \d+, [1-9]\d*>",
     "coarse_rerank": r"kern::k_coarse_rerank<",
@@ -509,16 +509,23 @@ def main():
         f32, q8 = amd.cvar.hnsw_row_stats
         work["hnsw_fp32_rows"], work["hnsw_q8_rows"] = float(f32), float(q8)
     kernels = []
+    # PMC summaries are per workload: a grid point (--nprobe / --efsearch)
+    # reads its own (profiles/rNN_<config>_np<P>_ef<E>_pmc.json), never the
+    # default point's, whose kernels differ (c4 at efSearch 768 runs the
+    # sequential HNSW kernel)
+    pmc_key = args.config
+    if args.nprobe or args.efsearch:
+        pmc_key = f"{args.config}_np{nprobe}_ef{cfg.get('efSearch', 0)}"
     for nm, ms in sorted(brk.items(), key=lambda kv: -kv[1]):
         if ms < 0.1 * ms_per_step and nm != dom:
             continue
         ent = {"name": nm, "ms_per_step": ms, "frac_of_step": ms / ms_per_step}
-        rf = kernel_roofline(nm, ms, work, args.config)
+        rf = kernel_roofline(nm, ms, work, pmc_key)
         if rf is not None:
             ent["roofline_frac"] = rf["frac"]
             ent["bound"] = rf["bound"]
         kernels.append(ent)
-    roofline = kernel_roofline(dom, dom_ms, work, args.config) if dom else None
+    roofline = kernel_roofline(dom, dom_ms, work, pmc_key) if dom else None
     if roofline is None and dom:
         roofline = {"bound": "latency", "achieved": None, "peak": None, "unit": None,
                     "frac": None, "traffic": None}
