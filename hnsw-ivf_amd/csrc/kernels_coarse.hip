@@ -540,12 +540,7 @@ struct CoarseStream {
     uint32_t lowmask;
     bool overflow;
     bool fold;                 // folded filter keys (ivf_decode_lo)
-    // failing streams: bit st & 63 of fmask[st >> 6], st = 4 * split + slot
-    // (up to 64 splits)
-    unsigned long long fmask[4];
-    __device__ __forceinline__ bool fails(int st) const {
-        return ((fmask[st >> 6] >> (st & 63)) & 1ull) != 0ull;
-    }
+    unsigned long long fmask;  // failing streams: bit 4 * split + slot
 
     __device__ __forceinline__ void emit(bool ok, int j, float& k1, long long& k2) const {
         k1 = WS_INF;
@@ -570,7 +565,7 @@ struct CoarseStream {
             const int st = c < E ? c / KT : 0;  // stream 4 * split + slot
             bool ok = false;
             int j = 0;
-            if (c < E && !fails(st)) {
+            if (c < E && !((fmask >> st) & 1ull)) {
                 const uint32_t key = keys[c];
                 ok = key != 0xffffffffu && ivf_decode_lo<L2>(key, lowmask, fold) - M <= U;
                 j = (st >> 2) * split_len + (int)ivf_key_row(key, lowmask, st & 3);
@@ -581,22 +576,20 @@ struct CoarseStream {
             emit(ok, j, k1, k2);
             f(ok && key_admissible(k1), k1, k2, (long long)j);
         }
-        for (int h = 0; h < 4; h++) {
-            unsigned long long m = fmask[h];
-            while (m) {
-                const int sidx = __ffsll((long long)m) - 1 + 64 * h;
-                m &= m - 1ull;
-                const int sp = sidx >> 2, slot = sidx & 3;
-                const int j0 = sp * split_len, j1 = min(nlist, j0 + split_len);
-                const int ne = (int)cdiv_dev((uint32_t)(j1 - j0), BV) * 16;
-                for (int e0 = 0; e0 < ne; e0 += 64) {
-                    const int j = j0 + ivf_stream_row(e0 + lane, slot);
-                    const bool ok = e0 + lane < ne && j < j1;
-                    float k1;
-                    long long k2;
-                    emit(ok, j, k1, k2);
-                    f(ok && key_admissible(k1), k1, k2, (long long)j);
-                }
+        unsigned long long m = fmask;
+        while (m) {
+            const int sidx = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const int sp = sidx >> 2, slot = sidx & 3;
+            const int j0 = sp * split_len, j1 = min(nlist, j0 + split_len);
+            const int ne = (int)cdiv_dev((uint32_t)(j1 - j0), BV) * 16;
+            for (int e0 = 0; e0 < ne; e0 += 64) {
+                const int j = j0 + ivf_stream_row(e0 + lane, slot);
+                const bool ok = e0 + lane < ne && j < j1;
+                float k1;
+                long long k2;
+                emit(ok, j, k1, k2);
+                f(ok && key_admissible(k1), k1, k2, (long long)j);
             }
         }
     }
@@ -638,11 +631,7 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
     const bool has = lane * V < E;
 #pragma unroll
     for (int i = 0; i < V; i++) kv[i] = has ? kq[lane * V + i] : 0xffffffffu;
-    // the streams' dropped bounds: lane holds streams lane + 64 h
-    float my_pb[4];
-#pragma unroll
-    for (int h = 0; h < 4; h++)
-        my_pb[h] = (valid && 64 * h + lane < NST) ? pbs[q * NST + 64 * h + lane] : WS_INF;
+    const float my_pb = (valid && lane < NST) ? pbs[q * NST + lane] : WS_INF;
     const float xn = xnorm ? xnorm[q] : 0.f;
     const float* xq = x + q * ldx;
     if (lane < BDM / 4 && 4 * lane < ((d + 3) & ~3))
@@ -656,18 +645,16 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
     float U = wave_kth_smallest<V>(ub, k);
     const unsigned long long t_u = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (!(U <= WS_INF)) U = WS_INF;
-    unsigned long long fmask[4];
-#pragma unroll
-    for (int h = 0; h < 4; h++) fmask[h] = __ballot(my_pb[h] < WS_INF && my_pb[h] <= U);
-    auto fails = [&](int st) { return ((fmask[st >> 6] >> (st & 63)) & 1ull) != 0ull; };
+    const unsigned long long fmask = __ballot(my_pb < WS_INF && my_pb <= U);
+    const int lst = has ? lane * V / KT : 0;  // this lane's stream (V <= KT)
+    const bool lfail = (fmask >> lst) & 1ull;
     // ---- candidates -> LDS
     int ns = 0;
 #pragma unroll
     for (int i = 0; i < V; i++) {
         bool sv = false;
         uint32_t j = 0;
-        const int lst = (lane * V + i) / KT;  // this key's stream
-        if (kv[i] != 0xffffffffu && !fails(lst)) {
+        if (kv[i] != 0xffffffffu && !lfail) {
             sv = ivf_decode_lo<L2>(kv[i], lowmask, fold) - M <= U;
             j = (uint32_t)((lst >> 2) * split_len) + ivf_key_row(kv[i], lowmask, lst & 3);
         }
@@ -676,10 +663,10 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
         if (sv && pos < CR_CAP) surv[pos] = j;
         ns += __popcll(m);
     }
-    for (int h = 0; h < 4; h++) {
-        unsigned long long m = fmask[h];
+    {
+        unsigned long long m = fmask;
         while (m) {
-            const int sidx = __ffsll((long long)m) - 1 + 64 * h;
+            const int sidx = __ffsll((long long)m) - 1;
             m &= m - 1ull;
             const int sp = sidx >> 2, slot = sidx & 3;
             const int j0 = sp * split_len, j1 = min(nlist, j0 + split_len);
@@ -717,8 +704,7 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
     st.lowmask = lowmask;
     st.overflow = ns > CR_CAP;
     st.fold = fold;
-#pragma unroll
-    for (int h = 0; h < 4; h++) st.fmask[h] = fmask[h];
+    st.fmask = fmask;
     bool done = false;
     unsigned long long t_e = 0ull;
     auto small = [&](auto nbc) {
@@ -771,18 +757,14 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
     if (trace && valid && lane == 0) {  // FAISS_AMD_CRERANK_TRACE (scripts/rtrace_summary.py)
         trace[8 * q + 0] = t_start;
         trace[8 * q + 1] = __builtin_amdgcn_s_memrealtime();
-        trace[8 * q + 2] = (unsigned long long)ns |
-                           ((unsigned long long)(__popcll(fmask[0]) + __popcll(fmask[1]) +
-                                                 __popcll(fmask[2]) + __popcll(fmask[3]))
-                            << 32);
+        trace[8 * q + 2] = (unsigned long long)ns | ((unsigned long long)__popcll(fmask) << 32);
         trace[8 * q + 3] = t_u;
         trace[8 * q + 4] = t_c;
         trace[8 * q + 5] = t_e;
     }
     if (stats && valid && lane == 0) {
         atomicAdd(&stats[0], (uint32_t)min(ns, CR_CAP));
-        atomicAdd(&stats[1], (uint32_t)(__popcll(fmask[0]) + __popcll(fmask[1]) +
-                                        __popcll(fmask[2]) + __popcll(fmask[3])));
+        atomicAdd(&stats[1], (uint32_t)__popcll(fmask));
         atomicAdd(&stats[2], st.overflow ? 1u : 0u);
         atomicAdd(&stats[3], done ? 0u : 1u);
     }
@@ -808,18 +790,11 @@ CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k) {
     CoarsePlan p{};
     if (n < 20 || nlist <= 0 || k < 1 || k > kMaxK || bf3_db(d) > BDM)
         return p;
-    // At most 64 splits (the re-rank keeps the dropped bounds of streams
-    // lane + 64 h, h < 4).  Each of the 4 * nsplit thread streams keeps KT
-    // keys; it "fails" (is re-scanned exactly) when more than KT of the
-    // top-k + margin fall in it.  With lam = k / (4 nsplit) expected members
-    // per stream, KT = 4 / 8 / 16 for lam <= 1/4 / 2 / 4 keeps the Poisson
-    // tail below ~1e-3 per query.  FAISS_AMD_COARSE_WIDE=1 allows up to 64
-    // (long) splits at KT = 4, where a push costs 5 VALU per candidate instead
-    // of 9 at KT = 8.  Off by default — r05 A/B on c5 (k = nprobe = 64 over
-    // 65536 centroids, 100k queries): 64 splits x KT 4 cut the filter 3.66 ->
-    // 3.24 ms and took the re-rank 0.92 -> 1.31 ms (1024 keys per query to
-    // rank instead of 512; step 7.11 -> 7.18 ms); 32 splits x KT 4 at lam =
-    // 1/2: filter 3.09 ms, re-rank 2.71 ms (failing streams).
+    // At most 16 splits (the re-rank keeps one thread stream per lane).
+    // Each of the 4 * nsplit thread streams keeps KT keys; it "fails" (is
+    // re-scanned exactly) when more than KT of the top-k + margin fall in it.
+    // With lam = k / (4 nsplit) expected members per stream, KT = 4 / 8 / 16
+    // for lam <= 1/4 / 2 / 4 keeps the Poisson tail below ~1e-3 per query.
     //
     // The split count sets the grid: cdiv(n, 128) query blocks x nsplit work
     // groups, two resident per CU (k_coarse_stream's two 64-centroid tile
@@ -843,9 +818,7 @@ CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k) {
     double best = 0.0;
     const char* nsenv = getenv("FAISS_AMD_COARSE_NSPLIT");  // forces the split count (tuning)
     const int ns_force = nsenv ? atoi(nsenv) : 0;
-    const char* wenv = getenv("FAISS_AMD_COARSE_WIDE");  // "1": up to 64 splits (A/B)
-    const int ns_max = (wenv && !strcmp(wenv, "1")) ? 64 : 16;
-    for (int ns = 1; ns <= std::min(ns_max, std::max(1, nlist / BV)); ns++) {
+    for (int ns = 1; ns <= std::min(16, std::max(1, nlist / BV)); ns++) {
         if (ns_force > 0 && ns != ns_force) continue;
         if (k > 16 * ns) continue;
         const double lam = (double)k / (4.0 * ns);
@@ -854,8 +827,6 @@ CoarsePlan coarse_bf3_plan(int64_t n, int nlist, int d, int k) {
         const int sl = (int)roundup(cdiv((size_t)nlist, (size_t)ns), BV);
         const int nsp = (int)cdiv((size_t)nlist, (size_t)sl);
         if ((size_t)sl > ((size_t)BV << 10)) continue;  // ordinals: 4 + log2(tiles) <= 14 bits
-        if (nsp > 16 && (sl < 16 * BV || kt1 > 4)) continue;  // (long splits, KT 4 only)
-        if (nsp * 4 * kt1 > 1024) continue;                    // the re-rank's entries
         // resident work groups (k_coarse_stream: 3 per CU for DB <= 96 and
         // KT <= 8, else 2)
         const int64_t slots = (bf3_db(d) <= 96 && kt1 <= 8 ? 3 : 2) * (int64_t)ncu;
@@ -977,7 +948,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     }
     const int E = p.entries;
     const int V = E <= 64 ? 1 : E <= 128 ? 2 : E <= 256 ? 4 : E <= 512 ? 8 : 16;
-    FAISS_THROW_IF_NOT(E <= 1024);  // (a lane's V keys may span several streams)
+    FAISS_THROW_IF_NOT(E <= 1024 && V <= p.kt);
 #define LAUNCH_R(L2V, OT, OUT, VV)                                                              \
     k_coarse_rerank<L2V, OT, VV><<<dim3((unsigned)n), dim3(64), 0, s>>>(                       \
             keys, pbs, x, ldx, xnorm, cent, ldc, cnorm, cnmax, coef, y3 ? 1 : 0, n, d, nlist,  \

@@ -260,13 +260,12 @@ def test_coarse_bf3_equals_f32_tile_and_oracle(amd, orc, gpu, monkeypatch, metri
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("metric", [1, 0])
-@pytest.mark.parametrize("k,nsplit", [(64, 64), (40, 64), (64, 16), (10, 0)])
-def test_coarse_bf3_wide_splits(amd, orc, gpu, monkeypatch, metric, k, nsplit):
-    # 64 splits x 4 thread streams of KT = 4 (r05: c5's coarse plan): 256
-    # streams per query, dropped bounds of streams lane + 64 h in the
-    # re-rank.  A tight cluster inside the first split puts far more than KT
-    # of a nearby query's top-k in single streams (those streams fail and
-    # are re-scanned exactly); duplicated rows give ties at the k boundary.
+@pytest.mark.parametrize("k,nsplit", [(64, 16), (40, 16), (64, 0), (10, 0)])
+def test_coarse_bf3_failing_streams(amd, orc, gpu, monkeypatch, metric, k, nsplit):
+    # 16 splits x 4 thread streams (c5's coarse plan at k = 64: KT = 8).  A
+    # tight cluster inside the first split puts far more than KT of a nearby
+    # query's top-k in single streams (those streams fail and are re-scanned
+    # exactly); duplicated rows give ties at the k boundary.
     d, ny = 64, 65536
     y = rand(orc, ny, d, 43)
     rng = np.random.default_rng(7)
@@ -275,7 +274,6 @@ def test_coarse_bf3_wide_splits(amd, orc, gpu, monkeypatch, metric, k, nsplit):
     x = np.ascontiguousarray(np.concatenate([rand(orc, 150, d, 44), y[:10] + 1e-3, y[1000:1010]]))
     idx = amd.IndexFlat(d, metric)
     idx.add(y)
-    monkeypatch.setenv("FAISS_AMD_COARSE_WIDE", "1")
     if nsplit:
         monkeypatch.setenv("FAISS_AMD_COARSE_NSPLIT", str(nsplit))
     monkeypatch.setenv("FAISS_AMD_COARSE", "bf3")
