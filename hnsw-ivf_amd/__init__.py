@@ -107,6 +107,13 @@ class _CVar:
 cvar = _CVar()
 
 
+def set_interrupt_timeout(seconds):
+    """faiss.TimeoutCallback.reset(seconds) (seconds >= 0) /
+    InterruptCallback.clear_instance() (None or < 0): a host search that polls
+    the callback after it fires raises FaissError("computation interrupted")."""
+    lib().faiss_amd_set_interrupt_timeout(-1.0 if seconds is None else float(seconds))
+
+
 def _declare(L):
     sig = {
         "faiss_get_last_error": (C.c_char_p, []),
@@ -184,6 +191,7 @@ def _declare(L):
         "faiss_amd_get_hnsw_row_stats": (None, [C.c_void_p, C.c_void_p]),
         "faiss_amd_get_hnsw_replay_stats": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
         "faiss_amd_fold_device_stats": (C.c_int, [_P]),
+        "faiss_amd_set_interrupt_timeout": (None, [C.c_double]),
         "faiss_IndexIVFFlat_new_with": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t]),
         "faiss_IndexIVFFlat_new_with_metric": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t, C.c_int]),
         "faiss_amd_IndexIVFPQ_new_with": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int]),

@@ -462,6 +462,10 @@ void faiss_amd_get_hnsw_replay_stats(uint64_t* replayed, uint64_t* searched_agai
     if (searched_again) *searched_again = hnsw_row_stats.searched_again;
     if (replay_bad) *replay_bad = hnsw_row_stats.replay_bad;
 }
+void faiss_amd_set_interrupt_timeout(double seconds) {
+    if (seconds < 0) InterruptCallback::clear_instance();
+    else TimeoutCallback::reset(seconds);
+}
 int faiss_amd_fold_device_stats(const FaissIndex* index) {
     C_TRY auto ix = IX(index);
     ix->fold_device_stats();

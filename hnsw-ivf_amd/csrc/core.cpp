@@ -16,6 +16,48 @@ IndexIVFStats indexIVF_stats;
 HNSWStats hnsw_stats;
 HNSWRowStats hnsw_row_stats;
 
+// ---------------------------------------------------------------- interrupts
+// faiss/impl/AuxIndexStructures.cpp:204-262 (behaviour restated)
+std::mutex InterruptCallback::lock;
+std::unique_ptr<InterruptCallback> InterruptCallback::instance;
+
+void InterruptCallback::clear_instance() { instance.reset(); }
+
+void InterruptCallback::check() {
+    if (instance && instance->want_interrupt()) FAISS_THROW_MSG("computation interrupted");
+}
+
+bool InterruptCallback::is_interrupted() {
+    if (!instance) return false;
+    std::lock_guard<std::mutex> g(lock);
+    return instance->want_interrupt();
+}
+
+size_t InterruptCallback::get_period_hint(size_t flops) {
+    if (!instance) return (size_t)1 << 30;  // no callback: never poll
+    // a poll every ~100 Mflop of work
+    return std::max<size_t>((size_t)100000000 / (flops + 1), 1);
+}
+
+bool TimeoutCallback::want_interrupt() {
+    if (timeout == 0) return false;
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - start).count();
+    if (el <= timeout) return false;
+    timeout = 0;  // fires once
+    return true;
+}
+
+void TimeoutCallback::set_timeout(double timeout_in_seconds) {
+    timeout = timeout_in_seconds;
+    start = std::chrono::steady_clock::now();
+}
+
+void TimeoutCallback::reset(double timeout_in_seconds) {
+    auto* tc = new TimeoutCallback();
+    InterruptCallback::instance.reset(tc);
+    tc->set_timeout(timeout_in_seconds);
+}
+
 // ---------------------------------------------------------------- devices
 namespace {
 std::mutex g_ctx_mu;
@@ -143,6 +185,9 @@ void Index::search(idx_t n, const float* x, idx_t k, float* distances, idx_t* la
     HIP_CHECK(hipMemcpyAsync(labels, h_i_.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     fold_device_stats();
+    // IndexHNSW::search polls the interrupt callback (faiss/IndexHNSW.cpp:315;
+    // the batch is one device pass); IndexFlat::search does not
+    if (dynamic_cast<const IndexHNSW*>(this)) InterruptCallback::check();
 }
 
 // ---------------------------------------------------------------- IndexFlat
@@ -453,6 +498,7 @@ void kmeans_train(int d, idx_t n, const float* x, int k, int niter, int64_t seed
     IndexFlat cent(d, METRIC_L2);
     cent.device = device;
     for (int it = 0; it < niter; it++) {
+        InterruptCallback::check();  // faiss/Clustering.cpp:487
         cent.reset();
         cent.add(k, centroids);
         cent.assign_device(nt, bx.as<float>(), ld, 1, bd.as<float>(), bi.as<int32_t>(), nullptr,

@@ -665,6 +665,7 @@ void IndexHNSW::search_stats(idx_t n, const float* x, idx_t k, float* distances,
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     fold_device_stats();
+    InterruptCallback::check();  // faiss/IndexHNSW.cpp:315 (one device pass)
     if (per_query_stats) {
         // no quantization phase; the batch's traversal time is each query's
         for (idx_t i = 0; i < n; i++) {

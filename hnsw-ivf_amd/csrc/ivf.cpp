@@ -866,6 +866,8 @@ void IndexIVF::search_preassigned_stats(idx_t n, const float* x, idx_t k, const 
     HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(st, s_stats_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    // faiss/IndexIVF.cpp:627, 707-713 (the batch is one device pass here)
+    if (InterruptCallback::is_interrupted()) FAISS_THROW_MSG("computation interrupted");
     IndexIVFStats* out = ivf_stats ? ivf_stats : &indexIVF_stats;
     out->nq += n;
     out->nlist += st[0];
@@ -950,7 +952,16 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
         unsigned long long*& p;
         ~ResetQ() { p = nullptr; }
     } reset_q{qdone_};
+    // InterruptCallback: polled before each chunk is queued and once the
+    // batch is done; when it fires the remaining chunks are not queued and
+    // the call throws after draining the queued ones (faiss/IndexIVF.cpp:627,
+    // 707-713)
+    bool interrupted = false;
     for (idx_t q0 = 0, c = 0; q0 < n; q0 += qchunk, c++) {
+        if (c > 0 && InterruptCallback::is_interrupted()) {
+            interrupted = true;
+            break;
+        }
         const idx_t nq = std::min(qchunk, n - q0);
         marks.push_back(ev.mark(s));
         if (stamps && c == 0) kern::device_stamp(stamps, s);
@@ -977,6 +988,7 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
     HIP_CHECK(hipMemcpyAsync(labels, bi.ptr, sizeof(idx_t) * n * k, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(st, s_stats_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    if (interrupted || InterruptCallback::is_interrupted()) FAISS_THROW_MSG("computation interrupted");
     quantizer->fold_device_stats();
     double qms = 0, sms = 0;
     for (size_t c = 0; c + 2 < marks.size(); c += 3) {

@@ -1,3 +1,4 @@
-// faiss/impl/AuxIndexStructures.h — RangeSearchResult
+// faiss/impl/AuxIndexStructures.h — RangeSearchResult, InterruptCallback,
+// TimeoutCallback
 #pragma once
 #include "faiss_amd_names.h"

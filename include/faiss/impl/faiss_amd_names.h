@@ -39,8 +39,10 @@ using faiss_amd::IDSelectorRange;
 
 // faiss/Index.h, faiss/impl/AuxIndexStructures.h
 using faiss_amd::Index;
+using faiss_amd::InterruptCallback;
 using faiss_amd::RangeSearchResult;
 using faiss_amd::SearchParameters;
+using faiss_amd::TimeoutCallback;
 
 // faiss/IndexFlat.h
 using faiss_amd::IndexFlat;

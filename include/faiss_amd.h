@@ -12,6 +12,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -162,6 +163,34 @@ struct RangeSearchResult {
     std::vector<float> distances;
     explicit RangeSearchResult(size_t nq = 0) : nq(nq), lims(nq + 1, 0) {}
     size_t buffer_size() const { return labels.size(); }
+};
+
+// faiss/impl/AuxIndexStructures.h:135-170: a callback that long computations
+// poll; the one installed in `instance` (if any) is asked want_interrupt().
+// Here a host search polls it between its query chunks and once the batch is
+// done (a GPU batch is not cut short inside its kernels), and k-means once
+// per iteration; a search that sees it fire throws "computation interrupted",
+// as IndexIVF::search_preassigned does after its loop (IndexIVF.cpp:627,
+// 707-713), and IndexHNSW::search per chunk (IndexHNSW.cpp:315).
+struct InterruptCallback {
+    virtual bool want_interrupt() = 0;
+    virtual ~InterruptCallback() {}
+    static std::mutex lock;  // serialises is_interrupted()
+    static std::unique_ptr<InterruptCallback> instance;
+    static void clear_instance();
+    static void check();          // throws "computation interrupted" when it fires
+    static bool is_interrupted();  // the same, as a flag
+    // iterations between polls for a loop of `flops` per iteration
+    static size_t get_period_hint(size_t flops);
+};
+
+// fires once, the first poll after `timeout` seconds from set_timeout()
+struct TimeoutCallback : InterruptCallback {
+    std::chrono::time_point<std::chrono::steady_clock> start;
+    double timeout = 0;
+    bool want_interrupt() override;
+    void set_timeout(double timeout_in_seconds);
+    static void reset(double timeout_in_seconds);  // installs a new one as `instance`
 };
 
 // ---------------------------------------------------------------- Index

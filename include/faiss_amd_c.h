@@ -344,6 +344,12 @@ void faiss_amd_get_hnsw_row_stats(uint64_t* fp32_rows, uint64_t* q8_rows);
 void faiss_amd_get_hnsw_replay_stats(uint64_t* replayed, uint64_t* searched_again,
                                      uint64_t* replay_bad);
 int faiss_amd_fold_device_stats(const FaissIndex* index);
+/* faiss::TimeoutCallback::reset / InterruptCallback::clear_instance
+ * (faiss/impl/AuxIndexStructures.h:135-170, C++ only in the reference; here
+ * for C / ctypes callers and tests): seconds >= 0 installs a timeout callback
+ * (a host search polled after it fires throws "computation interrupted"),
+ * seconds < 0 removes the installed callback. */
+void faiss_amd_set_interrupt_timeout(double seconds);
 /* graph export for tests: levels[ntotal], offsets[ntotal+1], neighbors[],
  * cum_nneighbor_per_level[]; pass NULL to query sizes only */
 int faiss_amd_IndexHNSW_graph(

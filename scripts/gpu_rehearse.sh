@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp FAISS_AMD_BENCH_BACKEND=gloo
 for extra in "" "--shard"; do
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-    --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --config c1 --steps 20 \
+    --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --config ${CFG:-c1} --steps 20 \
     --warmup 3 $extra > gpurun_out/rehearse$extra.json 2> gpurun_out/rehearse$extra.err
   rc=$?; echo "rehearse '$extra' rc=$rc"; cat gpurun_out/rehearse$extra.json; tail -3 gpurun_out/rehearse$extra.err
   [ $rc -eq 0 ] || exit $rc

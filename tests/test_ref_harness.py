@@ -47,10 +47,12 @@ def test_faiss_names_are_the_library_types(tmp_path):
 #include <faiss/IndexHNSW.h>
 #include <faiss/index_io.h>
 #include <faiss/impl/FaissAssert.h>
+#include <faiss/impl/AuxIndexStructures.h>
 #include <type_traits>
 static_assert(std::is_same<faiss::IndexIVFFlat, faiss_amd::IndexIVFFlat>::value, "");
 static_assert(std::is_same<faiss::Index, faiss_amd::Index>::value, "");
 static_assert(std::is_same<faiss::FaissException, faiss_amd::FaissException>::value, "");
+static_assert(std::is_base_of<faiss::InterruptCallback, faiss::TimeoutCallback>::value, "");
 static_assert(std::is_same<faiss::idx_t, int64_t>::value, "");
 static_assert(faiss::METRIC_L2 == 1 && faiss::METRIC_INNER_PRODUCT == 0, "");
 namespace faiss { int caller_extension = 1; }  // namespace faiss stays open
