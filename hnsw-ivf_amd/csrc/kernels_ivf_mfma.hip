@@ -358,6 +358,14 @@ __device__ __forceinline__ void wait_lgkmcnt0() {  // s_waitcnt lgkmcnt(0) alone
 // is -coarse_dis(query, probe) / 2, so the accumulator is -approx / 2 of
 // coarse_dis + term - 2 <x, y_R> (the IVF-PQ filter's key); ynmax / rmax are
 // the lists' max |y_R| / |y_R - bf16(y_R)|, margins as k_ivfpq_filter_w.
+// cache policy of the tile stream's global_load_lds: 2 = nt (streamed list
+// tiles are read once per item; marked non-temporal they leave the L2 to
+// what is re-read: the query fragments and the re-rank's rows).  r05 A/B on
+// c2: step 0.2867 -> 0.2786 ms (filter 100.9 -> 100.2 us, Flat re-rank 58.0
+// -> 54.5 us); 0 = the default policy
+#ifndef IVF_TILE_AUX
+#define IVF_TILE_AUX 2
+#endif
 template <bool L2, int KT, int NS, bool PIPE, bool FOLD = false, bool PQ = false>
 __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
         const float* __restrict__ x, int ldx, int d, const uint8_t* __restrict__ cbs,
@@ -417,7 +425,8 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
             if (g < G3 || blk < NG)  // wave-uniform
                 __builtin_amdgcn_global_load_lds(
                         (const void*)(src + blk * 1024),
-                        (__attribute__((address_space(3))) void*)(dst + blk * 1024), 16, 0, 0);
+                        (__attribute__((address_space(3))) void*)(dst + blk * 1024), 16, 0,
+                        IVF_TILE_AUX);
         }
     };
     // wait until at most `tiles_ahead` tiles of this wave's glds are pending

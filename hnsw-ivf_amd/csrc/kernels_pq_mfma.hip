@@ -454,6 +454,8 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
             if constexpr (CS % 16 == 0) {
 #pragma unroll
                 for (int i = 0; i < NWC; i += 4) {
+                    // (non-temporal code loads measured slower: r05 c3 filter
+                    // 105 -> 114 us, c5 1.37 -> 1.55 ms)
                     const uint4 v = *(const uint4*)(cp + 4 * i);
                     cw[bi][i] = v.x;
                     cw[bi][i + 1] = v.y;
