@@ -130,6 +130,55 @@ __device__ __forceinline__ bf16x8 pq_decode_frag(const uint32_t (&cw)[NWC], int 
     return cv.v;
 }
 
+// The same fragment with the lane half folded into a per-lane table base
+// (dec_lh = dec + 4096 lh: sub-quantizer m + E lh starts E * 256 * 2 DSUB =
+// 4096 bytes further) and into the byte's word / shift, so each gather is one
+// bit-field extract + one address add, its sub-quantizer's table offset an
+// immediate of the LDS read (pq_decode_frag selects between the two halves'
+// bytes and sub-quantizers per gather).  Byte m = 16 s / DSUB + E lh + u:
+//   DSUB 2: 8 s + 4 lh + u -> word 2 s + lh, byte u
+//   DSUB 4: 4 s + 2 lh + u -> word s, byte 2 lh + u
+//   DSUB 8: 2 s + lh       -> word s / 2, byte (2 s) % 4 + lh
+template <int DSUB, int NWC>
+__device__ __forceinline__ bf16x8 pq_decode_frag_l(const uint32_t (&cw)[NWC], int lh,
+                                                   const uint8_t* __restrict__ dec_lh, int s) {
+    static_assert(DSUB == 2 || DSUB == 4 || DSUB == 8, "dsub");
+    uint32_t w32[4];
+    if constexpr (DSUB == 2) {
+        const uint32_t w = lh ? cw[2 * s + 1] : cw[2 * s];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t j = (w >> (8 * u)) & 0xffu;
+            w32[u] = *(const uint32_t*)(dec_lh + (size_t)(8 * s + u) * 1024 + 4 * j);
+        }
+    } else if constexpr (DSUB == 4) {
+        const uint32_t w = cw[s];
+        const uint32_t sh = 16u * (uint32_t)lh;
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint32_t j = (w >> (sh + 8 * u)) & 0xffu;
+            const uint2 v = *(const uint2*)(dec_lh + (size_t)(4 * s + u) * 2048 + 8 * j);
+            w32[2 * u] = v.x;
+            w32[2 * u + 1] = v.y;
+        }
+    } else {
+        const uint32_t w = cw[s >> 1];
+        const uint32_t j = (w >> (8u * (uint32_t)((2 * s) & 3) + 8u * (uint32_t)lh)) & 0xffu;
+        const uint4 v = *(const uint4*)(dec_lh + (size_t)(2 * s) * 4096 + 16 * j);
+        w32[0] = v.x;
+        w32[1] = v.y;
+        w32[2] = v.z;
+        w32[3] = v.w;
+    }
+    union {
+        uint32_t w[4];
+        bf16x8 v;
+    } cv;
+#pragma unroll
+    for (int i = 0; i < 4; i++) cv.w[i] = w32[i];
+    return cv.v;
+}
+
 // One work item = (list, <= 64 queries); persistent work-groups walk the
 // items with stride gridDim.x, so the LDS decode table is loaded once per
 // work-group.  Wave layout, keys, streams and outputs as k_ivf_bf3_filter.
@@ -380,6 +429,7 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
     if (t == 0) grp_next = (uint32_t)wpb;
     __syncthreads();  // the decode table (the only barrier)
     const int li = lane & 31, lh = lane >> 5;
+    const uint8_t* dec_lh = dec + (lh ? 4096 : 0);  // (pq_decode_frag_l)
     const uint32_t lowmask = (1u << obits) - 1u;
     const uint32_t nitems = item_off[nlist];
     const uint32_t ntask = 2u * nitems;
@@ -529,7 +579,7 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
                 for (int r = 0; r < 16; r++) acc[r] = 0.f;
 #pragma unroll
                 for (int s = 0; s < NS; s++) {
-                    const bf16x8 ah = pq_decode_frag<DSUB, NWC>(cw[bi], lh, dec, s);
+                    const bf16x8 ah = pq_decode_frag_l<DSUB, NWC>(cw[bi], lh, dec_lh, s);
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
                 }
