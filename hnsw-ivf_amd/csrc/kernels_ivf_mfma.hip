@@ -388,14 +388,11 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
     constexpr int G2 = (NG + 1) / 4;
     constexpr int G3 = NG / 4;
     constexpr int NB = 2;
-    static_assert(FQ * 4 * 4 <= TB, "bounds fit in a tile buffer");
     static_assert(!(FOLD && (PIPE || !L2)), "fold: L2, sequential form");
     // all LDS in one array (a second __shared__ object can make hipcc wait
-    // vmcnt(0) before the tile reads): 2 tiles; after the loop tile buffer 0
-    // holds the bounds [FQ][4].
+    // vmcnt(0) before the tile reads): the 2 tile buffers
     __shared__ __attribute__((aligned(16))) uint8_t smem[NB * TB];
     uint8_t* tiles = smem;
-    float* bnd_s = (float*)smem;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t xcd = blockIdx.x & 7u, rest = blockIdx.x >> 3;
     const uint32_t item = 4u * ((rest >> 2) * 8u + xcd) + (rest & 3u);
@@ -612,8 +609,10 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
     }
 
     const unsigned long long ft2 = ftrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    // ---- outputs (no glds in flight: plain barriers from here)
-    __syncthreads();  // every wave is done with the tiles: bounds reuse buffer 0
+    // ---- outputs.  A query's 4 thread streams (slot 2 bi + lh) live in
+    // lanes li and li + 32 of one wave, so their dropped bounds meet by one
+    // lane swap (r05: no LDS round trip, no work-group barriers)
+    float bnd2[2];
 #pragma unroll
     for (int bi = 0; bi < 2; bi++) {
         const uint32_t last = tq[bi].q[KT - 1];
@@ -624,9 +623,9 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
             const int row = (int)((ord >> 4) * BV) + 32 * bi + 4 * lh + 8 * (r >> 2) + (r & 3);
             if (row < len) bnd = FOLD ? fold_decode_lo(last, lowmask) : key_decode_lo<L2>(last, lowmask);
         }
-        bnd_s[qloc * 4 + 2 * bi + lh] = bnd;
+        bnd2[bi] = bnd;
     }
-    __syncthreads();
+    const float bnd_p0 = __shfl_xor(bnd2[0], 32), bnd_p1 = __shfl_xor(bnd2[1], 32);
     if (qvalid) {
         const int64_t e = my_e;
         const uint32_t elen = min((uint32_t)len, lim_e);
@@ -653,11 +652,10 @@ __global__ __launch_bounds__(256, PIPE ? 3 : 4) void k_ivf_bf2_stream(
                 mmax = 2.f * (2.f * sqrtf(xn) * rmax_l + coef * (xn + ynmax_l)) + 1e-30f;
             }
             ProbeRec pr;
+            const float bb4[4] = {bnd2[0], bnd_p0, bnd2[1], bnd_p1};  // slots 0..3
 #pragma unroll
-            for (int sl = 0; sl < 4; sl++) {
-                const float bb = bnd_s[qloc * 4 + sl];
-                pr.pb[sl] = bb < WS_INF ? bb - mmax : WS_INF;
-            }
+            for (int sl = 0; sl < 4; sl++)
+                pr.pb[sl] = bb4[sl] < WS_INF ? bb4[sl] - mmax : WS_INF;
             pr.mmax = mmax;
             pr.off = (uint32_t)row0;
             pr.len = elen;
