@@ -3,7 +3,7 @@
 # the bench line's `traffic` reads this round's summary), the bench line
 # (with the reference CPU baseline), then a rocprofv3 kernel trace + stats
 # and the per-step kernel list.  Results under gpurun_out/r05_<cfg>_*.
-#   CFGS="c2 c3" bash scripts/gpu_r4_evidence.sh
+#   CFGS="c2 c3" bash scripts/gpu_r5_evidence.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out profiles
 export TMPDIR=/tmp
