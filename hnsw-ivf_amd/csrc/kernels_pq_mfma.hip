@@ -143,28 +143,32 @@ template <int DSUB, int NWC>
 __device__ __forceinline__ bf16x8 pq_decode_frag_l(const uint32_t (&cw)[NWC], int lh,
                                                    const uint8_t* __restrict__ dec_lh, int s) {
     static_assert(DSUB == 2 || DSUB == 4 || DSUB == 8, "dsub");
+    // (v_bfe_u32 with the per-lane shift, 32-bit LDS offsets: one extract
+    // and one v_lshl_add_u32 per gather; a shift-and-mask and 64-bit offset
+    // arithmetic compiled to four)
     uint32_t w32[4];
     if constexpr (DSUB == 2) {
         const uint32_t w = lh ? cw[2 * s + 1] : cw[2 * s];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const uint32_t j = (w >> (8 * u)) & 0xffu;
-            w32[u] = *(const uint32_t*)(dec_lh + (size_t)(8 * s + u) * 1024 + 4 * j);
+            const uint32_t j = __builtin_amdgcn_ubfe(w, 8u * u, 8u);
+            w32[u] = *(const uint32_t*)(dec_lh + (int)((8 * s + u) * 1024) + (int)(j << 2));
         }
     } else if constexpr (DSUB == 4) {
         const uint32_t w = cw[s];
         const uint32_t sh = 16u * (uint32_t)lh;
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            const uint32_t j = (w >> (sh + 8 * u)) & 0xffu;
-            const uint2 v = *(const uint2*)(dec_lh + (size_t)(4 * s + u) * 2048 + 8 * j);
+            const uint32_t j = __builtin_amdgcn_ubfe(w, sh + 8u * u, 8u);
+            const uint2 v = *(const uint2*)(dec_lh + (int)((4 * s + u) * 2048) + (int)(j << 3));
             w32[2 * u] = v.x;
             w32[2 * u + 1] = v.y;
         }
     } else {
         const uint32_t w = cw[s >> 1];
-        const uint32_t j = (w >> (8u * (uint32_t)((2 * s) & 3) + 8u * (uint32_t)lh)) & 0xffu;
-        const uint4 v = *(const uint4*)(dec_lh + (size_t)(2 * s) * 4096 + 16 * j);
+        const uint32_t j =
+                __builtin_amdgcn_ubfe(w, 8u * (uint32_t)((2 * s) & 3) + 8u * (uint32_t)lh, 8u);
+        const uint4 v = *(const uint4*)(dec_lh + (int)((2 * s) * 4096) + (int)(j << 4));
         w32[0] = v.x;
         w32[1] = v.y;
         w32[2] = v.z;
