@@ -67,6 +67,7 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector == fp32 MFMA peak
 PEAK_HBM_GBS = 8000.0
 PEAK_L2_GBS = 34500.0      # MI355X_MICROARCH.md: aggregate L2 (4 MiB per XCD), measured
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+PEAK_LDS_TBS = 150.0       # MI355X_MICROARCH.md: aggregate ds_read_b128 rate, every CU
 # kernel stage (library timer name) -> regular expression of the demangled
 # symbol of the kernel that stage launches in this round's code, matched in
 # this round's committed rocprofv3 PMC summaries (a summary of an older kernel
@@ -79,6 +80,7 @@ PMC_SYMBOL = {
     "coarse_filter": r"kern::k_coarse_stream<",
     "hnsw_search": r"kern::k_hnsw_search<",
     "hnsw_exact": r"kern::k_hnsw_exact(_reg)?[<(]",
+    "hnsw_wide": r"kern::k_hnsw_wide<",
     "ivf_rerank": r"kern::k_ivf_rerank<true, \d+, 0>",
     "ivfpq_rerank": r"kern::k_ivf_rerank<true, \d+, [1-9]\d*>",
     "coarse_rerank": r"kern::k_coarse_rerank<",
@@ -227,26 +229,28 @@ def kernel_roofline(name, ms, work, config):
              "mfma_frac": f / t / 1e12 / PEAK_BF16_TFLOPS,
              "pq_code_bytes_per_step": work["flat_rows"] * work.get("M", 0)}
     elif name == "ivfpq_filter":
-        # the default filter streams the code bytes (SURVEY 8d: list x
-        # code_size, one pass over the rows of every distinct probed list)
-        # and decodes each row's bf16 residual through the LDS table, 2
-        # products of 2 dpad flops per (query, row) candidate on the bf16
-        # MFMA: priced on the MFMA (the code bytes are a small fraction of
-        # HBM: list reuse across the batch's queries)
+        # SURVEY 8(d): the default filter streams the code bytes (list x
+        # code_size, one pass over the rows of every distinct probed list),
+        # priced against HBM; beside it the rate of its LDS decode-table
+        # gathers (one ds_read_b128 of 8 bf16 per lane and 16 B of table per
+        # (row, 8 dims) of each 32-query task: M / (8 / dsub) gathers of
+        # 16 B per row per task) and the bf16 MFMA work it feeds
         b = work["flat_rows"] * work.get("M", 0)
         f = work["cands"] * 4.0 * work["dpad16"]
-        r = {"bound": "mfma", "achieved": f / t / 1e12, "peak": PEAK_BF16_TFLOPS,
-             "unit": "TFLOP/s", "mfma_dtype": "bf16", "algorithmic_flops_per_step": f,
-             "flops_per_candidate": 4 * work["dpad16"],
+        lds_b = work["cands"] / 32.0 * work["dpad16"] * 2.0
+        r = {"bound": "hbm", "achieved": b / t / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
              "algorithmic_bytes_per_step": b, "bytes_per_row": work.get("M", 0),
-             "hbm_gbs": b / t / 1e9, "hbm_frac": b / t / 1e9 / PEAK_HBM_GBS}
+             "lds_gather_bytes_per_step": lds_b, "lds_gather_tbs": lds_b / t / 1e12,
+             "lds_gather_frac": lds_b / t / 1e12 / PEAK_LDS_TBS,
+             "mfma_dtype": "bf16", "mfma_flops_per_step": f, "mfma_tflops": f / t / 1e12,
+             "mfma_frac": f / t / 1e12 / PEAK_BF16_TFLOPS}
     elif name == "coarse_filter":
         # bf16x3 x.c of every (query, centroid): 3 products of 2 dpad flops
         f = work["nq_coarse"] * work["nlist"] * 6.0 * work["dpad16"]
         r = {"bound": "mfma", "achieved": f / t / 1e12, "peak": PEAK_BF16_TFLOPS,
              "unit": "TFLOP/s", "mfma_dtype": "bf16", "algorithmic_flops_per_step": f,
              "flops_per_query_centroid": 6 * work["dpad16"]}
-    elif name in ("hnsw_search", "hnsw_exact") and work.get("hnsw_ndis"):
+    elif name in ("hnsw_search", "hnsw_exact", "hnsw_wide") and work.get("hnsw_ndis"):
         # bytes the traversal must read: per hop the node's level-0 neighbour
         # ids (64 x 4 B); per distance either one fp32 row of the graph's
         # storage or, for the register kernel's prefiltered neighbours, the
@@ -464,6 +468,11 @@ def main():
         el = time.perf_counter() - t1
         amd.set_kernel_timing(False)
         dom_ms = kernel_breakdown(ix, steps).get(dom, float("nan")) if dom else float("nan")
+        if dom and not np.isfinite(dom_ms):
+            # a stage timer that could not be read (c_api.cpp resolve_times)
+            # fails the run instead of printing a NaN roofline
+            raise RuntimeError(f"the dominant stage {dom!r} has no readable time "
+                               f"({dom_ms}) over the timed steps")
         if world > 1:
             tt = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)

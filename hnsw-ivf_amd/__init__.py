@@ -236,6 +236,13 @@ def _declare(L):
         "faiss_amd_float_rand": (C.c_int, [_P, C.c_size_t, C.c_int64]),
         "faiss_amd_float_rand_rows": (C.c_int, [_P, _I64, C.c_int, C.c_int64, _I64, _I64, _I64]),
         "faiss_amd_last_kernel_times": (C.c_int, [_P, C.POINTER(C.c_int), _P, _P, _P]),
+        "faiss_amd_IndexIVF_debug_rows": (C.c_int, [_P, C.c_int, _I64, _I64, _P,
+                                                    C.POINTER(C.c_size_t), C.POINTER(C.c_int64)]),
+        "faiss_clone_index": (C.c_int, [_P, C.POINTER(_P)]),
+        "faiss_Index_reconstruct": (C.c_int, [_P, _I64, _P]),
+        "faiss_Index_reconstruct_n": (C.c_int, [_P, _I64, _I64, _P]),
+        "faiss_Index_assign": (C.c_int, [_P, _I64, _P, _P, _I64]),
+        "faiss_IndexIVF_imbalance_factor": (C.c_double, [_P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -528,6 +535,20 @@ class IndexIVF(Index):
         if n:
             lib().faiss_amd_IndexIVF_invlists_get_codes(self.h, l, _ptr(out))
         return out.reshape(n, self.code_size)
+
+    def debug_rows(self, what, row0=0, n=None):
+        """HBM arena rows [row0, row0 + n) as bytes [n][row_bytes] (diagnostic):
+        what 0 = code rows, 1 = row -> list table, 2 = the filter's stream image.
+        n = None returns (row_bytes, arena_rows) only."""
+        rb, rows = C.c_size_t(), C.c_int64()
+        _check(lib().faiss_amd_IndexIVF_debug_rows(self.h, int(what), 0, 0, None, C.byref(rb),
+                                                   C.byref(rows)))
+        if n is None:
+            return rb.value, rows.value
+        out = np.empty((int(n), rb.value), dtype=np.uint8)
+        _check(lib().faiss_amd_IndexIVF_debug_rows(self.h, int(what), int(row0), int(n),
+                                                   _ptr(out), None, None))
+        return out
 
     def search_preassigned(self, x, k, assign, centroid_dis, store_pairs=False):
         """centroid_dis may be None (NULL), as the reference allows where its
@@ -840,6 +861,13 @@ def read_index(fname, io_flags=0):
 
 def write_index(index, fname):
     _check(lib().faiss_write_index_fname(index.h, str(fname).encode()))
+
+
+def clone_index(index):
+    """faiss.clone_index (c_api/clone_index_c.h): a deep copy."""
+    p = C.c_void_p()
+    _check(lib().faiss_clone_index(index.h, C.byref(p)))
+    return _wrap(p)
 
 
 def write_index_ondisk(index, fname, lists_fname):

@@ -110,6 +110,22 @@ int faiss_Index_reset(FaissIndex* index) {
     C_TRY IX(index)->reset();
     C_CATCH
 }
+// faiss/Index.cpp:38-43 (assign = search with the distances discarded)
+int faiss_Index_assign(FaissIndex* index, idx_t n, const float* x, idx_t* labels, idx_t k) {
+    C_TRY std::vector<float> D((size_t)n * k);
+    IX(index)->search(n, x, k, D.data(), labels, nullptr);
+    C_CATCH
+}
+int faiss_Index_reconstruct(const FaissIndex* index, idx_t key, float* recons) {
+    C_TRY IX(index)->reconstruct(key, recons);
+    C_CATCH
+}
+// faiss/Index.cpp:50-55
+int faiss_Index_reconstruct_n(const FaissIndex* index, idx_t i0, idx_t ni, float* recons) {
+    C_TRY const Index* ix = IX(index);
+    for (idx_t i = 0; i < ni; i++) ix->reconstruct(i0 + i, recons + (size_t)i * ix->d);
+    C_CATCH
+}
 
 // ---------------- SearchParametersIVF
 int faiss_SearchParametersIVF_new(FaissSearchParametersIVF** p_sp) {
@@ -144,6 +160,16 @@ int faiss_IDSelector_is_member(const FaissIDSelector* sel, idx_t id) {
     return SEL(sel)->is_member(id) ? 1 : 0;
 }
 void faiss_IDSelector_free(FaissIDSelector* sel) { delete SEL(sel); }
+void faiss_IDSelectorRange_free(FaissIDSelectorRange* sel) { delete SEL(sel); }
+void faiss_IDSelectorBitmap_free(FaissIDSelectorBitmap* sel) { delete SEL(sel); }
+idx_t faiss_IDSelectorRange_imin(const FaissIDSelectorRange* sel) {
+    auto r = dynamic_cast<const IDSelectorRange*>(SEL(sel));
+    return r ? r->imin : 0;
+}
+idx_t faiss_IDSelectorRange_imax(const FaissIDSelectorRange* sel) {
+    auto r = dynamic_cast<const IDSelectorRange*>(SEL(sel));
+    return r ? r->imax : 0;
+}
 int faiss_IDSelectorRange_new(FaissIDSelectorRange** p_sel, idx_t imin, idx_t imax) {
     C_TRY* p_sel = reinterpret_cast<FaissIDSelectorRange*>(new IDSelectorRange(imin, imax));
     C_CATCH
@@ -184,6 +210,9 @@ int faiss_IDSelectorXOr_new(FaissIDSelectorXOr** p_sel, const FaissIDSelector* l
 
 void faiss_SearchParametersIVF_free(FaissSearchParametersIVF* obj) {
     delete reinterpret_cast<SearchParamsC*>(obj);
+}
+FaissSearchParametersIVF* faiss_SearchParametersIVF_cast(FaissSearchParameters* sp) {
+    return reinterpret_cast<FaissSearchParametersIVF*>(sp);
 }
 size_t faiss_SearchParametersIVF_nprobe(const FaissSearchParametersIVF* p) {
     return reinterpret_cast<const SearchParamsC*>(p)->ivf.nprobe;
@@ -229,6 +258,33 @@ int faiss_IndexFlatL2_new_with(FaissIndexFlatL2** p_index, idx_t d) {
 int faiss_IndexFlatIP_new_with(FaissIndexFlat** p_index, idx_t d) {
     C_TRY* p_index = FX(new IndexFlatIP(d));
     C_CATCH
+}
+int faiss_IndexFlat_new(FaissIndexFlat** p_index) {
+    C_TRY* p_index = FX(new IndexFlat());
+    C_CATCH
+}
+int faiss_IndexFlatIP_new(FaissIndexFlatIP** p_index) {
+    C_TRY* p_index = FX(new IndexFlatIP(0));
+    C_CATCH
+}
+int faiss_IndexFlatL2_new(FaissIndexFlatL2** p_index) {
+    C_TRY* p_index = FX(new IndexFlatL2(0));
+    C_CATCH
+}
+void faiss_IndexFlat_free(FaissIndexFlat* obj) { delete IX(obj); }
+void faiss_IndexFlatIP_free(FaissIndexFlatIP* obj) { delete IX(obj); }
+void faiss_IndexFlatL2_free(FaissIndexFlatL2* obj) { delete IX(obj); }
+// FAISS_DECLARE_INDEX_DOWNCAST (c_api/macros_impl.h:93-100): dynamic_cast
+FaissIndexFlat* faiss_IndexFlat_cast(FaissIndex* index) {
+    return dynamic_cast<IndexFlat*>(IX(index)) ? index : nullptr;
+}
+FaissIndexFlatIP* faiss_IndexFlatIP_cast(FaissIndex* index) {
+    auto f = dynamic_cast<IndexFlat*>(IX(index));
+    return f && f->metric_type == faiss_amd::METRIC_INNER_PRODUCT ? index : nullptr;
+}
+FaissIndexFlatL2* faiss_IndexFlatL2_cast(FaissIndex* index) {
+    auto f = dynamic_cast<IndexFlat*>(IX(index));
+    return f && f->metric_type == faiss_amd::METRIC_L2 ? index : nullptr;
 }
 void faiss_IndexFlat_xb(FaissIndexFlat* index, float** p_xb, size_t* p_size) {
     auto f = dynamic_cast<IndexFlat*>(IX(index));
@@ -282,6 +338,22 @@ int faiss_IndexIVF_own_fields(const FaissIndexIVF* i) {
 }
 void faiss_IndexIVF_set_own_fields(FaissIndexIVF* i, int v) {
     if (auto x = IVFm(i)) x->own_fields = v != 0;
+}
+
+void faiss_IndexIVF_free(FaissIndexIVF* obj) { delete IX(obj); }
+FaissIndexIVF* faiss_IndexIVF_cast(FaissIndex* index) {
+    return dynamic_cast<IndexIVF*>(IX(index)) ? index : nullptr;
+}
+double faiss_IndexIVF_imbalance_factor(const FaissIndexIVF* index) {
+    auto v = IVFc(index);
+    if (!v) return 0.0;
+    double tot = 0.0, uf = 0.0;
+    for (size_t l = 0; l < v->nlist; l++) {
+        const double sz = (double)v->get_list_size(l);
+        tot += sz;
+        uf += sz * sz;
+    }
+    return tot > 0 ? uf * (double)v->nlist / (tot * tot) : 0.0;
 }
 
 int faiss_IndexIVF_search_preassigned(const FaissIndexIVF* index, idx_t n, const float* x,
@@ -361,6 +433,32 @@ int faiss_IndexIVFFlat_new_with_metric(FaissIndexIVFFlat** p_index, FaissIndex* 
                                        size_t d, size_t nlist, FaissMetricType metric) {
     C_TRY* p_index = FX(new IndexIVFFlat(IX(quantizer), d, nlist, (MetricType)metric));
     C_CATCH
+}
+
+// default construction (IndexIVFFlat_c.h:34): no vectors, no lists; the
+// library's IndexIVF always has a quantizer, so it owns an empty IndexFlatL2
+int faiss_IndexIVFFlat_new(FaissIndexIVFFlat** p_index) {
+    C_TRY auto q = new IndexFlatL2(0);
+    auto ix = new IndexIVFFlat(q, 0, 0, faiss_amd::METRIC_L2);
+    ix->own_fields = true;
+    *p_index = FX(ix);
+    C_CATCH
+}
+void faiss_IndexIVFFlat_free(FaissIndexIVFFlat* obj) { delete IX(obj); }
+FaissIndexIVFFlat* faiss_IndexIVFFlat_cast(FaissIndex* index) {
+    return dynamic_cast<IndexIVFFlat*>(IX(index)) ? index : nullptr;
+}
+size_t faiss_IndexIVFFlat_nlist(const FaissIndexIVFFlat* i) { return faiss_IndexIVF_nlist(i); }
+size_t faiss_IndexIVFFlat_nprobe(const FaissIndexIVFFlat* i) { return faiss_IndexIVF_nprobe(i); }
+void faiss_IndexIVFFlat_set_nprobe(FaissIndexIVFFlat* i, size_t v) {
+    faiss_IndexIVF_set_nprobe(i, v);
+}
+FaissIndex* faiss_IndexIVFFlat_quantizer(const FaissIndexIVFFlat* i) {
+    return faiss_IndexIVF_quantizer(i);
+}
+int faiss_IndexIVFFlat_own_fields(const FaissIndexIVFFlat* i) { return faiss_IndexIVF_own_fields(i); }
+void faiss_IndexIVFFlat_set_own_fields(FaissIndexIVFFlat* i, int v) {
+    faiss_IndexIVF_set_own_fields(i, v);
 }
 
 // ---------------- IndexIVFPQ
@@ -598,6 +696,19 @@ int faiss_read_index_fname(const char* fname, int io_flags, FaissIndex** p_out) 
     C_TRY* p_out = FX(read_index(fname, io_flags));
     C_CATCH
 }
+// faiss/clone_index.cpp (Cloner::clone_Index): a deep copy.  Every index
+// type of this library round-trips its on-disk form byte for byte, so the
+// copy goes through it (an anonymous temporary file)
+int faiss_clone_index(const FaissIndex* idx, FaissIndex** p_out) {
+    C_TRY FILE* f = tmpfile();
+    FAISS_THROW_IF_NOT_MSG(f, "clone_index: no temporary file");
+    std::unique_ptr<FILE, int (*)(FILE*)> guard(f, fclose);
+    write_index(IX(idx), f);
+    FAISS_THROW_IF_NOT(fflush(f) == 0);
+    rewind(f);
+    *p_out = FX(read_index(f, 0));
+    C_CATCH
+}
 
 // ---------------- factory / parameter space
 int faiss_index_factory(FaissIndex** p_index, int d, const char* description,
@@ -787,6 +898,12 @@ int faiss_amd_last_kernel_times(const FaissIndex* index, int* n_kernels, char* n
     *n_kernels = cnt;
     C_CATCH
 }
+int faiss_amd_IndexIVF_debug_rows(const FaissIndex* index, int what, int64_t row0, int64_t n,
+                                  void* out, size_t* row_bytes, int64_t* rows) {
+    C_TRY IVF(index)->debug_rows(what, row0, n, out, row_bytes, rows);
+    C_CATCH
+}
+
 int faiss_amd_reset_kernel_times(FaissIndex* index) {
     C_TRY Index* ix = IX(index);
     ix->ktimes.clear();

@@ -5,6 +5,7 @@
 // (reference faiss/impl/FaissAssert.h, faiss/impl/FaissException.h) which the
 // C-ABI turns into return code -2 (reference c_api/macros_impl.h:22-56).
 #pragma once
+#include <algorithm>
 #include <atomic>
 
 #include <hip/hip_runtime.h>
@@ -81,6 +82,30 @@ class FaissException : public std::exception {
 
 inline size_t roundup(size_t a, size_t b) { return (a + b - 1) / b * b; }
 inline size_t cdiv(size_t a, size_t b) { return (a + b - 1) / b; }
+
+// Launch geometry.  An AQL dispatch packet counts the work-items of a grid
+// dimension (blocks x threads) in 32 bits, so a 1-D launch past 2^32 - 1
+// work-items does not fail on its own: the count wraps and the tail of the
+// range is never visited (the round-5 100M-row PQ image: rows x (DB + 8)
+// ≈ 1.2e10 work-items, most of the image unwritten).  Every launch takes its
+// grid from kgrid(), which throws instead; kernels over int64 element counts
+// take a bounded grid from stride_grid() and loop (GRID_STRIDE).
+inline dim3 kgrid(int64_t blocks, int threads) {
+    if (blocks < 1 || (uint64_t)blocks * (uint64_t)threads > 0xffffffffull) {
+        FAISS_THROW_FMT("launch of %lld blocks x %d threads is outside the 32-bit work-item "
+                        "count of a dispatch",
+                        (long long)blocks, threads);
+    }
+    return dim3((unsigned)blocks);
+}
+constexpr int64_t kStrideGridMax = 8192;  // 256 CUs x 32 blocks: fills the chip, then loops
+inline dim3 stride_grid(int64_t n, int threads) {
+    const int64_t b = (int64_t)cdiv((size_t)std::max<int64_t>(n, 1), (size_t)threads);
+    return dim3((unsigned)std::min<int64_t>(b, kStrideGridMax));
+}
+#define GRID_STRIDE(i, n)                                                                  \
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)(n);     \
+         i += (int64_t)gridDim.x * blockDim.x)
 
 // Owning device buffer (hipMalloc'ed), bound to the device current at alloc.
 // bumped by every DeviceBuffer (re)allocation: a captured search graph

@@ -24,7 +24,8 @@ std::unique_ptr<InterruptCallback> InterruptCallback::instance;
 void InterruptCallback::clear_instance() { instance.reset(); }
 
 void InterruptCallback::check() {
-    if (instance && instance->want_interrupt()) FAISS_THROW_MSG("computation interrupted");
+    // through is_interrupted(), under the lock (TimeoutCallback fires once)
+    if (is_interrupted()) FAISS_THROW_MSG("computation interrupted");
 }
 
 bool InterruptCallback::is_interrupted() {

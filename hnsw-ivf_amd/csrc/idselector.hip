@@ -67,7 +67,7 @@ __global__ void k_sel_combine(const int64_t* __restrict__ ids, int64_t n, uint8_
 }  // namespace kern
 
 namespace {
-unsigned grid_of(int64_t n) { return (unsigned)std::max<int64_t>(1, cdiv(n, 256)); }
+dim3 grid_of(int64_t n) { return kgrid(std::max<int64_t>(1, cdiv(n, 256)), 256); }
 
 // device copy of a host array for the duration of one mark_device call
 struct DevTmp {

@@ -96,6 +96,33 @@ int IndexIVF::device_code_stride() const {
     return (int)roundup(code_size, 4);
 }
 
+void IndexIVF::debug_rows(int what, idx_t row0, idx_t n, void* out, size_t* row_bytes,
+                          idx_t* rows) const {
+    sync_device();
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    DevGuard dg(device);
+    const void* base = nullptr;
+    size_t rb = 0;
+    if (what == 0) {
+        base = d_codes_.ptr;
+        rb = device_code_stride();
+    } else if (what == 1) {
+        base = d_row_list_.ptr;
+        rb = sizeof(uint32_t);
+    } else if (what == 2) {
+        base = stream_image(&rb);
+    }
+    FAISS_THROW_IF_NOT_MSG(base && rb > 0, "debug_rows: this index has no such buffer");
+    if (row_bytes) *row_bytes = rb;
+    if (rows) *rows = (idx_t)arena_rows_;
+    if (!out || n <= 0) return;
+    FAISS_THROW_IF_NOT(row0 >= 0 && row0 + n <= (idx_t)arena_rows_);
+    hipStream_t s = stream();
+    HIP_CHECK(hipMemcpyAsync(out, (const uint8_t*)base + (size_t)row0 * rb, (size_t)n * rb,
+                             hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
 void IndexIVF::train(idx_t n, const float* x) {
     // faiss/IndexIVF.cpp:1221-1260 (train) + Level1Quantizer::train_q1
     if (quantizer->is_trained && (size_t)quantizer->ntotal == nlist) {
@@ -1052,6 +1079,12 @@ void IndexIVFFlat::reconstruct(idx_t key, float* recons) const {
     FAISS_THROW_MSG("key not found");
 }
 
+const void* IndexIVFFlat::stream_image(size_t* row_bytes) const {
+    if (!d_cbs_.ptr || arena_rows_ == 0) return nullptr;
+    *row_bytes = 2 * (size_t)(kern::bf3_db_host(d) / 2 * 2) + 16;
+    return d_cbs_.ptr;
+}
+
 void IndexIVFFlat::upload_extra() const {
     hipStream_t s = stream();
     const int l = (int)roundup((size_t)d, 4);
@@ -1314,6 +1347,12 @@ void IndexIVFPQ::encode_vectors(idx_t n, const float* x, const idx_t* list_nos,
                                          code_size);
 }
 
+const void* IndexIVFPQ::stream_image(size_t* row_bytes) const {
+    if (!pq_stream_ready_ || !d_pcbs_.ptr) return nullptr;
+    *row_bytes = 2 * (size_t)kern::bf3_db_host(d) + 16;
+    return d_pcbs_.ptr;
+}
+
 void IndexIVFPQ::upload_extra() const {
     hipStream_t s = stream();
     const int ldc = ld();
@@ -1367,12 +1406,10 @@ void IndexIVFPQ::upload_extra() const {
         pq_stream_ready_ = false;
         const char* ienv = getenv("FAISS_AMD_PQ_FILTER");
         d_pcbs_.release();
-        // (at most 4 GiB of image: a 100M-row single-GPU index gave wrong
-        // filter keys through the image in a round-5 A/B, not root-caused;
-        // the 12.5M-row c5 shard, 2.6 GB, is bit-exact)
-        const int DBi = kern::bf3_db_host(d);
+        // (round 6: no size cap.  The round-5 100M-row wrong keys were the
+        // image builder's launch of rows x (DB + 8) work-items, past the
+        // dispatch's 32-bit count; it is grid-strided now, common.h kgrid)
         if (pq_mfma_ready_ && ienv && !strcmp(ienv, "image") &&
-            rows * (2 * (size_t)DBi + 16) <= ((size_t)4 << 30) &&
             kern::ivfpq_stream_eligible(d, (int)pq.M, 1, 1)) {
             const int DB = kern::bf3_db_host(d);
             d_pcbs_.reserve(rows * (2 * (size_t)DB + 16));

@@ -401,6 +401,10 @@ bool hnsw_visited_scratch_needed(int ld, int k, int efSearch, int64_t vwords);
 bool hnsw_register_eligible(int k, int efSearch);
 // the batched kernel (and its tie re-runs) runs for these parameters
 bool hnsw_uses_batched(int k, int efSearch);  // leave the flagged queries to the caller
+// 128 < max(efSearch, k) <= kHnswWideMaxEf: the wide kernel (k_hnsw_wide,
+// candidate set sorted in the LDS) + sequential re-runs of its flagged queries
+constexpr int kHnswWideMaxEf = 4096;
+bool hnsw_uses_wide(int k, int efSearch);
 // flagged queries (flags[q] != 0) -> idx[0 .. *count) (count zeroed first)
 void hnsw_flag_compact(const uint32_t* flags, int64_t n, uint32_t* idx, uint32_t* count,
                        hipStream_t s);

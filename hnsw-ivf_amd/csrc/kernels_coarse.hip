@@ -431,39 +431,38 @@ __global__ __launch_bounds__(256, NS <= 6 && KT <= 8 ? 3 : 2) void k_coarse_stre
 __global__ void k_coarse_image(const float* __restrict__ codes, int64_t rows, int64_t rows_pad,
                                int d, int ldc, int DB, const float* __restrict__ norms,
                                uint8_t* __restrict__ out, int fold) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int per = DB + 4;  // slots per row: DB (hi, lo) pairs, norm, 3 pad words
-    if (i >= rows_pad * per) return;
-    const int64_t r = i / per;
-    const int j = (int)(i - r * per);
-    uint8_t* row = out + r * (int64_t)(4 * DB + 16);
-    if (j < DB) {
-        const float v = (r < rows && j < d) ? codes[r * ldc + j] : 0.f;
-        const __bf16 h = (__bf16)v;
-        ((__bf16*)row)[j] = h;
-        ((__bf16*)row)[DB + j] = (__bf16)(v - (float)h);
-    } else if (fold) {
-        // bias A-fragment {-|c|^2/2 in three bf16 parts, 1, 1, 1, 0, 0}
-        // (padding rows: -inf, 0, 0, 1, 1, 1, 0, 0): two bf16 per slot
-        __bf16 h = (__bf16)(-WS_INF), m = (__bf16)0.f, lo = (__bf16)0.f;
-        if (r < rows) split3_bf16(-0.5f * norms[r], h, m, lo);
-        const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
-        const int t = j - DB;  // bf16 pair t of the 16-byte tail
-        __bf16* tail = (__bf16*)(row + 4 * DB);
-        const __bf16 v[8] = {h, m, lo, one, one, one, zero, zero};
-        tail[2 * t] = v[2 * t];
-        tail[2 * t + 1] = v[2 * t + 1];
-    } else {
-        float* tail = (float*)(row + 4 * DB);
-        tail[j - DB] = j == DB ? (r < rows ? norms[r] : WS_INF) : 0.f;
+    GRID_STRIDE(i, rows_pad * per) {
+        const int64_t r = i / per;
+        const int j = (int)(i - r * per);
+        uint8_t* row = out + r * (int64_t)(4 * DB + 16);
+        if (j < DB) {
+            const float v = (r < rows && j < d) ? codes[r * ldc + j] : 0.f;
+            const __bf16 h = (__bf16)v;
+            ((__bf16*)row)[j] = h;
+            ((__bf16*)row)[DB + j] = (__bf16)(v - (float)h);
+        } else if (fold) {
+            // bias A-fragment {-|c|^2/2 in three bf16 parts, 1, 1, 1, 0, 0}
+            // (padding rows: -inf, 0, 0, 1, 1, 1, 0, 0): two bf16 per slot
+            __bf16 h = (__bf16)(-WS_INF), m = (__bf16)0.f, lo = (__bf16)0.f;
+            if (r < rows) split3_bf16(-0.5f * norms[r], h, m, lo);
+            const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
+            const int t = j - DB;  // bf16 pair t of the 16-byte tail
+            __bf16* tail = (__bf16*)(row + 4 * DB);
+            const __bf16 v[8] = {h, m, lo, one, one, one, zero, zero};
+            tail[2 * t] = v[2 * t];
+            tail[2 * t + 1] = v[2 * t + 1];
+        } else {
+            float* tail = (float*)(row + 4 * DB);
+            tail[j - DB] = j == DB ? (r < rows ? norms[r] : WS_INF) : 0.f;
+        }
     }
 }
 void coarse_stream_image(const float* codes, int64_t rows, int d, int ldc, const float* norms,
                          void* out, hipStream_t s, int fold) {
     const int DB = bf3_db(d);
     const int64_t rows_pad = (int64_t)roundup((size_t)std::max<int64_t>(rows, 1), BV);
-    const int64_t tot = rows_pad * (DB + 4);
-    k_coarse_image<<<dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, s>>>(
+    k_coarse_image<<<stride_grid(rows_pad * (DB + 4), 256), dim3(256), 0, s>>>(
             codes, rows, rows_pad, d, ldc, DB, norms, (uint8_t*)out, fold);
     HIP_LAUNCH_CHECK();
 }
@@ -642,7 +641,7 @@ __global__ __launch_bounds__(64, CR_WAVES) void k_coarse_rerank(
 #pragma unroll
     for (int i = 0; i < V; i++)
         ub[i] = kv[i] != 0xffffffffu ? ivf_decode_hi<L2>(kv[i], lowmask, fold) + M : WS_INF;
-    float U = wave_kth_smallest<V>(ub, k);
+    float U = wave_kth_smallest<V, 12>(ub, k);  // an upper bound (wave_select.h)
     const unsigned long long t_u = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (!(U <= WS_INF)) U = WS_INF;
     const unsigned long long fmask = __ballot(my_pb < WS_INF && my_pb <= U);
@@ -902,16 +901,16 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     do {                                                                                      \
         if (stream)                                                                           \
             (fk ? k_coarse_stream<L2V, KTV, NSV, L2V> : k_coarse_stream<L2V, KTV, NSV, false>) \
-                    <<<dim3((unsigned)grid), dim3(256), 0, s>>>(                              \
+                    <<<kgrid(grid, 256), dim3(256), 0, s>>>(                              \
                     x, ldx, n, d, (const uint8_t*)cst, xnorm, nlist, p.nsplit, p.split_len,   \
                     (int)nqb, coef, cnmax, p.obits, keys, pbs, ctrace,                        \
                     (const uint8_t*)qimg);                                                    \
         else if (y3)                                                                          \
-            k_coarse_bf3_filter<L2V, KTV, NSV, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+            k_coarse_bf3_filter<L2V, KTV, NSV, true><<<kgrid(grid, 256), dim3(256), 0, s>>>( \
                     x, ldx, n, d, (const __bf16*)cbf, cnorm, xnorm, nlist, p.nsplit,          \
                     p.split_len, coef, cnmax, p.obits, keys, pbs);                            \
         else                                                                                  \
-            k_coarse_bf3_filter<L2V, KTV, NSV, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+            k_coarse_bf3_filter<L2V, KTV, NSV, false><<<kgrid(grid, 256), dim3(256), 0, s>>>( \
                     x, ldx, n, d, (const __bf16*)cbf, cnorm, xnorm, nlist, p.nsplit,          \
                     p.split_len, coef, cnmax, p.obits, keys, pbs);                            \
     } while (0)
@@ -950,7 +949,7 @@ void coarse_bf3_knn(const CoarsePlan& p, const float* x, int64_t n, int ldx, con
     const int V = E <= 64 ? 1 : E <= 128 ? 2 : E <= 256 ? 4 : E <= 512 ? 8 : 16;
     FAISS_THROW_IF_NOT(E <= 1024 && V <= p.kt);
 #define LAUNCH_R(L2V, OT, OUT, VV)                                                              \
-    k_coarse_rerank<L2V, OT, VV><<<dim3((unsigned)n), dim3(64), 0, s>>>(                       \
+    k_coarse_rerank<L2V, OT, VV><<<kgrid(n, 64), dim3(64), 0, s>>>(                       \
             keys, pbs, x, ldx, xnorm, cent, ldc, cnorm, cnmax, coef, y3 ? 1 : 0, n, d, nlist,  \
             p.nsplit,                                                                           \
             p.split_len, p.kt, p.obits, k, D, OUT, st_ptr, crtrace, fk ? 1 : 0)

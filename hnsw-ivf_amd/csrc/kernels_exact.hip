@@ -81,9 +81,9 @@ __global__ __launch_bounds__(64) void k_ex_flat(const float* __restrict__ x, int
                                                 const uint8_t* __restrict__ sel,
                                                 const uint32_t* __restrict__ eoff, int64_t cap,
                                                 uint32_t* __restrict__ okeys,
-                                                uint32_t* __restrict__ orows) {
+                                                uint32_t* __restrict__ orows, int64_t e0) {
     extern __shared__ float xs[];  // [ldx]
-    const int64_t e = blockIdx.x;
+    const int64_t e = e0 + blockIdx.x;
     const int64_t q = e / np;
     const int32_t key = assign[e];
     if (key < 0 || key >= nlist) return;
@@ -168,9 +168,9 @@ __global__ __launch_bounds__(256) void k_ex_pq(const float* __restrict__ x, int 
                                                ExactPQ pq, const uint8_t* __restrict__ sel,
                                                const uint32_t* __restrict__ eoff, int64_t cap,
                                                uint32_t* __restrict__ okeys,
-                                               uint32_t* __restrict__ orows) {
+                                               uint32_t* __restrict__ orows, int64_t e0) {
     extern __shared__ float lut[];
-    const int64_t e = blockIdx.x;
+    const int64_t e = e0 + blockIdx.x;
     const int64_t q = e / np;
     const int32_t key = assign[e];
     if (key < 0 || key >= nlist) return;
@@ -202,10 +202,10 @@ __global__ __launch_bounds__(256) void k_ex_pq_range(
         const uint8_t* __restrict__ sel, const int64_t* __restrict__ ids,
         const uint32_t* __restrict__ row_list, int store_pairs, uint32_t* __restrict__ counts,
         const uint64_t* __restrict__ offsets, float* __restrict__ outD,
-        int64_t* __restrict__ outI) {
+        int64_t* __restrict__ outI, int64_t e0) {
     extern __shared__ float lut[];
     __shared__ uint32_t wsum[4];
-    const int64_t e = blockIdx.x;
+    const int64_t e = e0 + blockIdx.x;
     const int64_t q = e / np;
     const int32_t key = assign[e];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -439,6 +439,10 @@ size_t select_lds(int k) {
 
 }  // namespace
 
+// (query, probe) work groups per launch of the k_ex_* scans: 2^20 x 256
+// work-items stays far inside a dispatch's 32-bit count (common.h kgrid)
+constexpr int64_t kExEntriesPerLaunch = (int64_t)1 << 20;
+
 // A query's candidate slot holds every row of its probes: np * max_list_len.
 // (Not clamped to the arena size: a caller-supplied assignment may name a list
 // twice, and the reference then scans it twice.)
@@ -454,7 +458,7 @@ void ivf_exact_search(const ExactScanArgs& a, uint32_t* eoff, uint32_t* total, u
     if (a.n <= 0) return;
     FAISS_THROW_IF_NOT_FMT(a.k >= 1 && a.k <= kMaxKExact, "k = %d must be in [1, %d]", a.k,
                            kMaxKExact);
-    k_ex_offsets<<<dim3((unsigned)cdiv(a.n, 256)), dim3(256), 0, s>>>(
+    k_ex_offsets<<<kgrid(cdiv(a.n, 256), 256), dim3(256), 0, s>>>(
             a.assign, a.n, a.np, a.list_len, a.nlist, a.lim, eoff, total);
     HIP_LAUNCH_CHECK();
     const int64_t entries = a.n * (int64_t)a.np;
@@ -468,28 +472,34 @@ void ivf_exact_search(const ExactScanArgs& a, uint32_t* eoff, uint32_t* total, u
             HIP_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)lds));
 #define EXPQ(L2)                                                                             \
-    k_ex_pq<L2><<<dim3((unsigned)entries), dim3(256), lds, s>>>(                            \
+    k_ex_pq<L2><<<kgrid(ne, 256), dim3(256), lds, s>>>(                                     \
             a.x, a.ldx, a.d, a.np, a.assign, a.cdis, a.lim, a.list_off, a.list_len, a.nlist, \
-            a.pq, a.sel, eoff, cap, keys, rows)
-        if (a.l2)
-            EXPQ(true);
-        else
-            EXPQ(false);
+            a.pq, a.sel, eoff, cap, keys, rows, e0)
+        for (int64_t e0 = 0; e0 < entries; e0 += kExEntriesPerLaunch) {
+            const int64_t ne = std::min(kExEntriesPerLaunch, entries - e0);
+            if (a.l2)
+                EXPQ(true);
+            else
+                EXPQ(false);
+        }
 #undef EXPQ
     } else {
         const size_t lds = sizeof(float) * a.ldx;
-        if (a.l2)
-            k_ex_flat<true><<<dim3((unsigned)entries), dim3(64), lds, s>>>(
-                    a.x, a.ldx, a.d, a.np, a.assign, a.lim, a.list_off, a.list_len, a.nlist,
-                    a.codes, a.ldc, a.sel, eoff, cap, keys, rows);
-        else
-            k_ex_flat<false><<<dim3((unsigned)entries), dim3(64), lds, s>>>(
-                    a.x, a.ldx, a.d, a.np, a.assign, a.lim, a.list_off, a.list_len, a.nlist,
-                    a.codes, a.ldc, a.sel, eoff, cap, keys, rows);
+        for (int64_t e0 = 0; e0 < entries; e0 += kExEntriesPerLaunch) {
+            const int64_t ne = std::min(kExEntriesPerLaunch, entries - e0);
+            if (a.l2)
+                k_ex_flat<true><<<kgrid(ne, 64), dim3(64), lds, s>>>(
+                        a.x, a.ldx, a.d, a.np, a.assign, a.lim, a.list_off, a.list_len,
+                        a.nlist, a.codes, a.ldc, a.sel, eoff, cap, keys, rows, e0);
+            else
+                k_ex_flat<false><<<kgrid(ne, 64), dim3(64), lds, s>>>(
+                        a.x, a.ldx, a.d, a.np, a.assign, a.lim, a.list_off, a.list_len,
+                        a.nlist, a.codes, a.ldc, a.sel, eoff, cap, keys, rows, e0);
+        }
     }
     HIP_LAUNCH_CHECK();
     SrcIVF src{keys, rows, total, cap, a.ids, a.row_list, a.list_off, a.store_pairs, a.qdone};
-    k_ex_select<SrcIVF, int64_t><<<dim3((unsigned)a.n), dim3(256), select_lds(a.k), s>>>(
+    k_ex_select<SrcIVF, int64_t><<<kgrid(a.n, 256), dim3(256), select_lds(a.k), s>>>(
             src, a.k, a.l2, D, I, a.k);
     HIP_LAUNCH_CHECK();
 }
@@ -508,9 +518,12 @@ void ivfpq_range_exact(const ExactScanArgs& a, float radius, uint32_t* counts,
             HIP_CHECK(hipFuncSetAttribute((const void*)k_ex_pq_range<L2, F>,                  \
                                           hipFuncAttributeMaxDynamicSharedMemorySize,         \
                                           (int)lds));                                         \
-        k_ex_pq_range<L2, F><<<dim3((unsigned)entries), dim3(256), lds, s>>>(                 \
-                a.x, a.ldx, a.d, a.np, a.assign, a.cdis, a.list_off, a.list_len, a.nlist, a.pq, \
-                radius, a.sel, a.ids, a.row_list, a.store_pairs, counts, offsets, outD, outI); \
+        for (int64_t e0 = 0; e0 < entries; e0 += kExEntriesPerLaunch)                        \
+            k_ex_pq_range<L2, F>                                                              \
+                    <<<kgrid(std::min(kExEntriesPerLaunch, entries - e0), 256), dim3(256), lds, \
+                       s>>>(a.x, a.ldx, a.d, a.np, a.assign, a.cdis, a.list_off, a.list_len,  \
+                            a.nlist, a.pq, radius, a.sel, a.ids, a.row_list, a.store_pairs,   \
+                            counts, offsets, outD, outI, e0);                                 \
     } while (0)
     if (a.l2) {
         if (offsets) EXR(true, true);
@@ -573,7 +586,7 @@ void merge_rows_general(const float* cand_d, const int64_t* cand_i, int64_t n, i
     FAISS_THROW_IF_NOT_FMT(nshard >= 1 && nshard <= MG_MAXS, "nshard = %d must be in [1, %d]",
                            nshard, MG_MAXS);
     FAISS_THROW_IF_NOT(kin >= 1 && kin <= 65535 && k >= 1);
-    k_merge_general<<<dim3((unsigned)cdiv(n, MG_T)), dim3(MG_T), 0, s>>>(
+    k_merge_general<<<kgrid(cdiv(n, MG_T), MG_T), dim3(MG_T), 0, s>>>(
             cand_d, cand_i, n, kin, nshard, k, metric_l2, out_d, out_i);
     HIP_LAUNCH_CHECK();
 }
@@ -586,7 +599,7 @@ void select_rows_exact(const float* Dt, int64_t nx, int64_t ny, int64_t ldD, int
     FAISS_THROW_IF_NOT_FMT(k >= 1, "k = %d must be >= 1", k);
     if (k <= kMaxKExact) {
         SrcDense src{Dt, ldD, ny, col0, metric_l2};
-        k_ex_select<SrcDense, OutIdx><<<dim3((unsigned)nx), dim3(256), select_lds(k), s>>>(
+        k_ex_select<SrcDense, OutIdx><<<kgrid(nx, 256), dim3(256), select_lds(k), s>>>(
                 src, k, metric_l2, out_d, out_i, ldo);
         HIP_LAUNCH_CHECK();
         return;
@@ -600,7 +613,7 @@ void select_rows_exact(const float* Dt, int64_t nx, int64_t ny, int64_t ldD, int
     for (int64_t q0 = 0; q0 < nx; q0 += qc) {
         const int64_t nq = std::min(qc, nx - q0);
         SrcDense src{Dt + q0 * ldD, ldD, ny, col0, metric_l2};
-        k_ex_select<SrcDense, OutIdx, true><<<dim3((unsigned)nq), dim3(256), 0, s>>>(
+        k_ex_select<SrcDense, OutIdx, true><<<kgrid(nq, 256), dim3(256), 0, s>>>(
                 src, k, metric_l2, out_d + q0 * ldo, out_i + q0 * ldo, ldo,
                 scratch->as<unsigned long long>(), words);
         HIP_LAUNCH_CHECK();

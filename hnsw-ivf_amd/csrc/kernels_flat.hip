@@ -41,27 +41,27 @@ __global__ __launch_bounds__(256) void k_direct_dist(const float* __restrict__ x
                                                      int ldx, const float* __restrict__ y,
                                                      int64_t ny, int ldy, int d, int metric_l2,
                                                      float* __restrict__ D, int64_t ldD) {
-    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= nx * ny) return;
-    const int64_t i = p / ny, j = p - i * ny;
-    const float* a = x + i * ldx;
-    const float* b = y + j * ldy;
-    D[i * ldD + j] = metric_l2 ? ref_l2(a, b, d) : ref_ip(a, b, d);
+    GRID_STRIDE(p, nx * ny) {
+        const int64_t i = p / ny, j = p - i * ny;
+        const float* a = x + i * ldx;
+        const float* b = y + j * ldy;
+        D[i * ldD + j] = metric_l2 ? ref_l2(a, b, d) : ref_ip(a, b, d);
+    }
 }
 
 void direct_distances(const float* x, int64_t nx, int ldx, const float* y, int64_t ny, int ldy,
                       int d, int metric_l2, float* D, int64_t ldD, hipStream_t s) {
     if (nx <= 0 || ny <= 0) return;
     FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldy % 4 == 0);
-    k_direct_dist<<<dim3((unsigned)cdiv(nx * ny, 256)), dim3(256), 0, s>>>(x, nx, ldx, y, ny, ldy,
-                                                                          d, metric_l2, D, ldD);
+    k_direct_dist<<<stride_grid(nx * ny, 256), dim3(256), 0, s>>>(x, nx, ldx, y, ny, ldy, d,
+                                                                 metric_l2, D, ldD);
     HIP_LAUNCH_CHECK();
 }
 
 void row_norms(const float* x, int64_t n, int d, int ld, float* out, hipStream_t s) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT(ld % 4 == 0);
-    k_row_norms<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s>>>(x, n, d, ld, out);
+    k_row_norms<<<kgrid(cdiv(n, 256), 256), dim3(256), 0, s>>>(x, n, d, ld, out);
     HIP_LAUNCH_CHECK();
 }
 
@@ -164,7 +164,7 @@ void pairwise_distances(const float* x, int64_t nx, int ldx, const float* xn, co
     FAISS_THROW_IF_NOT(ldx % 4 == 0 && ldy % 4 == 0 && dp % 4 == 0);
     int64_t tx = cdiv(nx, GB), ty = cdiv(ny, GB);
     FAISS_THROW_IF_NOT(tx * ty < (1ll << 31));
-    k_pairwise<<<dim3((unsigned)(tx * ty)), dim3(256), 0, s>>>(x, nx, ldx, xn, y, ny, ldy, yn, dp,
+    k_pairwise<<<kgrid(tx * ty, 256), dim3(256), 0, s>>>(x, nx, ldx, xn, y, ny, ldy, yn, dp,
                                                                metric_l2, D, ldD, (int)ty);
     HIP_LAUNCH_CHECK();
 }
@@ -275,7 +275,7 @@ void select_rows(const float* D, int64_t nx, int64_t ny, int64_t ldD, int k, int
                  hipStream_t s) {
     if (nx <= 0) return;
     FAISS_THROW_IF_NOT_MSG(k >= 1 && k <= kMaxK, "k must be in [1, 64] on this path");
-    k_select_rows<<<dim3((unsigned)cdiv(nx, 4)), dim3(256), 0, s>>>(
+    k_select_rows<<<kgrid(cdiv(nx, 4), 256), dim3(256), 0, s>>>(
             D, nx, ny, ldD, k, metric_l2, col0, out_d, out_i32, out_i64, ldo);
     HIP_LAUNCH_CHECK();
 }
@@ -405,7 +405,7 @@ void merge_rows(const float* cand_d, const int64_t* cand_i, int64_t n, int nin_x
         merge_rows_general(cand_d, cand_i, n, nshard, kin, k, metric_l2, out_d, out_i, s);
         return;
     }
-    k_merge_shards<<<dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s>>>(
+    k_merge_shards<<<kgrid(cdiv(n, 4), 256), dim3(256), 0, s>>>(
             cand_d, cand_i, n, kin, nshard, k, metric_l2, out_d, out_i);
     HIP_LAUNCH_CHECK();
 }
@@ -422,7 +422,7 @@ __global__ void k_translate_labels(int64_t* __restrict__ lab, int64_t n, int64_t
 }
 void translate_labels(int64_t* labels, int64_t n, int64_t offset, hipStream_t s) {
     if (n <= 0 || offset == 0) return;
-    k_translate_labels<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s>>>(labels, n, offset);
+    k_translate_labels<<<kgrid(cdiv(n, 256), 256), dim3(256), 0, s>>>(labels, n, offset);
     HIP_LAUNCH_CHECK();
 }
 }  // namespace kern

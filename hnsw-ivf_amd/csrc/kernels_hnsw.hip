@@ -1609,6 +1609,315 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
     }
 }
 
+// ---------------------------------------------------------------- wide
+// max(efSearch, k) > 128 (the reference harness's grid: efSearch up to 3
+// nprobe, nprobe into the thousands — 60 % of its rows past ef 64).  The
+// batched form of k_hnsw_search with the candidate set in the LDS instead
+// of registers: one wave per query, the MinimaxHeap's entries as one sorted
+// array of 64-bit keys (distance bits | id << 1 | alive) of at most ef
+// entries, so that
+//   * pop_min is the first alive entry (a position kept across hops; the
+//     next alive one is found by one 64-entry ballot), count_below(d0) its
+//     position (minus the dead entries of equal distance just before it);
+//   * a hop's arrivals that can enter (the set not full, or below its
+//     largest key) are compacted, sorted by the narrowest network and merged:
+//     arrival j lands at j + lower_bound(j) (one binary search per lane),
+//     every entry from the first arrival's place on moves up by the number of
+//     arrivals below it (a backward pass, 64 entries per step, read before
+//     written), entries pushed past ef are evicted (MinimaxHeap::push evicts
+//     the max, faiss/impl/HNSW.cpp:1096-1107);
+//   * the results are not kept: the result heap holds the k smallest
+//     arrivals with strict admission, the set the ef >= k smallest, so they
+//     are the set's first k entries below FLT_MAX.
+// For distinct distances every step equals the reference's sequential heap
+// updates (faiss/impl/HNSW.cpp:605-741); an equal distance where the
+// reference's heap layout or arrival order decides — pop_min among equal
+// alive minima, an arrival at the full set's largest distance, equal
+// distances at the kept-ef or the k-th boundary — flags the query for the
+// sequential kernel, as k_hnsw_search does.  Fresh neighbours whose certified
+// int8 lower bound exceeds the full set's largest distance (q8_filter) cannot
+// enter: their fp32 rows are not read.
+__device__ __forceinline__ uint64_t wkey(float d, int32_t id) {
+    return ((uint64_t)__float_as_uint(d) << 32) | ((uint64_t)(uint32_t)id << 1) | 1ull;
+}
+__device__ __forceinline__ float wdis(uint64_t e) { return __uint_as_float((uint32_t)(e >> 32)); }
+__device__ __forceinline__ int32_t wid(uint64_t e) { return (int32_t)((uint32_t)e >> 1); }
+
+// the LDS head of the wide kernel: the query (>= 128 floats), its int8 image
+// and scalars (exact_reg_head), then the candidate set and the visited bitmap
+__host__ __device__ inline size_t wide_lds_bytes(const HNSWDevice& g, int ef) {
+    return (size_t)exact_reg_head(g) + 8 * (size_t)ef;
+}
+
+template <bool LDS_VISITED>
+__global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __restrict__ x,
+                                                  int ldx, int64_t n, int k, int efSearch, int ef,
+                                                  float* __restrict__ D, int64_t* __restrict__ I,
+                                                  int32_t* __restrict__ I32,
+                                                  uint32_t* __restrict__ vis_global,
+                                                  int64_t vwords,
+                                                  unsigned long long* __restrict__ stats,
+                                                  uint32_t* __restrict__ tie_flags) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int qpad = exact_reg_qpad(g);
+    float* qs = sm;                                   // [qpad]
+    uint8_t* q8x = (uint8_t*)(sm + qpad);             // [128]
+    double* q8d = (double*)(q8x + 128);               // [6]
+    uint64_t* cs = (uint64_t*)(q8x + 176);            // sorted candidate set [ef]
+    uint32_t* vis = LDS_VISITED ? (uint32_t*)(cs + ef) : vis_global + blockIdx.x * vwords;
+    const int lane = threadIdx.x;
+    const int64_t q = blockIdx.x;
+    for (int j = lane; j < qpad; j += 64) qs[j] = j < g.d ? x[q * ldx + j] : 0.f;
+    for (int64_t w = lane; w < vwords; w += 64) vis[w] = 0u;
+    __syncthreads();
+    const bool use_q8 = g.q8 != nullptr && g.d <= 128;
+    if (use_q8) q8_query_prep(qs, g.d, q8x, q8d, lane);
+    __syncthreads();
+    uint32_t tie = 0u;     // reason bits, as k_hnsw_search
+    float rdisc = WS_INF;  // smallest distance the set ever turned away or evicted
+    uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0, st_q8 = 0, st_x32 = 0;
+    int S = 0;             // entries of the set
+    if (g.entry_point >= 0) {
+        // ---- greedy descent on the upper levels (HNSW.cpp:852-924)
+        int nearest = g.entry_point;
+        float d_nearest = l2_row(qs, g.storage + (int64_t)nearest * g.ld, g.d);
+        for (int level = g.max_level; level >= 1; level--) {
+            for (;;) {
+                const uint64_t o = g.offsets[nearest];
+                const int b = g.cum_nb[level], e = g.cum_nb[level + 1];
+                const int cnt = e - b;
+                int v = lane < cnt ? g.neighbors[o + b + lane] : -1;
+                unsigned long long neg =
+                        __ballot(lane < cnt && v < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
+                const int first_neg = neg ? __ffsll((long long)neg) - 1 : 64;
+                float dis = WS_INF;
+                if (lane < first_neg) dis = l2_row(qs, g.storage + (int64_t)v * g.ld, g.d);
+                st_ndis += (uint32_t)min(first_neg, 64);
+                st_nhops += 1;
+                float md = dis;
+                int ml = lane;
+#pragma unroll
+                for (int m = 32; m > 0; m >>= 1) {
+                    const float od = __shfl_xor(md, m);
+                    const int ol = __shfl_xor(ml, m);
+                    if (od < md || (od == md && ol < ml)) {
+                        md = od;
+                        ml = ol;
+                    }
+                }
+                if (md < d_nearest) {
+                    d_nearest = md;
+                    nearest = __shfl(v, ml);
+                } else {
+                    break;
+                }
+            }
+        }
+        // ---- level 0: the set seeded with the entry (HNSW.cpp:967-972)
+        if (lane == 0) {
+            cs[0] = wkey(d_nearest, nearest);
+            vis[nearest >> 5] |= 1u << (nearest & 31);
+        }
+        S = 1;
+        int nalive = 1, fa = 0;  // alive entries (MinimaxHeap::nvalid), first alive
+        __syncthreads();
+        const int cnt = g.cum_nb[1] - g.cum_nb[0];
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        for (;;) {
+            if (nalive <= 0) {  // candidates.size() == 0
+                st_n2 = 1;
+                break;
+            }
+            // ---- pop_min: the first alive entry.  An alive entry of equal
+            // distance right after it: the reference picks by heap slot
+            const uint64_t e0 = cs[fa];
+            const float d0 = wdis(e0);
+            const int32_t v0 = wid(e0);
+            const int i1 = fa + 1 + lane;
+            const uint64_t en = i1 < S ? cs[i1] : ~0ull;
+            const unsigned long long am = __ballot(i1 < S && (en & 1ull));
+            const unsigned long long eqm = __ballot(i1 < S && wdis(en) == d0);
+            if ((am & eqm) != 0ull || eqm == ~0ull) tie |= 1u;
+            __syncthreads();
+            if (lane == 0) cs[fa] = e0 & ~1ull;
+            nalive--;
+            int nfa = S;
+            if (am) {
+                nfa = fa + __ffsll((long long)am);
+            } else if (nalive > 0) {
+                for (int b0 = fa + 65; b0 < S; b0 += 64) {
+                    const int ii = b0 + lane;
+                    const unsigned long long m2 = __ballot(ii < S && (cs[ii] & 1ull));
+                    if (m2) {
+                        nfa = b0 + __ffsll((long long)m2) - 1;
+                        break;
+                    }
+                }
+            }
+            // ---- count_below(d0): every entry below d0, dead ones included
+            int nb = fa;
+            if (fa > 0 && wdis(cs[fa - 1]) == d0) {
+                for (int b1 = fa; b1 > 0; b1 -= 64) {
+                    const int ii = b1 - 64 + lane;
+                    const unsigned long long m3 = __ballot(ii >= 0 && wdis(cs[ii >= 0 ? ii : 0]) == d0);
+                    nb -= __popcll(m3);
+                    if (m3 != ~0ull) break;
+                }
+            }
+            if (nb >= efSearch) {
+                st_n2 = nalive == 0 ? 1u : 0u;
+                break;
+            }
+            fa = nfa;
+            // ---- neighbours of v0 in stored order, visited test-and-set (a
+            // node listed twice is fresh at its first position only)
+            int32_t v1 = -1;
+            if (lane < cnt)
+                v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
+                           : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
+            const unsigned long long neg =
+                    __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
+            const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
+            const uint32_t vbit = 1u << (v1 & 31);
+            bool fresh = lane < jmax && !(vis[v1 >> 5] & vbit);
+            uint32_t old = 0u;
+            if (fresh) old = atomicOr(&vis[v1 >> 5], vbit);
+            if (__ballot(fresh && (old & vbit)) != 0ull)
+                for (int i = 0; i < jmax; i++)
+                    fresh &= !(i < lane && __builtin_amdgcn_readlane(v1, i) == v1);
+            const unsigned long long fm = __ballot(fresh);
+            const int nf = __popcll(fm);
+            st_ndis += (uint32_t)nf;
+            st_nhops += 1;
+            if (nf == 0) {
+                __syncthreads();
+                continue;
+            }
+            const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
+            const int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
+            // ---- the full set admits only keys below its largest: the int8
+            // bound drops rows that cannot reach it (strictly above its
+            // distance, so no tie is skipped)
+            const bool full = S == ef;
+            const uint64_t emax = full ? cs[ef - 1] : ~0ull;
+            const float maxd = wdis(emax);
+            int32_t sv = fv;
+            int ns = nf;
+            if (use_q8 && full && maxd < FLT_MAX) {
+                st_q8 += (uint32_t)nf;
+                ns = q8_filter(g, q8x, q8d, fv, nf, __uint_as_float(__float_as_uint(maxd) + 1u),
+                               lane, sv);
+            }
+            st_x32 += (uint32_t)ns;
+            float fdis = WS_INF;
+            if (ns > 0) {
+                if (g.d <= 128)
+                    fdis = ref_rows64_4lane_pb<true, 16, 1>(qs, qs, g.storage, g.ld, g.d,
+                                                            lane < ns ? (uint32_t)sv : 0u, ns,
+                                                            lane);
+                else if (lane < ns)
+                    fdis = l2_row(qs, g.storage + (int64_t)sv * g.ld, g.d);
+            }
+            const long long ki = ((long long)(uint32_t)sv << 1) | 1ll;
+            bool enter = lane < ns;
+            float rej = WS_INF;
+            if (full) {
+                if (__ballot(lane < ns && fdis == maxd) != 0ull) tie |= 2u;  // push at the max
+                enter = enter && key_less(fdis, ki, maxd, (long long)(uint32_t)emax);
+                if (lane < ns && !enter) rej = fdis;
+            }
+            float cd = enter ? fdis : WS_INF;
+            long long ci = enter ? ki : WS_NOID;
+            const int m = wave_compact(cd, ci, enter, lane);
+            float disc = rej;
+            if (m > 0) {
+                wave_sort_m(cd, ci, lane, m);
+                const uint64_t akey =
+                        lane < m ? (((uint64_t)__float_as_uint(cd) << 32) | (uint32_t)ci) : ~0ull;
+                // lower_bound of each arrival in the set (entries below it)
+                int lb = 0;
+                {
+                    int st = 1;
+                    while (2 * st <= S) st *= 2;
+                    for (; st > 0; st >>= 1)
+                        if (lb + st <= S && cs[lb + st - 1] < akey) lb += st;
+                }
+                if (lane >= m) lb = S;
+                const int lb0 = __builtin_amdgcn_readfirstlane(lb);
+                // the entries from lb0 on move up by the arrivals below them
+                // (backward, 64 at a time: a step's reads precede its writes,
+                // and its writes land past every entry still to be read)
+                int ev_alive = 0;
+                for (int top = S; top > lb0; top -= 64) {
+                    const int i = top - 64 + lane;
+                    const bool vv = i >= lb0;
+                    const uint64_t e = vv ? cs[i] : 0ull;
+                    int c = 0;
+                    for (int j = 0; j < m; j++) c += __builtin_amdgcn_readlane(lb, j) <= i ? 1 : 0;
+                    const int np = i + c;
+                    __syncthreads();
+                    if (vv) {
+                        if (np < ef) {
+                            cs[np] = e;
+                        } else {
+                            disc = fminf(disc, wdis(e));
+                            ev_alive += (int)(e & 1ull);
+                        }
+                    }
+                }
+                const int pa = lane + lb;
+                const bool kept = lane < m && pa < ef;
+                if (kept) cs[pa] = akey;
+                else if (lane < m) disc = fminf(disc, cd);
+                // new first alive: the old one's new place, or the first arrival
+                int cfa = 0;
+                for (int j = 0; j < m; j++) cfa += __builtin_amdgcn_readlane(lb, j) <= fa ? 1 : 0;
+#pragma unroll
+                for (int mm = 32; mm > 0; mm >>= 1) ev_alive += __shfl_xor(ev_alive, mm);
+                nalive += __popcll(__ballot(kept)) - ev_alive;
+                int nfa2 = fa < S && fa + cfa < ef ? fa + cfa : ef;
+                if (lb0 < ef) nfa2 = min(nfa2, lb0);
+                S = min(S + m, ef);
+                fa = min(nfa2, S);
+            }
+#pragma unroll
+            for (int mm = 32; mm > 0; mm >>= 1) disc = fminf(disc, __shfl_xor(disc, mm));
+            __syncthreads();
+            // the kept-ef boundary: a discarded key of the ef-th kept distance
+            if (S == ef && disc < WS_INF && wdis(cs[ef - 1]) == disc) tie |= 4u;
+            rdisc = fminf(rdisc, disc);
+        }
+    }
+    // the k-th boundary: the reference's result heap (strict admission) and
+    // the set's first k (by id among equals) differ only when the k-th
+    // distance is shared by a later entry or a key the set turned away
+    if (S >= k) {
+        const float kd = wdis(cs[k - 1]);
+        float nd = S > k ? wdis(cs[k]) : WS_INF;
+        nd = fminf(nd, rdisc);
+        if (kd < FLT_MAX && nd == kd) tie |= 8u;
+    }
+    if (tie_flags && lane == 0) tie_flags[q] = tie;
+    if (tie && tie_flags) return;  // the sequential kernel redoes this query
+    if (stats && lane == 0 && g.entry_point >= 0) {
+        atomicAdd(&stats[0], 1ull);
+        atomicAdd(&stats[1], (unsigned long long)st_n2);
+        atomicAdd(&stats[2], (unsigned long long)st_ndis);
+        atomicAdd(&stats[3], (unsigned long long)st_nhops);
+        atomicAdd(&stats[4], (unsigned long long)(st_ndis - st_q8 + st_x32));
+        atomicAdd(&stats[5], (unsigned long long)st_q8);
+    }
+    for (int j = lane; j < k; j += 64) {
+        const uint64_t e = j < S ? cs[j] : ~0ull;
+        const bool ok = j < S && wdis(e) < FLT_MAX;
+        const float dv = ok ? wdis(e) : FLT_MAX;
+        const int32_t id = ok ? wid(e) : -1;
+        if (D) D[q * k + j] = dv;
+        if (I) I[q * k + j] = id;
+        if (I32) I32[q * k + j] = id;
+    }
+}
+
 // the sequential kernel over n queries (qidx: the listed ones, compact
 // outputs), register heaps for ef, k <= 64
 static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
@@ -1626,11 +1935,11 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
         FAISS_THROW_IF_NOT(gheap != nullptr);
         const size_t lds_g = seq_lds_bytes_gheap(g.ld);
         if (lds_g + vwords * 4 <= 64 * 1024)
-            k_hnsw_exact<true, true><<<dim3((unsigned)n), dim3(64), lds_g + vwords * 4, s>>>(
+            k_hnsw_exact<true, true><<<kgrid(n, 64), dim3(64), lds_g + vwords * 4, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
                     gheap);
         else
-            k_hnsw_exact<false, true><<<dim3((unsigned)n), dim3(64), lds_g, s>>>(
+            k_hnsw_exact<false, true><<<kgrid(n, 64), dim3(64), lds_g, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats, only,
                     qidx, gheap);
         HIP_LAUNCH_CHECK();
@@ -1661,7 +1970,7 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
             auto kt = lds_log ? k_hnsw_exact_reg<true, true, true, true>
                               : (g.nb0 ? k_hnsw_exact_reg<true, true, true, false>
                                        : k_hnsw_exact_reg<true, true, false, false>);
-            kt<<<dim3((unsigned)n), dim3(64), lds_r + vwords * 4 + lds_logx, s>>>(
+            kt<<<kgrid(n, 64), dim3(64), lds_r + vwords * 4 + lds_logx, s>>>(
                     g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
                     layout, tb, rlog, rcap);
             HIP_LAUNCH_CHECK();
@@ -1680,17 +1989,17 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
                                    : k_hnsw_exact_reg<true, false, false, false>)
                           : (g.nb0 ? k_hnsw_exact_reg<false, false, true, false>
                                    : k_hnsw_exact_reg<false, false, false, false>);
-        kr<<<dim3((unsigned)n), dim3(64), rvis ? lds_r + vwords * 4 + lds_logx : lds_r, s>>>(
+        kr<<<kgrid(n, 64), dim3(64), rvis ? lds_r + vwords * 4 + lds_logx : lds_r, s>>>(
                 g, x, ldx, n, k, efSearch, ef, D, I, I32, rvis ? nullptr : visited_scratch, vwords,
                 stats, only, qidx, layout, nullptr, rlog, rcap);
         HIP_LAUNCH_CHECK();
         return;
     }
     if (x_lds_vis)
-        k_hnsw_exact<true><<<dim3((unsigned)n), dim3(64), lds_x + vwords * 4, s>>>(
+        k_hnsw_exact<true><<<kgrid(n, 64), dim3(64), lds_x + vwords * 4, s>>>(
                 g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx);
     else
-        k_hnsw_exact<false><<<dim3((unsigned)n), dim3(64), lds_x, s>>>(
+        k_hnsw_exact<false><<<kgrid(n, 64), dim3(64), lds_x, s>>>(
                 g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats, only,
                 qidx);
     HIP_LAUNCH_CHECK();
@@ -1713,7 +2022,7 @@ void hnsw_flag_compact(const uint32_t* flags, int64_t n, uint32_t* idx, uint32_t
                        hipStream_t s) {
     HIP_CHECK(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
     if (n <= 0) return;
-    k_flag_compact<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s>>>(flags, n, idx, count);
+    k_flag_compact<<<kgrid(cdiv(n, 256), 256), dim3(256), 0, s>>>(flags, n, idx, count);
     HIP_LAUNCH_CHECK();
 }
 
@@ -1746,18 +2055,33 @@ bool hnsw_visited_scratch_needed(int ld, int k, int efSearch, int64_t vwords) {
         g.ld = ld;
         need = need || (size_t)exact_reg_head(g) + vb > kL;
     }
-    if (hnsw_uses_batched(k, efSearch)) need = need || lds_q + vb > kL;
+    if (hnsw_uses_wide(k, efSearch)) {
+        HNSWDevice g{};
+        g.ld = ld;
+        need = need || wide_lds_bytes(g, ef) + vb > kL;
+    } else if (hnsw_uses_batched(k, efSearch)) {
+        need = need || lds_q + vb > kL;
+    }
     return need;
 }
 bool hnsw_register_eligible(int k, int efSearch) {
     const int ef = efSearch > k ? efSearch : k;
     return ef <= 64 && k <= 64;
 }
+// the wide kernel (k_hnsw_wide): 128 < ef <= kHnswWideMaxEf (its sorted set
+// in the LDS, 8 B per entry); FAISS_AMD_HNSW_WIDE=0: the sequential kernel
+bool hnsw_uses_wide(int k, int efSearch) {
+    const int ef = efSearch > k ? efSearch : k;
+    const char* wenv = getenv("FAISS_AMD_HNSW_WIDE");
+    if (wenv && !strcmp(wenv, "0")) return false;
+    return ef > 128 && ef <= kHnswWideMaxEf;
+}
 bool hnsw_uses_batched(int k, int efSearch) {
     const int ef = efSearch > k ? efSearch : k;
     const char* menv = getenv("FAISS_AMD_HNSW");
     const bool prefer_batched = menv && !strcmp(menv, "batched");
-    return ef <= 128 && k <= kMaxK && (prefer_batched || !hnsw_register_eligible(k, efSearch));
+    return (ef <= 128 && k <= kMaxK && (prefer_batched || !hnsw_register_eligible(k, efSearch))) ||
+           hnsw_uses_wide(k, efSearch);
 }
 void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k, int efSearch,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
@@ -1793,14 +2117,25 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
         exact(nullptr);
         return;
     }
-    {
+    if (hnsw_uses_wide(k, efSearch)) {
+        ScopedKernelTimer tm(kt, "hnsw_wide", 0.0, s);
+        const size_t lds_w = wide_lds_bytes(g, ef);
+        if (lds_w + (size_t)vwords * 4 <= 64 * 1024)
+            k_hnsw_wide<true><<<kgrid(n, 64), dim3(64), lds_w + vwords * 4, s>>>(
+                    g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, flags);
+        else
+            k_hnsw_wide<false><<<kgrid(n, 64), dim3(64), lds_w, s>>>(
+                    g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
+                    flags);
+        HIP_LAUNCH_CHECK();
+    } else {
     ScopedKernelTimer tm(kt, "hnsw_search", 0.0, s);
     if (lds_vis) {
         size_t lds = lds_q + sizeof(uint32_t) * vwords;
-        k_hnsw_search<true><<<dim3((unsigned)n), dim3(64), lds, s>>>(
+        k_hnsw_search<true><<<kgrid(n, 64), dim3(64), lds, s>>>(
                 g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, flags);
     } else {
-        k_hnsw_search<false><<<dim3((unsigned)n), dim3(64), lds_q, s>>>(
+        k_hnsw_search<false><<<kgrid(n, 64), dim3(64), lds_q, s>>>(
                 g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats, flags);
     }
     HIP_LAUNCH_CHECK();
@@ -1840,7 +2175,7 @@ __global__ void k_gather_rows(const float* __restrict__ in, int ldi,
 void gather_rows(const float* in, int ldi, const uint32_t* idx, int64_t n, int d, float* out,
                  int ldo, hipStream_t s) {
     if (n <= 0) return;
-    k_gather_rows<<<dim3((unsigned)n), dim3(64), 0, s>>>(in, ldi, idx, n, d, out, ldo);
+    k_gather_rows<<<kgrid(n, 64), dim3(64), 0, s>>>(in, ldi, idx, n, d, out, ldo);
     HIP_LAUNCH_CHECK();
 }
 __global__ void k_scatter_rows(const uint32_t* __restrict__ src, int words,
@@ -1854,7 +2189,7 @@ __global__ void k_scatter_rows(const uint32_t* __restrict__ src, int words,
 void scatter_rows(const void* src, int row_words, const uint32_t* idx, int64_t n, void* dst,
                   hipStream_t s) {
     if (n <= 0 || row_words <= 0) return;
-    k_scatter_rows<<<dim3((unsigned)n), dim3(64), 0, s>>>((const uint32_t*)src, row_words, idx,
+    k_scatter_rows<<<kgrid(n, 64), dim3(64), 0, s>>>((const uint32_t*)src, row_words, idx,
                                                          n, (uint32_t*)dst);
     HIP_LAUNCH_CHECK();
 }

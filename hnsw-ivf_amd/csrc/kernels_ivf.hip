@@ -361,7 +361,7 @@ void ivf_visit_stats(const int32_t* assign, int64_t total, const uint32_t* list_
                      const uint32_t* lim, unsigned long long* stats, hipStream_t s) {
     if (total <= 0) return;
     const int64_t grid = std::min<int64_t>(cdiv(total, 256), 1024);
-    k_ivf_visit_stats<<<dim3((unsigned)grid), dim3(256), 0, s>>>(assign, total, list_len, nlist,
+    k_ivf_visit_stats<<<kgrid(grid, 256), dim3(256), 0, s>>>(assign, total, list_len, nlist,
                                                                  lim, stats);
     HIP_LAUNCH_CHECK();
 }
@@ -390,7 +390,7 @@ void probe_limits(const int32_t* assign, int64_t n, int nprobe, const uint32_t* 
                   int nlist, int64_t max_codes, int32_t* assign_out, uint32_t* lim,
                   hipStream_t s) {
     if (n <= 0) return;
-    k_probe_limits<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s>>>(
+    k_probe_limits<<<kgrid(cdiv(n, 256), 256), dim3(256), 0, s>>>(
             assign, n, nprobe, list_len, nlist, max_codes, assign_out, lim);
     HIP_LAUNCH_CHECK();
 }
@@ -436,7 +436,7 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
 #undef BSCAN
     HIP_LAUNCH_CHECK();
     if (total > 0) {
-        k_bucket_fill<<<dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s>>>(
+        k_bucket_fill<<<kgrid(cdiv(total, 256), 256), dim3(256), 0, s>>>(
                 assign, total, list_len, nlist, QT, b.bucket_off, b.item_off, b.cursor, b.entries,
                 b.item_entries, b.item_desc, b.counts, list_off, b.mark_keys, b.mark_recs,
                 b.mark_ke);

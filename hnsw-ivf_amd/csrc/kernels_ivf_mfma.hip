@@ -76,14 +76,14 @@ static_assert(FQ == IVF_FLAT_QT, "host and filter must agree on the work-item wi
 // f32 arena -> bf16 hi/lo arena: row r = hi[DB] | lo[DB], zero beyond d
 __global__ void k_split_bf16(const float* __restrict__ codes, int64_t rows, int d, int ldc, int DB,
                              __bf16* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= rows * DB) return;
-    const int64_t r = i / DB;
-    const int j = (int)(i - r * DB);
-    const float v = j < d ? codes[r * ldc + j] : 0.f;
-    const __bf16 h = (__bf16)v;
-    out[r * 2 * DB + j] = h;
-    out[r * 2 * DB + DB + j] = (__bf16)(v - (float)h);
+    GRID_STRIDE(i, rows * DB) {
+        const int64_t r = i / DB;
+        const int j = (int)(i - r * DB);
+        const float v = j < d ? codes[r * ldc + j] : 0.f;
+        const __bf16 h = (__bf16)v;
+        out[r * 2 * DB + j] = h;
+        out[r * 2 * DB + DB + j] = (__bf16)(v - (float)h);
+    }
 }
 
 // Y3: bf16x3 (codes split hi + lo, three MFMAs per k-step);  !Y3: bf16x2
@@ -682,39 +682,38 @@ __global__ void k_split_stream(const float* __restrict__ codes, int64_t rows, in
                                int DB, const float* __restrict__ ynorm,
                                const uint32_t* __restrict__ row_list, uint8_t* __restrict__ out,
                                int fold) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int per = DB + 8;  // bf16 slots per row (the last 8 = the 16-B tail)
-    if (i >= rows * per) return;
-    const int64_t r = i / per;
-    const int j = (int)(i - r * per);
-    uint8_t* row = out + r * (int64_t)(2 * DB + 16);
-    if (j < DB) {
-        const float v = j < d ? codes[r * ldc + j] : 0.f;
-        ((__bf16*)row)[j] = (__bf16)v;
-    } else if (fold) {
-        // bias A-fragment {-|y|^2/2 in three bf16 parts, 1, 1, 1, 0, 0}
-        const int t = j - DB;
-        __bf16 v = (__bf16)0.f;
-        if (t < 3) {
-            __bf16 h = (__bf16)(-WS_INF), m = (__bf16)0.f, lo = (__bf16)0.f;
-            if (row_list[r] != 0xffffffffu) split3_bf16(-0.5f * ynorm[r], h, m, lo);
-            v = t == 0 ? h : t == 1 ? m : lo;
-        } else if (t < 6) {
-            v = (__bf16)1.f;
+    GRID_STRIDE(i, rows * per) {
+        const int64_t r = i / per;
+        const int j = (int)(i - r * per);
+        uint8_t* row = out + r * (int64_t)(2 * DB + 16);
+        if (j < DB) {
+            const float v = j < d ? codes[r * ldc + j] : 0.f;
+            ((__bf16*)row)[j] = (__bf16)v;
+        } else if (fold) {
+            // bias A-fragment {-|y|^2/2 in three bf16 parts, 1, 1, 1, 0, 0}
+            const int t = j - DB;
+            __bf16 v = (__bf16)0.f;
+            if (t < 3) {
+                __bf16 h = (__bf16)(-WS_INF), m = (__bf16)0.f, lo = (__bf16)0.f;
+                if (row_list[r] != 0xffffffffu) split3_bf16(-0.5f * ynorm[r], h, m, lo);
+                v = t == 0 ? h : t == 1 ? m : lo;
+            } else if (t < 6) {
+                v = (__bf16)1.f;
+            }
+            ((__bf16*)row)[j] = v;
+        } else if (j == DB) {
+            *(float*)(row + 2 * DB) = row_list[r] == 0xffffffffu ? WS_INF : ynorm[r];
+        } else if (j > DB + 1) {
+            ((uint16_t*)row)[DB + (j - DB)] = 0;  // bytes 2 DB + 4 .. 2 DB + 15
         }
-        ((__bf16*)row)[j] = v;
-    } else if (j == DB) {
-        *(float*)(row + 2 * DB) = row_list[r] == 0xffffffffu ? WS_INF : ynorm[r];
-    } else if (j > DB + 1) {
-        ((uint16_t*)row)[DB + (j - DB)] = 0;  // bytes 2 DB + 4 .. 2 DB + 15
     }
 }
 void split_bf16_stream(const float* codes, int64_t rows, int d, int ldc, int DB,
                        const float* ynorm, const uint32_t* row_list, void* out, hipStream_t s,
                        int fold) {
     if (rows <= 0) return;
-    const int64_t tot = rows * (DB + 8);
-    k_split_stream<<<dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, s>>>(
+    k_split_stream<<<stride_grid(rows * (DB + 8), 256), dim3(256), 0, s>>>(
             codes, rows, d, ldc, DB, ynorm, row_list, (uint8_t*)out, fold);
     HIP_LAUNCH_CHECK();
 }
@@ -730,40 +729,39 @@ __global__ void k_pq_stream_image(const uint8_t* __restrict__ codes, int cs, int
                                   const float* __restrict__ terms,
                                   const uint32_t* __restrict__ row_list, int DB,
                                   uint8_t* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int per = DB + 8;
-    if (i >= rows * per) return;
-    const int64_t r = i / per;
-    const int j = (int)(i - r * per);
-    __bf16* row = (__bf16*)(out + r * (int64_t)(2 * DB + 16));
-    const bool pad = row_list[r] == 0xffffffffu;
-    if (j < DB) {
-        float v = 0.f;
-        if (j < d && !pad) {
-            const int m = j / dsub;
-            const int c = codes[r * cs + m];
-            v = pq_cent[((int64_t)m * 256 + c) * dsub + (j - m * dsub)];
+    GRID_STRIDE(i, rows * per) {
+        const int64_t r = i / per;
+        const int j = (int)(i - r * per);
+        __bf16* row = (__bf16*)(out + r * (int64_t)(2 * DB + 16));
+        const bool pad = row_list[r] == 0xffffffffu;
+        if (j < DB) {
+            float v = 0.f;
+            if (j < d && !pad) {
+                const int m = j / dsub;
+                const int c = codes[r * cs + m];
+                v = pq_cent[((int64_t)m * 256 + c) * dsub + (j - m * dsub)];
+            }
+            row[j] = (__bf16)v;
+        } else {
+            const int t = j - DB;
+            __bf16 v = (__bf16)0.f;
+            if (t < 3) {
+                __bf16 h = (__bf16)(-WS_INF), m = (__bf16)0.f, lo = (__bf16)0.f;
+                if (!pad) split3_bf16(-0.5f * terms[r], h, m, lo);
+                v = t == 0 ? h : t == 1 ? m : lo;
+            } else if (t < 6) {
+                v = (__bf16)1.f;
+            }
+            row[j] = v;
         }
-        row[j] = (__bf16)v;
-    } else {
-        const int t = j - DB;
-        __bf16 v = (__bf16)0.f;
-        if (t < 3) {
-            __bf16 h = (__bf16)(-WS_INF), m = (__bf16)0.f, lo = (__bf16)0.f;
-            if (!pad) split3_bf16(-0.5f * terms[r], h, m, lo);
-            v = t == 0 ? h : t == 1 ? m : lo;
-        } else if (t < 6) {
-            v = (__bf16)1.f;
-        }
-        row[j] = v;
     }
 }
 void pq_stream_image(const uint8_t* codes, int cs, int64_t rows, int d, int dsub,
                      const float* pq_cent, const float* terms, const uint32_t* row_list, int DB,
                      void* out, hipStream_t s) {
     if (rows <= 0) return;
-    const int64_t tot = rows * (DB + 8);
-    k_pq_stream_image<<<dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, s>>>(
+    k_pq_stream_image<<<stride_grid(rows * (DB + 8), 256), dim3(256), 0, s>>>(
             codes, cs, rows, d, dsub, pq_cent, terms, row_list, DB, (uint8_t*)out);
     HIP_LAUNCH_CHECK();
 }
@@ -801,7 +799,7 @@ void ivfpq_stream_filter(const float* x, int ldx, int d, int M, const void* pcbs
     FAISS_THROW_IF_NOT(grid < (1ll << 31));
     const float coef = (float)ivfpq_fold_coef(d, M);
 #define PQS(KTV, NSV)                                                                         \
-    k_ivf_bf2_stream<true, KTV, NSV, false, true, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+    k_ivf_bf2_stream<true, KTV, NSV, false, true, true><<<kgrid(grid, 256), dim3(256), 0, s>>>( \
             x, ldx, d, (const uint8_t*)pcbs, lRmax, lrmax, nprobe, coef, obits, b.item_off,  \
             b.item_desc, b.item_entries, (uint32_t)max_items, nlist, b.lim, keys, recs,      \
             nullptr, (const uint8_t*)qimg, qxn, cdis, cnorm)
@@ -827,7 +825,7 @@ __global__ void k_pad_rows_inf(float* __restrict__ v, const uint32_t* __restrict
 }
 void pad_rows_inf(float* v, const uint32_t* row_list, int64_t rows, hipStream_t s) {
     if (rows <= 0) return;
-    k_pad_rows_inf<<<dim3((unsigned)cdiv(rows, 256)), dim3(256), 0, s>>>(v, row_list, rows);
+    k_pad_rows_inf<<<kgrid(cdiv(rows, 256), 256), dim3(256), 0, s>>>(v, row_list, rows);
     HIP_LAUNCH_CHECK();
 }
 
@@ -848,7 +846,7 @@ __global__ void k_list_max(const float* __restrict__ yn, const uint32_t* __restr
 void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* list_len,
                     int nlist, float* out, hipStream_t s) {
     if (nlist <= 0) return;
-    k_list_max<<<dim3((unsigned)cdiv(nlist, 4)), dim3(256), 0, s>>>(yn, list_off, list_len,
+    k_list_max<<<kgrid(cdiv(nlist, 4), 256), dim3(256), 0, s>>>(yn, list_off, list_len,
                                                                     nlist, out);
     HIP_LAUNCH_CHECK();
 }
@@ -920,16 +918,15 @@ __global__ void k_row_resnorm(const float* __restrict__ codes, int64_t rows, int
 void row_resnorm_bf16(const float* codes, int64_t rows, int d, int ldc, float* out,
                       hipStream_t s) {
     if (rows <= 0) return;
-    k_row_resnorm<<<dim3((unsigned)cdiv(rows, 256)), dim3(256), 0, s>>>(codes, rows, d, ldc, out);
+    k_row_resnorm<<<kgrid(cdiv(rows, 256), 256), dim3(256), 0, s>>>(codes, rows, d, ldc, out);
     HIP_LAUNCH_CHECK();
 }
 
 void split_bf16(const float* codes, int64_t rows, int d, int ldc, int DB, void* out,
                 hipStream_t s) {
     if (rows <= 0) return;
-    const int64_t n = rows * DB;
-    k_split_bf16<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s>>>(codes, rows, d, ldc, DB,
-                                                                    (__bf16*)out);
+    k_split_bf16<<<stride_grid(rows * DB, 256), dim3(256), 0, s>>>(codes, rows, d, ldc, DB,
+                                                                   (__bf16*)out);
     HIP_LAUNCH_CHECK();
 }
 
@@ -1009,22 +1006,22 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
         if (stream_ok)                                                                        \
             (spipe ? k_ivf_bf2_stream<L2V, KTV, NSV, true>                                   \
              : fk  ? k_ivf_bf2_stream<L2V, KTV, NSV, false, L2V>                              \
-                   : k_ivf_bf2_stream<L2V, KTV, NSV, false>)<<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+                   : k_ivf_bf2_stream<L2V, KTV, NSV, false>)<<<kgrid(grid, 256), dim3(256), 0, s>>>( \
                     x, ldx, d, (const uint8_t*)cbs, ynmax, rmax, nprobe, coef, obits,         \
                     b.item_off, b.item_desc, b.item_entries, (uint32_t)max_items, nlist,      \
                     b.lim, keys, recs, ftrace, qimg, qxn, nullptr, nullptr);                  \
         else if (b.sel)                                                                       \
-            k_ivf_bf3_filter<L2V, KTV, NSV, false, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+            k_ivf_bf3_filter<L2V, KTV, NSV, false, true><<<kgrid(grid, 256), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
                     b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, b.sel, keys, recs, ftrace);    \
         else if (y3)                                                                          \
-            k_ivf_bf3_filter<L2V, KTV, NSV, true, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>( \
+            k_ivf_bf3_filter<L2V, KTV, NSV, true, false><<<kgrid(grid, 256), dim3(256), 0, s>>>( \
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
                     b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, b.sel, keys, recs, ftrace);    \
         else                                                                                  \
-            k_ivf_bf3_filter<L2V, KTV, NSV, false, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(\
+            k_ivf_bf3_filter<L2V, KTV, NSV, false, false><<<kgrid(grid, 256), dim3(256), 0, s>>>(\
                     x, ldx, d, (const __bf16*)cbf, ynorm, ynmax, rres, rmax, list_off,       \
                     list_len, nlist, nprobe, coef, obits, b.bucket_off, b.item_off,           \
                     b.item_desc, b.item_entries, (uint32_t)max_items, b.lim, b.sel, keys, recs, ftrace);    \

@@ -56,7 +56,7 @@ void ivfpq_terms(const uint8_t* codes, const uint32_t* row_list, int64_t nrows,
                  int dsub, float* terms, hipStream_t s) {
     if (nrows <= 0) return;
     const int code_stride = (int)roundup((size_t)M, 4);
-    k_ivfpq_terms<<<dim3((unsigned)cdiv(nrows, 256)), dim3(256), 0, s>>>(
+    k_ivfpq_terms<<<kgrid(cdiv(nrows, 256), 256), dim3(256), 0, s>>>(
             codes, code_stride, row_list, nrows, centroids, ldcent, pq_centroids, M, ksub, dsub,
             terms);
     HIP_LAUNCH_CHECK();
@@ -138,16 +138,16 @@ __global__ __launch_bounds__(256) void k_pq_encode(const float* __restrict__ x, 
 __global__ void k_pair_l2(const float* __restrict__ x, int ldx, const float* __restrict__ cent,
                           int ldc, int d, const int32_t* __restrict__ assign, int64_t n, int np,
                           float* __restrict__ out) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n * np) return;
-    const int32_t l = assign[e];
-    out[e] = l >= 0 ? ref_l2(x + (e / np) * ldx, cent + (int64_t)l * ldc, d) : 0.f;
+    GRID_STRIDE(e, n * np) {
+        const int32_t l = assign[e];
+        out[e] = l >= 0 ? ref_l2(x + (e / np) * ldx, cent + (int64_t)l * ldc, d) : 0.f;
+    }
 }
 void pair_l2(const float* x, int ldx, const float* cent, int ldc, int d, const int32_t* assign,
              int64_t n, int np, float* out, hipStream_t s) {
     if (n <= 0 || np <= 0) return;
-    k_pair_l2<<<dim3((unsigned)cdiv(n * np, 256)), dim3(256), 0, s>>>(x, ldx, cent, ldc, d, assign,
-                                                                     n, np, out);
+    k_pair_l2<<<stride_grid(n * np, 256), dim3(256), 0, s>>>(x, ldx, cent, ldc, d, assign, n,
+                                                            np, out);
     HIP_LAUNCH_CHECK();
 }
 

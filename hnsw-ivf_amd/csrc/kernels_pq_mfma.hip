@@ -71,10 +71,10 @@ __global__ void k_pq_row_res(const uint8_t* __restrict__ codes, int cs, int64_t 
 void pq_decode_prep(const float* pq_cent, int M, int dsub, const uint8_t* codes, int cs,
                     int64_t rows, void* dec, float* rnorm, float* rres, hipStream_t s) {
     const int n = M * 256 * dsub;
-    k_pq_dec_table<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s>>>(pq_cent, n, (__bf16*)dec);
+    k_pq_dec_table<<<kgrid(cdiv(n, 256), 256), dim3(256), 0, s>>>(pq_cent, n, (__bf16*)dec);
     HIP_LAUNCH_CHECK();
     if (rows > 0) {
-        k_pq_row_res<<<dim3((unsigned)cdiv(rows, 256)), dim3(256), 0, s>>>(
+        k_pq_row_res<<<kgrid(cdiv(rows, 256), 256), dim3(256), 0, s>>>(
                 codes, cs, rows, M, dsub, pq_cent, rnorm, rres);
         HIP_LAUNCH_CHECK();
     }
@@ -551,6 +551,15 @@ __global__ __launch_bounds__(768, 3) void k_ivfpq_filter_w(
             __bf16 h, m, lo;
             split3_bf16(-0.5f * term, h, m, lo);
             const __bf16 one = (__bf16)1.f, zero = (__bf16)0.f;
+            // padding rows and IDSelector non-members (term +inf): -inf, 0, 0
+            // as the image builders write them, so the accumulator is -inf
+            // (key 0xff80xxxx, after every real key) — split3 of -inf would
+            // leave NaN in the residual parts and a NaN key, which sorts ahead
+            // of the real keys and gives its stream a dropped bound of 0
+            if (!(term < WS_INF)) {
+                m = zero;
+                lo = zero;
+            }
             bf16x8 ab;
             ab[0] = lh ? zero : h;
             ab[1] = lh ? zero : m;
@@ -734,7 +743,7 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
                          : k_ivfpq_filter_w<DS, NSV, KTV, false>;                               \
         HIP_CHECK(hipFuncSetAttribute((const void*)kfn,                                        \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsw)); \
-        kfn<<<dim3((unsigned)gridw), dim3(64 * wpb), ldsw, s>>>(                               \
+        kfn<<<kgrid(gridw, 64 * wpb), dim3(64 * wpb), ldsw, s>>>(                               \
                 (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, nlist, nprobe,    \
                 coefw, obits, b.item_off, b.item_desc, b.item_entries, b.lim, b.sel, keys,      \
                 recs, (const uint8_t*)qimg, qxn, b.item_ctr, trace, sched);                    \
@@ -760,7 +769,7 @@ void ivfpq_filter(const float* x, int ldx, int d, int M, const void* dec, const 
                                           (int)lds));                                          \
             attr[b.sel ? 1 : 0] = true;                                                        \
         }                                                                                      \
-        kfn<<<dim3((unsigned)grid), dim3(256), lds, s>>>(                                      \
+        kfn<<<kgrid(grid, 256), dim3(256), lds, s>>>(                                      \
                 x, ldx, (const __bf16*)dec, codes, terms, cdis, cnorm, lrmax, lRmax, nlist,    \
                 nprobe, coef, obits, b.item_off, b.item_desc, b.item_entries, b.lim, b.sel,    \
                 keys, recs, (const uint8_t*)qimg, qxn);                                        \

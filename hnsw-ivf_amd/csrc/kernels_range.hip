@@ -26,39 +26,41 @@ __global__ __launch_bounds__(64) void k_ivf_range(
         const uint32_t* __restrict__ list_off, const uint32_t* __restrict__ list_len, int nlist,
         int d, float radius, const uint8_t* __restrict__ selm, uint32_t* __restrict__ counts,
         const uint64_t* __restrict__ offsets, float* __restrict__ outD,
-        int64_t* __restrict__ outI) {
-    const int64_t qp = blockIdx.x;
-    const int64_t q = qp / np;
+        int64_t* __restrict__ outI, int64_t npairs) {
     const int lane = threadIdx.x;
-    const int32_t key = assign[qp];
-    uint32_t cnt = 0;
-    if (key >= 0 && key < nlist) {
-        const uint32_t off = list_off[key], len = list_len[key];
-        const float* xq = x + q * (int64_t)ldx;
-        const uint64_t base = FILL ? offsets[qp] : 0;
-        const uint64_t below = (1ull << lane) - 1ull;
-        for (uint32_t r0 = 0; r0 < len; r0 += 64) {
-            const uint32_t r = r0 + lane;
-            bool hit = false;
-            float dis = 0.f;
-            if (r < len) {
-                const uint64_t row = (uint64_t)off + r;
-                if (!selm || selm[row]) {
-                    dis = ref_dist<L2>(xq, codes + row * (uint64_t)ldc, d);
-                    hit = L2 ? (dis < radius) : (radius < dis);
+    // one wave per (query, probe), block-strided over the n np pairs
+    for (int64_t qp = blockIdx.x; qp < npairs; qp += gridDim.x) {
+        const int64_t q = qp / np;
+        const int32_t key = assign[qp];
+        uint32_t cnt = 0;
+        if (key >= 0 && key < nlist) {
+            const uint32_t off = list_off[key], len = list_len[key];
+            const float* xq = x + q * (int64_t)ldx;
+            const uint64_t base = FILL ? offsets[qp] : 0;
+            const uint64_t below = (1ull << lane) - 1ull;
+            for (uint32_t r0 = 0; r0 < len; r0 += 64) {
+                const uint32_t r = r0 + lane;
+                bool hit = false;
+                float dis = 0.f;
+                if (r < len) {
+                    const uint64_t row = (uint64_t)off + r;
+                    if (!selm || selm[row]) {
+                        dis = ref_dist<L2>(xq, codes + row * (uint64_t)ldc, d);
+                        hit = L2 ? (dis < radius) : (radius < dis);
+                    }
                 }
+                const uint64_t m = __ballot(hit);
+                if (FILL && hit) {
+                    const uint64_t o = base + cnt + (uint32_t)__popcll(m & below);
+                    outD[o] = dis;
+                    // ids == nullptr: store_pairs, lo_build(list_no, offset)
+                    outI[o] = ids ? ids[(uint64_t)off + r] : (((int64_t)key << 32) | (int64_t)r);
+                }
+                cnt += (uint32_t)__popcll(m);
             }
-            const uint64_t m = __ballot(hit);
-            if (FILL && hit) {
-                const uint64_t o = base + cnt + (uint32_t)__popcll(m & below);
-                outD[o] = dis;
-                // ids == nullptr: store_pairs, lo_build(list_no, offset)
-                outI[o] = ids ? ids[(uint64_t)off + r] : (((int64_t)key << 32) | (int64_t)r);
-            }
-            cnt += (uint32_t)__popcll(m);
         }
+        if (!FILL && lane == 0) counts[qp] = cnt;
     }
-    if (!FILL && lane == 0) counts[qp] = cnt;
 }
 }  // namespace
 
@@ -68,12 +70,12 @@ void ivf_range_flat(const float* x, int64_t n, int ldx, const int32_t* assign, i
                     const uint8_t* selm, uint32_t* counts, const uint64_t* offsets, float* outD,
                     int64_t* outI, hipStream_t s) {
     if (n <= 0 || np <= 0) return;
-    const dim3 grid((unsigned)(n * np)), block(64);
+    const dim3 grid((unsigned)std::min<int64_t>(n * np, 65536)), block(64);
     const bool fill = offsets != nullptr;
 #define RANGE_LAUNCH(L2, F)                                                                       \
     hipLaunchKernelGGL((k_ivf_range<L2, F>), grid, block, 0, s, x, ldx, assign, np, codes, ldc,  \
                        ids, list_off, list_len, nlist, d, radius, selm, counts, offsets, outD,    \
-                       outI)
+                       outI, n * np)
     if (metric_l2) {
         if (fill) RANGE_LAUNCH(true, true); else RANGE_LAUNCH(true, false);
     } else {

@@ -189,25 +189,54 @@ struct ThreadQueue {
 }  // namespace faiss_amd
 
 namespace faiss_amd {
-// k-th smallest (1-based k) of the V*64 values held V per lane, by a 32-step
-// radix descent on the ordered bit patterns: every step is V compares whose
+// k-th smallest (1-based k) of the V*64 values held V per lane, by a radix
+// descent on the ordered bit patterns: every step is V compares whose
 // ballots are popcounted on the scalar unit — no cross-lane shuffles.  +inf
-// (or NaN-free padding) sorts last.  Returns +inf when fewer than k values
-// are finite... (precisely: the k-th smallest key, whatever it is).
-template <int V>
+// (or NaN-free padding) sorts last; fewer than k finite values give +inf.
+//
+// The descent starts below the bits every finite value shares (wave min /
+// max of the patterns: c2's keys span one or two binades, so ~8 of the 32
+// steps are skipped) and, with LOWB > 0, stops at bit LOWB and returns the
+// top of the 2^LOWB-pattern bucket holding the k-th value: an upper bound
+// >= the k-th smallest, above it by < 2^(LOWB - 23) relative.  The re-ranks'
+// thresholds (T, U) only need such a bound (a larger U admits more exact
+// candidates, never fewer), so they take LOWB = 12 (2^-11: ~10 steps left
+// instead of 32; r05 PMC: the 32-step descents were ~40 % of the re-ranks'
+// SALU).
+template <int V, int LOWB = 0>
 __device__ __forceinline__ float wave_kth_smallest(const float (&v)[V], int k) {
+    constexpr uint32_t ORD_INF = 0xff800000u;  // ordered_f32(+inf)
     uint32_t key[V];
+    uint32_t lo = 0xffffffffu, hi = 0u;
+    int nfin = 0;
 #pragma unroll
-    for (int i = 0; i < V; i++) key[i] = ordered_f32(v[i]);
-    uint32_t prefix = 0u;
-#pragma unroll 4
-    for (int bit = 31; bit >= 0; bit--) {
+    for (int i = 0; i < V; i++) {
+        key[i] = ordered_f32(v[i]);
+        const bool fin = key[i] < ORD_INF;
+        nfin += __popcll(__ballot(fin));
+        lo = min(lo, key[i]);
+        hi = max(hi, fin ? key[i] : 0u);
+    }
+    if (nfin < k) return WS_INF;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, m));
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, m));
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    const uint32_t diff = lo ^ hi;  // the k-th value lies in [lo, hi]
+    if (diff == 0u) return unordered_f32(lo);
+    const int hb = 31 - __builtin_clz(diff);
+    uint32_t prefix = hb == 31 ? 0u : lo & ~((2u << hb) - 1u);
+    for (int bit = hb; bit >= LOWB; bit--) {
         const uint32_t cand = prefix | (1u << bit);
         int cnt = 0;
 #pragma unroll
         for (int i = 0; i < V; i++) cnt += __popcll(__ballot(key[i] < cand));
         if (cnt < k) prefix = cand;
     }
+    if constexpr (LOWB > 0) prefix = min(prefix | ((1u << LOWB) - 1u), ORD_INF);
     return unordered_f32(prefix);
 }
 }  // namespace faiss_amd

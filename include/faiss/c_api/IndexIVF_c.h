@@ -1,0 +1,15 @@
+/*
+ * IndexIVF_c.h — drop-in for the reference C API header `c_api/IndexIVF_c.h`
+ * (Quaternijkon/hnsw-ivf = Faiss 1.10.0).  A C caller of the reference keeps
+ * its `#include "IndexIVF_c.h"` (or <faiss/c_api/IndexIVF_c.h>) and links
+ * libfaiss_amd.so: the declarations — IndexIVF, SearchParametersIVF, IndexIVFStats: nprobe / nlist /
+ * quantizer getters, search_preassigned, list sizes and ids, imbalance —
+ * are this library's, with the reference's names, signatures and return codes
+ * (include/faiss_amd_c.h, which cites each reference declaration).
+ */
+#ifndef FAISS_INDEX_IVF_C_H
+#define FAISS_INDEX_IVF_C_H
+
+#include "faiss_c.h"
+
+#endif /* FAISS_INDEX_IVF_C_H */

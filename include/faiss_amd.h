@@ -568,9 +568,20 @@ struct IndexIVF : Index {
                                 uint8_t* codes) const = 0;
     size_t get_list_size(size_t l) const { return invlists->list_size(l); }
     int device_code_stride() const;  // bytes per arena row
+    // diagnostic read-back of HBM arena rows [row0, row0 + n) into host
+    // `out` (tests): what = 0 the code rows (device_code_stride() bytes), 1
+    // the row -> list table (uint32, ~0 for padding rows), 2 the filter's
+    // stream image (IVF-Flat: always; IVF-PQ: when FAISS_AMD_PQ_FILTER=image
+    // built it).  *row_bytes = bytes per row, *rows = the arena's rows; out
+    // may be null to query them.  Throws when the buffer does not exist.
+    void debug_rows(int what, idx_t row0, idx_t n, void* out, size_t* row_bytes,
+                    idx_t* rows) const;
 
    protected:
     virtual void upload_extra() const {}
+    // the filter's stream image (debug_rows what = 2): pointer and row bytes,
+    // nullptr when this index has none
+    virtual const void* stream_image(size_t* row_bytes) const { return nullptr; }
     // search_preassigned with caller coarse distances (device copy cdis,
     // [n][np]): an index whose scan must not trust them rewrites them (IVF-PQ
     // table 0: the reference ignores them, its filter keys on them)
@@ -688,6 +699,7 @@ struct IndexIVFFlat : IndexIVF {
    protected:
     void upload_extra() const override;
     void exact_args(void* args) const override;
+    const void* stream_image(size_t* row_bytes) const override;
     // one pass of the range scan (counts when offs == nullptr, else fill);
     // cdis = coarse distances [n][np] on the device (PQ table 1 dis0)
     virtual void range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,
@@ -731,6 +743,7 @@ struct IndexIVFPQ : IndexIVF {
                         float* cdis, hipStream_t s) const override;
     void upload_extra() const override;
     void exact_args(void* args) const override;
+    const void* stream_image(size_t* row_bytes) const override;
     // one pass of the range scan (counts when offs == nullptr, else fill);
     // cdis = coarse distances [n][np] on the device (PQ table 1 dis0)
     virtual void range_launch(const float* x, idx_t n, int ldx, const int32_t* assign,

@@ -52,6 +52,7 @@ typedef enum FaissErrorCode {
 typedef struct FaissIndex_H FaissIndex;
 typedef struct FaissIndex_H FaissIndexFlat;
 typedef struct FaissIndex_H FaissIndexFlatL2;
+typedef struct FaissIndex_H FaissIndexFlatIP;
 typedef struct FaissIndex_H FaissIndexIVF;
 typedef struct FaissIndex_H FaissIndexIVFFlat;
 typedef struct FaissIndex_H FaissIndexIVFPQ;
@@ -104,6 +105,12 @@ int faiss_Index_search_with_params(
         idx_t* labels);
 /* Index_c.h:172 */
 int faiss_Index_reset(FaissIndex* index);
+/* Index_c.h:121-126: labels [n][k] of the k nearest (the search without the
+ * distances) */
+int faiss_Index_assign(FaissIndex* index, idx_t n, const float* x, idx_t* labels, idx_t k);
+/* Index_c.h:196-205 (IndexFlat / IndexIVFFlat / IndexHNSWFlat storage) */
+int faiss_Index_reconstruct(const FaissIndex* index, idx_t key, float* recons);
+int faiss_Index_reconstruct_n(const FaissIndex* index, idx_t i0, idx_t ni, float* recons);
 
 /* ---------------- SearchParametersIVF (c_api/IndexIVF_c.h:22-35) -------- */
 int faiss_SearchParametersIVF_new(FaissSearchParametersIVF** p_sp);
@@ -113,6 +120,9 @@ int faiss_SearchParametersIVF_new_with(
         size_t nprobe,
         size_t max_codes);
 void faiss_SearchParametersIVF_free(FaissSearchParametersIVF* obj);
+/* IndexIVF_c.h:27 (FAISS_DECLARE_SEARCH_PARAMETERS_DOWNCAST): every search
+ * parameter object here carries the IVF fields, so the cast always succeeds */
+FaissSearchParametersIVF* faiss_SearchParametersIVF_cast(FaissSearchParameters* sp);
 
 /* ---------------- IDSelector (c_api/impl/AuxIndexStructures_c.h:50-110,
  * c_api/Index_c.h:44-46).  Membership as faiss/impl/IDSelector.cpp; the IVF
@@ -131,6 +141,11 @@ int faiss_SearchParameters_new(FaissSearchParameters** p_sp, FaissIDSelector* se
 void faiss_SearchParameters_free(FaissSearchParameters* obj);
 int faiss_IDSelector_is_member(const FaissIDSelector* sel, idx_t id);
 void faiss_IDSelector_free(FaissIDSelector* sel);
+/* AuxIndexStructures_c.h:62-78 (FAISS_DECLARE_DESTRUCTOR / GETTER) */
+void faiss_IDSelectorRange_free(FaissIDSelectorRange* sel);
+idx_t faiss_IDSelectorRange_imin(const FaissIDSelectorRange* sel);
+idx_t faiss_IDSelectorRange_imax(const FaissIDSelectorRange* sel);
+void faiss_IDSelectorBitmap_free(FaissIDSelectorBitmap* sel);
 int faiss_IDSelectorRange_new(FaissIDSelectorRange** p_sel, idx_t imin, idx_t imax);
 int faiss_IDSelectorBatch_new(FaissIDSelectorBatch** p_sel, size_t n, const idx_t* indices);
 /* extension: faiss::IDSelectorArray (faiss/impl/IDSelector.h:54-66), ids borrowed */
@@ -171,6 +186,17 @@ int faiss_IndexFlatL2_new_with(FaissIndexFlatL2** p_index, idx_t d);
 int faiss_IndexFlatIP_new_with(FaissIndexFlat** p_index, idx_t d);
 /* IndexFlat_c.h:40: pointer to the host mirror of xb (d*ntotal floats) */
 void faiss_IndexFlat_xb(FaissIndexFlat* index, float** p_xb, size_t* p_size);
+/* IndexFlat_c.h:24-26, 71-93: default constructors (d = 0), destructors and
+ * FAISS_DECLARE_INDEX_DOWNCAST (NULL when the index is not of that type) */
+int faiss_IndexFlat_new(FaissIndexFlat** p_index);
+int faiss_IndexFlatIP_new(FaissIndexFlatIP** p_index);
+int faiss_IndexFlatL2_new(FaissIndexFlatL2** p_index);
+void faiss_IndexFlat_free(FaissIndexFlat* obj);
+void faiss_IndexFlatIP_free(FaissIndexFlatIP* obj);
+void faiss_IndexFlatL2_free(FaissIndexFlatL2* obj);
+FaissIndexFlat* faiss_IndexFlat_cast(FaissIndex* index);
+FaissIndexFlatIP* faiss_IndexFlatIP_cast(FaissIndex* index);
+FaissIndexFlatL2* faiss_IndexFlatL2_cast(FaissIndex* index);
 
 /* ---------------- IndexIVF (c_api/IndexIVF_c.h) ---------------- */
 size_t faiss_IndexIVF_nlist(const FaissIndexIVF*);              /* :59 */
@@ -192,6 +218,12 @@ int faiss_IndexIVF_search_preassigned(
         int store_pairs);
 /* IndexIVF_c.h:123 */
 size_t faiss_IndexIVF_get_list_size(const FaissIndexIVF* index, size_t list_no);
+/* IndexIVF_c.h:46-52, 141: destructor, downcast, list-size imbalance
+ * (faiss/invlists/InvertedLists.cpp imbalance_factor: nlist * sum(size^2) /
+ * sum(size)^2) */
+void faiss_IndexIVF_free(FaissIndexIVF* obj);
+FaissIndexIVF* faiss_IndexIVF_cast(FaissIndex* index);
+double faiss_IndexIVF_imbalance_factor(const FaissIndexIVF* index);
 /* IndexIVF_c.h:151-155 */
 void faiss_IndexIVF_invlists_get_ids(
         const FaissIndexIVF* index,
@@ -270,6 +302,19 @@ int faiss_IndexIVFFlat_new_with_metric(
         size_t d,
         size_t nlist,
         FaissMetricType metric);
+
+/* IndexIVFFlat_c.h:25-45: constructor without arguments (an empty index
+ * whose quantizer is set by reading), destructor, downcast and the IndexIVF
+ * getters under the IndexIVFFlat name */
+int faiss_IndexIVFFlat_new(FaissIndexIVFFlat** p_index);
+void faiss_IndexIVFFlat_free(FaissIndexIVFFlat* obj);
+FaissIndexIVFFlat* faiss_IndexIVFFlat_cast(FaissIndex* index);
+size_t faiss_IndexIVFFlat_nlist(const FaissIndexIVFFlat*);
+size_t faiss_IndexIVFFlat_nprobe(const FaissIndexIVFFlat*);
+void faiss_IndexIVFFlat_set_nprobe(FaissIndexIVFFlat*, size_t);
+FaissIndex* faiss_IndexIVFFlat_quantizer(const FaissIndexIVFFlat*);
+int faiss_IndexIVFFlat_own_fields(const FaissIndexIVFFlat*);
+void faiss_IndexIVFFlat_set_own_fields(FaissIndexIVFFlat*, int);
 
 /* ---------------- IndexIVFPQ (no reference C binding; mirrors the C++
  * constructor faiss/IndexIVFPQ.h:IndexIVFPQ(quantizer,d,nlist,M,nbits)) --- */
@@ -438,6 +483,11 @@ int faiss_read_index_fname(const char* fname, int io_flags, FaissIndex** p_out);
 int faiss_amd_write_index_ondisk(const FaissIndex* idx, const char* fname,
                                  const char* lists_fname);
 
+/* c_api/clone_index_c.h:23 (faiss/clone_index.cpp): a deep copy of the
+ * index, made through the serialized form (write_index + read_index), on the
+ * calling thread's device */
+int faiss_clone_index(const FaissIndex* idx, FaissIndex** p_out);
+
 /* ---------------- factory / tuning ---------------- */
 /* c_api/index_factory_c.h:24-28; supports "Flat", "IVF<n>,Flat",
  * "IVF<n>,PQ<M>[x<nbits>][np]", "IVF<n>_HNSW<M>,Flat|PQ..", "HNSW<M>[,Flat]" */
@@ -543,6 +593,13 @@ int faiss_amd_last_kernel_times(
         double* units);   /* n_kernels: work units (bytes or flops) */
 
 int faiss_amd_reset_kernel_times(FaissIndex* index);
+/* diagnostic (tests): copy HBM arena rows [row0, row0 + n) of an IVF index to
+ * host `out`: what = 0 the code rows, 1 the row -> list table (uint32, ~0 =
+ * padding row), 2 the MFMA filter's stream image (IVF-Flat; IVF-PQ when built
+ * with FAISS_AMD_PQ_FILTER=image).  *row_bytes = bytes per row, *rows = arena
+ * rows (either may be NULL); out = NULL only queries them. */
+int faiss_amd_IndexIVF_debug_rows(const FaissIndex* index, int what, int64_t row0, int64_t n,
+                                  void* out, size_t* row_bytes, int64_t* rows);
 /* faiss::float_rand (faiss/utils/random.cpp:95-112), bit-exact restatement:
  * the synthetic inputs of the benchmark are regenerated on the GPU box */
 int faiss_amd_float_rand(float* x, size_t n, int64_t seed);

@@ -138,6 +138,40 @@ def test_c4_harness_grid_corners(amd, orc, gpu, c4_index, nprobe, ef):
         amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", 64)
 
 
+@pytest.mark.parametrize("nprobe,ef", [(64, 200), (128, 384), (256, 768), (1024, 1024),
+                                       (2048, 4096)])
+def test_c4_wide_hnsw_grid(amd, orc, gpu, c4_index, nprobe, ef):
+    """128 < max(efSearch, nprobe) <= 4096: the wide kernel (k_hnsw_wide, the
+    candidate set sorted in the LDS) + sequential re-runs of the queries it
+    flags, bit-exact against the oracle, through search() and the device
+    entry point (IndexIVF::scan_hnsw_split overlaps the re-runs with the
+    scan); the wide stage must be the one that ran."""
+    from conftest import device_search
+    d, nq = 128, 500
+    idx = c4_index
+    idx.nprobe = nprobe
+    amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", ef)
+    try:
+        xq = amd.float_rand(nq * d, 4242).reshape(nq, d)
+        q = idx.quantizer
+        amd.set_kernel_timing(True)
+        try:
+            q.reset_kernel_times()
+            D, I = idx.search(xq, 10)
+            names = {nm for nm, _, _ in q.kernel_times()}
+        finally:
+            amd.set_kernel_timing(False)
+        assert "hnsw_wide" in names, names
+        ref = orc.IVFOracle.from_index(idx)
+        Dr, Ir, _, _ = ref.search(xq, 10, nprobe, efSearch=ef, nslices=1)
+        check(D, I, Dr, Ir, f"c4 wide nprobe {nprobe} efSearch {ef}")
+        D2, I2 = device_search(idx, xq, 10)
+        check(D2, I2, Dr, Ir, f"c4 wide device nprobe {nprobe} efSearch {ef}")
+    finally:
+        idx.nprobe = 64
+        amd.ParameterSpace().set_index_parameter(idx, "quantizer_efSearch", 64)
+
+
 @pytest.mark.parametrize("nprobe", [2049, 4096])
 def test_flat_coarse_nprobe_beyond_2048(amd, orc, gpu, nprobe):
     """A flat quantizer's top-nprobe beyond 2048 (the global-scratch select)."""

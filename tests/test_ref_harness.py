@@ -23,7 +23,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference"
 HDIR = os.path.join(ROOT, "oracle", "_ref", "harness")
-HARNESSES = ["benchmark_hnsw_ivf", "benchmark_ivf", "benchmark_ivf_ondisk", "benchmark_hnsw"]
+HARNESSES = ["benchmark_hnsw_ivf", "benchmark_ivf", "benchmark_ivf_ondisk", "benchmark_hnsw",
+             "example_c", "example_c_refhdr"]
 HEADERS = sorted(os.path.relpath(p, os.path.join(ROOT, "include"))
                  for p in glob.glob(os.path.join(ROOT, "include", "faiss", "**", "*.h"),
                                     recursive=True))
@@ -36,6 +37,24 @@ def test_faiss_header_compiles_alone(hdr, tmp_path):
     subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror",
                     "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
                     f"-I{os.path.join(ROOT, 'include')}", str(src)], check=True)
+
+
+C_HEADERS = sorted(os.path.relpath(p, os.path.join(ROOT, "include", "faiss", "c_api"))
+                   for p in glob.glob(os.path.join(ROOT, "include", "faiss", "c_api", "**", "*.h"),
+                                      recursive=True))
+
+
+@pytest.mark.parametrize("hdr", C_HEADERS)
+def test_c_api_header_compiles_alone(hdr, tmp_path):
+    """Each reference C header name (c_api/*.h) as a plain C99 translation
+    unit, both as "X_c.h" from the c_api directory and as <faiss/c_api/X_c.h>."""
+    for inc, flag in ((f'"{hdr}"', ["-I-", f"-I{os.path.join(ROOT, 'include', 'faiss', 'c_api')}"]),
+                      (f"<faiss/c_api/{hdr}>", [f"-I{os.path.join(ROOT, 'include')}"])):
+        src = tmp_path / "tu.c"
+        src.write_text(f"#include {inc}\nint main(void) {{ return 0; }}\n")
+        r = subprocess.run(["gcc", "-std=c99", "-fsyntax-only", "-Wall", "-Wextra", "-pedantic",
+                            *flag, str(src)], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
 
 
 def test_faiss_names_are_the_library_types(tmp_path):
@@ -206,3 +225,59 @@ search
         Dr, Ir, _, _ = ref.search(s["xq"], s["k"], nprobe, nslices=1)
         assert np.array_equal(I, Ir) and np.array_equal(D, Dr), nprobe
         assert abs(float(r["recall"]) - harness_recall(I, s["gt"], s["k"])) < 6e-5, r
+
+
+# ------------------------------------------------ the reference's C example
+def parse_example_blocks(out):
+    """The I= tables example_c.c prints (5 queries x 5 results each), keyed by
+    the line announcing the search."""
+    import re
+    blocks, title, rows = {}, None, []
+    for ln in out.splitlines():
+        if ln.startswith("Searching"):
+            title = ln.strip()
+            rows = []
+            blocks.setdefault(title, [])
+        elif ln.startswith("I="):
+            rows = []
+            blocks.setdefault(title, []).append(rows)
+        else:
+            pairs = re.findall(r"(-?\d+) \(d=\s*([-\d.]+)\)", ln)
+            if pairs and title is not None:
+                rows.append([(int(a), float(b)) for a, b in pairs])
+    return blocks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exe", ["example_c", "example_c_refhdr"])
+def test_reference_c_example_runs(amd, gpu, tmp_path, exe):
+    """c_api/example_c.c compiled in place and unchanged — against
+    include/faiss/c_api (example_c) and against the reference's own C headers
+    (example_c_refhdr, the ABI) — runs on the library: IndexFlat through
+    faiss_index_factory, add, search, search_with_params with IDSelectorRange /
+    Or / And, write_index_fname.  Its data is rand()-seeded by the clock, so
+    the checks are the properties its searches must hold: xb[i]'s nearest
+    neighbour is i at distance 0, and every label lies in its selector's set."""
+    path = os.path.join(HDIR, exe)
+    assert os.access(path, os.X_OK), f"{path} missing: built by __graft_entry__.build()"
+    r = subprocess.run([path], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "ntotal = 100000" in r.stdout and r.stdout.rstrip().endswith("Done.")
+    b = parse_example_blocks(r.stdout)
+    first, xq = b["Searching..."]
+    assert len(first) == 5 and len(xq) == 5
+    for i, row in enumerate(first):
+        assert row[0] == (i, 0.0), row
+    sets = {"Searching w/ IDSelectorRange [50,100]": lambda i: 50 <= i < 100,
+            "Searching w/ IDSelectorRange [20,40] OR [45,60]": lambda i: 20 <= i < 40 or 45 <= i < 60,
+            "Searching w/ IDSelectorRange [20,40] AND [15,35] = [20,35]": lambda i: 20 <= i < 35}
+    for title, member in sets.items():
+        (rows,) = b[title]
+        assert len(rows) == 5
+        for row in rows:
+            labels = [i for i, _ in row]
+            dists = [dv for _, dv in row]
+            assert all(member(i) for i in labels), (title, row)
+            assert dists == sorted(dists) and len(set(labels)) == 5, (title, row)
+    idx = amd.read_index(str(tmp_path / "example.index"))
+    assert idx.ntotal == 100000 and idx.d == 128
