@@ -11,6 +11,11 @@
 #include "kernels.h"
 
 namespace faiss_amd {
+namespace kern {
+// idselector.hip: D[r][c] = v for every column c whose mask byte is 0
+void mask_columns(float* D, int64_t nx, int64_t ny, int64_t ldD, const uint8_t* mask, float v,
+                  hipStream_t s);
+}  // namespace kern
 
 IndexIVFStats indexIVF_stats;
 HNSWStats hnsw_stats;
@@ -428,10 +433,85 @@ bool IndexFlat::knn_impl(idx_t n, const float* x, int ldx, int k, float* distanc
 void IndexFlat::search_device(idx_t n, const float* x, int ldx, idx_t k, float* distances,
                               idx_t* labels, const SearchParameters* params,
                               hipStream_t s) const {
-    FAISS_THROW_IF_NOT_MSG(!params || !params->sel,
-                           "IDSelector is supported by the IVF indexes only on this path");
     DeviceGuard g(device);
+    if (params && params->sel) {
+        search_selected(n, x, ldx, k, distances, labels, params->sel, s);
+        return;
+    }
     knn_device<idx_t>(n, x, ldx, (int)k, distances, labels, s);
+}
+
+void IndexFlat::search_selected(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                                idx_t* labels, const IDSelector* sel, hipStream_t s) const {
+    FAISS_THROW_IF_NOT_FMT(k >= 1, "k = %lld must be >= 1", (long long)k);
+    if (n <= 0) return;
+    sync_device();
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    order_.enter(s);
+    const int l = ld();
+    const int metric_l2 = metric_type == METRIC_L2;
+    int64_t y0 = 0, ny = ntotal;
+    const uint8_t* mask = nullptr;
+    // faiss/utils/distances.cpp:807-823: below distance_compute_blas_threshold
+    // (20) queries the direct form; with a selector other than a range the
+    // direct form always (res.sel)
+    bool direct = n < 20;
+    if (auto r = dynamic_cast<const IDSelectorRange*>(sel)) {
+        // knn_L2sqr / knn_inner_product (:840-935): the rows [imin, imax),
+        // labels shifted back by imin, no selector left
+        y0 = std::max<idx_t>(r->imin, 0);
+        ny = std::max<idx_t>(std::min<idx_t>(r->imax, ntotal) - y0, 0);
+        if (ny == 0) y0 = 0;
+    } else if (ntotal > 0) {
+        // (IDSelectorArray takes this membership form too: the reference's
+        // knn_*_by_idx visits the array in its own order, which differs
+        // only for an array that lists an id twice or under distance ties)
+        direct = true;
+        if (selids_n_ != ntotal) {
+            std::vector<idx_t> iota((size_t)ntotal);
+            for (idx_t i = 0; i < ntotal; i++) iota[(size_t)i] = i;
+            s_selids_.reserve(sizeof(idx_t) * ntotal);
+            HIP_CHECK(hipMemcpyAsync(s_selids_.ptr, iota.data(), sizeof(idx_t) * ntotal,
+                                     hipMemcpyHostToDevice, s));
+            HIP_CHECK(hipStreamSynchronize(s));  // (iota is a host temporary)
+            selids_n_ = ntotal;
+        }
+        s_selmask_.reserve((size_t)ntotal);
+        sel->mark_device(s_selids_.as<idx_t>(), ntotal, s_selmask_.as<uint8_t>(), s);
+        mask = s_selmask_.as<uint8_t>();
+    }
+    if (metric_l2 && !direct && ny > 0) {
+        s_xn_.reserve(sizeof(float) * n);
+        kern::row_norms(x, n, d, ldx, s_xn_.as<float>(), s);
+    }
+    const idx_t qc = std::max<idx_t>(1, std::min<idx_t>(n, ((idx_t)1 << 28) / std::max<idx_t>(ny, 1)));
+    s_tile_.reserve(sizeof(float) * qc * std::max<idx_t>(ny, 1));
+    float* tile = s_tile_.as<float>();
+    for (idx_t q0 = 0; q0 < n; q0 += qc) {
+        const idx_t nq = std::min(qc, n - q0);
+        if (ny > 0 && direct)
+            kern::direct_distances(x + q0 * ldx, nq, ldx, d_xb_.as<float>() + y0 * l, ny, l, d,
+                                   metric_l2, tile, ny, s);
+        else if (ny > 0)
+            kern::pairwise_distances(x + q0 * ldx, nq, ldx, s_xn_.as<float>() + q0,
+                                     d_xb_.as<float>() + y0 * l, ny, l,
+                                     d_norms_.as<float>() + y0, l, metric_l2, tile, ny, s);
+        // non-members never reach the heap: a key the select does not admit
+        if (mask && ny > 0)
+            kern::mask_columns(tile, nq, ny, ny, mask, metric_l2 ? HUGE_VALF : -HUGE_VALF, s);
+        float* Dq = distances + q0 * k;
+        idx_t* Iq = labels + q0 * k;
+        if (k <= kern::kMaxK) {
+            kern::select_rows(tile, nq, ny, ny, (int)k, metric_l2, 0, Dq, nullptr, Iq, k, s);
+            if (!metric_l2 && ny > 0)
+                kern::select_fix_ip(tile, nq, ny, ny, (int)k, Dq, nullptr, Iq, k, s);
+        } else {
+            kern::select_rows_exact<idx_t>(tile, nq, ny, ny, (int)k, metric_l2, 0, Dq, Iq, k, s,
+                                           &s_sel_);
+        }
+    }
+    if (y0 > 0) kern::translate_labels(labels, n * k, y0, s);
+    order_.leave(s);
 }
 
 void IndexFlat::assign_device(idx_t n, const float* x, int ldx, int k, float* distances,

@@ -64,6 +64,22 @@ __global__ void k_sel_combine(const int64_t* __restrict__ ids, int64_t n, uint8_
     a[r] = ids[r] >= 0 ? v : 0;
 }
 
+// IndexFlat::search_selected: non-member columns of a distance tile get a
+// value the select does not admit
+__global__ void k_mask_cols(float* __restrict__ D, int64_t nx, int64_t ny, int64_t ldD,
+                            const uint8_t* __restrict__ mask, float v) {
+    GRID_STRIDE(i, nx * ny) {
+        const int64_t r = i / ny, c = i - r * ny;
+        if (!mask[c]) D[r * ldD + c] = v;
+    }
+}
+void mask_columns(float* D, int64_t nx, int64_t ny, int64_t ldD, const uint8_t* mask, float v,
+                  hipStream_t s) {
+    if (nx <= 0 || ny <= 0) return;
+    k_mask_cols<<<stride_grid(nx * ny, 256), dim3(256), 0, s>>>(D, nx, ny, ldD, mask, v);
+    HIP_LAUNCH_CHECK();
+}
+
 }  // namespace kern
 
 namespace {

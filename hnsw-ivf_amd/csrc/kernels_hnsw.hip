@@ -1674,7 +1674,6 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
     if (use_q8) q8_query_prep(qs, g.d, q8x, q8d, lane);
     __syncthreads();
     uint32_t tie = 0u;     // reason bits, as k_hnsw_search
-    float rdisc = WS_INF;  // smallest distance the set ever turned away or evicted
     uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0, st_q8 = 0, st_x32 = 0;
     int S = 0;             // entries of the set
     if (g.entry_point >= 0) {
@@ -1819,17 +1818,14 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
                     fdis = l2_row(qs, g.storage + (int64_t)sv * g.ld, g.d);
             }
             const long long ki = ((long long)(uint32_t)sv << 1) | 1ll;
-            bool enter = lane < ns;
-            float rej = WS_INF;
-            if (full) {
-                if (__ballot(lane < ns && fdis == maxd) != 0ull) tie |= 2u;  // push at the max
-                enter = enter && key_less(fdis, ki, maxd, (long long)(uint32_t)emax);
-                if (lane < ns && !enter) rej = fdis;
-            }
+            // MinimaxHeap::push into the full set drops v >= max by distance
+            // alone (HNSW.cpp:1096-1101): the same rule, so an arrival at the
+            // max distance is no divergence
+            const bool enter = lane < ns && (!full || fdis < maxd);
             float cd = enter ? fdis : WS_INF;
             long long ci = enter ? ki : WS_NOID;
             const int m = wave_compact(cd, ci, enter, lane);
-            float disc = rej;
+            float disc = WS_INF;  // smallest distance the merge pushed past ef
             if (m > 0) {
                 wave_sort_m(cd, ci, lane, m);
                 const uint64_t akey =
@@ -1883,19 +1879,19 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
 #pragma unroll
             for (int mm = 32; mm > 0; mm >>= 1) disc = fminf(disc, __shfl_xor(disc, mm));
             __syncthreads();
-            // the kept-ef boundary: a discarded key of the ef-th kept distance
+            // the kept-ef boundary: a key the merge pushed out at the ef-th
+            // kept distance (the reference's sequential pushes may keep the
+            // other one of the two)
             if (S == ef && disc < WS_INF && wdis(cs[ef - 1]) == disc) tie |= 4u;
-            rdisc = fminf(rdisc, disc);
         }
     }
-    // the k-th boundary: the reference's result heap (strict admission) and
-    // the set's first k (by id among equals) differ only when the k-th
-    // distance is shared by a later entry or a key the set turned away
-    if (S >= k) {
+    // the k-th boundary (k < ef; at k == ef the result heap and the set are
+    // the same process): the reference's result heap admits strictly, the
+    // set's first k order equal distances by id — they differ only when the
+    // k-th distance is shared by the next entry
+    if (k < ef && S > k) {
         const float kd = wdis(cs[k - 1]);
-        float nd = S > k ? wdis(cs[k]) : WS_INF;
-        nd = fminf(nd, rdisc);
-        if (kd < FLT_MAX && nd == kd) tie |= 8u;
+        if (kd < FLT_MAX && wdis(cs[k]) == kd) tie |= 8u;
     }
     if (tie_flags && lane == 0) tie_flags[q] = tie;
     if (tie && tie_flags) return;  // the sequential kernel redoes this query

@@ -308,6 +308,14 @@ struct IndexFlat : Index {
     mutable bool dirty_ = true;
     mutable std::recursive_mutex mu_;
     mutable DeviceBuffer s_xn_, s_tile_, s_cand_d_, s_cand_i_, s_qimg_, s_sel_;
+    // search with an IDSelector (faiss/IndexFlat.cpp:38-57 ->
+    // faiss/utils/distances.cpp:840-935): IDSelectorRange narrows the rows
+    // and keeps the batch-size form choice; any other selector takes the
+    // direct per-row form over its members (exhaustive_*_seq)
+    void search_selected(idx_t n, const float* x, int ldx, idx_t k, float* distances,
+                         idx_t* labels, const IDSelector* sel, hipStream_t stream) const;
+    mutable DeviceBuffer s_selids_, s_selmask_;  // 0 .. ntotal - 1 (int64) and membership
+    mutable idx_t selids_n_ = 0;
 };
 struct IndexFlatL2 : IndexFlat {
     explicit IndexFlatL2(idx_t d = 0) : IndexFlat(d, METRIC_L2) {}

@@ -14,4 +14,9 @@ rc=$?; echo "suite rc=$rc"; grep -E "passed|failed|error" gpurun_out/r6_suite.lo
 fi
 timeout -k 10 300 python -u bench.py --steps 100 --warmup 5 --no-cpu-baseline > gpurun_out/r6_c2.json 2> gpurun_out/r6_c2.err
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/r6_c2.json | head -c 3000
+[ "$rc" -eq 0 ] || exit $rc
+if [ -n "$C4GRID" ]; then
+timeout -k 10 600 python -u bench.py --config c4 --nprobe 256 --efsearch 768 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/r6_c4_np256_ef768.json 2> gpurun_out/r6_c4_np256_ef768.err
+rc=$?; echo "bench c4 grid rc=$rc"; head -c 2500 gpurun_out/r6_c4_np256_ef768.json
+fi
 exit $rc

@@ -100,10 +100,35 @@ def test_pq_selector_equals_subset_index(amd, orc, gpu, tmp_path):
         assert_same_results(D, I, Ds, Is)
 
 
-def test_selector_rejected_where_unsupported(amd, orc, gpu):
+@pytest.mark.parametrize("metric", [1, 0])
+@pytest.mark.parametrize("nq,k", [(7, 5), (64, 10), (40, 100)])
+def test_flat_index_with_selectors(amd, orc, gpu, metric, nq, k):
+    """IndexFlat search with an IDSelector (faiss/IndexFlat.cpp:38-57 ->
+    faiss/utils/distances.cpp:840-935, c_api/example_c.c's searches):
+    IDSelectorRange searches the rows [imin, imax) in the batch size's form
+    (direct below 20 queries, BLAS form above) and shifts the labels; any
+    other selector takes the direct form over its members in id order."""
+    rng = np.random.default_rng(7 + nq + k + metric)
+    xb = rand(orc, NB, D_, 85)
+    xq = rand(orc, nq, D_, 86)
+    flat = amd.IndexFlatL2(D_) if metric == 1 else amd.IndexFlatIP(D_)
+    flat.add(xb)
+    for name, (sel, member) in selectors(amd, rng).items():
+        D, I = flat.search(xq, k, params=amd.SearchParametersIVF(sel=sel))
+        ids = np.nonzero(member)[0]
+        if name == "range":
+            Dr, Ir = orc.knn(xq, xb[2000:7000], k, metric, blas_form=nq >= 20)
+            Ir = np.where(Ir >= 0, Ir + 2000, -1)
+        else:
+            Dr, Ir = orc.knn(xq, xb[ids], k, metric, blas_form=False)
+            Ir = np.where(Ir >= 0, ids[np.maximum(Ir, 0)], -1)
+        assert_same_results(D, I, Dr, Ir)
+
+
+def test_flat_selector_range_outside(amd, orc, gpu):
+    """A range past the stored rows selects nothing: (FLT_MAX, -1) rows."""
     xb = rand(orc, 500, 16, 85)
     flat = amd.IndexFlatL2(16)
     flat.add(xb)
-    with pytest.raises(amd.FaissError, match="IDSelector"):
-        flat.search(xb[:5], 3, params=amd.SearchParametersIVF(nprobe=1,
-                                                             sel=amd.IDSelectorRange(0, 10)))
+    D, I = flat.search(xb[:5], 3, params=amd.SearchParametersIVF(sel=amd.IDSelectorRange(600, 900)))
+    assert (I == -1).all() and (D == np.finfo(np.float32).max).all()

@@ -157,7 +157,7 @@ def wide_search(nbrs, dist, entry, k, ef, efSearch):
     """k_hnsw_wide's level 0: returns (results, tie bits, ndis, nhops, n2)."""
     cs = [(dist[entry], entry, 1)]  # sorted (dis, id, alive)
     vis = {entry}
-    nalive, fa, tie, rdisc = 1, 0, 0, float("inf")
+    nalive, fa, tie = 1, 0, 0
     ndis = nhops = 0
     n2 = 0
     while True:
@@ -200,12 +200,9 @@ def wide_search(nbrs, dist, entry, k, ef, efSearch):
         arr = [(dist[v], v) for v in fresh]
         disc = float("inf")
         if full:
-            if any(dv == emax[0] for dv, _ in arr):
-                tie |= 2
-            enter = [(dv, v) for dv, v in arr if (dv, v) < (emax[0], emax[1])]
-            for dv, v in arr:
-                if not (dv, v) < (emax[0], emax[1]):
-                    disc = min(disc, dv)
+            # MinimaxHeap::push drops v >= max (by distance alone), as the
+            # reference does: no divergence, so no flag and no disc entry
+            enter = [(dv, v) for dv, v in arr if dv < emax[0]]
         else:
             enter = arr
         enter.sort()
@@ -237,13 +234,11 @@ def wide_search(nbrs, dist, entry, k, ef, efSearch):
             assert nalive == 0 or fa == min(i for i, e in enumerate(cs) if e[2])
         if len(cs) == ef and disc < float("inf") and cs[ef - 1][0] == disc:
             tie |= 4
-        rdisc = min(rdisc, disc)
     S = len(cs)
-    if S >= k:
+    # (k == ef: the result heap and the set are the same process)
+    if k < ef and S > k:
         kd = cs[k - 1][0]
-        nd = cs[k][0] if S > k else float("inf")
-        nd = min(nd, rdisc)
-        if kd < FMAX and nd == kd:
+        if kd < FMAX and cs[k][0] == kd:
             tie |= 8
     out = [(e[0], e[1]) for e in cs[:k] if e[0] < FMAX]
     out += [(FMAX, -1)] * (k - len(out))
