@@ -1637,11 +1637,22 @@ __global__ __launch_bounds__(64, HNSW_WPE) void k_hnsw_exact_reg(HNSWDevice g, c
 // sequential kernel, as k_hnsw_search does.  Fresh neighbours whose certified
 // int8 lower bound exceeds the full set's largest distance (q8_filter) cannot
 // enter: their fp32 rows are not read.
+constexpr uint64_t kWAlive = 1ull << 31;
 __device__ __forceinline__ uint64_t wkey(float d, int32_t id) {
-    return ((uint64_t)__float_as_uint(d) << 32) | ((uint64_t)(uint32_t)id << 1) | 1ull;
+    return ((uint64_t)__float_as_uint(d) << 32) | kWAlive | (uint64_t)(uint32_t)id;
 }
 __device__ __forceinline__ float wdis(uint64_t e) { return __uint_as_float((uint32_t)(e >> 32)); }
-__device__ __forceinline__ int32_t wid(uint64_t e) { return (int32_t)((uint32_t)e >> 1); }
+__device__ __forceinline__ int32_t wid(uint64_t e) { return (int32_t)((uint32_t)e & 0x7fffffffu); }
+// entries of cs[0, S) below an alive key (dead entries of its distance
+// included, whatever their ids): a branchless binary search
+__device__ __forceinline__ int wide_lower_bound(const uint64_t* cs, int S, uint64_t key) {
+    int lb = 0;
+    int st = 1;
+    while (2 * st <= S) st *= 2;
+    for (; st > 0; st >>= 1)
+        if (lb + st <= S && cs[lb + st - 1] < key) lb += st;
+    return lb;
+}
 
 // the LDS head of the wide kernel: the query (>= 128 floats), its int8 image
 // and scalars (exact_reg_head), then the candidate set and the visited bitmap
@@ -1649,7 +1660,7 @@ __host__ __device__ inline size_t wide_lds_bytes(const HNSWDevice& g, int ef) {
     return (size_t)exact_reg_head(g) + 8 * (size_t)ef;
 }
 
-template <bool LDS_VISITED>
+template <bool LDS_VISITED, bool TRACE = false>
 __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __restrict__ x,
                                                   int ldx, int64_t n, int k, int efSearch, int ef,
                                                   float* __restrict__ D, int64_t* __restrict__ I,
@@ -1657,7 +1668,21 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
                                                   uint32_t* __restrict__ vis_global,
                                                   int64_t vwords,
                                                   unsigned long long* __restrict__ stats,
-                                                  uint32_t* __restrict__ tie_flags) {
+                                                  uint32_t* __restrict__ tie_flags,
+                                                  unsigned long long* __restrict__ tb = nullptr) {
+    // TRACE (FAISS_AMD_HNSW_TRACE, profiling): per query the cycles of the
+    // level-0 phases summed over its hops — [0] pop_min + count_below, [1]
+    // neighbour ids, [2] visited, [3] int8 bound, [4] fp32 rows, [5] compact +
+    // sort + lower_bound, [6] merge, [7] whole query; [8] flagged, [9] hops,
+    // [10] fresh, [11] arrivals that enter, [12] fp32 rows, [13] merge steps,
+    // [14] hops pushed one at a time, [15] set size at the end
+    HopTrace tr;
+    if (TRACE) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) tr.t[j] = 0;
+        tr.tc = clock64();
+    }
+    const unsigned long long tq = TRACE ? tr.tc : 0ull;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int qpad = exact_reg_qpad(g);
     float* qs = sm;                                   // [qpad]
@@ -1673,7 +1698,8 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
     const bool use_q8 = g.q8 != nullptr && g.d <= 128;
     if (use_q8) q8_query_prep(qs, g.d, q8x, q8d, lane);
     __syncthreads();
-    uint32_t tie = 0u;     // reason bits, as k_hnsw_search
+    uint32_t tie = 0u;     // 1 pop-tie window, 4 (k == ef) eviction at a tied max, 8 k-th boundary
+    float dvmin = WS_INF;  // (k == ef) smallest distance of an eviction at a tied max
     uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0, st_q8 = 0, st_x32 = 0;
     int S = 0;             // entries of the set
     if (g.entry_point >= 0) {
@@ -1719,34 +1745,41 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
         }
         S = 1;
         int nalive = 1, fa = 0;  // alive entries (MinimaxHeap::nvalid), first alive
+        float win = WS_INF;      // the distance of an open pop-tie window
         __syncthreads();
         const int cnt = g.cum_nb[1] - g.cum_nb[0];
         const unsigned long long lt = (1ull << lane) - 1ull;
         for (;;) {
+            if (TRACE) tr.tick(7);
+            // the window closes once its distance's members are all popped
+            if (win < WS_INF && (nalive <= 0 || wdis(cs[fa]) > win)) win = WS_INF;
             if (nalive <= 0) {  // candidates.size() == 0
                 st_n2 = 1;
                 break;
             }
-            // ---- pop_min: the first alive entry.  An alive entry of equal
-            // distance right after it: the reference picks by heap slot
-            const uint64_t e0 = cs[fa];
+            // ---- pop_min: the first alive entry.  Another alive entry of its
+            // distance (right after it: dead entries of a distance sort
+            // first) — the reference pops the highest heap slot among them,
+            // so the members' expansion order is its layout's: a window opens
+            // in which an arrival at or below that distance flags the query
+            // (one LDS read: lane l holds entry fa - 1 + l)
+            const int ip = fa - 1 + lane;
+            const uint64_t ew = ip >= 0 && ip < S ? cs[ip] : ~0ull;
+            const uint64_t e0 = rdlane64(ew, 1);
             const float d0 = wdis(e0);
             const int32_t v0 = wid(e0);
-            const int i1 = fa + 1 + lane;
-            const uint64_t en = i1 < S ? cs[i1] : ~0ull;
-            const unsigned long long am = __ballot(i1 < S && (en & 1ull));
-            const unsigned long long eqm = __ballot(i1 < S && wdis(en) == d0);
-            if ((am & eqm) != 0ull || eqm == ~0ull) tie |= 1u;
+            if (fa + 1 < S && wdis(rdlane64(ew, 2)) == d0) win = d0;
+            const unsigned long long am = __ballot(lane >= 2 && ip < S && (ew & kWAlive)) >> 2;
             __syncthreads();
-            if (lane == 0) cs[fa] = e0 & ~1ull;
+            if (lane == 0) cs[fa] = e0 & ~kWAlive;
             nalive--;
             int nfa = S;
             if (am) {
                 nfa = fa + __ffsll((long long)am);
             } else if (nalive > 0) {
-                for (int b0 = fa + 65; b0 < S; b0 += 64) {
+                for (int b0 = fa + 63; b0 < S; b0 += 64) {
                     const int ii = b0 + lane;
-                    const unsigned long long m2 = __ballot(ii < S && (cs[ii] & 1ull));
+                    const unsigned long long m2 = __ballot(ii < S && (cs[ii] & kWAlive));
                     if (m2) {
                         nfa = b0 + __ffsll((long long)m2) - 1;
                         break;
@@ -1755,7 +1788,7 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
             }
             // ---- count_below(d0): every entry below d0, dead ones included
             int nb = fa;
-            if (fa > 0 && wdis(cs[fa - 1]) == d0) {
+            if (fa > 0 && wdis(rdlane64(ew, 0)) == d0) {
                 for (int b1 = fa; b1 > 0; b1 -= 64) {
                     const int ii = b1 - 64 + lane;
                     const unsigned long long m3 = __ballot(ii >= 0 && wdis(cs[ii >= 0 ? ii : 0]) == d0);
@@ -1770,6 +1803,7 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
             fa = nfa;
             // ---- neighbours of v0 in stored order, visited test-and-set (a
             // node listed twice is fresh at its first position only)
+            if (TRACE) tr.tick(0);
             int32_t v1 = -1;
             if (lane < cnt)
                 v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
@@ -1778,6 +1812,7 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
                     __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
             const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
             const uint32_t vbit = 1u << (v1 & 31);
+            if (TRACE) tr.tick(1);
             bool fresh = lane < jmax && !(vis[v1 >> 5] & vbit);
             uint32_t old = 0u;
             if (fresh) old = atomicOr(&vis[v1 >> 5], vbit);
@@ -1789,17 +1824,25 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
             st_ndis += (uint32_t)nf;
             st_nhops += 1;
             if (nf == 0) {
+                if (TRACE) {
+                    tr.tick(2);
+                    tr.t[9]++;
+                }
                 __syncthreads();
                 continue;
             }
             const int dst = fresh ? __popcll(fm & lt) : nf + __popcll(~fm & lt);
             const int32_t fv = __builtin_amdgcn_ds_permute(dst << 2, v1);
-            // ---- the full set admits only keys below its largest: the int8
-            // bound drops rows that cannot reach it (strictly above its
-            // distance, so no tie is skipped)
+            if (TRACE) {
+                tr.tick(2);
+                tr.t[9]++;
+                tr.t[10] += (unsigned)nf;
+            }
+            // ---- the full set admits only keys below its largest distance:
+            // the int8 bound drops rows that cannot reach it (strictly above
+            // it, so no arrival at that distance is skipped)
             const bool full = S == ef;
-            const uint64_t emax = full ? cs[ef - 1] : ~0ull;
-            const float maxd = wdis(emax);
+            const float maxd = full ? wdis(cs[ef - 1]) : WS_INF;
             int32_t sv = fv;
             int ns = nf;
             if (use_q8 && full && maxd < FLT_MAX) {
@@ -1808,6 +1851,10 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
                                lane, sv);
             }
             st_x32 += (uint32_t)ns;
+            if (TRACE) {
+                tr.tick(3);
+                tr.t[12] += (unsigned)ns;
+            }
             float fdis = WS_INF;
             if (ns > 0) {
                 if (g.d <= 128)
@@ -1817,83 +1864,169 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
                 else if (lane < ns)
                     fdis = l2_row(qs, g.storage + (int64_t)sv * g.ld, g.d);
             }
-            const long long ki = ((long long)(uint32_t)sv << 1) | 1ll;
+            if (TRACE) tr.tick(4);
+            if (win < WS_INF) {
+                // inside a window: an arrival reaching its distance, or one
+                // at the full set's largest distance (dropped here, perhaps
+                // entered in the reference's member order)
+                if (__ballot(lane < ns && (fdis <= win || (full && fdis == maxd))) != 0ull) {
+                    tie |= 1u;
+                    break;
+                }
+            }
             // MinimaxHeap::push into the full set drops v >= max by distance
-            // alone (HNSW.cpp:1096-1101): the same rule, so an arrival at the
-            // max distance is no divergence
+            // alone (HNSW.cpp:1096-1101)
             const bool enter = lane < ns && (!full || fdis < maxd);
             float cd = enter ? fdis : WS_INF;
-            long long ci = enter ? ki : WS_NOID;
+            long long ci = enter ? (long long)(kWAlive | (uint32_t)sv) : WS_NOID;
             const int m = wave_compact(cd, ci, enter, lane);
-            float disc = WS_INF;  // smallest distance the merge pushed past ef
             if (m > 0) {
                 wave_sort_m(cd, ci, lane, m);
                 const uint64_t akey =
                         lane < m ? (((uint64_t)__float_as_uint(cd) << 32) | (uint32_t)ci) : ~0ull;
-                // lower_bound of each arrival in the set (entries below it)
-                int lb = 0;
-                {
-                    int st = 1;
-                    while (2 * st <= S) st *= 2;
-                    for (; st > 0; st >>= 1)
-                        if (lb + st <= S && cs[lb + st - 1] < akey) lb += st;
+                if (TRACE) {
+                    tr.tick(5);
+                    tr.t[11] += (unsigned)m;
                 }
-                if (lane >= m) lb = S;
-                const int lb0 = __builtin_amdgcn_readfirstlane(lb);
-                // the entries from lb0 on move up by the arrivals below them
-                // (backward, 64 at a time: a step's reads precede its writes,
-                // and its writes land past every entry still to be read)
-                int ev_alive = 0;
-                for (int top = S; top > lb0; top -= 64) {
-                    const int i = top - 64 + lane;
-                    const bool vv = i >= lb0;
+                // ---- the merge, from the top of the set down, 64 entries a
+                // step: each step's entries move up by the arrivals below
+                // them; an arrival is placed (its lower_bound lbr) in the step
+                // whose entries it exceeds, the largest first.  The top step
+                // decides, before anything is written, whether the largest
+                // kept distance is shared by an arrival (then the hop's
+                // pushes go one at a time, in arrival order)
+                int lbr = S;      // lane j: arrival j's lower_bound once placed
+                int jhi = m;      // arrivals [0, jhi) not yet placed
+                int evl = 0;      // alive entries evicted
+                float disc = WS_INF;  // smallest distance pushed past ef
+                bool btie = false;
+                for (int top = S;; top -= 64) {
+                    const int base = top - 64;
+                    const int i = base + lane;
+                    const bool vv = i >= 0;
                     const uint64_t e = vv ? cs[i] : 0ull;
-                    int c = 0;
-                    for (int j = 0; j < m; j++) c += __builtin_amdgcn_readlane(lb, j) <= i ? 1 : 0;
-                    const int np = i + c;
-                    __syncthreads();
-                    if (vv) {
-                        if (np < ef) {
-                            cs[np] = e;
-                        } else {
-                            disc = fminf(disc, wdis(e));
-                            ev_alive += (int)(e & 1ull);
-                        }
+                    int jlo = jhi;
+                    int le = 0;  // arrivals placed here at or below this lane's entry
+                    while (jlo > 0) {
+                        const uint64_t kj = rdlane64(akey, jlo - 1);
+                        const int cj = __popcll(__ballot(vv && e < kj));
+                        if (cj == 0 && base > 0) break;  // below this step
+                        const int lbj = (base > 0 ? base : 0) + cj;
+                        jlo--;
+                        if (lane == jlo) lbr = lbj;
+                        le += lbj <= i ? 1 : 0;
                     }
+                    const int np = i + jlo + le;
+                    if (top == S && S + m > ef) {
+                        // arrivals kept: those below this step, and the ones
+                        // placed here that land below ef
+                        const int a = jlo + __popcll(__ballot(lane >= jlo && lane < m &&
+                                                              lbr + lane < ef));
+                        float Bd = a > 0 ? __int_as_float(__builtin_amdgcn_readlane(
+                                                   __float_as_int(cd), a - 1))
+                                         : -WS_INF;
+                        const int sl = ef - a - 1;  // the last set entry kept
+                        float ds0 = -WS_INF, ds1 = -WS_INF;
+                        if (sl >= 0) ds0 = wdis(sl >= base ? rdlane64(e, sl - base) : cs[sl]);
+                        if (sl + 1 < S) ds1 = wdis(sl + 1 >= base ? rdlane64(e, sl + 1 - base) : cs[sl + 1]);
+                        Bd = fmaxf(Bd, ds0);
+                        const int na = __popcll(__ballot(lane < ns && fdis == Bd));
+                        btie = na >= 1 && (na >= 2 || ds0 == Bd || ds1 == Bd);
+                        if (btie) break;  // (nothing written yet)
+                    }
+                    __syncthreads();
+                    if (vv && np < ef) cs[np] = e;
+                    const unsigned long long evm = __ballot(vv && np >= ef);
+                    if (evm) {
+                        evl += __popcll(__ballot(vv && np >= ef && (e & kWAlive)));
+                        disc = fminf(disc, wdis(rdlane64(e, __ffsll((long long)evm) - 1)));
+                    }
+                    if (TRACE) tr.t[13]++;
+                    jhi = jlo;
+                    if (jhi == 0) break;
                 }
-                const int pa = lane + lb;
-                const bool kept = lane < m && pa < ef;
-                if (kept) cs[pa] = akey;
-                else if (lane < m) disc = fminf(disc, cd);
-                // new first alive: the old one's new place, or the first arrival
-                int cfa = 0;
-                for (int j = 0; j < m; j++) cfa += __builtin_amdgcn_readlane(lb, j) <= fa ? 1 : 0;
-#pragma unroll
-                for (int mm = 32; mm > 0; mm >>= 1) ev_alive += __shfl_xor(ev_alive, mm);
-                nalive += __popcll(__ballot(kept)) - ev_alive;
-                int nfa2 = fa < S && fa + cfa < ef ? fa + cfa : ef;
-                if (lb0 < ef) nfa2 = min(nfa2, lb0);
-                S = min(S + m, ef);
-                fa = min(nfa2, S);
+                if (btie && win < WS_INF) {
+                    tie |= 1u;
+                    break;
+                }
+                if (btie) {
+                    if (TRACE) tr.t[14]++;
+                    // the hop's pushes one at a time in arrival order
+                    for (int j = 0; j < ns; j++) {
+                        const float dv =
+                                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), j));
+                        const uint32_t vj = (uint32_t)__builtin_amdgcn_readlane(sv, j);
+                        if (S == ef && dv >= wdis(cs[ef - 1])) continue;
+                        const uint64_t key = ((uint64_t)__float_as_uint(dv) << 32) | kWAlive | vj;
+                        const int p = wide_lower_bound(cs, S, key);
+                        const int S1 = S < ef ? S + 1 : ef;
+                        const uint64_t ev = S == ef ? cs[ef - 1] : 0ull;
+                        for (int hi = S1 - 1; hi > p; hi -= 64) {
+                            const int i = hi - lane;
+                            const uint64_t e = i > p ? cs[i - 1] : 0ull;
+                            __syncthreads();
+                            if (i > p) cs[i] = e;
+                            __syncthreads();
+                        }
+                        if (lane == 0) cs[p] = key;
+                        __syncthreads();
+                        nalive += 1;
+                        if (S == ef) {
+                            nalive -= (int)((ev & kWAlive) != 0ull);
+                            if (wdis(ev) == wdis(cs[ef - 1])) dvmin = fminf(dvmin, wdis(ev));
+                        }
+                        if (p <= fa) fa = p;
+                        S = S1;
+                    }
+                } else {
+                    const int pa = lane + lbr;
+                    const bool kept = lane < m && pa < ef;
+                    if (kept) cs[pa] = akey;
+                    // (arrival j lands at j + lbr_j, increasing: the kept ones
+                    // are a prefix)
+                    const int nk = __popcll(__ballot(kept));
+                    if (nk < m)
+                        disc = fminf(disc, __int_as_float(__builtin_amdgcn_readlane(
+                                                   __float_as_int(cd), nk)));
+                    // new first alive: the old one's new place, or the first arrival
+                    const int cfa = __popcll(__ballot(lane < m && lbr <= fa));
+                    nalive += nk - evl;
+                    int nfa2 = fa < S && fa + cfa < ef ? fa + cfa : ef;
+                    const int lb0 = __builtin_amdgcn_readfirstlane(lbr);
+                    if (lb0 < ef) nfa2 = min(nfa2, lb0);
+                    S = min(S + m, ef);
+                    fa = min(nfa2, S);
+                    __syncthreads();
+                    // (k == ef) an eviction at a largest distance shared by a
+                    // kept entry: the result heap evicts by (dis, id), the set
+                    // dead entries first — they may keep different ids there
+                    if (S == ef && disc < WS_INF && wdis(cs[ef - 1]) == disc)
+                        dvmin = fminf(dvmin, disc);
+                }
+                if (TRACE) tr.tick(6);
             }
-#pragma unroll
-            for (int mm = 32; mm > 0; mm >>= 1) disc = fminf(disc, __shfl_xor(disc, mm));
             __syncthreads();
-            // the kept-ef boundary: a key the merge pushed out at the ef-th
-            // kept distance (the reference's sequential pushes may keep the
-            // other one of the two)
-            if (S == ef && disc < WS_INF && wdis(cs[ef - 1]) == disc) tie |= 4u;
         }
     }
-    // the k-th boundary (k < ef; at k == ef the result heap and the set are
-    // the same process): the reference's result heap admits strictly, the
-    // set's first k order equal distances by id — they differ only when the
-    // k-th distance is shared by the next entry
-    if (k < ef && S > k) {
-        const float kd = wdis(cs[k - 1]);
-        if (kd < FLT_MAX && wdis(cs[k]) == kd) tie |= 8u;
+    if (tie == 0u) {
+        // the k-th boundary (k < ef): the reference's result heap admits
+        // strictly, so its k-th distance shared by the next entry leaves the
+        // kept ids to the arrival order
+        if (k < ef && S > k) {
+            const float kd = wdis(cs[k - 1]);
+            if (kd < FLT_MAX && wdis(cs[k]) == kd) tie |= 8u;
+        }
+        // (k == ef) the divergent eviction's distance still the largest kept
+        if (k == ef && S == ef && dvmin == wdis(cs[ef - 1])) tie |= 4u;
     }
     if (tie_flags && lane == 0) tie_flags[q] = tie;
+    if (TRACE && lane == 0) {
+        tr.t[7] = clock64() - tq;
+        tr.t[8] = tie != 0u;
+        tr.t[15] = (unsigned)S;
+#pragma unroll
+        for (int j = 0; j < 16; j++) tb[q * 16 + j] = tr.t[j];
+    }
     if (tie && tie_flags) return;  // the sequential kernel redoes this query
     if (stats && lane == 0 && g.entry_point >= 0) {
         atomicAdd(&stats[0], 1ull);
@@ -1903,14 +2036,32 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
         atomicAdd(&stats[4], (unsigned long long)(st_ndis - st_q8 + st_x32));
         atomicAdd(&stats[5], (unsigned long long)st_q8);
     }
+    // heap_reorder (Heap.h:421-450): ascending by (dis, id) — the set orders
+    // equal distances dead entries first, so a run of equal distances is
+    // ranked by id
+    const int kk = min(S, k);
     for (int j = lane; j < k; j += 64) {
-        const uint64_t e = j < S ? cs[j] : ~0ull;
-        const bool ok = j < S && wdis(e) < FLT_MAX;
-        const float dv = ok ? wdis(e) : FLT_MAX;
-        const int32_t id = ok ? wid(e) : -1;
-        if (D) D[q * k + j] = dv;
-        if (I) I[q * k + j] = id;
-        if (I32) I32[q * k + j] = id;
+        float dv = FLT_MAX;
+        int32_t id = -1;
+        int pos = j;
+        if (j < kk) {
+            const uint64_t e = cs[j];
+            dv = wdis(e);
+            id = wid(e);
+            if (!(dv < FLT_MAX)) {
+                dv = FLT_MAX;
+                id = -1;
+            } else if ((j > 0 && wdis(cs[j - 1]) == dv) || (j + 1 < kk && wdis(cs[j + 1]) == dv)) {
+                int s0 = j, s1 = j;
+                while (s0 > 0 && wdis(cs[s0 - 1]) == dv) s0--;
+                while (s1 + 1 < kk && wdis(cs[s1 + 1]) == dv) s1++;
+                pos = s0;
+                for (int i = s0; i <= s1; i++) pos += wid(cs[i]) < id ? 1 : 0;
+            }
+        }
+        if (D) D[q * k + pos] = dv;
+        if (I) I[q * k + pos] = id;
+        if (I32) I32[q * k + pos] = id;
     }
 }
 
@@ -2116,12 +2267,33 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
     if (hnsw_uses_wide(k, efSearch)) {
         ScopedKernelTimer tm(kt, "hnsw_wide", 0.0, s);
         const size_t lds_w = wide_lds_bytes(g, ef);
-        if (lds_w + (size_t)vwords * 4 <= 64 * 1024)
+        // FAISS_AMD_HNSW_WIDE_Q8=0: every fresh row's fp32 distance (no int8 bound)
+        const char* wq = getenv("FAISS_AMD_HNSW_WIDE_Q8");
+        HNSWDevice gw = g;
+        if (wq && !strcmp(wq, "0")) gw.q8 = nullptr;
+        // FAISS_AMD_HNSW_TRACE=<file>: per-query level-0 phase cycles (profiling)
+        const char* tenv = getenv("FAISS_AMD_HNSW_TRACE");
+        if (tenv && lds_w + (size_t)vwords * 4 <= 64 * 1024) {
+            unsigned long long* tb = nullptr;
+            HIP_CHECK(hipMalloc(&tb, 128 * n));
+            HIP_CHECK(hipMemsetAsync(tb, 0, 128 * n, s));
+            k_hnsw_wide<true, true><<<kgrid(n, 64), dim3(64), lds_w + vwords * 4, s>>>(
+                    gw, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, flags, tb);
+            HIP_LAUNCH_CHECK();
+            std::vector<unsigned long long> h((size_t)n * 16);
+            HIP_CHECK(hipMemcpyAsync(h.data(), tb, 128 * n, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            HIP_CHECK(hipFree(tb));
+            if (FILE* f = fopen(tenv, "ab")) {
+                fwrite(h.data(), 128, n, f);
+                fclose(f);
+            }
+        } else if (lds_w + (size_t)vwords * 4 <= 64 * 1024)
             k_hnsw_wide<true><<<kgrid(n, 64), dim3(64), lds_w + vwords * 4, s>>>(
-                    g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, flags);
+                    gw, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, flags);
         else
             k_hnsw_wide<false><<<kgrid(n, 64), dim3(64), lds_w, s>>>(
-                    g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
+                    gw, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
                     flags);
         HIP_LAUNCH_CHECK();
     } else {

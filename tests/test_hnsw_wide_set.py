@@ -154,31 +154,48 @@ def ref_search(nbrs, dist, entry, k, ef, efSearch):
 
 # ------------------------------------------------ the wide form, restated
 def wide_search(nbrs, dist, entry, k, ef, efSearch):
-    """k_hnsw_wide's level 0: returns (results, tie bits, ndis, nhops, n2)."""
-    cs = [(dist[entry], entry, 1)]  # sorted (dis, id, alive)
+    """k_hnsw_wide's level 0: returns (results, tie bits, ndis, nhops, n2).
+
+    The set is a list of (dis, alive, id) sorted by (dis, alive) and, among
+    alive entries of equal distance, by id: a dead entry sorts before an
+    alive one of its distance, as CMax's cmp2 with the popped slot's id -1
+    (HNSW.cpp:1096-1107), and dead entries of one distance in any order (the
+    reference cannot tell them apart either)."""
+    cs = [(dist[entry], 1, entry)]
     vis = {entry}
     nalive, fa, tie = 1, 0, 0
     ndis = nhops = 0
     n2 = 0
+    win = None    # the distance of an open pop-tie window
+    dvmin = float("inf")  # (k == ef) smallest distance of an eviction at a tied max
+    FL = float("inf")
+
+    def key_lt(e, dv, v):  # entry e below the arrival (dv, alive, v)
+        return (e[0], e[1], e[2] if e[1] else -1) < (dv, 1, v)
+
+    def lower_bound(dv, v):
+        return sum(1 for e in cs if key_lt(e, dv, v))
+
     while True:
         S = len(cs)
         if nalive <= 0:
             n2 = 1
             break
-        d0, v0, _ = cs[fa]
-        after = cs[fa + 1:fa + 65]
-        if any(e[0] == d0 and e[2] for e in after) or (
-                len(after) == 64 and all(e[0] == d0 for e in after)):
-            tie |= 1
-        cs[fa] = (d0, v0, 0)
+        d0, _, v0 = cs[fa]
+        # pop_min: the first alive entry.  Another alive one at d0 (right
+        # after it: dead entries of a distance sort first): the reference
+        # pops the highest heap slot among them — a pop-tie window opens
+        if fa + 1 < S and cs[fa + 1][0] == d0:
+            win = d0
+        cs[fa] = (d0, 0, v0)
         nalive -= 1
         nfa = S
         for i in range(fa + 1, S):
-            if cs[i][2]:
+            if cs[i][1]:
                 nfa = i
                 break
-        nb = sum(1 for e in cs if e[0] < d0)  # (the kernel: fa minus equal ones before)
-        assert nb == fa - sum(1 for e in cs[:fa] if e[0] == d0)
+        nb = fa - sum(1 for e in cs[:fa] if e[0] == d0)
+        assert nb == sum(1 for e in cs if e[0] < d0)
         if nb >= efSearch:
             n2 = 1 if nalive == 0 else 0
             break
@@ -193,54 +210,80 @@ def wide_search(nbrs, dist, entry, k, ef, efSearch):
             fresh.append(v1)
         ndis += len(fresh)
         nhops += 1
-        if not fresh:
-            continue
-        full = S == ef
-        emax = cs[ef - 1] if full else None
         arr = [(dist[v], v) for v in fresh]
-        disc = float("inf")
-        if full:
-            # MinimaxHeap::push drops v >= max (by distance alone), as the
-            # reference does: no divergence, so no flag and no disc entry
-            enter = [(dv, v) for dv, v in arr if dv < emax[0]]
-        else:
-            enter = arr
-        enter.sort()
+        # inside a window the members' expansion order is the reference's
+        # heap layout's: equal as long as no arrival reaches the window's
+        # distance (the members are then popped back to back, whatever order)
+        if win is not None and any(dv <= win for dv, _ in arr):
+            tie |= 1
+            break
+        full = S == ef
+        maxd = cs[ef - 1][0] if full else FL
+        # (inside a window: an arrival at the full set's largest distance is
+        # dropped here, but may enter in the reference's member order)
+        if win is not None and full and any(dv == maxd for dv, _ in arr):
+            tie |= 1
+            break
+        enter = sorted((dv, v) for dv, v in arr if dv < maxd)
         m = len(enter)
         if m:
-            lbs = [sum(1 for e in cs if (e[0], e[1]) < a) for a in enter]
-            new = [None] * (S + m)
-            ev_alive = 0
-            for i, e in enumerate(cs):
-                c = sum(1 for lb in lbs if lb <= i)
-                new[i + c] = e
-            for j, a in enumerate(enter):
-                new[j + lbs[j]] = (a[0], a[1], 1)
-            assert all(x is not None for x in new)
-            kept_arr = sum(1 for j in range(m) if j + lbs[j] < ef)
-            for e in new[ef:]:
-                disc = min(disc, e[0])
-                if e[2] and not any(e[1] == a[1] for a in enter):
-                    ev_alive += 1
-            # (an evicted arrival was never alive in the set: not counted)
-            cfa = sum(1 for lb in lbs if lb <= fa)
-            nfa2 = fa + cfa if fa < S and fa + cfa < ef else ef
-            if lbs[0] < ef:
-                nfa2 = min(nfa2, lbs[0])
-            cs = new[:ef]
-            nalive += kept_arr - ev_alive
-            fa = min(nfa2, len(cs))
-            assert nalive == sum(e[2] for e in cs)
-            assert nalive == 0 or fa == min(i for i, e in enumerate(cs) if e[2])
-        if len(cs) == ef and disc < float("inf") and cs[ef - 1][0] == disc:
-            tie |= 4
+            lbs = [lower_bound(dv, v) for dv, v in enter]
+            kept = sum(1 for j in range(m) if lbs[j] + j < ef)
+            if S + m > ef:
+                # the kept max after a batch merge: the last kept arrival or
+                # the set entry at ef - kept - 1
+                cand = []
+                if kept:
+                    cand.append(enter[kept - 1][0])
+                if ef - kept - 1 >= 0:
+                    cand.append(cs[ef - kept - 1][0])
+                Bd = max(cand)
+                na = sum(1 for dv, _ in arr if dv == Bd)
+                ns_ = sum(1 for e in cs if e[0] == Bd)
+                boundary_tie = na >= 1 and na + ns_ >= 2
+            else:
+                boundary_tie = False
+            if boundary_tie and win is not None:
+                tie |= 1
+                break
+            if boundary_tie:
+                # the hop's pushes one at a time, in arrival order
+                # (MinimaxHeap::push: drop v >= max by distance, else evict
+                # the max by cmp2)
+                for dv, v in arr:
+                    if len(cs) == ef and dv >= cs[ef - 1][0]:
+                        continue
+                    p = lower_bound(dv, v)
+                    cs.insert(p, (dv, 1, v))
+                    nalive += 1
+                    if len(cs) > ef:
+                        ev = cs.pop()
+                        nalive -= ev[1]
+                        if ev[0] == cs[ef - 1][0]:
+                            dvmin = min(dvmin, ev[0])
+                fa = next((i for i, e in enumerate(cs) if e[1]), len(cs))
+            else:
+                new = list(cs)
+                for j, (dv, v) in enumerate(enter):
+                    new.insert(lbs[j] + j, (dv, 1, v))
+                assert len(new) == S + m and all(x is not None for x in new)
+                for ev in new[ef:]:
+                    nalive -= ev[1]
+                    if ev[0] == new[ef - 1][0]:
+                        dvmin = min(dvmin, ev[0])
+                nalive += m
+                cs = new[:ef]
+                fa = next((i for i, e in enumerate(cs) if e[1]), len(cs))
+            assert nalive == sum(e[1] for e in cs)
+        if win is not None and (nalive == 0 or cs[fa][0] > win):
+            win = None
     S = len(cs)
-    # (k == ef: the result heap and the set are the same process)
-    if k < ef and S > k:
-        kd = cs[k - 1][0]
-        if kd < FMAX and cs[k][0] == kd:
+    if tie == 0:
+        if k < ef and S > k and cs[k - 1][0] < FMAX and cs[k][0] == cs[k - 1][0]:
             tie |= 8
-    out = [(e[0], e[1]) for e in cs[:k] if e[0] < FMAX]
+        if k == ef and S == ef and dvmin == cs[ef - 1][0]:
+            tie |= 4
+    out = sorted((e[0], e[2]) for e in cs[:k] if e[0] < FMAX)
     out += [(FMAX, -1)] * (k - len(out))
     return out, tie, ndis, nhops, n2
 
