@@ -72,7 +72,7 @@ PEAK_LDS_TBS = 150.0       # MI355X_MICROARCH.md: aggregate ds_read_b128 rate, e
 # symbol of the kernel that stage launches in this round's code, matched in
 # this round's committed rocprofv3 PMC summaries (a summary of an older kernel
 # or round is never used: traffic is null instead)
-ROUND = 5
+ROUND = 6
 PMC_SYMBOL = {
     "ivf_flat_scan": r"kern::k_ivf_bf2_stream<true, \d+, \d+, false, true, false>",
     # (rocprofv3 leaves this one mangled: its name holds a __bf16, "DF16b")

@@ -50,6 +50,9 @@ for pt in os.environ.get("POINTS", "256:768,1024:1024").split(","):
     q.efSearch = ef
     q.search(xq, k)
     t_wide = timed(k)
+    if os.environ.get("DIAG_PMC"):  # (under rocprofv3 --pmc: the plain searches only)
+        print(f"k {k} ef {ef}: wide+reruns {t_wide:.3f} ms", flush=True)
+        continue
     os.environ["FAISS_AMD_HNSW_WIDE_Q8"] = "0"
     t_noq8 = timed(k)
     del os.environ["FAISS_AMD_HNSW_WIDE_Q8"]
