@@ -641,6 +641,11 @@ void IndexIVF::search_device_eager(idx_t n, const float* x, int ldx, idx_t k, fl
         } reset{shared_qimg_};
         const int nt = (int)std::min<idx_t>(get_search_slices(), std::max<idx_t>(nq, 1));
         const bool one_form = nt <= 1 || (nq / nt >= 20);  // the whole batch's BLAS form
+        if (qf && qf->d == d && one_form && mc == 0 && !selm &&
+            scan_flat_pipelined(nq, x + q0 * ldx, ldx, k, (int)np, distances + q0 * k,
+                                labels + q0 * k, s)) {
+            continue;
+        }
         if (qf && qf->d == d && one_form) {
             if (qf->assign_device_qimg(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
                                        s_ci_.as<int32_t>(), s_q_.ptr, s))
@@ -708,6 +713,59 @@ bool IndexIVF::scan_hnsw_pipelined(idx_t nq, const float* x, int ldx, idx_t k, i
         quantizer->assign_device(b - a, x + a * ldx, ldx, np, cd, ci, qparams, pipe_s_);
         HIP_CHECK(hipEventRecord(pipe_ev_[c], pipe_s_));
         HIP_CHECK(hipStreamWaitEvent(s, pipe_ev_[c], 0));
+        search_preassigned_device(b - a, x + a * ldx, ldx, k, np, ci, cd, distances + a * k,
+                                  labels + a * k, s, nullptr, nullptr);
+    }
+    return true;
+}
+
+// A flat quantizer's batch in P chunks (FAISS_AMD_PIPE=<P>): chunk c's
+// coarse search (query image, bf16x3 filter, exact re-rank) on pipe_s_
+// overlaps chunk c - 1's list scan on the caller's stream, so the scan's
+// latency-bound re-rank shares the CUs with the next chunk's MFMA filter.
+// Chunks are whole 128-query blocks of at least 1024 queries, so every
+// chunk takes the batch's BLAS form; each chunk's query image lives in its
+// own slice of s_q_ (the scan of chunk c reads it while chunk c + 1's is
+// written).  Results identical to the one-chunk search.
+bool IndexIVF::scan_flat_pipelined(idx_t nq, const float* x, int ldx, idx_t k, int np,
+                                   float* distances, idx_t* labels, hipStream_t s) const {
+    const auto* qf = dynamic_cast<const IndexFlat*>(quantizer);
+    const char* env = getenv("FAISS_AMD_PIPE");
+    const int P = env ? atoi(env) : 1;
+    if (!qf || qdone_ || P <= 1 || nq < (idx_t)P * 1024) return false;
+    if (!pipe_s_) HIP_CHECK(hipStreamCreateWithFlags(&pipe_s_, hipStreamNonBlocking));
+    while ((int)pipe_ev_.size() < P + 1) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        pipe_ev_.push_back(e);
+    }
+    std::vector<idx_t> cut(P + 1);
+    for (int c = 0; c < P; c++) cut[c] = std::min<idx_t>(nq, (idx_t)roundup((size_t)(nq * c / P), 128));
+    cut[P] = nq;
+    size_t tot = 0;
+    for (int c = 0; c < P; c++)
+        if (cut[c + 1] > cut[c]) tot += roundup(qf->query_image_size(cut[c + 1] - cut[c]), 256);
+    s_q_.reserve(tot);
+    // the chunks' coarse searches follow the caller's prior work (x, and the
+    // previous readers of the coarse buffers and query images)
+    HIP_CHECK(hipEventRecord(pipe_ev_[P], s));
+    HIP_CHECK(hipStreamWaitEvent(pipe_s_, pipe_ev_[P], 0));
+    size_t off = 0;
+    for (int c = 0; c < P; c++) {
+        const idx_t a = cut[c], b = cut[c + 1];
+        if (b <= a) continue;
+        float* cd = s_cd_.as<float>() + a * np;
+        int32_t* ci = s_ci_.as<int32_t>() + a * np;
+        void* qi = (uint8_t*)s_q_.ptr + off;
+        off += roundup(qf->query_image_size(b - a), 256);
+        const bool img = qf->assign_device_qimg(b - a, x + a * ldx, ldx, np, cd, ci, qi, pipe_s_);
+        HIP_CHECK(hipEventRecord(pipe_ev_[c], pipe_s_));
+        HIP_CHECK(hipStreamWaitEvent(s, pipe_ev_[c], 0));
+        struct Reset {
+            const void*& p;
+            ~Reset() { p = nullptr; }
+        } reset{shared_qimg_};
+        shared_qimg_ = img ? qi : nullptr;
         search_preassigned_device(b - a, x + a * ldx, ldx, k, np, ci, cd, distances + a * k,
                                   labels + a * k, s, nullptr, nullptr);
     }

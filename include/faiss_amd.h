@@ -627,6 +627,10 @@ struct IndexIVF : Index {
     bool scan_hnsw_pipelined(idx_t nq, const float* x, int ldx, idx_t k, int np,
                              float* distances, idx_t* labels, const SearchParameters* qparams,
                              hipStream_t s) const;
+    // flat quantizer (FAISS_AMD_PIPE=<chunks>): the same overlap, each
+    // chunk's query image in its own slice of s_q_
+    bool scan_flat_pipelined(idx_t nq, const float* x, int ldx, idx_t k, int np,
+                             float* distances, idx_t* labels, hipStream_t s) const;
     mutable hipStream_t pipe_s_ = nullptr;
     mutable std::vector<hipEvent_t> pipe_ev_;
     // search_device replayed from a hipGraph captured on the second identical
