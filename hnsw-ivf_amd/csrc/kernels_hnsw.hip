@@ -1675,7 +1675,8 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
     // neighbour ids, [2] visited, [3] int8 bound, [4] fp32 rows, [5] compact +
     // sort + lower_bound, [6] merge, [7] whole query; [8] flagged, [9] hops,
     // [10] fresh, [11] arrivals that enter, [12] fp32 rows, [13] merge steps,
-    // [14] hops pushed one at a time, [15] set size at the end
+    // [14] hops pushed one at a time, [15] hops whose neighbour ids were
+    // prefetched
     HopTrace tr;
     if (TRACE) {
 #pragma unroll
@@ -1746,6 +1747,10 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
         S = 1;
         int nalive = 1, fa = 0;  // alive entries (MinimaxHeap::nvalid), first alive
         float win = WS_INF;      // the distance of an open pop-tie window
+        // the next hop's neighbour ids, loaded during this hop for the entry
+        // expected to be popped next (the next alive one; a hint: a wrong
+        // guess only costs the load)
+        int32_t pf_v = -1, pf_nb = -1;
         __syncthreads();
         const int cnt = g.cum_nb[1] - g.cum_nb[0];
         const unsigned long long lt = (1ull << lane) - 1ull;
@@ -1805,9 +1810,18 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
             // node listed twice is fresh at its first position only)
             if (TRACE) tr.tick(0);
             int32_t v1 = -1;
-            if (lane < cnt)
+            if (v0 == pf_v) {
+                v1 = pf_nb;
+                if (TRACE) tr.t[15]++;
+            } else if (lane < cnt) {
                 v1 = g.nb0 ? g.nb0[(int64_t)v0 * g.nb0_stride + lane]
                            : g.neighbors[g.offsets[v0] + g.cum_nb[0] + lane];
+            }
+            pf_v = -1;
+            if (g.nb0 && nfa < S) {
+                pf_v = wid(cs[nfa]);
+                pf_nb = lane < cnt ? g.nb0[(int64_t)pf_v * g.nb0_stride + lane] : -1;
+            }
             const unsigned long long neg =
                     __ballot(lane < cnt && v1 < 0) | (cnt < 64 ? (~0ull << cnt) : 0ull);
             const int jmax = neg ? __ffsll((long long)neg) - 1 : 64;
@@ -2023,7 +2037,6 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
     if (TRACE && lane == 0) {
         tr.t[7] = clock64() - tq;
         tr.t[8] = tie != 0u;
-        tr.t[15] = (unsigned)S;
 #pragma unroll
         for (int j = 0; j < 16; j++) tb[q * 16 + j] = tr.t[j];
     }

@@ -78,7 +78,8 @@ for pt in os.environ.get("POINTS", "256:768,1024:1024").split(","):
           f"query {un[:, 7].mean():.0f} cycles (max {un[:, 7].max():.0f}); per hop: fresh "
           f"{un[:, 10].sum() / hops:.1f}, enter {un[:, 11].sum() / hops:.1f}, fp32 rows "
           f"{un[:, 12].sum() / hops:.1f}, merge steps {un[:, 13].sum() / hops:.2f}; one-at-a-time "
-          f"hops {int(un[:, 14].sum())}", flush=True)
+          f"hops {int(un[:, 14].sum())}, neighbour ids prefetched for {un[:, 15].sum() / hops:.2f} of "
+          f"the hops", flush=True)
     fl = tr[tr[:, 8] != 0]
     if len(fl):
         print(f"  flagged {len(fl)}: at hop {fl[:, 9].mean():.1f} on average "
