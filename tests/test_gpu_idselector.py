@@ -132,3 +132,36 @@ def test_flat_selector_range_outside(amd, orc, gpu):
     flat.add(xb)
     D, I = flat.search(xb[:5], 3, params=amd.SearchParametersIVF(sel=amd.IDSelectorRange(600, 900)))
     assert (I == -1).all() and (D == np.finfo(np.float32).max).all()
+
+
+def test_pq_selector_keeps_filter_pruning(amd, orc, gpu, monkeypatch, capfd):
+    """the code-decoding PQ filter gives a padding row or
+    a selector non-member the bias fragment {-inf, 0, 0, 1, 1, 1, 0, 0}
+    (kernels_pq_mfma.hip bias_frag), so its key sorts after every real one;
+    the round-5 form split -inf into (-inf, NaN, NaN) and its NaN keys made
+    streams fail (the re-rank then rescans them: results still exact, the
+    pruning lost).  The failing streams per query with a 40 % selector stay
+    at the unfiltered search's level (FAISS_AMD_IVF_STATS counters)."""
+    import re
+    d, nb, nlist = 64, 20000, 32
+    xb = rand(orc, nb, d, 83)
+    xq = rand(orc, 300, d, 84)
+    idx = amd.index_factory(d, f"IVF{nlist},PQ16")
+    idx.train(xb)
+    idx.add(xb)
+    idx.nprobe = 8
+    keep = np.nonzero(np.random.default_rng(3).random(nb) < 0.4)[0]
+    sel = amd.IDSelectorBatch(keep)
+    monkeypatch.setenv("FAISS_AMD_IVF_STATS", "1")
+
+    def failing(params):
+        capfd.readouterr()
+        idx.search(xq, 10, params=params)
+        err = capfd.readouterr().err
+        m = re.findall(r"ivfpq mfma scan: .*failing streams/q=([0-9.]+)", err)
+        assert m, err
+        return float(m[-1])
+
+    f0 = failing(None)
+    f1 = failing(amd.SearchParametersIVF(nprobe=8, sel=sel))
+    assert f1 <= 2.0 * f0 + 0.25, (f0, f1)

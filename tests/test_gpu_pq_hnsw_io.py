@@ -292,3 +292,35 @@ def test_hnsw_sequential_kernel_wide_ef(amd, orc, gpu, d):
         D, I = h.search(xq, k)
         Dr, Ir = g.search(xq, k, ef)
         assert_same_results(D, I, Dr, Ir)
+
+
+@pytest.mark.parametrize("nb,ef,k", [(300, 500, 10), (300, 1000, 300), (6000, 200, 200),
+                                     (6000, 700, 50), (6000, 2000, 2000)])
+@pytest.mark.parametrize("ties", [False, True])
+def test_hnsw_wide_edges_bit_exact(amd, orc, gpu, nb, ef, k, ties):
+    """The wide kernel (128 < max(efSearch, k) <= 4096) at its edges: efSearch
+    beyond the graph (the candidate set never fills: nalive reaches 0, n2),
+    k == ef (the result-heap eviction rule), and heavy exact-distance ties
+    (coordinates on a 1/4 grid: many equal fp32 distances, so pop-tie windows,
+    one-at-a-time pushes and re-runs all occur) — bit-exact against the
+    oracle's HNSW::search, and the wide stage must be the one that ran."""
+    d = 32
+    xb = rand(orc, nb, d, 71)
+    xq = rand(orc, 200, d, 72)
+    if ties:
+        xb = np.round(xb * 4) / 4
+        xq = np.round(xq * 4) / 4
+    h = amd.IndexHNSWFlat(d, 16)
+    h.add(np.ascontiguousarray(xb, dtype=np.float32))
+    h.efSearch = ef
+    amd.set_kernel_timing(True)
+    try:
+        h.reset_kernel_times()
+        D, I = h.search(np.ascontiguousarray(xq, dtype=np.float32), k)
+        names = {nm for nm, _, _ in h.kernel_times()}
+    finally:
+        amd.set_kernel_timing(False)
+    assert "hnsw_wide" in names, names
+    g = orc.HNSWGraph.from_index(h)
+    Dr, Ir = g.search(np.ascontiguousarray(xq, dtype=np.float32), k, ef)
+    assert_same_results(D, I, Dr, Ir)
