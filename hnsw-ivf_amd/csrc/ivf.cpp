@@ -1222,8 +1222,9 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     s_ient_.reserve(sizeof(uint32_t) * max_items * QT);
     b.item_desc = s_idesc_.as<kern::ItemDesc>();
     b.item_entries = s_ient_.as<uint32_t>();
-    s_ictr_.reserve(16);
+    s_ictr_.reserve(16 + 4 * 3 * 64);
     b.item_ctr = s_ictr_.as<uint32_t>();
+    b.scan_tmp = s_ictr_.as<uint32_t>() + 4;
     {
         ScopedKernelTimer tb(&ktimes, "ivf_bucket", 0.0, s);
         kern::ivf_bucket(assign, n, np, d_list_len_.as<uint32_t>(), d_list_off_.as<uint32_t>(),
@@ -1529,8 +1530,9 @@ void IndexIVFPQ::search_preassigned_device(idx_t n, const float* x, int ldx, idx
         s_ent_.reserve(sizeof(uint32_t) * n * np);
         kern::IVFBuckets b{counts, s_boff_.as<uint32_t>(), s_ioff_.as<uint32_t>(),
                            s_cur_.as<uint32_t>(), s_ent_.as<uint32_t>()};
-        s_ictr_.reserve(16);
+        s_ictr_.reserve(16 + 4 * 3 * 64);
         b.item_ctr = s_ictr_.as<uint32_t>();  // the PQ filter's work counter
+        b.scan_tmp = s_ictr_.as<uint32_t>() + 4;
         b.counts_next = counts_next;
         b.lim = lim;
         b.sel = sel;

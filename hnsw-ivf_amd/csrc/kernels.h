@@ -130,6 +130,7 @@ struct IVFBuckets {
     uint32_t* entries;     // [n * nprobe], entry = q * nprobe + rank
     uint32_t* item_list = nullptr;  // [max_items]: list of each work item
     uint32_t* item_ctr = nullptr;   // [1]: zeroed by the scan (persistent filter's counter)
+    uint32_t* scan_tmp = nullptr;   // [3 * 64]: the many-group scan's block totals
     // optional: lists by decreasing length; work items are numbered in this
     // order (longest first: the filters' launch order, so the long items do
     // not start last and set the kernel's tail)

@@ -45,19 +45,20 @@ __global__ void k_bucket_count(const int32_t* __restrict__ assign, int64_t total
 // Same with a block-local LDS histogram (nlist <= BC_MAXL): BC_PER entries
 // per thread take their slot from an LDS atomic, then one global atomic per
 // non-empty bin reserves the block's range of each bucket.
-constexpr int BC_MAXL = 16384;
+constexpr int BC_MAXL = 16384;       // lists per range in 64 KB of LDS
+constexpr int BC_MAXL_BIG = 32768;   // 128 KB (a work group may hold 160 KB on gfx950)
 template <int BC_PER>
 __global__ __launch_bounds__(1024) void k_bucket_count_lds(const int32_t* __restrict__ assign,
                                                            int64_t total,
                                                            const uint32_t* __restrict__ list_len,
                                                            int nlist, uint32_t* __restrict__ counts,
-                                                           uint32_t* __restrict__ pos) {
-    extern __shared__ uint32_t hist[];  // [min(nlist, BC_MAXL)]
+                                                           uint32_t* __restrict__ pos, int maxl) {
+    extern __shared__ uint32_t hist[];  // [min(nlist, maxl)]
     const int t = threadIdx.x;
-    // lists [lbase, lbase + nl) of this block row (nlist > BC_MAXL: one row
-    // of blocks per range, each reading every entry)
-    const int lbase = (int)blockIdx.y * BC_MAXL;
-    const int nl = min(BC_MAXL, nlist - lbase);
+    // lists [lbase, lbase + nl) of this block row (nlist > maxl: one row of
+    // blocks per range, each reading every entry)
+    const int lbase = (int)blockIdx.y * maxl;
+    const int nl = min(maxl, nlist - lbase);
     for (int i = t; i < nl; i += 1024) hist[i] = 0u;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * 1024 * BC_PER;
@@ -272,6 +273,127 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* counts,
     }
 }
 
+// The scan of k_bucket_scan over many work groups (nlist > 8192; c5: 65536
+// lists, where the single work group's chunks and its gathers of the
+// permuted counts took 133 us).  Part: each group scans its 4096 E-runs of
+// counts (bucket sizes, and work items in list order or, with perm, in perm
+// order — the counts gathered through perm) into local exclusive prefixes
+// and writes its three totals; fix: each group adds the totals of the groups
+// before it, clears its counts (counts_next) and the last one writes the
+// ends and the work counter.
+template <int E>
+__global__ __launch_bounds__(1024) void k_bucket_scan_part(const uint32_t* __restrict__ counts,
+                                                           int nlist, int QT,
+                                                           uint32_t* __restrict__ bucket_off,
+                                                           uint32_t* __restrict__ item_off,
+                                                           const uint32_t* __restrict__ perm,
+                                                           uint32_t* __restrict__ tot) {
+    __shared__ uint32_t wb[16], wi[16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int qs = (QT & (QT - 1)) == 0 ? __builtin_ctz((unsigned)QT) : -1;
+    auto nitems = [&](uint32_t c) -> uint32_t {
+        return qs >= 0 ? (c + (uint32_t)QT - 1u) >> qs : (c + (uint32_t)QT - 1u) / (uint32_t)QT;
+    };
+    auto block_scan = [&](uint32_t sb, uint32_t si, uint32_t& pb, uint32_t& pi, uint32_t& tb,
+                          uint32_t& ti) {
+        uint32_t ib = sb, ii = si;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t vb = __shfl_up(ib, off), vi = __shfl_up(ii, off);
+            if (lane >= off) {
+                ib += vb;
+                ii += vi;
+            }
+        }
+        if (lane == 63) {
+            wb[w] = ib;
+            wi[w] = ii;
+        }
+        __syncthreads();
+        pb = pi = tb = ti = 0u;
+#pragma unroll
+        for (int v = 0; v < 16; v++) {
+            pb += v < w ? wb[v] : 0u;
+            pi += v < w ? wi[v] : 0u;
+            tb += wb[v];
+            ti += wi[v];
+        }
+        __syncthreads();
+        pb += ib - sb;
+        pi += ii - si;
+    };
+    const int l0 = (int)blockIdx.x * 1024 * E + E * t;
+    uint32_t c[E], sb = 0u, si = 0u;
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+        c[j] = l0 + j < nlist ? counts[l0 + j] : 0u;
+        sb += c[j];
+        si += nitems(c[j]);
+    }
+    uint32_t pb, pi, tb, ti;
+    block_scan(sb, si, pb, pi, tb, ti);
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+        if (l0 + j < nlist) {
+            bucket_off[l0 + j] = pb;
+            if (!perm) item_off[l0 + j] = pi;
+        }
+        pb += c[j];
+        pi += nitems(c[j]);
+    }
+    uint32_t tp = 0u;
+    if (perm) {
+        int ls[E];
+        uint32_t nj[E], sp = 0u;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+            ls[j] = l0 + j < nlist ? (int)perm[l0 + j] : -1;
+            nj[j] = ls[j] >= 0 ? nitems(counts[ls[j]]) : 0u;
+            sp += nj[j];
+        }
+        uint32_t pp, dummy, tdummy;
+        block_scan(sp, 0u, pp, dummy, tp, tdummy);
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+            if (ls[j] >= 0) item_off[ls[j]] = pp;
+            pp += nj[j];
+        }
+    }
+    if (t == 0) {
+        tot[3 * blockIdx.x] = tb;
+        tot[3 * blockIdx.x + 1] = ti;
+        tot[3 * blockIdx.x + 2] = tp;
+    }
+}
+template <int E>
+__global__ __launch_bounds__(1024) void k_bucket_scan_fix(int nlist, uint32_t* __restrict__ bucket_off,
+                                                          uint32_t* __restrict__ item_off,
+                                                          const uint32_t* __restrict__ perm,
+                                                          const uint32_t* __restrict__ tot,
+                                                          uint32_t* __restrict__ zero_next,
+                                                          uint32_t* __restrict__ item_ctr) {
+    const int t = threadIdx.x, b = (int)blockIdx.x;
+    uint32_t ob = 0u, oi = 0u;
+    for (int v = 0; v < b; v++) {
+        ob += tot[3 * v];
+        oi += tot[3 * v + (perm ? 2 : 1)];
+    }
+    const int l0 = b * 1024 * E + E * t;
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+        if (l0 + j < nlist) {
+            bucket_off[l0 + j] += ob;
+            item_off[perm ? (int)perm[l0 + j] : l0 + j] += oi;
+            if (zero_next) zero_next[l0 + j] = 0u;
+        }
+    }
+    if (b == (int)gridDim.x - 1 && t == 0) {
+        bucket_off[nlist] = ob + tot[3 * b];
+        item_off[nlist] = oi + tot[3 * b + (perm ? 2 : 1)];
+        if (item_ctr) *item_ctr = 0u;
+    }
+}
+
 __global__ void k_bucket_fill(const int32_t* __restrict__ assign, int64_t total,
                               const uint32_t* __restrict__ list_len, int nlist, int QT,
                               const uint32_t* __restrict__ bucket_off,
@@ -401,7 +523,6 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
     FAISS_THROW_IF_NOT_MSG(total < (1ll << 32), "n * nprobe must fit in 32 bits");
     if (!b.counts_next) HIP_CHECK(hipMemsetAsync(b.counts, 0, sizeof(uint32_t) * nlist, s));
     if (total > 0) {
-        const int nr = (int)cdiv(nlist, BC_MAXL);  // list ranges (LDS histogram each)
         // entries per thread: enough work groups to spread the histogram
         // merge's global atomics over the chip (FAISS_AMD_BC_PER: tuning)
         // (c2, 4096 lists: 4 -> 7.6 us, 16 -> 12.9 us; c5, 65536 lists in 4
@@ -410,10 +531,22 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
         const char* pe = getenv("FAISS_AMD_BC_PER");
         const int per = pe ? atoi(pe) : nlist > BC_MAXL ? 16 : 4;
         {
-        const size_t lds = sizeof(uint32_t) * std::min(nlist, BC_MAXL);
+        // beyond 16384 lists: 32768-list ranges in 128 KB of LDS (half the
+        // passes over the entries; FAISS_AMD_BC_BIG=0: 64 KB ranges)
+        const char* be = getenv("FAISS_AMD_BC_BIG");
+        const int maxl = nlist > BC_MAXL && !(be && !strcmp(be, "0")) ? BC_MAXL_BIG : BC_MAXL;
+        const int nr2 = (int)cdiv(nlist, maxl);
+        const size_t lds = sizeof(uint32_t) * std::min(nlist, maxl);
 #define BCL(P)                                                                              \
-    k_bucket_count_lds<P><<<dim3((unsigned)cdiv(total, 1024 * P), (unsigned)nr), dim3(1024), \
-                            lds, s>>>(assign, total, list_len, nlist, b.counts, b.cursor)
+    do {                                                                                    \
+        if (lds > 65536)                                                                    \
+            HIP_CHECK(hipFuncSetAttribute((const void*)k_bucket_count_lds<P>,               \
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,       \
+                                          (int)lds));                                       \
+        k_bucket_count_lds<P><<<dim3((unsigned)cdiv(total, 1024 * P), (unsigned)nr2),       \
+                                dim3(1024), lds, s>>>(assign, total, list_len, nlist,       \
+                                                      b.counts, b.cursor, maxl);            \
+    } while (0)
         if (per >= 16) BCL(16);
         else if (per >= 8) BCL(8);
         else if (per >= 4) BCL(4);
@@ -423,6 +556,19 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
         HIP_LAUNCH_CHECK();
         }
     }
+    // beyond 8192 lists (and up to 64 groups of 4096): the scan over many
+    // work groups, its block totals after the work counter (b.scan_tmp);
+    // FAISS_AMD_SCAN_PAR=0: the single-group scan
+    const char* pp = getenv("FAISS_AMD_SCAN_PAR");
+    const int nbs = (int)cdiv(nlist, 4096);
+    if (nlist > 8192 && nbs <= 64 && b.scan_tmp && !b.item_list && !(pp && !strcmp(pp, "0"))) {
+        k_bucket_scan_part<4><<<dim3((unsigned)nbs), dim3(1024), 0, s>>>(
+                b.counts, nlist, QT, b.bucket_off, b.item_off, b.perm, b.scan_tmp);
+        HIP_LAUNCH_CHECK();
+        k_bucket_scan_fix<4><<<dim3((unsigned)nbs), dim3(1024), 0, s>>>(
+                nlist, b.bucket_off, b.item_off, b.perm, b.scan_tmp, b.counts_next, b.item_ctr);
+        HIP_LAUNCH_CHECK();
+    } else {
 #define BSCAN(E)                                                                            \
     k_bucket_scan<E><<<dim3(1), dim3(1024), 0, s>>>(b.counts, nlist, QT, b.bucket_off,         \
                                                     b.item_off, b.item_list, b.counts_next,    \
@@ -435,6 +581,7 @@ void ivf_bucket(const int32_t* assign, int64_t n, int nprobe, const uint32_t* li
     else BSCAN(4);
 #undef BSCAN
     HIP_LAUNCH_CHECK();
+    }
     if (total > 0) {
         k_bucket_fill<<<kgrid(cdiv(total, 256), 256), dim3(256), 0, s>>>(
                 assign, total, list_len, nlist, QT, b.bucket_off, b.item_off, b.cursor, b.entries,
