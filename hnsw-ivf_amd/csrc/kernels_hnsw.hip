@@ -2199,6 +2199,12 @@ size_t hnsw_heap_scratch_words(int k, int efSearch, int ld) {
     const int ef = efSearch > k ? efSearch : k;
     return seq_lds_bytes(ld, ef, k) > 64 * 1024 ? seq_heap_bytes(ef, k) / 4 : 0;
 }
+// FAISS_AMD_HNSW_WIDE_GVIS=1: the wide kernel's visited bitmap in global
+// scratch even where it fits the LDS (fewer LDS bytes per wave: occupancy)
+static bool wide_global_visited() {
+    const char* e = getenv("FAISS_AMD_HNSW_WIDE_GVIS");
+    return e && !strcmp(e, "1");
+}
 bool hnsw_visited_scratch_needed(int ld, int k, int efSearch, int64_t vwords) {
     // mirrors the LDS choices of the three kernels: any query may reach the
     // sequential kernel (ties of the batched one), the register kernel keeps
@@ -2218,7 +2224,7 @@ bool hnsw_visited_scratch_needed(int ld, int k, int efSearch, int64_t vwords) {
     if (hnsw_uses_wide(k, efSearch)) {
         HNSWDevice g{};
         g.ld = ld;
-        need = need || wide_lds_bytes(g, ef) + vb > kL;
+        need = need || wide_lds_bytes(g, ef) + vb > kL || wide_global_visited();
     } else if (hnsw_uses_batched(k, efSearch)) {
         need = need || lds_q + vb > kL;
     }
@@ -2301,7 +2307,7 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
                 fwrite(h.data(), 128, n, f);
                 fclose(f);
             }
-        } else if (lds_w + (size_t)vwords * 4 <= 64 * 1024)
+        } else if (lds_w + (size_t)vwords * 4 <= 64 * 1024 && !wide_global_visited())
             k_hnsw_wide<true><<<kgrid(n, 64), dim3(64), lds_w + vwords * 4, s>>>(
                     gw, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, flags);
         else

@@ -56,6 +56,10 @@ for pt in os.environ.get("POINTS", "256:768,1024:1024").split(","):
     os.environ["FAISS_AMD_HNSW_WIDE_Q8"] = "0"
     t_noq8 = timed(k)
     del os.environ["FAISS_AMD_HNSW_WIDE_Q8"]
+    os.environ["FAISS_AMD_HNSW_WIDE_GVIS"] = "1"
+    t_gvis = timed(k)
+    del os.environ["FAISS_AMD_HNSW_WIDE_GVIS"]
+    print(f"  visited bitmap in global scratch: {t_gvis:.3f} ms", flush=True)
     os.environ["FAISS_AMD_HNSW_STATS"] = "1"
     q.search(xq, k)
     del os.environ["FAISS_AMD_HNSW_STATS"]
