@@ -505,6 +505,11 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
     if (rlog) s_rlog_.reserve(8 * (size_t)kern::kHnswReplayCap * qc);
     if (scratch) s_visited_.reserve(sizeof(uint32_t) * vwords * qc);
     if (hw) s_heaps_.reserve(sizeof(float) * hw * qc);
+    // the sequential kernel's arrival logs (k_hnsw_exact without the result
+    // heap) for the queries it serves: every query past the batched / wide
+    // kernels' range, else their flagged ones (a pool; the rest keep the heap)
+    const size_t alb = kern::hnsw_arrival_log_bytes(qc, ntotal);
+    s_alog_.reserve(alb);
     s_flags_.reserve(sizeof(uint32_t) * std::max<idx_t>(qc, 1));
     // defer (split_begin): one chunk, the batched kernel in use
     defer = defer && !scratch && !hw && i32 && kern::hnsw_uses_batched(k, efSearch);
@@ -515,7 +520,8 @@ void IndexHNSW::hnsw_device(idx_t n, const float* x, int ldx, int k, float* dist
                           i32 ? (int32_t*)labels + q0 * k : nullptr, s_visited_.as<uint32_t>(),
                           vwords, d_stats_.as<unsigned long long>(), s_flags_.as<uint32_t>(), s,
                           &ktimes, defer, hw ? s_heaps_.as<float>() : nullptr,
-                          rlog ? s_rlog_.as<uint64_t>() : nullptr, rlog ? rcap : 0);
+                          rlog ? s_rlog_.as<uint64_t>() : nullptr, rlog ? rcap : 0, s_alog_.ptr,
+                          alb);
     }
     if (!defer) {
         order_.leave(s);
@@ -598,9 +604,12 @@ IndexHNSW::Split IndexHNSW::split_finish() const {
     HIP_CHECK(hipStreamWaitEvent(side_, ev_split_, 0));
     {
         ScopedKernelTimer tm(&ktimes, "hnsw_exact", 0.0, side_);
+        const size_t alb = kern::hnsw_arrival_log_bytes(r.nf, ntotal);
+        s_alog_.reserve(alb);
         kern::hnsw_exact_listed(gd, split_.x, split_.ldx, s_fidx_.as<uint32_t>(), r.nf, k,
                                 split_.efSearch, s_fD_.as<float>(), s_fI_.as<int32_t>(),
-                                nullptr, vwords, d_stats_.as<unsigned long long>(), side_);
+                                nullptr, vwords, d_stats_.as<unsigned long long>(), side_,
+                                s_alog_.ptr, alb);
     }
     HIP_CHECK(hipEventRecord(ev_exact_, side_));
     r.idx = s_fidx_.as<uint32_t>();

@@ -382,7 +382,8 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
                  hipStream_t s, KernelTimes* kt = nullptr,
                  bool defer = false, float* heap_scratch = nullptr,
-                 uint64_t* replay_log = nullptr, int64_t replay_cap = 0);
+                 uint64_t* replay_log = nullptr, int64_t replay_cap = 0,
+                 void* arrival_log = nullptr, size_t arrival_log_bytes = 0);
 // the register kernel's CandSet update log (64-bit entries per query in
 // replay_log): a query whose candidate set meets a layout-dependent decision
 // continues from a replayed heap instead of searching level 0 again; a query
@@ -414,7 +415,10 @@ void hnsw_flag_compact(const uint32_t* flags, int64_t n, uint32_t* idx, uint32_t
 void hnsw_exact_listed(const HNSWDevice& g, const float* x, int ldx, const uint32_t* qidx,
                        int64_t nf, int k, int efSearch, float* D, int32_t* I32,
                        uint32_t* visited_scratch, int64_t vwords, unsigned long long* stats,
-                       hipStream_t s);
+                       hipStream_t s, void* arrival_log = nullptr, size_t arrival_log_bytes = 0);
+// bytes of the sequential kernel's arrival-log pool (k_hnsw_exact without
+// the result heap) worth providing for n queries of an ntotal-node graph
+size_t hnsw_arrival_log_bytes(int64_t n, int64_t ntotal);
 // rows: out[i] = in[idx[i]] (d floats, strides ldi / ldo); scatter of
 // packed rows of row_words 32-bit words: dst row idx[i] = src row i
 void gather_rows(const float* in, int ldi, const uint32_t* idx, int64_t n, int d, float* out,

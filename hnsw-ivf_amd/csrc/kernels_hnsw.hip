@@ -393,6 +393,15 @@ namespace {
 // as faiss's does.  The code runs wave-uniform (every lane computes the same
 // serial steps; lane 0 stores), so the lanes can load a push's ancestors and a
 // sift's next three levels at once.
+// the sequential kernel's arrival log (k_hnsw_exact without the result
+// heap): per running work group a slot of `cap` keys from a pool of `slots`
+// (ctr: the slots handed out, zeroed before the launch)
+struct ArrivalLog {
+    uint64_t* base = nullptr;
+    uint32_t* ctr = nullptr;
+    int64_t slots = 0;
+    int64_t cap = 0;
+};
 __device__ __forceinline__ uint64_t sx_key(float d, int32_t id) {
     return ((uint64_t)(uint32_t)__float_as_int(d) << 32) | (uint32_t)(id ^ (int32_t)0x80000000);
 }
@@ -473,7 +482,8 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
                                                    int64_t vwords,
                                                    unsigned long long* __restrict__ stats,
                                                    const uint32_t* __restrict__ only,
-        const uint32_t* __restrict__ qidx, float* __restrict__ gheap = nullptr) {
+        const uint32_t* __restrict__ qidx, float* __restrict__ gheap = nullptr,
+        ArrivalLog alog = ArrivalLog{}) {
     // qidx: compact launch over listed queries (input row qidx[b], output
     // row b); else query b, output row b
     const int64_t q = qidx ? (int64_t)qidx[blockIdx.x] : (int64_t)blockIdx.x;
@@ -492,6 +502,17 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
     const uint64_t rinit = sx_key(FLT_MAX, -1);  // heap_heapify<CMax> (Heap.h:316-339)
     for (int j = lane; j < k; j += 64) rb[1 + j] = rinit;
     for (int64_t w = lane; w < vwords; w += 64) vis[w] = 0u;
+    // without the result heap (ArrivalLog): the query's arrivals logged in
+    // order, the results selected from them at the end (a log slot per
+    // work group from the pool; none left: the result heap as before)
+    uint64_t* lg = nullptr;
+    if (!GH && alog.base) {
+        uint32_t slot = 0u;
+        if (lane == 0) slot = atomicAdd(alog.ctr, 1u);
+        slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)slot);
+        if ((int64_t)slot < alog.slots) lg = alog.base + (int64_t)slot * alog.cap;
+    }
+    int64_t lpos = 0;
     __syncthreads();
     uint32_t st_n2 = 0, st_ndis = 0, st_nhops = 0;
     if (g.entry_point >= 0) {
@@ -539,7 +560,10 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
         }
         __syncthreads();
         float rthr = sx_dis(rb[1]);
-        if (d_nearest < rthr) {
+        if (lg) {
+            if (lane == 0) lg[0] = sx_key(d_nearest, nearest);
+            lpos = 1;
+        } else if (d_nearest < rthr) {
             sx_sift(rb, k, sx_key(d_nearest, nearest), lane);
             rthr = sx_dis(rb[1]);
         }
@@ -656,13 +680,18 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
             // enter neither heap (dis >= the result threshold, and >= the
             // full candidate heap's top) changes nothing
             uint64_t top = hk == ef ? cb[1] : 0ull;  // the full heap's top
+            if (lg) {  // the hop's arrivals, in order
+                if (lane < nf) lg[lpos + lane] = sx_key(fdis, fv);
+                lpos += nf;
+            }
             for (int t = 0; t < nf; t++) {
                 const float dis = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fdis), t));
                 const bool cin = hk < ef || dis < sx_dis(top);
-                if (!(dis < rthr) && !cin) continue;
+                const bool rin = !lg && dis < rthr;
+                if (!rin && !cin) continue;
                 const int32_t id = __builtin_amdgcn_readlane(fv, t);
                 const uint64_t key = sx_key(dis, id);
-                if (dis < rthr) {
+                if (rin) {
                     sx_sift(rb, k, key, lane);  // res.add_result: heap_replace_top
                     rthr = sx_dis(rb[1]);
                 }
@@ -686,6 +715,137 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
         atomicAdd(&stats[2], (unsigned long long)st_ndis);
         atomicAdd(&stats[3], (unsigned long long)st_nhops);
         atomicAdd(&stats[4], (unsigned long long)st_ndis);
+    }
+    if (lg) {
+        __syncthreads();
+        // the result heap's final content from the arrival log (lg[0, L)):
+        // it holds the k smallest arrivals by distance when the k-th
+        // distance is not shared (strict admission keeps any k smallest, and
+        // an arrival it turned away was at least its k-th); a shared k-th
+        // distance leaves the kept ids to the arrival order, and the heap is
+        // then rebuilt by replaying the log
+        uint64_t* sb = (uint64_t*)(sm + qpad);  // the heaps' LDS (dead now)
+        const int64_t L = lpos;
+        bool replay = false;
+        int nsel = (int)min<int64_t>(L, (int64_t)k);
+        uint32_t T = 0xffffffffu;  // select dis bits <= T
+        if (L > k) {
+            // radix select of the k-th smallest distance (bits as unsigned)
+            uint32_t* hist = (uint32_t*)sb;
+            uint32_t prefix = 0u, pmask = 0u;
+            int64_t kk = k;
+            for (int sh = 24; sh >= 0; sh -= 8) {
+                for (int j = lane; j < 256; j += 64) hist[j] = 0u;
+                __syncthreads();
+                for (int64_t i = lane; i < L; i += 64) {
+                    const uint32_t bits = (uint32_t)(lg[i] >> 32);
+                    if ((bits & pmask) == prefix) atomicAdd(&hist[(bits >> sh) & 255u], 1u);
+                }
+                __syncthreads();
+                // the bin holding the kk-th: 4 bins per lane, a lane scan
+                uint32_t c4[4], cs = 0u;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    c4[u] = hist[4 * lane + u];
+                    cs += c4[u];
+                }
+                uint32_t inc = cs;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t v = __shfl_up(inc, off);
+                    if (lane >= off) inc += v;
+                }
+                const uint32_t exc = inc - cs;
+                const unsigned long long hit = __ballot((int64_t)exc < kk && kk <= (int64_t)inc);
+                const int hl = __ffsll((long long)hit) - 1;
+                uint32_t below = (uint32_t)__builtin_amdgcn_readlane((int)exc, hl);
+                int bin = 4 * hl;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t cu = (uint32_t)__builtin_amdgcn_readlane((int)c4[u], hl);
+                    if (bin == 4 * hl + u && (int64_t)(below + cu) < kk) {
+                        below += cu;
+                        bin++;
+                    }
+                }
+                kk -= below;
+                prefix |= (uint32_t)bin << sh;
+                pmask |= 255u << sh;
+                __syncthreads();
+            }
+            T = prefix;
+            int64_t nle = 0;
+            for (int64_t i0 = 0; i0 < L; i0 += 64) {
+                const int64_t i = i0 + lane;
+                const uint32_t bits = i < L ? (uint32_t)(lg[i] >> 32) : 0xffffffffu;
+                nle += __popcll(__ballot(i < L && bits <= T));
+            }
+            replay = nle > k;
+            nsel = k;
+        }
+        if (replay) {
+            // heap_heapify + every arrival through res.add_result, in order
+            for (int j = lane; j < k; j += 64) rb[1 + j] = rinit;
+            __syncthreads();
+            float rt = FLT_MAX;
+            for (int64_t i0 = 0; i0 < L; i0 += 64) {
+                const int64_t i = i0 + lane;
+                const uint64_t e = i < L ? lg[i] : ~0ull;
+                const int nl = (int)min<int64_t>(64, L - i0);
+                for (int t = 0; t < nl; t++) {
+                    const uint64_t kt =
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(e >> 32), t) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, t);
+                    if (sx_dis(kt) < rt) {
+                        sx_sift(rb, k, kt, lane);
+                        rt = sx_dis(rb[1]);
+                    }
+                }
+            }
+            __syncthreads();
+        } else {
+            // the selected arrivals ascending by (dis, id): a bitonic sort
+            int P = 1;
+            while (P < nsel) P <<= 1;
+            int m = 0;
+            for (int64_t i0 = 0; i0 < L; i0 += 64) {
+                const int64_t i = i0 + lane;
+                const uint64_t e = i < L ? lg[i] : ~0ull;
+                const bool in = i < L && (uint32_t)(e >> 32) <= T;
+                const unsigned long long bm = __ballot(in);
+                if (in) sb[m + __popcll(bm & ((1ull << lane) - 1ull))] = e;
+                m += __popcll(bm);
+            }
+            for (int j = m + lane; j < P; j += 64) sb[j] = ~0ull;
+            __syncthreads();
+            for (int sz = 2; sz <= P; sz <<= 1) {
+                for (int st = sz >> 1; st > 0; st >>= 1) {
+                    for (int t = lane; t < P / 2; t += 64) {
+                        const int i = 2 * t - (t & (st - 1));
+                        const int jx = i + st;
+                        const bool up = (i & sz) == 0;
+                        const uint64_t ai = sb[i], aj = sb[jx];
+                        if ((ai > aj) == up) {
+                            sb[i] = aj;
+                            sb[jx] = ai;
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            for (int j = lane; j < k; j += 64) {
+                float dv = FLT_MAX;
+                int32_t id = -1;
+                if (j < nsel) {
+                    dv = sx_dis(sb[j]);
+                    id = sx_id(sb[j]);
+                }
+                if (D) D[qo * k + j] = dv;
+                if (I) I[qo * k + j] = id;
+                if (I32) I32[qo * k + j] = id;
+            }
+            return;
+        }
     }
     // heap_reorder<CMax> (Heap.h:421-450): pops into the vacated tail, then
     // the kept ones to the front and (FLT_MAX, -1) padding
@@ -2085,7 +2245,8 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
                               uint32_t* visited_scratch, int64_t vwords,
                               unsigned long long* stats, const uint32_t* only,
                               const uint32_t* qidx, hipStream_t s, float* gheap = nullptr,
-                              uint64_t* rlog = nullptr, int rcap = 0) {
+                              uint64_t* rlog = nullptr, int rcap = 0, void* alog = nullptr,
+                              size_t alog_bytes = 0) {
     const int ef = efSearch > k ? efSearch : k;
     const size_t lds_x = seq_lds_bytes(g.ld, ef, k);
     const bool x_lds_vis = lds_x + vwords * 4 <= 64 * 1024;
@@ -2155,14 +2316,43 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
         HIP_LAUNCH_CHECK();
         return;
     }
+    // the arrival log instead of the result heap (FAISS_AMD_HNSW_NORB=0: off,
+    // =1: at any k): a pool of per-query slots after a 256-byte counter, when
+    // the final selection's sort fits the heaps' LDS; by default for k <= 512
+    // (c4 quantizer, 2000 queries all sequential: k 256 / ef 768 7.74 ->
+    // 6.97 ms; k = ef = 1024 13.41 -> 13.55 ms, the selection's cost growing
+    // with k while a replace_top near the heap's top stays shallow)
+    ArrivalLog al;
+    const char* nenv = getenv("FAISS_AMD_HNSW_NORB");
+    const bool norb_on = nenv ? strcmp(nenv, "0") != 0 : k <= 512;
+    if (alog && norb_on && g.ntotal > 0) {
+        size_t P = 1;
+        while (P < (size_t)k) P <<= 1;
+        const size_t region = 8 * (seq_slots(ef) + seq_slots(k));
+        al.cap = (int64_t)g.ntotal + 2;
+        al.slots = alog_bytes > 256 ? (int64_t)((alog_bytes - 256) / (8 * (size_t)al.cap)) : 0;
+        if (8 * P <= region && region >= 1024 && al.slots > 0) {
+            al.ctr = (uint32_t*)alog;
+            al.base = (uint64_t*)((char*)alog + 256);
+            HIP_CHECK(hipMemsetAsync(al.ctr, 0, sizeof(uint32_t), s));
+        } else {
+            al = ArrivalLog{};
+        }
+    }
     if (x_lds_vis)
         k_hnsw_exact<true><<<kgrid(n, 64), dim3(64), lds_x + vwords * 4, s>>>(
-                g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx);
+                g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
+                nullptr, al);
     else
         k_hnsw_exact<false><<<kgrid(n, 64), dim3(64), lds_x, s>>>(
                 g, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats, only,
-                qidx);
+                qidx, nullptr, al);
     HIP_LAUNCH_CHECK();
+}
+size_t hnsw_arrival_log_bytes(int64_t n, int64_t ntotal) {
+    // (at most 256 MiB; slots past the pool fall back to the result heap)
+    const size_t per = 8 * (size_t)(std::max<int64_t>(ntotal, 0) + 2);
+    return std::min<size_t>((size_t)256 << 20, 256 + per * (size_t)std::max<int64_t>(n, 1));
 }
 
 // flagged queries -> compact list (any order: the queries are independent)
@@ -2189,10 +2379,11 @@ void hnsw_flag_compact(const uint32_t* flags, int64_t n, uint32_t* idx, uint32_t
 void hnsw_exact_listed(const HNSWDevice& g, const float* x, int ldx, const uint32_t* qidx,
                        int64_t nf, int k, int efSearch, float* D, int32_t* I32,
                        uint32_t* visited_scratch, int64_t vwords, unsigned long long* stats,
-                       hipStream_t s) {
+                       hipStream_t s, void* arrival_log, size_t arrival_log_bytes) {
     if (nf <= 0) return;
     hnsw_exact_launch(g, x, ldx, nf, k, efSearch, D, nullptr, I32, visited_scratch, vwords,
-                      stats, nullptr, qidx, s);
+                      stats, nullptr, qidx, s, nullptr, nullptr, 0, arrival_log,
+                      arrival_log_bytes);
 }
 
 size_t hnsw_heap_scratch_words(int k, int efSearch, int ld) {
@@ -2253,7 +2444,8 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
                  float* D, int64_t* I, int32_t* I32, uint32_t* visited_scratch,
                  int64_t visited_words_per_query, unsigned long long* stats, uint32_t* flags,
                  hipStream_t s, KernelTimes* kt, bool defer, float* heap_scratch,
-                 uint64_t* replay_log, int64_t replay_cap) {
+                 uint64_t* replay_log, int64_t replay_cap, void* arrival_log,
+                 size_t arrival_log_bytes) {
     if (n <= 0) return;
     FAISS_THROW_IF_NOT_FMT(k >= 1, "k = %d must be >= 1", k);
     const int ef = efSearch > k ? efSearch : k;
@@ -2275,7 +2467,8 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
         ScopedKernelTimer tm(kt, "hnsw_exact", 0.0, s);
         hnsw_exact_launch(g, x, ldx, n, k, efSearch, D, I, I32, visited_scratch, vwords, stats,
                           only, nullptr, s, heap_scratch, replay_cap > 0 ? replay_log : nullptr,
-                          (int)std::min<int64_t>(replay_cap, kHnswReplayCap));
+                          (int)std::min<int64_t>(replay_cap, kHnswReplayCap), arrival_log,
+                          arrival_log_bytes);
     };
     // FAISS_AMD_HNSW_EXACT=1: every query through the sequential kernel (tests)
     const char* xenv = getenv("FAISS_AMD_HNSW_EXACT");

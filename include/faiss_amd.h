@@ -410,7 +410,8 @@ struct IndexHNSW : Index {
                      const SearchParameters* params, hipStream_t stream,
                      bool defer = false) const;
     mutable DeviceBuffer d_levels_, d_offsets_, d_neighbors_, d_cum_, d_nb0_, s_visited_, d_stats_,
-            s_flags_, s_fidx_, s_fcnt_, s_fD_, s_fI_, s_heaps_, s_rlog_, d_q8_, d_q8p_, d_q8q1_;
+            s_flags_, s_fidx_, s_fcnt_, s_fD_, s_fI_, s_heaps_, s_rlog_, d_q8_, d_q8p_, d_q8q1_,
+            s_alog_;  // the sequential kernel's arrival-log pool
     mutable bool q8_ = false;  // the int8 level-0 row image is built
     mutable uint32_t* h_fcnt_ = nullptr;  // pinned read-back of the flagged count
     mutable hipEvent_t ev_split_ = nullptr, ev_exact_ = nullptr;

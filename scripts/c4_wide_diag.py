@@ -71,7 +71,20 @@ for pt in os.environ.get("POINTS", "256:768,1024:1024").split(","):
     del os.environ["FAISS_AMD_HNSW_TRACE"]
     os.environ["FAISS_AMD_HNSW_WIDE"] = "0"
     t_seq = timed(k, 1)
+    # the sequential kernel alone on 2000 queries (every one with an
+    # arrival-log slot), with and without the result heap
+    x2 = np.ascontiguousarray(xq[:2000])
+    ts2 = {}
+    for nrb in ("1", "0"):
+        os.environ["FAISS_AMD_HNSW_NORB"] = nrb
+        q.search(x2, k)
+        t = time.perf_counter()
+        q.search(x2, k)
+        ts2[nrb] = (time.perf_counter() - t) * 1e3
+    del os.environ["FAISS_AMD_HNSW_NORB"]
     del os.environ["FAISS_AMD_HNSW_WIDE"]
+    print(f"  sequential kernel, 2000 queries: arrival log {ts2['1']:.3f} ms, result heap "
+          f"{ts2['0']:.3f} ms", flush=True)
     print(f"k {k} ef {ef}: wide+reruns {t_wide:.3f} ms (no int8 bound {t_noq8:.3f} ms), "
           f"all-sequential {t_seq:.3f} ms", flush=True)
     tr = np.fromfile(tf, dtype=np.uint64).reshape(-1, 16).astype(np.float64)
