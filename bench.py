@@ -570,8 +570,11 @@ def main():
     # upload + result download); reported beside `value`, never as it
     pcie = None
     if world == 1 and args.steps > 0:
-        index.search(xq, k)
-        nh = min(args.steps, 5)
+        # three warm calls: a paged host search captures its pages' graphs
+        # on the second and replays them from the third
+        for _ in range(3):
+            index.search(xq, k)
+        nh = min(args.steps, 10)
         th = time.perf_counter()
         for _ in range(nh):
             index.search(xq, k)

@@ -85,9 +85,11 @@ IndexIVF::IndexIVF(Index* q, size_t d_, size_t nl, size_t cs, MetricType metric)
 }
 
 IndexIVF::~IndexIVF() {
-    graph_.clear();
+    for (auto& gr : graphs_) gr.clear();
     for (hipEvent_t e : pipe_ev_) (void)hipEventDestroy(e);
     if (pipe_s_) (void)hipStreamDestroy(pipe_s_);
+    for (hipEvent_t e : host_ev_) (void)hipEventDestroy(e);
+    if (host_cs_) (void)hipStreamDestroy(host_cs_);
     if (own_fields) delete quantizer;
 }
 
@@ -423,6 +425,7 @@ void IndexIVF::SearchGraph::clear() {
     key.clear();
     seen = 0;
     failed = false;
+    used = 0;
 }
 
 namespace {
@@ -458,7 +461,6 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     const bool eligible = !(genv && !strcmp(genv, "0")) && params_in == nullptr && !qdone_ &&
                           qflat != nullptr && get_search_slices() <= 1 && n > 0 && !dirty_;
     if (!eligible) {
-        graph_.clear();
         search_device_eager(n, x, ldx, k, distances, labels, params_in, s);
         return;
     }
@@ -472,7 +474,20 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
              (unsigned long long)devbuf_epoch().load(), device, pq ? pq->use_precomputed_table : -1,
              (int)by_residual);
     const std::string key = std::string(buf) + kernel_timing_state() + "|" + amd_env_key();
-    if (graph_.exec && graph_.key == key) {
+    SearchGraph* G = nullptr;
+    for (auto& e : graphs_)
+        if (e.key == key) G = &e;
+    if (!G) {
+        // a new call: the entry used least recently (or an empty one)
+        G = &graphs_[0];
+        for (auto& e : graphs_)
+            if (e.used < G->used) G = &e;
+        G->clear();
+        G->key = key;
+    }
+    SearchGraph& graph_ = *G;
+    graph_.used = ++graph_tick_;
+    if (graph_.exec) {
         // replay: fresh events at the timed stages' record nodes
         for (size_t i = 0; i < graph_.tnodes.size(); i++) {
             hipEvent_t a, b;
@@ -494,10 +509,6 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
         order_.leave(s);
         qflat->stream_leave(s);
         return;
-    }
-    if (graph_.key != key) {
-        graph_.clear();
-        graph_.key = key;
     }
     if (graph_.failed || graph_.seen++ == 0) {
         search_device_eager(n, x, ldx, k, distances, labels, params_in, s);
@@ -529,11 +540,13 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
         return;
     }
     bool ok = true;
+    capturing_ = true;
     try {
         search_device_eager(n, x, ldx, k, distances, labels, params_in, s);
     } catch (...) {
         ok = false;
     }
+    capturing_ = false;
     hipError_t e = hipStreamEndCapture(s, &gr);
     hipGraphExec_t ex = nullptr;
     if (ok && e == hipSuccess && gr) e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
@@ -666,6 +679,12 @@ void IndexIVF::search_device_eager(idx_t n, const float* x, int ldx, idx_t k, fl
         } else {
             quantize_device(nq, x + q0 * ldx, ldx, (int)np, s_cd_.as<float>(),
                             s_ci_.as<int32_t>(), params ? params->quantizer_params : nullptr, s);
+        }
+        if (paged_marks_ && !capturing_) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            HIP_CHECK(hipEventRecord(e, s));
+            paged_marks_->push_back(e);
         }
         const uint32_t* lim = nullptr;
         const int32_t* asg = apply_max_codes(nq, (int)np, s_ci_.as<int32_t>(), mc, &lim, s);
@@ -983,6 +1002,150 @@ void IndexIVF::search_stats(idx_t n, const float* x, idx_t k, float* distances, 
     search_host(n, x, k, distances, labels, params, per_query_stats, false);
 }
 
+namespace {
+// query pages of a host-buffer search: FAISS_AMD_HOST_PAGES=<P> (1 = one
+// upload, one search, one download); by default up to 4 pages of >= 16384
+// queries: a device search of fewer queries does not take proportionally
+// less time (c2, 10k queries: 1 page 0.57 ms, 2 pages 0.70 ms per call,
+// scripts/exp_host_pages.py).  A page keeps >= 20 queries, the flat
+// quantizer's batch form (faiss/utils/distances.cpp:807-823), so every page
+// computes the batch's coarse distances.
+int host_pages(idx_t n) {
+    const char* e = getenv("FAISS_AMD_HOST_PAGES");
+    const idx_t want = e ? std::max(1, atoi(e)) : 4;
+    const idx_t min_page = e ? 20 : 16384;
+    return (int)std::max<idx_t>(1, std::min<idx_t>(want, n / min_page));
+}
+}  // namespace
+
+// faiss/gpu/GpuIndex.cu:259,307-333 (searchFromCpuPaged_): host queries go
+// to the device in pages, each page's upload overlapping the previous page's
+// search; here the downloads overlap too.  Page i: upload on host_cs_ ->
+// event up[i] -> the index stream waits and runs search_device on the page
+// (a hipGraph replay from the third call on: one entry per page), then the
+// page's list / distance counts into s_stats_ -> event done[i] -> host_cs_
+// waits and downloads the page's results while page i + 1 searches.  The
+// results are the whole batch's: every page is scanned exactly as the batch
+// would be (per-query work only, the same coarse form).  Taken where the
+// device search replays a graph (flat quantizer, no per-call parameters,
+// max_codes 0, one slice, FAISS_AMD_GRAPH / FAISS_AMD_PIPE unset) and the
+// batch fits one scratch chunk; otherwise false (one page: an eager search
+// per page costs more host time than the overlap saves).
+bool IndexIVF::search_host_paged(idx_t n, const float* x, idx_t k, float* distances,
+                                 idx_t* labels, const SearchParameters* params_in,
+                                 bool update_times) const {
+    const auto* qf = dynamic_cast<const IndexFlat*>(quantizer);
+    const char* genv = getenv("FAISS_AMD_GRAPH");
+    if (!qf || params_in || max_codes != 0 || get_search_slices() > 1 ||
+        (genv && !strcmp(genv, "0")) || getenv("FAISS_AMD_PIPE"))
+        return false;
+    const int P = host_pages(n);
+    if (P <= 1) return false;
+    const size_t np = std::min(nlist, nprobe);
+    if (search_chunk(n, np, k) < n) return false;
+    DevGuard dg(device);
+    sync_device();
+    hipStream_t s = stream();
+    const int ldx = ld();
+    std::lock_guard<std::mutex> hg(host_mu_);
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    DeviceBuffer &bx = h_x_, &bd = h_d_, &bi = h_i_;
+    bx.reserve(sizeof(float) * n * ldx);
+    bd.reserve(sizeof(float) * n * k);
+    bi.reserve(sizeof(idx_t) * n * k);
+    s_stats_.reserve(2 * sizeof(unsigned long long));
+    if (!host_cs_) HIP_CHECK(hipStreamCreateWithFlags(&host_cs_, hipStreamNonBlocking));
+    while ((int)host_ev_.size() < 2 * P + 1) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        host_ev_.push_back(e);
+    }
+    hipStream_t cs = host_cs_;
+    // the copy stream writes h_x_ after the index stream's earlier work
+    HIP_CHECK(hipMemsetAsync(s_stats_.ptr, 0, 2 * sizeof(unsigned long long), s));
+    HIP_CHECK(hipEventRecord(host_ev_[2 * P], s));
+    HIP_CHECK(hipStreamWaitEvent(cs, host_ev_[2 * P], 0));
+    std::vector<idx_t> b(P + 1);
+    for (int i = 0; i <= P; i++) b[i] = n * i / P;
+    auto h2d = [&](int i) {
+        const idx_t r = b[i + 1] - b[i];
+        float* dst = bx.as<float>() + b[i] * ldx;
+        if (ldx != d) HIP_CHECK(hipMemsetAsync(dst, 0, sizeof(float) * r * ldx, cs));
+        HIP_CHECK(hipMemcpy2DAsync(dst, sizeof(float) * ldx, x + b[i] * d, sizeof(float) * d,
+                                   sizeof(float) * d, r, hipMemcpyHostToDevice, cs));
+        HIP_CHECK(hipEventRecord(host_ev_[i], cs));
+    };
+    auto d2h = [&](int i) {
+        const idx_t r = b[i + 1] - b[i];
+        HIP_CHECK(hipStreamWaitEvent(cs, host_ev_[P + i], 0));
+        HIP_CHECK(hipMemcpyAsync(distances + b[i] * k, bd.as<float>() + b[i] * k,
+                                 sizeof(float) * r * k, hipMemcpyDeviceToHost, cs));
+        HIP_CHECK(hipMemcpyAsync(labels + b[i] * k, bi.as<idx_t>() + b[i] * k,
+                                 sizeof(idx_t) * r * k, hipMemcpyDeviceToHost, cs));
+    };
+    StageEvents ev;
+    std::vector<hipEvent_t> pm, cm, cpage(P, nullptr);
+    struct Reset {
+        const IndexIVF* ix;
+        std::vector<hipEvent_t>& cm;
+        ~Reset() {
+            ix->paged_marks_ = nullptr;
+            for (auto e : cm) (void)hipEventDestroy(e);
+        }
+    } reset{this, cm};
+    paged_marks_ = &cm;
+    bool interrupted = false;
+    int issued = 0;
+    h2d(0);
+    for (int i = 0; i < P; i++) {
+        // InterruptCallback, polled before each page is queued
+        // (faiss/IndexIVF.cpp:627, 707-713)
+        if (i > 0 && InterruptCallback::is_interrupted()) {
+            interrupted = true;
+            break;
+        }
+        const idx_t r = b[i + 1] - b[i];
+        HIP_CHECK(hipStreamWaitEvent(s, host_ev_[i], 0));
+        pm.push_back(ev.mark(s));
+        const size_t m0 = cm.size();
+        search_device(r, bx.as<float>() + b[i] * ldx, ldx, k, bd.as<float>() + b[i] * k,
+                      bi.as<idx_t>() + b[i] * k, nullptr, s);
+        if (cm.size() > m0) cpage[i] = cm.back();  // an eager run marked its coarse end
+        pm.push_back(ev.mark(s));
+        // the page's assignment is in s_ci_ (max_codes 0: the scan's own)
+        kern::ivf_visit_stats(s_ci_.as<int32_t>(), r * (int64_t)np, d_list_len_.as<uint32_t>(),
+                              (int)nlist, nullptr, s_stats_.as<unsigned long long>(), s);
+        HIP_CHECK(hipEventRecord(host_ev_[P + i], s));
+        issued++;
+        if (i + 1 < P) h2d(i + 1);
+        if (i > 0) d2h(i - 1);
+    }
+    if (issued) d2h(issued - 1);
+    unsigned long long st[2];
+    HIP_CHECK(hipMemcpyAsync(st, s_stats_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipStreamSynchronize(cs));
+    if (interrupted || InterruptCallback::is_interrupted()) FAISS_THROW_MSG("computation interrupted");
+    quantizer->fold_device_stats();
+    // stage times: a page searched eagerly marked its coarse stage's end;
+    // a replayed page takes the coarse share of the last marked page
+    double qms = 0, sms = 0;
+    for (int i = 0; i < issued; i++) {
+        const double t = StageEvents::ms(pm[2 * i], pm[2 * i + 1]);
+        if (cpage[i] && t > 0) paged_qshare_ = StageEvents::ms(pm[2 * i], cpage[i]) / t;
+        qms += t * paged_qshare_;
+        sms += t * (1.0 - paged_qshare_);
+    }
+    indexIVF_stats.nq += n;
+    indexIVF_stats.nlist += st[0];
+    indexIVF_stats.ndis += st[1];
+    if (update_times) {
+        indexIVF_stats.quantization_time += qms;
+        indexIVF_stats.search_time += qms + sms;
+    }
+    return true;
+}
+
 // faiss/IndexIVF.cpp:303-397 and :725-867 on one slice (the whole batch):
 // coarse stage, scan stage, stats.  update_times: search() adds the stage
 // times to indexIVF_stats (search_stats() does not, like the reference).
@@ -1001,6 +1164,8 @@ void IndexIVF::search_host(idx_t n, const float* x, idx_t k, float* distances, i
     check_parallel_mode(parallel_mode);
     const size_t mc = params ? params->max_codes : max_codes;
     if (n == 0) return;
+    if (!per_query_stats && search_host_paged(n, x, k, distances, labels, params_in, update_times))
+        return;
     DevGuard dg(device);
     sync_device();
     hipStream_t s = stream();

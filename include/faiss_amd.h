@@ -12,6 +12,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <chrono>
 #include <cstdint>
 #include <memory>
@@ -634,6 +635,18 @@ struct IndexIVF : Index {
                              float* distances, idx_t* labels, hipStream_t s) const;
     mutable hipStream_t pipe_s_ = nullptr;
     mutable std::vector<hipEvent_t> pipe_ev_;
+    // search() on host buffers in query pages (faiss/gpu/GpuIndex.cu:307-333):
+    // page i + 1's upload on host_cs_ while page i searches on the index
+    // stream, page i - 1's results downloaded behind it; false = not applicable
+    bool search_host_paged(idx_t n, const float* x, idx_t k, float* distances, idx_t* labels,
+                           const SearchParameters* params, bool update_times) const;
+    mutable hipStream_t host_cs_ = nullptr;
+    mutable std::vector<hipEvent_t> host_ev_;
+    // set inside search_host_paged: an eager (not captured) scan marks the
+    // end of each chunk's coarse stage there; replays take the coarse share
+    // of the page time from the last marked page
+    mutable std::vector<hipEvent_t>* paged_marks_ = nullptr;
+    mutable double paged_qshare_ = 0.1;
     // search_device replayed from a hipGraph captured on the second identical
     // call (flat quantizer, no parameters); FAISS_AMD_GRAPH=0: off
     void search_device_eager(idx_t n, const float* x, int ldx, idx_t k, float* distances,
@@ -652,9 +665,13 @@ struct IndexIVF : Index {
         std::vector<std::string> tnames;
         std::vector<double> tunits;
         std::vector<std::pair<hipGraphNode_t, hipGraphNode_t>> tnodes;
+        uint64_t used = 0;  // last use (the least recent entry is replaced)
         void clear();
     };
-    mutable SearchGraph graph_;
+    // one entry per distinct call (a paged host search replays one per page)
+    mutable std::array<SearchGraph, 8> graphs_;
+    mutable uint64_t graph_tick_ = 0;
+    mutable bool capturing_ = false;
     // query image the flat quantizer prepared into s_q_ for the chunk
     // search() is scanning (IndexFlat::assign_device_qimg), null outside it
     mutable const void* shared_qimg_ = nullptr;
