@@ -1004,16 +1004,19 @@ void IndexIVF::search_stats(idx_t n, const float* x, idx_t k, float* distances, 
 
 namespace {
 // query pages of a host-buffer search: FAISS_AMD_HOST_PAGES=<P> (1 = one
-// upload, one search, one download); by default up to 4 pages of >= 16384
-// queries: a device search of fewer queries does not take proportionally
-// less time (c2, 10k queries: 1 page 0.57 ms, 2 pages 0.70 ms per call,
-// scripts/exp_host_pages.py).  A page keeps >= 20 queries, the flat
-// quantizer's batch form (faiss/utils/distances.cpp:807-823), so every page
-// computes the batch's coarse distances.
+// upload, one graph-replayed search, one download; 0 = the eager host path);
+// by default up to 4 pages of >= 25000 queries: a device search of fewer
+// queries does not take proportionally less time (c2's index, per call: 10k
+// queries 1 page 0.62 ms, 2 pages 0.68; 50k 1.82 / 1.69; 100k 3.44 / 2.85,
+// 4 pages 2.89; scripts/exp_host_pages_big.py).  A page
+// keeps >= 20 queries, the flat quantizer's batch form
+// (faiss/utils/distances.cpp:807-823), so every page computes the batch's
+// coarse distances.
 int host_pages(idx_t n) {
     const char* e = getenv("FAISS_AMD_HOST_PAGES");
-    const idx_t want = e ? std::max(1, atoi(e)) : 4;
-    const idx_t min_page = e ? 20 : 16384;
+    if (e && atoi(e) <= 0) return 0;
+    const idx_t want = e ? atoi(e) : 4;
+    const idx_t min_page = e ? 20 : 25000;
     return (int)std::max<idx_t>(1, std::min<idx_t>(want, n / min_page));
 }
 }  // namespace
@@ -1029,8 +1032,9 @@ int host_pages(idx_t n) {
 // would be (per-query work only, the same coarse form).  Taken where the
 // device search replays a graph (flat quantizer, no per-call parameters,
 // max_codes 0, one slice, FAISS_AMD_GRAPH / FAISS_AMD_PIPE unset) and the
-// batch fits one scratch chunk; otherwise false (one page: an eager search
-// per page costs more host time than the overlap saves).
+// batch fits one scratch chunk; otherwise false (the eager host path: an
+// eager search per page costs more host time than the overlap saves).  One
+// page is the upload, the replayed search and the download on two streams.
 bool IndexIVF::search_host_paged(idx_t n, const float* x, idx_t k, float* distances,
                                  idx_t* labels, const SearchParameters* params_in,
                                  bool update_times) const {
@@ -1040,7 +1044,7 @@ bool IndexIVF::search_host_paged(idx_t n, const float* x, idx_t k, float* distan
         (genv && !strcmp(genv, "0")) || getenv("FAISS_AMD_PIPE"))
         return false;
     const int P = host_pages(n);
-    if (P <= 1) return false;
+    if (P < 1) return false;
     const size_t np = std::min(nlist, nprobe);
     if (search_chunk(n, np, k) < n) return false;
     DevGuard dg(device);
@@ -1054,17 +1058,20 @@ bool IndexIVF::search_host_paged(idx_t n, const float* x, idx_t k, float* distan
     bd.reserve(sizeof(float) * n * k);
     bi.reserve(sizeof(idx_t) * n * k);
     s_stats_.reserve(2 * sizeof(unsigned long long));
-    if (!host_cs_) HIP_CHECK(hipStreamCreateWithFlags(&host_cs_, hipStreamNonBlocking));
+    if (!host_cs_ && P > 1) HIP_CHECK(hipStreamCreateWithFlags(&host_cs_, hipStreamNonBlocking));
     while ((int)host_ev_.size() < 2 * P + 1) {
         hipEvent_t e;
         HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         host_ev_.push_back(e);
     }
-    hipStream_t cs = host_cs_;
-    // the copy stream writes h_x_ after the index stream's earlier work
+    // one page: the copies on the index stream too (nothing to overlap)
+    hipStream_t cs = P > 1 ? host_cs_ : s;
     HIP_CHECK(hipMemsetAsync(s_stats_.ptr, 0, 2 * sizeof(unsigned long long), s));
-    HIP_CHECK(hipEventRecord(host_ev_[2 * P], s));
-    HIP_CHECK(hipStreamWaitEvent(cs, host_ev_[2 * P], 0));
+    if (cs != s) {
+        // the copy stream writes h_x_ after the index stream's earlier work
+        HIP_CHECK(hipEventRecord(host_ev_[2 * P], s));
+        HIP_CHECK(hipStreamWaitEvent(cs, host_ev_[2 * P], 0));
+    }
     std::vector<idx_t> b(P + 1);
     for (int i = 0; i <= P; i++) b[i] = n * i / P;
     auto h2d = [&](int i) {
@@ -1073,11 +1080,11 @@ bool IndexIVF::search_host_paged(idx_t n, const float* x, idx_t k, float* distan
         if (ldx != d) HIP_CHECK(hipMemsetAsync(dst, 0, sizeof(float) * r * ldx, cs));
         HIP_CHECK(hipMemcpy2DAsync(dst, sizeof(float) * ldx, x + b[i] * d, sizeof(float) * d,
                                    sizeof(float) * d, r, hipMemcpyHostToDevice, cs));
-        HIP_CHECK(hipEventRecord(host_ev_[i], cs));
+        if (cs != s) HIP_CHECK(hipEventRecord(host_ev_[i], cs));
     };
     auto d2h = [&](int i) {
         const idx_t r = b[i + 1] - b[i];
-        HIP_CHECK(hipStreamWaitEvent(cs, host_ev_[P + i], 0));
+        if (cs != s) HIP_CHECK(hipStreamWaitEvent(cs, host_ev_[P + i], 0));
         HIP_CHECK(hipMemcpyAsync(distances + b[i] * k, bd.as<float>() + b[i] * k,
                                  sizeof(float) * r * k, hipMemcpyDeviceToHost, cs));
         HIP_CHECK(hipMemcpyAsync(labels + b[i] * k, bi.as<idx_t>() + b[i] * k,
@@ -1105,7 +1112,7 @@ bool IndexIVF::search_host_paged(idx_t n, const float* x, idx_t k, float* distan
             break;
         }
         const idx_t r = b[i + 1] - b[i];
-        HIP_CHECK(hipStreamWaitEvent(s, host_ev_[i], 0));
+        if (cs != s) HIP_CHECK(hipStreamWaitEvent(s, host_ev_[i], 0));
         pm.push_back(ev.mark(s));
         const size_t m0 = cm.size();
         search_device(r, bx.as<float>() + b[i] * ldx, ldx, k, bd.as<float>() + b[i] * k,
@@ -1115,7 +1122,7 @@ bool IndexIVF::search_host_paged(idx_t n, const float* x, idx_t k, float* distan
         // the page's assignment is in s_ci_ (max_codes 0: the scan's own)
         kern::ivf_visit_stats(s_ci_.as<int32_t>(), r * (int64_t)np, d_list_len_.as<uint32_t>(),
                               (int)nlist, nullptr, s_stats_.as<unsigned long long>(), s);
-        HIP_CHECK(hipEventRecord(host_ev_[P + i], s));
+        if (cs != s) HIP_CHECK(hipEventRecord(host_ev_[P + i], s));
         issued++;
         if (i + 1 < P) h2d(i + 1);
         if (i > 0) d2h(i - 1);
@@ -1124,7 +1131,7 @@ bool IndexIVF::search_host_paged(idx_t n, const float* x, idx_t k, float* distan
     unsigned long long st[2];
     HIP_CHECK(hipMemcpyAsync(st, s_stats_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    HIP_CHECK(hipStreamSynchronize(cs));
+    if (cs != s) HIP_CHECK(hipStreamSynchronize(cs));
     if (interrupted || InterruptCallback::is_interrupted()) FAISS_THROW_MSG("computation interrupted");
     quantizer->fold_device_stats();
     // stage times: a page searched eagerly marked its coarse stage's end;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Paged host-buffer search by batch size on c2's index (IVF4096,Flat, 1M,
 nprobe 32): faiss_Index_search wall time per call for FAISS_AMD_HOST_PAGES
-= 1 / 2 / 4 / 8 at 10k, 50k and 100k queries beside search_device on the
+= 0 (eager host path) / 1 / 2 / 4 / 8 at 10k, 50k and 100k queries beside search_device on the
 same batch (graph replay; inputs resident); best and median of 7 calls after
 3 warm ones.  Every page count must return the single-page results."""
 import ctypes as C
@@ -53,7 +53,7 @@ for nq in (10_000, 50_000, 100_000):
     b, m = timeit(dev)
     print("nq %6d search_device      best %.3f ms, median %.3f ms" % (nq, b, m), flush=True)
     ref = None
-    for P in (1, 2, 4, 8):
+    for P in (0, 1, 2, 4, 8):
         os.environ["FAISS_AMD_HOST_PAGES"] = str(P)
         D, I = idx.search(xq, k)
         if ref is None:

@@ -28,13 +28,13 @@ def test_flat_pages_bit_exact(amd, orc, gpu, monkeypatch, d):
     idx.add(xb)
     idx.nprobe = 8
     xq = rand(orc, 1000, d, 92)
-    D1, I1, c1, _ = _search_pages(amd, idx, xq, 10, 1, monkeypatch)
+    D1, I1, c1, _ = _search_pages(amd, idx, xq, 10, 0, monkeypatch)  # the eager path
     ref = orc.IVFOracle.from_index(idx)
     Dr, Ir, _, _ = ref.search(xq, 10, 8, nslices=1)
     assert_same_results(D1, I1, Dr, Ir)
     # ragged pages; 50 pages of 20 queries; pages 3 four times: an eager
     # search per page, then the pages' graphs captured, then replayed
-    for pages in (2, 3, 7, 50, 3, 3, 3):
+    for pages in (1, 1, 1, 2, 3, 7, 50, 3, 3, 3):
         D, I, c, (qt, stt) = _search_pages(amd, idx, xq, 10, pages, monkeypatch)
         assert np.array_equal(I, I1) and np.array_equal(D, D1), pages
         assert c == c1 == (1000, c1[1], c1[2])
@@ -77,7 +77,7 @@ def test_default_pages_large_batch(amd, orc, gpu, monkeypatch):
     idx.add(xb)
     idx.nprobe = 4
     xq = rand(orc, 40_000, d, 96)
-    D1, I1, c1, _ = _search_pages(amd, idx, xq, 5, 1, monkeypatch)
+    D1, I1, c1, _ = _search_pages(amd, idx, xq, 5, 0, monkeypatch)
     monkeypatch.delenv("FAISS_AMD_HOST_PAGES")
     amd.cvar.indexIVF_stats.reset()
     for _ in range(3):  # eager, captured, replayed
