@@ -26,6 +26,12 @@ if marker is None:  # the step's last kernel: the IVF re-rank (MFMA paths) or th
     marker = next(m for m in ("k_ivf_rerank", "k_ex_select", "k_ivfpq_scan")
                   if any(m in n for n in names))
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+# the device-resident steps only: the bench's host-buffer calls (its
+# pcie_inclusive leg, paged for large batches) follow them and start with the
+# host path's visit-count kernel; cut the window there
+host0 = next((i for i in range(idx[0] + 1, len(rows)) if "k_ivf_visit_stats" in rows[i]["Kernel_Name"]),
+             len(rows))
+idx = [i for i in idx if i < host0]
 # the bench's timed steps run back to back: take the consecutive pair of
 # step-end kernels with the shortest wall time between them
 pairs = list(zip(idx, idx[1:]))
@@ -53,4 +59,4 @@ if wstats:
                     "MaxNs", "Window"])
         for nm, (c, t, mn, mx) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
             w.writerow([nm, c, t, t / c, 100.0 * t / tot, mn, mx,
-                        "search steps after the first (build launches excluded)"])
+                        "device search steps after the first (build and host-buffer calls excluded)"])
