@@ -458,8 +458,9 @@ void IndexIVF::search_device(idx_t n, const float* x, int ldx, idx_t k, float* d
     const char* genv = getenv("FAISS_AMD_GRAPH");
     std::lock_guard<std::recursive_mutex> g(mu_);
     const auto* qflat = dynamic_cast<const IndexFlat*>(quantizer);
+    // (FAISS_AMD_IVF_STATS: the debug counters synchronise inside the scan)
     const bool eligible = !(genv && !strcmp(genv, "0")) && params_in == nullptr && !qdone_ &&
-                          qflat != nullptr && get_search_slices() <= 1 && n > 0 && !dirty_;
+                          !getenv("FAISS_AMD_IVF_STATS") && qflat != nullptr && get_search_slices() <= 1 && n > 0 && !dirty_;
     if (!eligible) {
         search_device_eager(n, x, ldx, k, distances, labels, params_in, s);
         return;
