@@ -49,6 +49,26 @@ def test_c2_ivf4096_flat_full(amd, orc, gpu):
     check(D, I, Dr, Ir, "c2")
 
 
+def test_c2_host_pages_full(amd, orc, gpu, monkeypatch):
+    # c2's index, a 60k-query host batch: the default pages it (2 pages of
+    # 30k, uploads overlapping searches); equal to the eager one-call path
+    # and, on queries around the page boundary and a spread, to the oracle
+    d, nq = 128, 60_000
+    idx = build(amd, "IVF4096,Flat", d, 1_000_000, 200_000)
+    idx.nprobe = 32
+    xq = amd.float_rand(nq * d, 5678).reshape(nq, d)
+    monkeypatch.delenv("FAISS_AMD_HOST_PAGES", raising=False)
+    for _ in range(3):  # eager pages, captured, replayed
+        D, I = idx.search(xq, 10)
+    monkeypatch.setenv("FAISS_AMD_HOST_PAGES", "0")
+    D0, I0 = idx.search(xq, 10)
+    check(D, I, D0, I0, "c2 pages vs eager")
+    sel = np.r_[0:50, 29_950:30_050, 59_950:60_000, 1_000:60_000:300]
+    ref = orc.IVFOracle.from_index(idx)
+    Dr, Ir, _, _ = ref.search(np.ascontiguousarray(xq[sel]), 10, 32, nslices=1)
+    check(D[sel], I[sel], Dr, Ir, "c2 pages vs oracle")
+
+
 def test_c3_ivf4096_pq32_full(amd, orc, gpu):
     d, nq = 128, 10_000
     idx = build(amd, "IVF4096,PQ32", d, 1_000_000, 200_000)
