@@ -472,31 +472,24 @@ __device__ __forceinline__ void sx_push(uint64_t* b, int n, uint64_t val, int la
 // GH: the two heaps in global scratch (gheap: seq_heap_bytes per block) —
 // max(efSearch, k) beyond what the work group's LDS holds (the reference's
 // harness sweeps efSearch up to 3 nprobe, nprobe into the thousands)
-template <bool LDS_VISITED, bool GH = false>
-__global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __restrict__ x,
-                                                   int ldx, int64_t n, int k, int efSearch,
-                                                   int ef, float* __restrict__ D,
-                                                   int64_t* __restrict__ I,
-                                                   int32_t* __restrict__ I32,
-                                                   uint32_t* __restrict__ vis_global,
-                                                   int64_t vwords,
-                                                   unsigned long long* __restrict__ stats,
-                                                   const uint32_t* __restrict__ only,
-        const uint32_t* __restrict__ qidx, float* __restrict__ gheap = nullptr,
-        ArrivalLog alog = ArrivalLog{}) {
-    // qidx: compact launch over listed queries (input row qidx[b], output
-    // row b); else query b, output row b
-    const int64_t q = qidx ? (int64_t)qidx[blockIdx.x] : (int64_t)blockIdx.x;
-    const int64_t qo = blockIdx.x;
-    if (only && only[q] == 0u) return;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
+// The search of query q (input row q, output row qo) by one wave: the body
+// of k_hnsw_exact, also run in place by k_hnsw_wide<.., INPLACE> for the
+// queries it flags.  blk: the work group's slot of the global heaps and
+// visited words; sm: the work group's dynamic LDS (seq_lds_bytes + visited).
+template <bool LDS_VISITED, bool GH>
+__device__ __forceinline__ void hnsw_exact_query(
+        HNSWDevice g, const float* __restrict__ x, int ldx, int k, int efSearch, int ef,
+        float* __restrict__ D, int64_t* __restrict__ I, int32_t* __restrict__ I32,
+        uint32_t* __restrict__ vis_global, int64_t vwords, unsigned long long* __restrict__ stats,
+        float* __restrict__ gheap, ArrivalLog alog, int64_t q, int64_t qo, int64_t blk,
+        float* sm) {
     const int qpad = seq_qpad(g.ld);
     float* qs = sm;  // [qpad]
-    uint64_t* cb = GH ? (uint64_t*)((char*)gheap + (int64_t)blockIdx.x * seq_heap_bytes(ef, k))
+    uint64_t* cb = GH ? (uint64_t*)((char*)gheap + blk * seq_heap_bytes(ef, k))
                       : (uint64_t*)(sm + qpad);         // MinimaxHeap [1 .. ef]
     uint64_t* rb = cb + seq_slots(ef);                  // result heap [1 .. k]
     int32_t* fi = GH ? (int32_t*)(sm + qpad) : (int32_t*)((char*)(sm + qpad) + seq_heap_bytes(ef, k));
-    uint32_t* vis = LDS_VISITED ? (uint32_t*)(fi + 64) : vis_global + blockIdx.x * vwords;
+    uint32_t* vis = LDS_VISITED ? (uint32_t*)(fi + 64) : vis_global + blk * vwords;
     const int lane = threadIdx.x;
     for (int j = lane; j < qpad; j += 64) qs[j] = j < g.d ? x[q * ldx + j] : 0.f;
     const uint64_t rinit = sx_key(FLT_MAX, -1);  // heap_heapify<CMax> (Heap.h:316-339)
@@ -869,6 +862,28 @@ __global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __
         if (I) I[qo * k + j] = id;
         if (I32) I32[qo * k + j] = id;
     }
+}
+
+template <bool LDS_VISITED, bool GH = false>
+__global__ __launch_bounds__(64) void k_hnsw_exact(HNSWDevice g, const float* __restrict__ x,
+                                                   int ldx, int64_t n, int k, int efSearch,
+                                                   int ef, float* __restrict__ D,
+                                                   int64_t* __restrict__ I,
+                                                   int32_t* __restrict__ I32,
+                                                   uint32_t* __restrict__ vis_global,
+                                                   int64_t vwords,
+                                                   unsigned long long* __restrict__ stats,
+                                                   const uint32_t* __restrict__ only,
+        const uint32_t* __restrict__ qidx, float* __restrict__ gheap = nullptr,
+        ArrivalLog alog = ArrivalLog{}) {
+    // qidx: compact launch over listed queries (input row qidx[b], output
+    // row b); else query b, output row b
+    const int64_t q = qidx ? (int64_t)qidx[blockIdx.x] : (int64_t)blockIdx.x;
+    const int64_t qo = blockIdx.x;
+    if (only && only[q] == 0u) return;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    hnsw_exact_query<LDS_VISITED, GH>(g, x, ldx, k, efSearch, ef, D, I, I32, vis_global, vwords,
+                                      stats, gheap, alog, q, qo, (int64_t)blockIdx.x, sm);
 }
 
 // The same sequential search for ef, k <= 64 with both heaps in registers.
@@ -1820,7 +1835,11 @@ __host__ __device__ inline size_t wide_lds_bytes(const HNSWDevice& g, int ef) {
     return (size_t)exact_reg_head(g) + 8 * (size_t)ef;
 }
 
-template <bool LDS_VISITED, bool TRACE = false>
+// INPLACE (FAISS_AMD_HNSW_INPLACE=1): a flagged query is searched again by
+// the sequential body right here, as soon as the wave knows (no re-run
+// launch after the whole batch); its flag is written 0.  The launch's LDS
+// then holds the larger of the two layouts.
+template <bool LDS_VISITED, bool TRACE = false, bool INPLACE = false>
 __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __restrict__ x,
                                                   int ldx, int64_t n, int k, int efSearch, int ef,
                                                   float* __restrict__ D, int64_t* __restrict__ I,
@@ -1829,7 +1848,8 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
                                                   int64_t vwords,
                                                   unsigned long long* __restrict__ stats,
                                                   uint32_t* __restrict__ tie_flags,
-                                                  unsigned long long* __restrict__ tb = nullptr) {
+                                                  unsigned long long* __restrict__ tb = nullptr,
+                                                  ArrivalLog alog = ArrivalLog{}) {
     // TRACE (FAISS_AMD_HNSW_TRACE, profiling): per query the cycles of the
     // level-0 phases summed over its hops — [0] pop_min + count_below, [1]
     // neighbour ids, [2] visited, [3] int8 bound, [4] fp32 rows, [5] compact +
@@ -2193,14 +2213,22 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
         // (k == ef) the divergent eviction's distance still the largest kept
         if (k == ef && S == ef && dvmin == wdis(cs[ef - 1])) tie |= 4u;
     }
-    if (tie_flags && lane == 0) tie_flags[q] = tie;
+    if (tie_flags && lane == 0) tie_flags[q] = INPLACE ? 0u : tie;
     if (TRACE && lane == 0) {
         tr.t[7] = clock64() - tq;
         tr.t[8] = tie != 0u;
 #pragma unroll
         for (int j = 0; j < 16; j++) tb[q * 16 + j] = tr.t[j];
     }
-    if (tie && tie_flags) return;  // the sequential kernel redoes this query
+    if (tie && tie_flags) {  // the sequential kernel redoes this query
+        if constexpr (INPLACE) {
+            __syncthreads();  // the set's LDS becomes the heaps'
+            hnsw_exact_query<LDS_VISITED, false>(g, x, ldx, k, efSearch, ef, D, I, I32,
+                                                 vis_global, vwords, stats, nullptr, alog, q, q,
+                                                 (int64_t)blockIdx.x, sm);
+        }
+        return;
+    }
     if (stats && lane == 0 && g.entry_point >= 0) {
         atomicAdd(&stats[0], 1ull);
         atomicAdd(&stats[1], (unsigned long long)st_n2);
@@ -2238,6 +2266,28 @@ __global__ __launch_bounds__(64) void k_hnsw_wide(HNSWDevice g, const float* __r
     }
 }
 
+// the sequential kernel's arrival log (see hnsw_exact_launch); empty when off
+static ArrivalLog make_arrival_log(const HNSWDevice& g, int k, int ef, void* alog,
+                                   size_t alog_bytes, hipStream_t s) {
+    ArrivalLog al;
+    const char* nenv = getenv("FAISS_AMD_HNSW_NORB");
+    const bool norb_on = nenv ? strcmp(nenv, "0") != 0 : k <= 512;
+    if (alog && norb_on && g.ntotal > 0) {
+        size_t P = 1;
+        while (P < (size_t)k) P <<= 1;
+        const size_t region = 8 * (seq_slots(ef) + seq_slots(k));
+        al.cap = (int64_t)g.ntotal + 2;
+        al.slots = alog_bytes > 256 ? (int64_t)((alog_bytes - 256) / (8 * (size_t)al.cap)) : 0;
+        if (8 * P <= region && region >= 1024 && al.slots > 0) {
+            al.ctr = (uint32_t*)alog;
+            al.base = (uint64_t*)((char*)alog + 256);
+            HIP_CHECK(hipMemsetAsync(al.ctr, 0, sizeof(uint32_t), s));
+        } else {
+            al = ArrivalLog{};
+        }
+    }
+    return al;
+}
 // the sequential kernel over n queries (qidx: the listed ones, compact
 // outputs), register heaps for ef, k <= 64
 static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
@@ -2322,23 +2372,7 @@ static void hnsw_exact_launch(const HNSWDevice& g, const float* x, int ldx, int6
     // (c4 quantizer, 2000 queries all sequential: k 256 / ef 768 7.74 ->
     // 6.97 ms; k = ef = 1024 13.41 -> 13.55 ms, the selection's cost growing
     // with k while a replace_top near the heap's top stays shallow)
-    ArrivalLog al;
-    const char* nenv = getenv("FAISS_AMD_HNSW_NORB");
-    const bool norb_on = nenv ? strcmp(nenv, "0") != 0 : k <= 512;
-    if (alog && norb_on && g.ntotal > 0) {
-        size_t P = 1;
-        while (P < (size_t)k) P <<= 1;
-        const size_t region = 8 * (seq_slots(ef) + seq_slots(k));
-        al.cap = (int64_t)g.ntotal + 2;
-        al.slots = alog_bytes > 256 ? (int64_t)((alog_bytes - 256) / (8 * (size_t)al.cap)) : 0;
-        if (8 * P <= region && region >= 1024 && al.slots > 0) {
-            al.ctr = (uint32_t*)alog;
-            al.base = (uint64_t*)((char*)alog + 256);
-            HIP_CHECK(hipMemsetAsync(al.ctr, 0, sizeof(uint32_t), s));
-        } else {
-            al = ArrivalLog{};
-        }
-    }
+    const ArrivalLog al = make_arrival_log(g, k, ef, alog, alog_bytes, s);
     if (x_lds_vis)
         k_hnsw_exact<true><<<kgrid(n, 64), dim3(64), lds_x + vwords * 4, s>>>(
                 g, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, only, qidx,
@@ -2485,6 +2519,14 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
         if (wq && !strcmp(wq, "0")) gw.q8 = nullptr;
         // FAISS_AMD_HNSW_TRACE=<file>: per-query level-0 phase cycles (profiling)
         const char* tenv = getenv("FAISS_AMD_HNSW_TRACE");
+        // FAISS_AMD_HNSW_INPLACE=1: a flagged query is searched again by the
+        // sequential body inside the wide kernel (its heaps in the LDS: the
+        // launch holds the larger layout), not by a re-run after the batch
+        const char* ienv = getenv("FAISS_AMD_HNSW_INPLACE");
+        const size_t lds_x = seq_lds_bytes(g.ld, ef, k);
+        const size_t lds_wi = std::max(lds_w, lds_x);
+        const bool inplace = ienv && !strcmp(ienv, "1") && flags != nullptr &&
+                             lds_wi <= 64 * 1024;
         if (tenv && lds_w + (size_t)vwords * 4 <= 64 * 1024) {
             unsigned long long* tb = nullptr;
             HIP_CHECK(hipMalloc(&tb, 128 * n));
@@ -2500,6 +2542,16 @@ void hnsw_search(const HNSWDevice& g, const float* x, int ldx, int64_t n, int k,
                 fwrite(h.data(), 128, n, f);
                 fclose(f);
             }
+        } else if (inplace) {
+            const ArrivalLog al = make_arrival_log(g, k, ef, arrival_log, arrival_log_bytes, s);
+            if (lds_wi + (size_t)vwords * 4 <= 64 * 1024 && !wide_global_visited())
+                k_hnsw_wide<true, false, true><<<kgrid(n, 64), dim3(64), lds_wi + vwords * 4, s>>>(
+                        gw, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, flags,
+                        nullptr, al);
+            else
+                k_hnsw_wide<false, false, true><<<kgrid(n, 64), dim3(64), lds_wi, s>>>(
+                        gw, x, ldx, n, k, efSearch, ef, D, I, I32, visited_scratch, vwords, stats,
+                        flags, nullptr, al);
         } else if (lds_w + (size_t)vwords * 4 <= 64 * 1024 && !wide_global_visited())
             k_hnsw_wide<true><<<kgrid(n, 64), dim3(64), lds_w + vwords * 4, s>>>(
                     gw, x, ldx, n, k, efSearch, ef, D, I, I32, nullptr, vwords, stats, flags);

@@ -297,7 +297,7 @@ def test_hnsw_sequential_kernel_wide_ef(amd, orc, gpu, d):
 @pytest.mark.parametrize("nb,ef,k", [(300, 500, 10), (300, 1000, 300), (6000, 200, 200),
                                      (6000, 700, 50), (6000, 2000, 2000)])
 @pytest.mark.parametrize("ties", [False, True])
-@pytest.mark.parametrize("mode", ["wide", "sequential", "sequential_heap"])
+@pytest.mark.parametrize("mode", ["wide", "wide_inplace", "sequential", "sequential_heap"])
 def test_hnsw_wide_edges_bit_exact(amd, orc, gpu, monkeypatch, nb, ef, k, ties, mode):
     """The wide kernel (128 < max(efSearch, k) <= 4096) at its edges: efSearch
     beyond the graph (the candidate set never fills: nalive reaches 0, n2),
@@ -308,9 +308,13 @@ def test_hnsw_wide_edges_bit_exact(amd, orc, gpu, monkeypatch, nb, ef, k, ties, 
     The same through the sequential kernel for every query
     (FAISS_AMD_HNSW_EXACT=1): with its results selected from the arrival log
     (the result heap rebuilt by a replay where the k-th distance is shared)
-    and, FAISS_AMD_HNSW_NORB=0, with the result heap kept throughout."""
-    if mode != "wide":
+    and, FAISS_AMD_HNSW_NORB=0, with the result heap kept throughout; and
+    with the flagged queries searched again inside the wide kernel
+    (FAISS_AMD_HNSW_INPLACE=1)."""
+    if mode.startswith("sequential"):
         monkeypatch.setenv("FAISS_AMD_HNSW_EXACT", "1")
+    if mode == "wide_inplace":
+        monkeypatch.setenv("FAISS_AMD_HNSW_INPLACE", "1")
     monkeypatch.setenv("FAISS_AMD_HNSW_NORB", "0" if mode == "sequential_heap" else "1")
     d = 32
     xb = rand(orc, nb, d, 71)
@@ -328,7 +332,7 @@ def test_hnsw_wide_edges_bit_exact(amd, orc, gpu, monkeypatch, nb, ef, k, ties, 
         names = {nm for nm, _, _ in h.kernel_times()}
     finally:
         amd.set_kernel_timing(False)
-    assert ("hnsw_wide" in names) == (mode == "wide"), names
+    assert ("hnsw_wide" in names) == mode.startswith("wide"), names
     g = orc.HNSWGraph.from_index(h)
     Dr, Ir = g.search(np.ascontiguousarray(xq, dtype=np.float32), k, ef)
     assert_same_results(D, I, Dr, Ir)
