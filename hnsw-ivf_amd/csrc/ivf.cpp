@@ -1364,7 +1364,13 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
     int mode = scan_mode;
     if (env && !strcmp(env, "exact")) mode = 1;
     if (env && !strcmp(env, "mfma")) mode = 0;
-    const int KQ = obits_ <= 14 ? kern::ivf_mfma_kq((int)k, d, np) : 0;
+    // long lists (>= 512 rows on average, nprobe <= 64): 8 keys per filter
+    // thread stream, so a stream of ~1/4 of a list rarely drops a key that
+    // may reach the top k (c4, 610 rows per list: failing probes 0.029 -> 0
+    // per query, overflowing queries 105 -> 0; step 2.29 -> 2.21 ms; c2's
+    // 244-row lists measured slower with 8: 0.291 -> 0.311 ms)
+    const int ktm = np <= 64 && nlist > 0 && ntotal / (idx_t)nlist >= 512 ? 8 : 0;
+    const int KQ = obits_ <= 14 ? kern::ivf_mfma_kq((int)k, d, np, ktm) : 0;
     if (mode != 0 || KQ <= 0 || np > kern::kMaxNprobeFilter || store_pairs || dup_probes_) {
         exact_scan_device(n, x, ldx, k, np, assign, cdis, distances, labels, s, lim, sel,
                           store_pairs);
@@ -1419,7 +1425,7 @@ void IndexIVFFlat::search_preassigned_device(idx_t n, const float* x, int ldx, i
                              dbg ? s_flags_.as<uint32_t>() : nullptr, distances, labels, &ktimes,
                              s, kern::ARENA_ALIGN, d_cbs_.ptr,
                              qready ? const_cast<void*>(qready) : s_q_.ptr, qready != nullptr,
-                             qdone_, fold_);
+                             qdone_, fold_, ktm);
     if (dbg) {
         uint32_t st[4];
         HIP_CHECK(hipMemcpyAsync(st, s_flags_.ptr, sizeof(st), hipMemcpyDeviceToHost, s));

@@ -293,7 +293,8 @@ inline int64_t ivf_max_items(int64_t n, int nprobe, int nlist, int QT) {
 // results are identical to the general exact scan (ivf_exact_search).
 // ivf_mfma_kq = entries kept per (query, list); 0 = not eligible
 // (k > 32 or roundup(d, 16) > 128).
-int ivf_mfma_kq(int k, int d, int nprobe = 0);
+// kt_min: at least that many keys per thread stream (2, 4 or 8; 0: by k)
+int ivf_mfma_kq(int k, int d, int nprobe = 0, int kt_min = 0);
 int ivf_bf3_obits(uint32_t max_list_len);
 // padded dim of the bf16 hi/lo images (multiple of 32)
 constexpr int BDM_HOST = 128;  // bf3.h BDM: max padded dim of the MFMA paths
@@ -321,7 +322,9 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         void* qscratch = nullptr,  // query_image_bytes(n, d) + 4 n bytes
                         bool qready = false,  // qscratch already holds x's image
                         unsigned long long* qdone = nullptr,
-                        int fold = 0);  // cbs is the fold image (split_bf16_stream fold = 1)
+                        int fold = 0,
+                        // ivf_mfma_kq's: keys per thread stream
+                        int kt_min = 0);  // cbs is the fold image (split_bf16_stream fold = 1)
 // stream image of the arena for the streamed filter: per row bf16(code) (DB
 // dims) + a 16-byte tail = 2 DB + 16 bytes.  fold = 0: the tail is the fp32
 // norm (+inf for padding rows) + 12 zero bytes; fold = 1 (L2): the tail is the

@@ -851,7 +851,7 @@ void ivf_list_ynmax(const float* yn, const uint32_t* list_off, const uint32_t* l
     HIP_LAUNCH_CHECK();
 }
 
-int ivf_mfma_kq(int k, int dp, int nprobe) {
+int ivf_mfma_kq(int k, int dp, int nprobe, int kt_min) {
     // entries kept per (query, list) = 4 threads x KT.  A thread stream that
     // drops a key which may reach the top-k "fails" and is re-scanned whole by
     // the re-rank; with few probes the top-k crowds into the query's nearest
@@ -859,7 +859,13 @@ int ivf_mfma_kq(int k, int dp, int nprobe) {
     // (c2 with 2 per stream: filter 105 -> 96 us, but 3.3 failing probes per
     // query take the re-rank from 55 to 347 us.)
     if (bf3_db(dp) > BDM || k > 32) return 0;
-    const int kt = k <= 2 ? 2 : k <= 12 ? 4 : 8;
+    int kt = k <= 2 ? 2 : k <= 12 ? 4 : 8;
+    if (kt_min == 2 || kt_min == 4 || kt_min == 8) kt = std::max(kt, kt_min);
+    // FAISS_AMD_IVF_KT=2|4|8: at least that many (tuning; same results)
+    if (const char* e = getenv("FAISS_AMD_IVF_KT")) {
+        const int v = atoi(e);
+        if (v == 2 || v == 4 || v == 8) kt = std::max(kt, v);
+    }
     return 4 * (nprobe > 0 && nprobe < k ? 8 : kt);
 }
 
@@ -938,10 +944,10 @@ void ivf_flat_scan_mfma(const float* x, int ldx, const float* codes, int ldc, co
                         int64_t max_items, uint32_t* keys, ProbeRec* recs, uint32_t* stats,
                         float* D, int64_t* I, KernelTimes* kt, hipStream_t s, int list_align,
                         const void* cbs, void* qscratch, bool qready,
-                        unsigned long long* qdone, int fold) {
+                        unsigned long long* qdone, int fold, int kt_min) {
     if (n <= 0) return;
     const bool aligned_lists = list_align % BV == 0 && cbs != nullptr;
-    const int KE = ivf_mfma_kq(k, d, nprobe);
+    const int KE = ivf_mfma_kq(k, d, nprobe, kt_min);
     FAISS_THROW_IF_NOT(KE > 0);
     FAISS_THROW_IF_NOT(ldc % 4 == 0);
     FAISS_THROW_IF_NOT(nprobe <= kMaxNprobeFilter);
